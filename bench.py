@@ -1,0 +1,268 @@
+"""Benchmark: batched 10-NN QPS on MI355X (BASELINE.json metric).
+
+Default workload (configs[1] of BASELINE.json): exact brute-force 10-NN over a
+1M x 128-d L2Squared corpus with a 10k-query batch -- recall@10 = 1.0 by
+construction and ids identical to the reference distancer path.  A "step" is
+one batch of queries searched over the whole corpus.
+
+N GPUs (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
+the corpus is sharded by contiguous id range over the ranks (local top-k per
+shard), the per-shard (dist, id) lists are all-gathered over RCCL/xGMI and
+merged on every rank (index.go:967-1044 restated on device).  Total work is
+fixed, so scaling is "strong"; value = queries/s over the whole corpus.
+
+--workload hnsw: layer-0 beam search over a graph built by the CPU
+restatement (oracle/, test infrastructure) on a smaller corpus; reports QPS
+and recall@10.  Not the headline line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "batched 10-NN QPS at recall@10≥0.95, 1M×128-d L2, on 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+FP32_MFMA_PEAK_TF = 157.3    # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
+
+
+def counter_uniform(seed: int, row0: int, nrows: int, dim: int) -> np.ndarray:
+    """Counter-based U[0,1) float32: value(row, col) depends only on (seed, row,
+    col), so every rank can generate exactly its own rows of the corpus."""
+    out = np.empty((nrows, dim), np.float32)
+    chunk = max(1, (1 << 22) // dim)
+    cols = np.arange(dim, dtype=np.uint64)
+    for r0 in range(0, nrows, chunk):
+        r1 = min(nrows, r0 + chunk)
+        rows = np.arange(row0 + r0, row0 + r1, dtype=np.uint64)[:, None]
+        x = rows * np.uint64(dim) + cols[None, :]
+        x = x * np.uint64(0x9E3779B97F4A7C15) + np.uint64((seed * 0xD1B54A32D192ED03) & 0xFFFFFFFFFFFFFFFF)
+        x ^= x >> np.uint64(30)
+        x *= np.uint64(0xBF58476D1CE4E5B9)
+        x ^= x >> np.uint64(27)
+        x *= np.uint64(0x94D049BB133111EB)
+        x ^= x >> np.uint64(31)
+        out[r0:r1] = (x >> np.uint64(40)).astype(np.float32) * np.float32(1.0 / (1 << 24))
+    return out
+
+
+def dist_env():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return ws, rank, local
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", choices=["exact", "hnsw"], default="exact")
+    ap.add_argument("--n", type=int, default=1_000_000)
+    ap.add_argument("--dim", type=int, default=128)
+    ap.add_argument("--nq", type=int, default=10_000)
+    ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--ef", type=int, default=64)
+    ap.add_argument("--metric", default="l2-squared")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample time")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--hnsw-build-threads", type=int, default=16)
+    args = ap.parse_args()
+
+    ws, rank, local = dist_env()
+    import torch
+    import torch.distributed as dist
+
+    import weaviate_amd as W
+
+    if ws > 1:
+        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    # ---- corpus shard of this rank (contiguous id range) ----
+    N, D, NQ, K = args.n, args.dim, args.nq, args.k
+    lo = N * rank // ws
+    hi = N * (rank + 1) // ws
+    n_local = hi - lo
+    base = counter_uniform(1, lo, n_local, D)
+    queries = counter_uniform(2, 0, NQ, D)
+
+    ix = W.GPUVectorIndex(D, args.metric, capacity=max(n_local, 1), device=local, id_base=lo,
+                          max_connections=16 if args.workload == "hnsw" else 64)
+    ix.upload_vectors(base)
+    mode = "exact"
+    graph_info = None
+    ref = None
+    if args.workload == "hnsw":
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pyoracle as O  # graph construction = test infrastructure (CPU restatement)
+        t0 = time.time()
+        ref = O.Index(D, args.metric, 16, 64, capacity=n_local, seed=1)
+        ref.add_batch(base, threads=args.hnsw_build_threads)
+        g = ref.export_graph()
+        ix.upload_graph(g)
+        graph_info = {"build_s": round(time.time() - t0, 1), "M": 16, "efConstruction": 64,
+                      "max_level": g["max_level"]}
+        mode = "hnsw"
+
+    dpad = (D + 3) & ~3
+    qt = torch.zeros((NQ, dpad), dtype=torch.float32, device=dev)
+    qt[:, :D] = torch.from_numpy(queries).to(dev)
+    out_ids = torch.empty((NQ, K), dtype=torch.int64, device=dev)
+    out_d = torch.empty((NQ, K), dtype=torch.float32, device=dev)
+    out_n = torch.empty((NQ,), dtype=torch.int32, device=dev)
+    if ws > 1:
+        g_ids = torch.empty((ws, NQ, K), dtype=torch.int64, device=dev)
+        g_d = torch.empty((ws, NQ, K), dtype=torch.float32, device=dev)
+        g_n = torch.empty((ws, NQ), dtype=torch.int32, device=dev)
+        m_ids = torch.empty((NQ, K), dtype=torch.int64, device=dev)
+        m_d = torch.empty((NQ, K), dtype=torch.float32, device=dev)
+        m_n = torch.empty((NQ,), dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    kern_ms = []
+
+    def step(timed=False):
+        ix.search_batch_device(qt.data_ptr(), NQ, K, out_ids.data_ptr(), out_d.data_ptr(), out_n.data_ptr(),
+                               ef=args.ef if mode == "hnsw" else 0, mode=mode, stream=stream)
+        if timed:
+            kern_ms.append(ix.last_kernel_times())
+        if ws > 1:
+            dist.all_gather_into_tensor(g_ids, out_ids)
+            dist.all_gather_into_tensor(g_d, out_d)
+            dist.all_gather_into_tensor(g_n, out_n)
+            W.merge_shards_device(g_d.data_ptr(), g_ids.data_ptr(), g_n.data_ptr(), ws, NQ, K, m_d.data_ptr(),
+                                  m_ids.data_ptr(), m_n.data_ptr(), stream=stream)
+
+    ix.set_timing(True)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if ws > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(timed=True)
+    torch.cuda.synchronize(dev)
+    if ws > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if ws > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    stats = ix.last_batch_stats()
+
+    final_ids = (m_ids if ws > 1 else out_ids).cpu().numpy().view(np.uint64)
+    final_d = (m_d if ws > 1 else out_d).cpu().numpy()
+
+    qps = NQ * args.steps / elapsed
+    result = {
+        "metric": METRIC,
+        "value": round(qps, 1),
+        "unit": "queries/s",
+        "n_gpus": ws,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1000 * elapsed / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic: counter-based U[0,1) float32 corpus (seed 1) and queries (seed 2)",
+        "config": {
+            "workload": ("exact brute-force %d-NN, %s x %d-d %s, %d-query batch (BASELINE configs[1])"
+                         % (K, f"{N:,}", D, args.metric, NQ)) if mode == "exact" else
+                        ("hnsw layer-0 beam search ef=%d, %s x %d-d %s, %d-query batch" % (args.ef, f"{N:,}", D,
+                                                                                         args.metric, NQ)),
+            "N": N, "dim": D, "nq": NQ, "k": K, "metric": args.metric, "mode": mode,
+            "parallelism": f"corpus sharded over {ws} GPU(s) by id range" + (
+                ", RCCL all-gather of per-shard top-k + device merge" if ws > 1 else ""),
+        },
+    }
+
+    # ---- roofline of the dominant kernel (HIP events on its launch stream) ----
+    if mode == "exact":
+        mfma_ms = float(np.mean([k["bf_mfma_ms"] for k in kern_ms]))
+        flops = 2.0 * D * n_local * NQ    # algorithmic: 2*D*N per query
+        achieved = flops / (mfma_ms * 1e-3) / 1e12
+        result["roofline"] = {"bound": "mfma", "kernel": "wv_bf_mfma_kernel", "achieved": round(achieved, 2),
+                              "peak": FP32_MFMA_PEAK_TF, "unit": "TFLOP/s",
+                              "frac": round(achieved / FP32_MFMA_PEAK_TF, 4), "traffic": None,
+                              "kernel_ms": round(mfma_ms, 3),
+                              "finalize_ms": round(float(np.mean([k["bf_finalize_ms"] for k in kern_ms])), 3),
+                              "fallback_queries": stats["fallbacks"]}
+    else:
+        hnsw_ms = float(np.mean([k["hnsw_ms"] for k in kern_ms]))
+        e, x = stats["dist_evals"], stats["expansions"]
+        by = 4.0 * D * e + 4.0 * 32 * x   # 4*D*E + 4*deg_slots*X (deg0 = 2M = 32)
+        achieved = by / (hnsw_ms * 1e-3) / 1e9
+        result["roofline"] = {"bound": "hbm", "kernel": "wv_hnsw_kernel", "achieved": round(achieved, 1),
+                              "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                              "traffic": None, "kernel_ms": round(hnsw_ms, 3),
+                              "dist_evals_per_query": round(e / NQ, 1), "expansions_per_query": round(x / NQ, 1)}
+        result["graph"] = graph_info
+    pmc = os.path.join(ROOT, "profiles", "pmc_%s.json" % result["roofline"]["kernel"])
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            p = json.load(f)
+        if p.get("N") == n_local and p.get("nq") == NQ and p.get("dim") == D:
+            result["roofline"]["traffic"] = p.get("hbm_bytes_per_launch")
+
+    # ---- CPU baseline + parity sample (rank 0, N=1 only) ----
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pyoracle as O
+        threads = args.cpu_threads
+        metric_id = O.METRICS[args.metric]
+        if mode == "exact":
+            probe = 32
+            t0 = time.perf_counter()
+            oi, od, on = O.flat_scan(metric_id, base, queries[:probe], K, threads=threads)
+            per_q = (time.perf_counter() - t0) / probe
+            ns = int(min(NQ, max(probe, args.cpu_seconds / max(per_q, 1e-9))))
+            t0 = time.perf_counter()
+            oi, od, on = O.flat_scan(metric_id, base, queries[:ns], K, threads=threads)
+            cpu_t = time.perf_counter() - t0
+            kind_desc = "flatSearch restated in C (AVX2 asm-order distancer, oracle/)"
+            parity = bool((oi == final_ids[:ns]).all() and np.array_equal(od.view(np.uint32),
+                                                                            final_d[:ns].view(np.uint32)))
+            result["parity_sample"] = {"queries": ns, "ids_and_dists_bit_identical": parity}
+        else:
+            ns = min(NQ, 2000)
+            t0 = time.perf_counter()
+            oi, od, on, _ = ref.search_batch(queries[:ns], K, args.ef, threads=threads)
+            cpu_t = time.perf_counter() - t0
+            kind_desc = "knnSearchByVector restated in C on the same graph (oracle/)"
+            same = float((oi == final_ids[:ns]).mean())
+            ti, td, tn = O.flat_scan(metric_id, base, queries[:ns], K, threads=threads)
+            rec_gpu = float(np.mean([len(set(a) & set(b)) / K for a, b in zip(final_ids[:ns].tolist(), ti.tolist())]))
+            rec_cpu = float(np.mean([len(set(a) & set(b)) / K for a, b in zip(oi.tolist(), ti.tolist())]))
+            result["parity_sample"] = {"queries": ns, "id_match_frac": same, "recall@10_gpu": rec_gpu,
+                                       "recall@10_cpu_restatement": rec_cpu}
+        result["cpu_baseline"] = {"value": round(ns / cpu_t, 1), "unit": "queries/s", "cores": threads,
+                                  "kind": "port",
+                                  "sample": f"{ns} of the {NQ} queries over the full {N:,}-row corpus "
+                                            f"({cpu_t:.1f} s, {threads} threads, GOMAXPROCS-equivalent); "
+                                            + kind_desc}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    ix.close()
+    if ws > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

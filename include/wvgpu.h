@@ -1,0 +1,161 @@
+/*
+ * wvgpu.h -- C ABI of the MI355X vector-index engine (libwvgpu.so).
+ *
+ * This is the drop-in boundary a cgo package (adapters/repos/db/vector/gpu,
+ * see INTEGRATION.md) binds.  It replaces, for the search path, the methods of
+ * the reference's VectorIndex interface
+ *   adapters/repos/db/vector_index.go:23-40
+ *     SearchByVector(vector []float32, k int, allow helpers.AllowList)
+ *         ([]uint64, []float32, error)                          -> wv_search_by_vector
+ *     SearchByVectorDistance(vector []float32, dist float32, maxLimit int64,
+ *         allow helpers.AllowList) ([]uint64, []float32, error)  -> wv_search_by_vector_distance
+ * as implemented by the hnsw package
+ *   adapters/repos/db/vector/hnsw/search.go:64-79 (SearchByVector)
+ *   adapters/repos/db/vector/hnsw/search.go:90-158 (SearchByVectorDistance)
+ *   adapters/repos/db/vector/hnsw/search.go:460-550 (knnSearchByVector)
+ *   adapters/repos/db/vector/hnsw/flat_search.go:19-74 (flatSearch)
+ * plus a batched entry point (wv_search_batch*) that a Go-side micro-batcher
+ * uses to coalesce concurrent single-query calls.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only.  Host pointers unless the name says
+ *    _device.  The library copies inputs during the call and never retains a
+ *    caller pointer after returning (cgo pointer rules).
+ *  - Every function returns a wv_status; on failure wv_last_error() returns a
+ *    thread-local message.  Nothing aborts or exits across the ABI.
+ *  - Ids: the index holds local ids 0..capacity-1 (Weaviate docIDs are dense per
+ *    shard, adapters/repos/db/indexcounter); results are returned as uint64
+ *    ids = id_base + local id (id_base set at creation, for corpus sharding).
+ *  - The AllowList (adapters/repos/db/helpers/allow_list.go:19-118) crosses
+ *    the boundary as a dense little-endian uint64 bitmap: bit i of word i/64
+ *    set <=> docID i allowed.  allow_bits == NULL means "no filter".
+ *  - Results are ascending by distance; equal distances are ordered by id.
+ *  - Thread safety: an index may be searched from many threads at once; each
+ *    call uses its own stream and scratch.  Uploads (vectors, graph,
+ *    tombstones, config) must not race with searches on the same index.
+ */
+#ifndef WVGPU_H
+#define WVGPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    WV_OK = 0,
+    WV_EINVAL = 1,    /* bad argument */
+    WV_EOOM = 2,      /* device allocation failed */
+    WV_EDEVICE = 3,   /* HIP runtime / kernel launch failure */
+    WV_ESTATE = 4,    /* index not ready for this call (e.g. no graph for HNSW) */
+    WV_EDELETED = 5   /* entrypoint deleted (search.go:473-476) */
+} wv_status;
+
+/* distancer.Provider.Type() (distancer/provider.go:14-24) */
+typedef enum { WV_L2_SQUARED = 0, WV_DOT = 1, WV_COSINE_DOT = 2 } wv_metric;
+
+typedef enum {
+    WV_MODE_AUTO = 0,   /* SearchByVector dispatch: flat if allow && !forbidFlat && |allow| < cutoff */
+    WV_MODE_EXACT = 1,  /* flatSearch over the allow list (or every id) */
+    WV_MODE_HNSW = 2    /* knnSearchByVector */
+} wv_mode;
+
+/* The subset of ent.UserConfig (entities/vectorindex/hnsw/config.go:53-185)
+ * that the search path reads (index.go:79-87). */
+typedef struct {
+    int device;                 /* HIP device ordinal */
+    int max_connections;        /* M; layer-0 degree 2M (index.go:223) */
+    int64_t ef;                 /* -1 = dynamic */
+    int64_t dynamic_ef_min;
+    int64_t dynamic_ef_max;
+    int64_t dynamic_ef_factor;
+    int64_t flat_search_cutoff;
+    int forbid_flat;
+    uint64_t id_base;           /* global id of local id 0 */
+} wv_config;
+
+typedef struct wv_index wv_index;
+
+/* Fill cfg with the reference defaults (config.go:33-50). */
+void wv_config_default(wv_config *cfg);
+
+int wv_index_create(int dim, int metric, const wv_config *cfg, uint64_t capacity, wv_index **out);
+int wv_index_destroy(wv_index *ix);
+int wv_index_update_config(wv_index *ix, const wv_config *cfg);
+
+/* Upload n rows (row-major float32 [n][dim]) for local ids first_id..first_id+n-1.
+ * Cosine vectors are normalized on the device exactly as Normalize does
+ * (distancer/normalize.go:16-32). */
+int wv_index_upload_vectors(wv_index *ix, const float *rows, uint64_t n, uint64_t first_id);
+/* Same, from a device pointer (row stride ld floats). */
+int wv_index_upload_vectors_device(wv_index *ix, const float *d_rows, uint64_t n, uint64_t first_id, int ld);
+
+/* HNSW graph as a fixed-degree CSR snapshot of the reference graph
+ * (vertex.go:18-24 connections[level]):
+ *   levels[n]                 node level, -1 for nil nodes
+ *   layer0[n*deg0]            layer-0 neighbours in stored order, pad 0xFFFFFFFF
+ *   upper_row[n]              row of the node in `upper` (0xFFFFFFFF if level 0)
+ *   upper[n_upper*max_level*degU]  neighbours at level l in row[l-1]
+ * deg0 <= 256 and degU <= 256. */
+int wv_index_upload_graph(wv_index *ix, uint64_t n, const int8_t *levels, const uint32_t *layer0, int deg0,
+                          const uint32_t *upper_row, const uint32_t *upper, uint64_t n_upper, int degU,
+                          int max_level, uint64_t entrypoint);
+
+/* Tombstones (delete.go:546-566) as a bitmap over local ids (replaces the set). */
+int wv_index_set_tombstones(wv_index *ix, const uint64_t *bits, uint64_t nbits);
+
+/* searchTimeEF (search.go:30-62) for the current config. */
+int wv_search_time_ef(const wv_index *ix, int k);
+
+/* SearchByVector (search.go:64-79). out_ids/out_dists have room for k;
+ * *out_n receives the count (0 for an empty index). */
+int wv_search_by_vector(wv_index *ix, const float *vector, int k, const uint64_t *allow_bits,
+                        uint64_t allow_nbits, uint64_t *out_ids, float *out_dists, int32_t *out_n);
+
+/* SearchByVectorDistance (search.go:90-158).  max_limit < 0 means unlimited.
+ * At most out_cap results are written; *out_n receives the full count. */
+int wv_search_by_vector_distance(wv_index *ix, const float *vector, float target_distance,
+                                 int64_t max_limit, const uint64_t *allow_bits, uint64_t allow_nbits,
+                                 uint64_t *out_ids, float *out_dists, int64_t out_cap, int64_t *out_n);
+
+/* Batched search of nq queries (row-major [nq][dim]).  ef <= 0 selects
+ * searchTimeEF(k).  allow_bits may be NULL, one bitmap shared by the batch
+ * (allow_stride_words == 0) or one bitmap per query.  out_* are [nq][k]. */
+int wv_search_batch(wv_index *ix, const float *queries, int nq, int k, int ef, const uint64_t *allow_bits,
+                    uint64_t allow_nbits, uint64_t allow_stride_words, int mode, uint64_t *out_ids,
+                    float *out_dists, int32_t *out_n);
+
+/* Device-resident variant: every pointer is device memory; the call is
+ * asynchronous on `stream` (a hipStream_t, NULL = the index's own stream) and
+ * needs no host synchronisation except for queries that fall back to the
+ * exact re-scan (reported through *d_status).  Used by the benchmark so that
+ * the timed region sees only device work. */
+int wv_search_batch_device(wv_index *ix, const float *d_queries, int nq, int k, int ef,
+                           const uint64_t *d_allow_bits, uint64_t allow_nbits, uint64_t allow_stride_words,
+                           int mode, uint64_t *d_out_ids, float *d_out_dists, int32_t *d_out_n, void *stream);
+
+/* Merge per-shard results: for each query, the k best (dist, id) of the
+ * n_shards lists d_in_*[shard][nq][k] (entries beyond d_in_n are ignored).
+ * Used after the RCCL all-gather of corpus-shard results. */
+int wv_merge_shards_device(const float *d_in_dists, const uint64_t *d_in_ids, const int32_t *d_in_n, int n_shards,
+                           int nq, int k, float *d_out_dists, uint64_t *d_out_ids, int32_t *d_out_n, void *stream);
+
+/* Per-query statistics of the last HNSW batch on this thread (nullable
+ * outputs): distance evaluations and expansions summed over the batch. */
+int wv_last_batch_stats(wv_index *ix, uint64_t *dist_evals, uint64_t *expansions, uint64_t *fallbacks);
+
+/* Kernel timing with HIP events on the launch stream (off by default).  When
+ * enabled, the last batch records the device time of its dominant kernels:
+ * the MFMA brute-force kernel, the exact re-rank/finalize kernel and the HNSW
+ * beam-search kernel (milliseconds, summed over the launches of the batch). */
+int wv_index_set_timing(wv_index *ix, int enable);
+int wv_last_kernel_times(wv_index *ix, float *bf_mfma_ms, float *bf_finalize_ms, float *hnsw_ms);
+
+const char *wv_last_error(void);
+const char *wv_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* WVGPU_H */

@@ -1,0 +1,284 @@
+"""Parity of the HIP path (through the C ABI) against the CPU restatement.
+
+Bar: bit-identical ids and distances on tie-free float data (uniform [0,1)),
+since every distance the GPU returns is computed in the reference's own
+summation order.  Runs on an MI355X (-m gpu).
+"""
+import numpy as np
+import pytest
+
+import pyoracle as O
+import weaviate_amd as W
+
+pytestmark = pytest.mark.gpu
+
+METRIC_NAMES = {O.L2: "l2-squared", O.DOT: "dot", O.COSINE: "cosine-dot"}
+
+
+def _data(n, d, nq, seed=0, metric=O.L2):
+    rng = np.random.default_rng(seed)
+    base = rng.random((n, d), dtype=np.float32)
+    qs = rng.random((nq, d), dtype=np.float32)
+    if metric == O.DOT:
+        base -= 0.5
+        qs -= 0.5
+    return base, qs
+
+
+def _norm_rows(a):
+    return np.stack([O.normalize(r) for r in a])
+
+
+def _same(a_ids, a_d, b_ids, b_d):
+    assert a_ids.tolist() == b_ids.tolist()
+    assert np.array_equal(a_d.view(np.uint32), b_d.view(np.uint32))
+
+
+def _same_tie_aware(a_ids, a_d, b_ids, b_d):
+    """Distances bit-identical; ids identical up to the order among equal
+    distances, and free at the k-boundary distance (the reference breaks ties
+    by heap layout, the GPU by id: SURVEY 8c)."""
+    assert np.array_equal(a_d.view(np.uint32), b_d.view(np.uint32))
+    if len(a_d) == 0:
+        return
+    last = a_d[-1]
+    for v in np.unique(a_d):
+        if v == last:
+            continue
+        assert set(a_ids[a_d == v].tolist()) == set(b_ids[b_d == v].tolist())
+
+
+@pytest.mark.parametrize("dim", [1, 3, 4, 16, 31, 32, 35, 64, 100, 128, 130, 256, 777])
+@pytest.mark.parametrize("metric", [O.L2, O.DOT, O.COSINE])
+def test_exact_distance_bitwise_all_dims(dim, metric):
+    """Rows D1-D3 of SURVEY 8a: the GPU distancer equals asm.L2/asm.Dot bit for bit
+    (lengths of distancer/l2_amd64_test.go:36)."""
+    base, qs = _data(257, dim, 4, seed=dim, metric=metric)
+    ix = W.GPUVectorIndex(dim, METRIC_NAMES[metric], capacity=257)
+    ix.upload_vectors(base)
+    k = 40  # > 32: the exact-scan path, every distance reference-order
+    ids, ds, n = ix.search_batch(qs, k, mode="exact")
+    b = _norm_rows(base) if metric == O.COSINE else base
+    q = _norm_rows(qs) if metric == O.COSINE else qs
+    oi, od, on = O.flat_scan(metric, b, q, k)
+    for i in range(len(qs)):
+        _same_tie_aware(ids[i, : n[i]], ds[i, : n[i]], oi[i, : on[i]], od[i, : on[i]])
+    ix.close()
+
+
+@pytest.mark.parametrize("metric", [O.L2, O.DOT, O.COSINE])
+def test_bruteforce_mfma_ids_identical(metric):
+    base, qs = _data(20000, 128, 300, seed=1, metric=metric)
+    ix = W.GPUVectorIndex(128, METRIC_NAMES[metric], capacity=20000)
+    ix.upload_vectors(base)
+    ids, ds, n = ix.search_batch(qs, 10, mode="exact")
+    b = _norm_rows(base) if metric == O.COSINE else base
+    q = _norm_rows(qs) if metric == O.COSINE else qs
+    oi, od, on = O.flat_scan(metric, b, q, 10)
+    assert (n == 10).all()
+    _same(ids, ds, oi, od)
+    st = ix.last_batch_stats()
+    assert st["fallbacks"] <= 3, st  # the certificate holds on almost every query
+    ix.close()
+
+
+def test_bruteforce_ragged_sizes_and_small_batches():
+    for n_base, nq, k in [(1, 1, 10), (5, 3, 10), (129, 1, 1), (1000, 7, 32), (3001, 129, 10)]:
+        base, qs = _data(n_base, 96, nq, seed=n_base)
+        ix = W.GPUVectorIndex(96, "l2-squared", capacity=n_base)
+        ix.upload_vectors(base)
+        ids, ds, n = ix.search_batch(qs, k, mode="exact")
+        oi, od, on = O.flat_scan(O.L2, base, qs, k)
+        assert n.tolist() == on.tolist()
+        for i in range(nq):
+            _same(ids[i, : n[i]], ds[i, : n[i]], oi[i, : on[i]], od[i, : on[i]])
+        ix.close()
+
+
+def test_bruteforce_allow_list_and_tombstones():
+    n_base = 8000
+    base, qs = _data(n_base, 64, 64, seed=3)
+    rng = np.random.default_rng(4)
+    allow_ids = np.nonzero(rng.random(n_base) < 0.1)[0]
+    tomb_ids = np.nonzero(rng.random(n_base) < 0.05)[0]
+    ix = W.GPUVectorIndex(64, "l2-squared", capacity=n_base)
+    ix.upload_vectors(base)
+    ix.set_tombstones(tomb_ids)
+    al = W.AllowList.from_ids(allow_ids, n_base)
+    ids, ds, n = ix.search_batch(qs, 10, allow=al, mode="exact")
+    tb = O.bits_from_ids(tomb_ids, n_base)
+    oi, od, on = O.flat_scan(O.L2, base, qs, 10, allow_bits=al.words, tomb_bits=tb)
+    _same(ids, ds, oi, od)
+    assert not set(ids.ravel().tolist()) & set(tomb_ids.tolist())
+    # per-query allow lists
+    per = [W.AllowList.from_ids(np.nonzero(rng.random(n_base) < 0.2)[0], n_base) for _ in range(len(qs))]
+    ids, ds, n = ix.search_batch(qs, 10, allow=per, mode="exact")
+    for i in range(len(qs)):
+        oi, od, on = O.flat_scan(O.L2, base, qs[i : i + 1], 10, allow_bits=per[i].words, tomb_bits=tb)
+        _same(ids[i], ds[i], oi[0], od[0])
+    ix.close()
+
+
+def test_large_k_exact_path():
+    base, qs = _data(5000, 32, 5, seed=6)
+    ix = W.GPUVectorIndex(32, "dot", capacity=5000)
+    ix.upload_vectors(base)
+    ids, ds, n = ix.search_batch(qs, 150, mode="exact")
+    oi, od, on = O.flat_scan(O.DOT, base, qs, 150)
+    _same(ids, ds, oi, od)
+    ix.close()
+
+
+def _build_graph(n, d, metric=O.L2, M=16, efc=64, seed=11):
+    rng = np.random.default_rng(seed)
+    base = rng.random((n, d), dtype=np.float32)
+    idx = O.Index(d, metric, M, efc, capacity=n, seed=seed)
+    idx.add_batch(base, threads=8)
+    return base, idx
+
+
+@pytest.mark.parametrize("metric", [O.L2, O.COSINE, O.DOT])
+def test_hnsw_identical_to_reference_restatement(metric):
+    n, d = 6000, 48
+    base, idx = _build_graph(n, d, metric)
+    qs = np.random.default_rng(99).random((200, d), dtype=np.float32)
+    g = idx.export_graph()
+    ix = W.GPUVectorIndex(d, METRIC_NAMES[metric], capacity=n, max_connections=16)
+    ix.upload_vectors(base)
+    ix.upload_graph(g)
+    for ef in (10, 32, 100):
+        ids, ds, cnt = ix.search_batch(qs, 10, ef=ef, mode="hnsw")
+        # the restatement normalizes cosine queries itself (search.go:68-72)
+        oi, od, on, st = idx.search_batch(qs, 10, ef, threads=8)
+        assert cnt.tolist() == on.tolist()
+        _same(ids, ds, oi, od)
+    ix.close()
+
+
+def test_hnsw_filtered_and_tombstoned_identical():
+    n, d = 5000, 32
+    base, idx = _build_graph(n, d, O.L2)
+    qs = np.random.default_rng(7).random((100, d), dtype=np.float32)
+    rng = np.random.default_rng(8)
+    allow = np.nonzero(rng.random(n) < 0.5)[0]
+    tomb = np.nonzero(rng.random(n) < 0.03)[0]
+    for t in tomb:
+        idx.add_tombstone(int(t))
+    g = idx.export_graph()
+    ix = W.GPUVectorIndex(d, "l2-squared", capacity=n, max_connections=16, forbid_flat=True)
+    ix.upload_vectors(base)
+    ix.upload_graph(g)
+    ix.set_tombstones(tomb)
+    al = W.AllowList.from_ids(allow, n)
+    ids, ds, cnt = ix.search_batch(qs, 10, ef=64, allow=al, mode="hnsw")
+    oi, od, on, st = idx.search_batch(qs, 10, 64, allow=al.words)
+    assert ix.last_batch_stats()["fallbacks"] == 0
+    _same(ids, ds, oi, od)
+    ix.close()
+
+
+def test_kat_hand_built_graph_on_gpu(kats):
+    c = kats["hand_built_graph"]
+    vec = np.array(c["vectors"], np.float32)
+    n = len(vec)
+    levels = np.full(n, -1, np.int8)
+    layer0 = np.full((n, 4), 0xFFFFFFFF, np.uint32)
+    upper_row = np.full(n, 0xFFFFFFFF, np.uint32)
+    upper = np.full((1, c["max_level"], 4), 0xFFFFFFFF, np.uint32)
+    r = 0
+    for nd in c["nodes"]:
+        levels[nd["id"]] = nd["level"]
+        layer0[nd["id"], : len(nd["connections"][0])] = nd["connections"][0]
+        if nd["level"] >= 1:
+            upper_row[nd["id"]] = r
+            for lv in range(1, nd["level"] + 1):
+                upper[r, lv - 1, : len(nd["connections"][lv])] = nd["connections"][lv]
+            r += 1
+    g = dict(n=n, entrypoint=c["entrypoint"], max_level=c["max_level"], levels=levels, layer0=layer0,
+             upper_row=upper_row, upper=upper)
+    ix = W.GPUVectorIndex(2, "l2-squared", capacity=n, max_connections=2, ef=0, dynamic_ef_min=0,
+                          dynamic_ef_max=0, dynamic_ef_factor=0, flat_search_cutoff=0)
+    ix.upload_vectors(vec)
+    ix.upload_graph(g)
+    ids, _ = ix.search_by_vector(c["query"], c["k"])
+    assert ids.tolist() == c["expect"]
+    ix.close()
+
+
+def test_kat_delete_snapshot_on_gpu(kats):
+    c = kats["delete_snapshot"]
+    snap = c["snapshot"]
+    vec = np.array(c["vectors"], np.float32)
+    ref = O.Index(3, c["metric"], 30, 128, capacity=len(vec))
+    for i, v in enumerate(vec):
+        ref.set_vector(i, v)
+    for nd in snap["nodes"]:
+        ref.import_node(nd["id"], nd["level"], [nd["connections"][str(l)] for l in range(nd["level"] + 1)])
+    ref.set_entrypoint(snap["entrypoint"], snap["currentMaximumLayer"])
+    g = ref.export_graph(deg0=64, degU=32)
+    ix = W.GPUVectorIndex(3, "cosine-dot", capacity=len(vec), max_connections=30, ef=0, dynamic_ef_min=0,
+                          dynamic_ef_max=0, dynamic_ef_factor=0, flat_search_cutoff=0, forbid_flat=True)
+    ix.upload_vectors(vec)
+    ix.upload_graph(g)
+    odd = W.AllowList.from_ids([i for i in range(len(vec)) if i % 2 == 1], len(vec))
+    control, _ = ix.search_by_vector(c["query"], c["k"], allow=odd)
+    ref.set_search_config(ef=0, ef_min=0, ef_max=0, ef_factor=0, flat_search_cutoff=0, forbid_flat=True)
+    rids, _ = ref.search_by_vector(c["query"], c["k"], allow=odd.words)
+    assert control.tolist() == rids.tolist()
+    ix.set_tombstones(c["tombstone_after"])
+    res, _ = ix.search_by_vector(c["query"], c["k"])
+    assert res.tolist() == control.tolist()
+    ix.close()
+
+
+def test_acceptance_distances_on_gpu(kats):
+    a = kats["acceptance_distances"]
+    for name, metric in (("l2", "l2-squared"), ("dot", "dot"), ("cosine", "cosine-dot")):
+        c = a[name]
+        ix = W.GPUVectorIndex(len(c["query"]), metric, capacity=len(c["objects"]))
+        ix.upload_vectors(np.array(c["objects"], np.float32))
+        _, d = ix.search_by_vector(c["query"], 10)
+        assert d.tolist() == pytest.approx(c["expect"], abs=0.01)
+        if name != "cosine":
+            lim = c["limited"] if isinstance(c["limited"], list) else [c["limited"]]
+            for l in lim:
+                _, d = ix.search_by_vector_distance(c["query"], l["distance"])
+                assert d.tolist() == pytest.approx(l["expect"], abs=0.01)
+        ix.close()
+
+
+def test_search_by_vector_distance_matches_restatement():
+    base, idx = _build_graph(3000, 16, O.L2)
+    g = idx.export_graph()
+    ix = W.GPUVectorIndex(16, "l2-squared", capacity=3000, max_connections=16)
+    ix.upload_vectors(base)
+    ix.upload_graph(g)
+    q = np.random.default_rng(3).random(16, dtype=np.float32)
+    for target in (0.3, 0.6):
+        a_ids, a_d = ix.search_by_vector_distance(q, target)
+        b_ids, b_d = idx.search_by_vector_distance(q, target)
+        assert a_ids.tolist() == b_ids.tolist()
+    ix.close()
+
+
+def test_merge_shards_device():
+    import torch
+    rng = np.random.default_rng(0)
+    S, nq, k = 3, 50, 10
+    d = np.sort(rng.random((S, nq, k)).astype(np.float32), axis=2)
+    ids = rng.integers(0, 1 << 40, (S, nq, k)).astype(np.uint64)
+    n = np.full((S, nq), k, np.int32)
+    n[1, :10] = 3
+    dev = torch.device("cuda:0")
+    td = torch.from_numpy(d).to(dev)
+    ti = torch.from_numpy(ids.view(np.int64)).to(dev)
+    tn = torch.from_numpy(n).to(dev)
+    od = torch.empty((nq, k), dtype=torch.float32, device=dev)
+    oi = torch.empty((nq, k), dtype=torch.int64, device=dev)
+    on = torch.empty(nq, dtype=torch.int32, device=dev)
+    W.merge_shards_device(td.data_ptr(), ti.data_ptr(), tn.data_ptr(), S, nq, k, od.data_ptr(), oi.data_ptr(),
+                          on.data_ptr())
+    torch.cuda.synchronize()
+    for q in range(nq):
+        cand = sorted((float(d[s, q, j]), int(ids[s, q, j])) for s in range(S) for j in range(n[s, q]))[:k]
+        assert [c[1] for c in cand] == oi[q].cpu().numpy().view(np.uint64).tolist()

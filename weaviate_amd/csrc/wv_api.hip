@@ -1,0 +1,893 @@
+// wv_api.hip -- host side of the C ABI declared in include/wvgpu.h.
+//
+// Owns device memory for one index (vectors, norms, CSR graph, bitmaps),
+// dispatches SearchByVector the way the reference does (search.go:64-79) and
+// runs the device pipelines of wv_bf.hip / wv_hnsw.hip.  No CPU search code:
+// every distance and every selection happens on the GPU.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/wvgpu.h"
+#include "wv_device.h"
+
+#include "wv_params.h"
+
+extern "C" {
+hipError_t wv_launch_bf_mfma(const wv::BfParams* p, hipStream_t s);
+hipError_t wv_launch_bf_finalize(const wv::BfFinParams* p, hipStream_t s);
+hipError_t wv_launch_exact_scan(const wv::ScanParams* p, hipStream_t s);
+hipError_t wv_launch_rownorm(const float* X, uint64_t N, int D, int ldx, float* norm2, unsigned int* maxbits,
+                             hipStream_t s);
+hipError_t wv_launch_normalize(const float* in, float* out, uint64_t n, int D, int ld, hipStream_t s);
+hipError_t wv_launch_qnorm(const float* Q, int nq, int D, int ldq, int metric, float* out, hipStream_t s);
+hipError_t wv_launch_hnsw(const wv::HnswParams* p, int waves_per_block, hipStream_t s);
+int wv_hnsw_per_wave_words(int dpad, int efc, int sc, int vc_log2, int xs_log2);
+}
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                          \
+    do {                                                                                       \
+        hipError_t _e = (expr);                                                                \
+        if (_e != hipSuccess)                                                                  \
+            return fail(_e == hipErrorOutOfMemory ? WV_EOOM : WV_EDEVICE,                      \
+                        std::string(#expr) + ": " + hipGetErrorString(_e));                   \
+    } while (0)
+
+// growable device scratch buffer
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max<size_t>(bytes, 256);
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    template <class T> T* as() const { return reinterpret_cast<T*>(p); }
+    void release() { if (p) (void)hipFree(p); p = nullptr; cap = 0; }
+};
+
+__global__ void gather_rows_kernel(const float* src, int ld_src, const int32_t* idx, int n, int D, float* dst,
+                                   int ld_dst) {
+    const int r = blockIdx.x;
+    if (r >= n) return;
+    const float* s = src + (size_t)idx[r] * ld_src;
+    float* d = dst + (size_t)r * ld_dst;
+    for (int i = threadIdx.x; i < ld_dst; i += blockDim.x) d[i] = i < D ? s[i] : 0.f;
+}
+
+// copy rows [n][ld_src] into the padded layout [n][ld_dst], zero-filling D..ld_dst
+__global__ void pad_rows_kernel(const float* src, uint64_t ld_src, uint64_t n, int D, float* dst, int ld_dst) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t r = i / ld_dst;
+    const int c = (int)(i % ld_dst);
+    if (r >= n) return;
+    dst[r * ld_dst + c] = c < D ? src[r * ld_src + c] : 0.f;
+}
+
+hipError_t launch_pad_rows(const float* src, uint64_t ld_src, uint64_t n, int D, float* dst, int ld_dst, hipStream_t s) {
+    const uint64_t total = n * (uint64_t)ld_dst;
+    if (total == 0) return hipSuccess;
+    hipLaunchKernelGGL(pad_rows_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, src, ld_src, n, D, dst,
+                       ld_dst);
+    return hipGetLastError();
+}
+
+__global__ void gather_words_kernel(const uint64_t* src, uint64_t stride, const int32_t* idx, int n, uint64_t* dst) {
+    const int r = blockIdx.x;
+    if (r >= n) return;
+    for (uint64_t i = threadIdx.x; i < stride; i += blockDim.x) dst[r * stride + i] = src[(uint64_t)idx[r] * stride + i];
+}
+
+__global__ void scatter_results_kernel(const uint64_t* ids, const float* ds, const int32_t* ns, const int32_t* idx,
+                                       int n, int k, uint64_t* out_ids, float* out_d, int32_t* out_n) {
+    const int r = blockIdx.x;
+    if (r >= n) return;
+    const int q = idx[r];
+    for (int i = threadIdx.x; i < k; i += blockDim.x) {
+        out_ids[(size_t)q * k + i] = ids[(size_t)r * k + i];
+        out_d[(size_t)q * k + i] = ds[(size_t)r * k + i];
+    }
+    if (threadIdx.x == 0) out_n[q] = ns[r];
+}
+
+__global__ void copy_topk_kernel(const float* sd, const uint32_t* si, uint64_t n_eligible_cap, int k, uint64_t id_base,
+                                 uint64_t* out_ids, float* out_d, int32_t* out_n) {
+    // first k of a sorted (dist, id) array; +inf marks ineligible rows
+    __shared__ int cnt;
+    if (threadIdx.x == 0) cnt = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < k; i += blockDim.x) {
+        if ((uint64_t)i < n_eligible_cap && sd[i] != __builtin_inff()) {
+            out_ids[i] = id_base + si[i];
+            out_d[i] = sd[i];
+            atomicAdd(&cnt, 1);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) *out_n = cnt;
+}
+
+__global__ void merge_shards_kernel(const float* in_d, const uint64_t* in_ids, const int32_t* in_n, int n_shards,
+                                    int nq, int k, float* out_d, uint64_t* out_ids, int32_t* out_n) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nq) return;
+    int head[16];
+    for (int s = 0; s < n_shards; ++s) head[s] = 0;
+    int n = 0;
+    for (; n < k; ++n) {
+        int best = -1;
+        float bd = 0.f;
+        uint64_t bi = 0;
+        for (int s = 0; s < n_shards; ++s) {
+            const int cnt = in_n[(size_t)s * nq + q];
+            if (head[s] >= cnt) continue;
+            const size_t off = ((size_t)s * nq + q) * k + head[s];
+            const float d = in_d[off];
+            const uint64_t id = in_ids[off];
+            if (best < 0 || d < bd || (d == bd && id < bi)) { best = s; bd = d; bi = id; }
+        }
+        if (best < 0) break;
+        head[best]++;
+        out_d[(size_t)q * k + n] = bd;
+        out_ids[(size_t)q * k + n] = bi;
+    }
+    out_n[q] = n;
+}
+
+__global__ void popcount_rows_kernel(const uint64_t* bits, uint64_t words, uint64_t stride, int nrows,
+                                     unsigned long long* out) {
+    const int r = blockIdx.x;
+    if (r >= nrows) return;
+    unsigned long long c = 0;
+    for (uint64_t i = threadIdx.x; i < words; i += blockDim.x) c += __popcll(bits[r * stride + i]);
+    atomicAdd(&out[r], c);
+}
+
+}  // namespace
+
+struct wv_index {
+    int dim = 0, dpad = 0, metric = 0;
+    wv_config cfg{};
+    uint64_t capacity = 0;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    // corpus
+    DevBuf vecs;            // [capacity][dpad]
+    DevBuf xnorm;           // [capacity]
+    DevBuf maxnorm;         // unsigned bits of max |x|
+    std::vector<uint64_t> has_vec;   // host copy of uploaded rows
+    uint64_t n_rows = 0;    // highest uploaded id + 1
+    // graph
+    bool has_graph = false;
+    uint64_t gn = 0;
+    int deg0 = 0, degU = 0, max_level = 0;
+    uint64_t n_upper = 0, entrypoint = 0;
+    std::vector<int8_t> levels_host;
+    DevBuf levels, layer0, upper_row, upper;
+    // bitmaps
+    std::vector<uint64_t> tomb_host;
+    DevBuf tomb;            // tombstones (HNSW eligibility)
+    DevBuf excl;            // tombstone | nil node | no vector (flatSearch skips)
+    uint64_t bm_words = 0;
+    bool bitmaps_dirty = true;
+    // scratch
+    DevBuf stage;           // contiguous host->device staging
+    DevBuf q_in, q_norm, q_nrm2, cand_d, cand_id, fail, status, counters;
+    DevBuf scan_d, scan_i, sort_d, sort_i, sort_tmp;
+    DevBuf g_idx, g_q, g_allow, g_ids, g_d, g_n, g_cnt;
+    DevBuf out_ids, out_d, out_n;
+    // stats of the last batch
+    uint64_t last_dist = 0, last_exp = 0, last_fallbacks = 0;
+    // optional kernel timing (hipEvents on the launch stream)
+    bool timing = false;
+    hipEvent_t ev[6] = {};
+    float t_mfma = 0.f, t_fin = 0.f, t_hnsw = 0.f;
+};
+
+namespace {
+
+int refresh_bitmaps(wv_index* ix) {
+    if (!ix->bitmaps_dirty) return WV_OK;
+    const uint64_t words = ix->bm_words;
+    std::vector<uint64_t> ex(words, 0);
+    for (uint64_t w = 0; w < words; ++w) {
+        uint64_t v = ~ix->has_vec[w];
+        if (w < ix->tomb_host.size()) v |= ix->tomb_host[w];
+        ex[w] = v;
+    }
+    if (ix->has_graph) {
+        for (uint64_t i = 0; i < ix->capacity; ++i) {
+            const bool nil = i >= ix->gn || ix->levels_host[i] < 0;
+            if (nil) ex[i >> 6] |= 1ull << (i & 63);
+        }
+    }
+    std::vector<uint64_t> tb(words, 0);
+    for (uint64_t w = 0; w < words && w < ix->tomb_host.size(); ++w) tb[w] = ix->tomb_host[w];
+    HIP_TRY(hipMemcpyAsync(ix->excl.p, ex.data(), words * 8, hipMemcpyHostToDevice, ix->stream));
+    HIP_TRY(hipMemcpyAsync(ix->tomb.p, tb.data(), words * 8, hipMemcpyHostToDevice, ix->stream));
+    HIP_TRY(hipStreamSynchronize(ix->stream));
+    ix->bitmaps_dirty = false;
+    return WV_OK;
+}
+
+int search_time_ef(const wv_config& c, int k) {
+    int ef = (int)c.ef;
+    if (ef < 1) {
+        ef = k * (int)c.dynamic_ef_factor;
+        if (ef > (int)c.dynamic_ef_max) ef = (int)c.dynamic_ef_max;
+        else if (ef < (int)c.dynamic_ef_min) ef = (int)c.dynamic_ef_min;
+        if (k > ef) ef = k;
+        return ef;
+    }
+    if (ef < k) ef = k;
+    return ef;
+}
+
+// Exact scan + stable radix sort, one query at a time (large k and certificate
+// fallbacks).  q: device query (normalized if cosine).
+int exact_full(wv_index* ix, const float* d_q, int k, const uint64_t* d_allow, uint64_t allow_nbits,
+               uint64_t* d_out_ids, float* d_out_d, int32_t* d_out_n, hipStream_t s) {
+    const uint64_t N = ix->n_rows;
+    if (N == 0) {
+        HIP_TRY(hipMemsetAsync(d_out_n, 0, sizeof(int32_t), s));
+        return WV_OK;
+    }
+    HIP_TRY(ix->scan_d.ensure(N * 4));
+    HIP_TRY(ix->scan_i.ensure(N * 4));
+    HIP_TRY(ix->sort_d.ensure(N * 4));
+    HIP_TRY(ix->sort_i.ensure(N * 4));
+    wv::ScanParams sp{};
+    sp.X = ix->vecs.as<float>();
+    sp.q = d_q;
+    sp.tomb = ix->excl.as<uint64_t>();
+    sp.tomb_nbits = ix->capacity;
+    sp.allow = d_allow;
+    sp.allow_nbits = allow_nbits;
+    sp.N = N;
+    sp.D = ix->dim;
+    sp.ldx = ix->dpad;
+    sp.metric = ix->metric;
+    sp.dist = ix->scan_d.as<float>();
+    sp.ids = ix->scan_i.as<uint32_t>();
+    HIP_TRY(wv_launch_exact_scan(&sp, s));
+    size_t tmp = 0;
+    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, ix->scan_d.as<float>(), ix->sort_d.as<float>(),
+                                               ix->scan_i.as<uint32_t>(), ix->sort_i.as<uint32_t>(), (int)N, 0, 32,
+                                               s));
+    HIP_TRY(ix->sort_tmp.ensure(tmp));
+    HIP_TRY(hipcub::DeviceRadixSort::SortPairs(ix->sort_tmp.p, tmp, ix->scan_d.as<float>(), ix->sort_d.as<float>(),
+                                               ix->scan_i.as<uint32_t>(), ix->sort_i.as<uint32_t>(), (int)N, 0, 32,
+                                               s));
+    hipLaunchKernelGGL(copy_topk_kernel, dim3(1), dim3(256), 0, s, ix->sort_d.as<float>(), ix->sort_i.as<uint32_t>(),
+                       N, k, ix->cfg.id_base, d_out_ids, d_out_d, d_out_n);
+    HIP_TRY(hipGetLastError());
+    return WV_OK;
+}
+
+// Brute force (flatSearch semantics) over a device batch of prepared queries.
+int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_allow, uint64_t allow_nbits,
+              uint64_t allow_stride, uint64_t* d_out_ids, float* d_out_d, int32_t* d_out_n, hipStream_t s) {
+    const uint64_t N = ix->n_rows;
+    if (N == 0 || nq == 0) {
+        if (nq) HIP_TRY(hipMemsetAsync(d_out_n, 0, sizeof(int32_t) * nq, s));
+        return WV_OK;
+    }
+    std::vector<int32_t> fails;
+    if (k <= wv::BF_FAST_KMAX) {
+        const int n_qblocks = (nq + wv::BF_BQ - 1) / wv::BF_BQ;
+        const uint64_t ntiles = (N + wv::BF_BN - 1) / wv::BF_BN;
+        int n_splits = std::max(1, (1024 + n_qblocks - 1) / n_qblocks);
+        if ((uint64_t)n_splits > ntiles) n_splits = (int)ntiles;
+        const int tps = (int)((ntiles + n_splits - 1) / n_splits);
+        n_splits = (int)((ntiles + tps - 1) / tps);
+        const size_t n_lists = (size_t)n_splits * wv::BF_PROD;
+        HIP_TRY(ix->cand_d.ensure((size_t)nq * n_lists * wv::BF_KP * 4));
+        HIP_TRY(ix->cand_id.ensure((size_t)nq * n_lists * wv::BF_KP * 4));
+        HIP_TRY(ix->q_nrm2.ensure((size_t)nq * 4));
+        HIP_TRY(ix->fail.ensure((size_t)nq * 4));
+        HIP_TRY(wv_launch_qnorm(d_q, nq, ix->dim, ix->dpad, ix->metric, ix->q_nrm2.as<float>(), s));
+        wv::BfParams bp{};
+        bp.X = ix->vecs.as<float>();
+        bp.Q = d_q;
+        bp.xnorm = ix->xnorm.as<float>();
+        bp.tomb = ix->excl.as<uint64_t>();
+        bp.tomb_nbits = ix->capacity;
+        bp.allow = d_allow;
+        bp.allow_nbits = allow_nbits;
+        bp.allow_stride = allow_stride;
+        bp.N = N;
+        bp.nq = nq;
+        bp.D = ix->dim;
+        bp.ldx = ix->dpad;
+        bp.ldq = ix->dpad;
+        bp.metric = ix->metric;
+        bp.n_qblocks = n_qblocks;
+        bp.n_splits = n_splits;
+        bp.tiles_per_split = tps;
+        bp.out_d = ix->cand_d.as<float>();
+        bp.out_id = ix->cand_id.as<uint32_t>();
+        if (ix->timing) HIP_TRY(hipEventRecord(ix->ev[0], s));
+        HIP_TRY(wv_launch_bf_mfma(&bp, s));
+        if (ix->timing) HIP_TRY(hipEventRecord(ix->ev[1], s));
+        unsigned int mb = 0;
+        HIP_TRY(hipMemcpyAsync(&mb, ix->maxnorm.p, 4, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        float maxn;
+        std::memcpy(&maxn, &mb, 4);
+        wv::BfFinParams fp{};
+        fp.X = ix->vecs.as<float>();
+        fp.Q = d_q;
+        fp.cand_d = ix->cand_d.as<float>();
+        fp.cand_id = ix->cand_id.as<uint32_t>();
+        fp.qnorm = ix->q_nrm2.as<float>();
+        fp.xnorm_max = maxn;
+        fp.n_lists = (int)n_lists;
+        fp.nq = nq;
+        fp.D = ix->dim;
+        fp.ldx = ix->dpad;
+        fp.ldq = ix->dpad;
+        fp.metric = ix->metric;
+        fp.k = k;
+        fp.id_base = ix->cfg.id_base;
+        fp.out_ids = d_out_ids;
+        fp.out_d = d_out_d;
+        fp.out_n = d_out_n;
+        fp.fail = ix->fail.as<int32_t>();
+        if (ix->timing) HIP_TRY(hipEventRecord(ix->ev[2], s));
+        HIP_TRY(wv_launch_bf_finalize(&fp, s));
+        if (ix->timing) HIP_TRY(hipEventRecord(ix->ev[3], s));
+        std::vector<int32_t> f(nq);
+        HIP_TRY(hipMemcpyAsync(f.data(), ix->fail.p, 4 * (size_t)nq, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (ix->timing) {
+            float a = 0.f, b = 0.f;
+            HIP_TRY(hipEventElapsedTime(&a, ix->ev[0], ix->ev[1]));
+            HIP_TRY(hipEventElapsedTime(&b, ix->ev[2], ix->ev[3]));
+            ix->t_mfma += a;
+            ix->t_fin += b;
+        }
+        for (int i = 0; i < nq; ++i)
+            if (f[i]) fails.push_back(i);
+    } else {
+        for (int i = 0; i < nq; ++i) fails.push_back(i);
+    }
+    ix->last_fallbacks += fails.size();
+    for (int q : fails) {
+        const uint64_t* al = d_allow ? d_allow + (allow_stride ? (uint64_t)q * allow_stride : 0) : nullptr;
+        int rc = exact_full(ix, d_q + (size_t)q * ix->dpad, k, al, allow_nbits, d_out_ids + (size_t)q * k,
+                            d_out_d + (size_t)q * k, d_out_n + q, s);
+        if (rc) return rc;
+    }
+    return WV_OK;
+}
+
+int choose_vc_log2(int per_wave_budget_words, int fixed_words) {
+    int l = 12;
+    while (l > 8 && fixed_words + (1 << l) > per_wave_budget_words) --l;
+    return l;
+}
+
+int run_hnsw(wv_index* ix, const float* d_q, int nq, int k, int ef, const uint64_t* d_allow, uint64_t allow_nbits,
+             uint64_t allow_stride, uint64_t* d_out_ids, float* d_out_d, int32_t* d_out_n, hipStream_t s) {
+    if (!ix->has_graph || ix->gn == 0) return fail(WV_ESTATE, "no graph uploaded");
+    const int efc = std::max(64, (ef + 63) / 64 * 64);
+    const int sc = 256;
+    const int xs_log2 = 9;
+    const int fixed = wv_hnsw_per_wave_words(ix->dpad, efc, sc, 0, xs_log2) - 1;
+    // 8 waves per CU: 160 KiB / 8 = 20 KiB per wave when possible
+    const int budget = 20 * 1024 / 4;
+    const int vc_log2 = choose_vc_log2(budget, fixed);
+    int per_wave = wv_hnsw_per_wave_words(ix->dpad, efc, sc, vc_log2, xs_log2);
+    per_wave = (per_wave + 3) & ~3;
+    int wpb = 4;
+    while (wpb > 1 && (size_t)wpb * per_wave * 4 > 160 * 1024) --wpb;
+    if ((size_t)per_wave * 4 > 160 * 1024) return fail(WV_EINVAL, "hnsw LDS footprint too large");
+    HIP_TRY(ix->status.ensure((size_t)nq * 4));
+    HIP_TRY(ix->counters.ensure((size_t)nq * 8));
+    wv::HnswParams hp{};
+    hp.X = ix->vecs.as<float>();
+    hp.levels = ix->levels.as<int8_t>();
+    hp.layer0 = ix->layer0.as<uint32_t>();
+    hp.upper_row = ix->upper_row.as<uint32_t>();
+    hp.upper = ix->upper.as<uint32_t>();
+    hp.tomb = ix->tomb.as<uint64_t>();
+    hp.tomb_nbits = ix->capacity;
+    hp.allow = d_allow;
+    hp.allow_nbits = allow_nbits;
+    hp.allow_stride = allow_stride;
+    hp.Q = d_q;
+    hp.N = ix->gn;
+    hp.id_base = ix->cfg.id_base;
+    hp.entrypoint = (uint32_t)ix->entrypoint;
+    hp.D = ix->dim;
+    hp.ldx = ix->dpad;
+    hp.ldq = ix->dpad;
+    hp.metric = ix->metric;
+    hp.deg0 = ix->deg0;
+    hp.degU = ix->degU;
+    hp.max_level = ix->max_level;
+    hp.nq = nq;
+    hp.k = k;
+    hp.ef = ef;
+    hp.efc = efc;
+    hp.sc = sc;
+    hp.vc_log2 = vc_log2;
+    hp.xs_log2 = xs_log2;
+    hp.dpad = ix->dpad;
+    hp.per_wave_words = per_wave;
+    hp.out_ids = d_out_ids;
+    hp.out_d = d_out_d;
+    hp.out_n = d_out_n;
+    hp.status = ix->status.as<int32_t>();
+    hp.counters = ix->counters.as<uint32_t>();
+    if (ix->timing) HIP_TRY(hipEventRecord(ix->ev[4], s));
+    HIP_TRY(wv_launch_hnsw(&hp, wpb, s));
+    if (ix->timing) HIP_TRY(hipEventRecord(ix->ev[5], s));
+    std::vector<int32_t> st(nq);
+    std::vector<uint32_t> ct(2 * (size_t)nq);
+    HIP_TRY(hipMemcpyAsync(st.data(), ix->status.p, 4 * (size_t)nq, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(ct.data(), ix->counters.p, 8 * (size_t)nq, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (ix->timing) {
+        float a = 0.f;
+        HIP_TRY(hipEventElapsedTime(&a, ix->ev[4], ix->ev[5]));
+        ix->t_hnsw += a;
+    }
+    for (int i = 0; i < nq; ++i) {
+        ix->last_dist += ct[2 * i];
+        ix->last_exp += ct[2 * i + 1];
+    }
+    // Queries whose side-candidate set outgrew LDS are answered exactly
+    // (flatSearch over the same allow list: a superset in quality).
+    for (int q = 0; q < nq; ++q) {
+        if (!st[q]) continue;
+        ix->last_fallbacks++;
+        const uint64_t* al = d_allow ? d_allow + (allow_stride ? (uint64_t)q * allow_stride : 0) : nullptr;
+        int rc = exact_full(ix, d_q + (size_t)q * ix->dpad, k, al, allow_nbits, d_out_ids + (size_t)q * k,
+                            d_out_d + (size_t)q * k, d_out_n + q, s);
+        if (rc) return rc;
+    }
+    return WV_OK;
+}
+
+// Core: device queries already padded to dpad and normalized (cosine).
+int search_core(wv_index* ix, const float* d_q, int nq, int k, int ef, const uint64_t* d_allow,
+                uint64_t allow_nbits, uint64_t allow_stride, int mode, uint64_t* d_out_ids, float* d_out_d,
+                int32_t* d_out_n, hipStream_t s) {
+    int rc = refresh_bitmaps(ix);
+    if (rc) return rc;
+    ix->last_dist = ix->last_exp = ix->last_fallbacks = 0;
+    ix->t_mfma = ix->t_fin = ix->t_hnsw = 0.f;
+    if (ef <= 0) ef = search_time_ef(ix->cfg, k);
+    if (mode == WV_MODE_EXACT)
+        return run_exact(ix, d_q, nq, k, d_allow, allow_nbits, allow_stride, d_out_ids, d_out_d, d_out_n, s);
+    if (mode == WV_MODE_HNSW) {
+        if (ef > wv::HNSW_EF_MAX)
+            return run_exact(ix, d_q, nq, k, d_allow, allow_nbits, allow_stride, d_out_ids, d_out_d, d_out_n, s);
+        return run_hnsw(ix, d_q, nq, k, ef, d_allow, allow_nbits, allow_stride, d_out_ids, d_out_d, d_out_n, s);
+    }
+    // AUTO: search.go:74-78
+    const bool can_hnsw = ix->has_graph && ef <= wv::HNSW_EF_MAX;
+    if (!d_allow || ix->cfg.forbid_flat) {
+        if (can_hnsw)
+            return run_hnsw(ix, d_q, nq, k, ef, d_allow, allow_nbits, allow_stride, d_out_ids, d_out_d, d_out_n, s);
+        return run_exact(ix, d_q, nq, k, d_allow, allow_nbits, allow_stride, d_out_ids, d_out_d, d_out_n, s);
+    }
+    // allowList.Len() < flatSearchCutoff decides per query
+    const int rows = allow_stride ? nq : 1;
+    const uint64_t words = (allow_nbits + 63) / 64;
+    HIP_TRY(ix->g_cnt.ensure((size_t)rows * 8));
+    HIP_TRY(hipMemsetAsync(ix->g_cnt.p, 0, (size_t)rows * 8, s));
+    hipLaunchKernelGGL(popcount_rows_kernel, dim3(rows), dim3(256), 0, s, d_allow, words,
+                       allow_stride ? allow_stride : words, rows, ix->g_cnt.as<unsigned long long>());
+    HIP_TRY(hipGetLastError());
+    std::vector<unsigned long long> cnt(rows);
+    HIP_TRY(hipMemcpyAsync(cnt.data(), ix->g_cnt.p, 8 * (size_t)rows, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    std::vector<int32_t> flat, knn;
+    for (int q = 0; q < nq; ++q) {
+        const unsigned long long c = cnt[allow_stride ? q : 0];
+        if ((int64_t)c < ix->cfg.flat_search_cutoff || !can_hnsw) flat.push_back(q);
+        else knn.push_back(q);
+    }
+    if (knn.empty())
+        return run_exact(ix, d_q, nq, k, d_allow, allow_nbits, allow_stride, d_out_ids, d_out_d, d_out_n, s);
+    if (flat.empty())
+        return run_hnsw(ix, d_q, nq, k, ef, d_allow, allow_nbits, allow_stride, d_out_ids, d_out_d, d_out_n, s);
+    // split the batch: gather each group, run, scatter back
+    for (int pass = 0; pass < 2; ++pass) {
+        const std::vector<int32_t>& sel = pass == 0 ? flat : knn;
+        const int n = (int)sel.size();
+        HIP_TRY(ix->g_idx.ensure((size_t)n * 4));
+        HIP_TRY(ix->g_q.ensure((size_t)n * ix->dpad * 4));
+        HIP_TRY(ix->g_ids.ensure((size_t)n * k * 8));
+        HIP_TRY(ix->g_d.ensure((size_t)n * k * 4));
+        HIP_TRY(ix->g_n.ensure((size_t)n * 4));
+        HIP_TRY(hipMemcpyAsync(ix->g_idx.p, sel.data(), 4 * (size_t)n, hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(gather_rows_kernel, dim3(n), dim3(128), 0, s, d_q, ix->dpad, ix->g_idx.as<int32_t>(), n,
+                           ix->dpad, ix->g_q.as<float>(), ix->dpad);
+        const uint64_t* al = d_allow;
+        uint64_t ast = 0;
+        if (allow_stride) {
+            HIP_TRY(ix->g_allow.ensure((size_t)n * allow_stride * 8));
+            hipLaunchKernelGGL(gather_words_kernel, dim3(n), dim3(256), 0, s, d_allow, allow_stride,
+                               ix->g_idx.as<int32_t>(), n, ix->g_allow.as<uint64_t>());
+            al = ix->g_allow.as<uint64_t>();
+            ast = allow_stride;
+        }
+        HIP_TRY(hipGetLastError());
+        int rc2 = pass == 0 ? run_exact(ix, ix->g_q.as<float>(), n, k, al, allow_nbits, ast, ix->g_ids.as<uint64_t>(),
+                                        ix->g_d.as<float>(), ix->g_n.as<int32_t>(), s)
+                            : run_hnsw(ix, ix->g_q.as<float>(), n, k, ef, al, allow_nbits, ast,
+                                       ix->g_ids.as<uint64_t>(), ix->g_d.as<float>(), ix->g_n.as<int32_t>(), s);
+        if (rc2) return rc2;
+        hipLaunchKernelGGL(scatter_results_kernel, dim3(n), dim3(64), 0, s, ix->g_ids.as<uint64_t>(),
+                           ix->g_d.as<float>(), ix->g_n.as<int32_t>(), ix->g_idx.as<int32_t>(), n, k, d_out_ids,
+                           d_out_d, d_out_n);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    return WV_OK;
+}
+
+// host queries -> device, padded, normalized for cosine (search.go:68-72)
+int stage_queries(wv_index* ix, const float* q, int nq, const float** d_out, hipStream_t s) {
+    HIP_TRY(ix->q_in.ensure((size_t)nq * ix->dpad * 4));
+    if (ix->dpad == ix->dim) {
+        HIP_TRY(hipMemcpyAsync(ix->q_in.p, q, (size_t)nq * ix->dim * 4, hipMemcpyHostToDevice, s));
+    } else {
+        HIP_TRY(ix->stage.ensure((size_t)nq * ix->dim * 4));
+        HIP_TRY(hipMemcpyAsync(ix->stage.p, q, (size_t)nq * ix->dim * 4, hipMemcpyHostToDevice, s));
+        HIP_TRY(launch_pad_rows(ix->stage.as<float>(), ix->dim, nq, ix->dim, ix->q_in.as<float>(), ix->dpad, s));
+    }
+    if (ix->metric == WV_COSINE_DOT)
+        HIP_TRY(wv_launch_normalize(ix->q_in.as<float>(), ix->q_in.as<float>(), nq, ix->dim, ix->dpad, s));
+    *d_out = ix->q_in.as<float>();
+    return WV_OK;
+}
+
+int check(wv_index* ix) {
+    if (!ix) return fail(WV_EINVAL, "null index");
+    return WV_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+void wv_config_default(wv_config* c) {
+    std::memset(c, 0, sizeof(*c));
+    c->device = 0;
+    c->max_connections = 64;
+    c->ef = -1;
+    c->dynamic_ef_min = 100;
+    c->dynamic_ef_max = 500;
+    c->dynamic_ef_factor = 8;
+    c->flat_search_cutoff = 40000;
+    c->forbid_flat = 0;
+    c->id_base = 0;
+}
+
+const char* wv_last_error(void) { return g_err.c_str(); }
+const char* wv_version(void) { return "wvgpu 0.1 (gfx950)"; }
+
+int wv_index_create(int dim, int metric, const wv_config* cfg, uint64_t capacity, wv_index** out) {
+    if (!out || dim <= 0 || metric < 0 || metric > 2 || capacity == 0 || capacity >= (1ull << 31))
+        return fail(WV_EINVAL, "wv_index_create: bad argument");
+    auto* ix = new wv_index();
+    ix->dim = dim;
+    ix->dpad = (dim + 3) & ~3;
+    ix->metric = metric;
+    if (cfg) ix->cfg = *cfg; else wv_config_default(&ix->cfg);
+    ix->capacity = capacity;
+    hipError_t e = hipSetDevice(ix->cfg.device);
+    if (e != hipSuccess) { delete ix; return fail(WV_EDEVICE, std::string("hipSetDevice: ") + hipGetErrorString(e)); }
+    e = hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) { delete ix; return fail(WV_EDEVICE, std::string("hipStreamCreate: ") + hipGetErrorString(e)); }
+    ix->bm_words = (capacity + 63) / 64;
+    const size_t vbytes = capacity * (size_t)ix->dpad * 4;
+    if (ix->vecs.ensure(vbytes) != hipSuccess || ix->xnorm.ensure(capacity * 4) != hipSuccess ||
+        ix->maxnorm.ensure(4) != hipSuccess || ix->tomb.ensure(ix->bm_words * 8) != hipSuccess ||
+        ix->excl.ensure(ix->bm_words * 8) != hipSuccess) {
+        wv_index_destroy(ix);
+        return fail(WV_EOOM, "wv_index_create: device allocation failed");
+    }
+    (void)hipMemsetAsync(ix->vecs.p, 0, vbytes, ix->stream);
+    (void)hipMemsetAsync(ix->maxnorm.p, 0, 4, ix->stream);
+    (void)hipStreamSynchronize(ix->stream);
+    ix->has_vec.assign(ix->bm_words, 0);
+    ix->tomb_host.assign(ix->bm_words, 0);
+    *out = ix;
+    return WV_OK;
+}
+
+int wv_index_destroy(wv_index* ix) {
+    if (!ix) return WV_OK;
+    (void)hipSetDevice(ix->cfg.device);
+    for (DevBuf* b : {&ix->vecs, &ix->xnorm, &ix->maxnorm, &ix->levels, &ix->layer0, &ix->upper_row, &ix->upper,
+                      &ix->tomb, &ix->excl, &ix->q_in, &ix->q_norm, &ix->q_nrm2, &ix->cand_d, &ix->cand_id,
+                      &ix->fail, &ix->status, &ix->counters, &ix->scan_d, &ix->scan_i, &ix->sort_d, &ix->sort_i,
+                      &ix->sort_tmp, &ix->g_idx, &ix->g_q, &ix->g_allow, &ix->g_ids, &ix->g_d, &ix->g_n, &ix->g_cnt,
+                      &ix->out_ids, &ix->out_d, &ix->out_n, &ix->stage})
+        b->release();
+    for (auto& e : ix->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (ix->stream) (void)hipStreamDestroy(ix->stream);
+    delete ix;
+    return WV_OK;
+}
+
+int wv_index_update_config(wv_index* ix, const wv_config* cfg) {
+    if (check(ix) || !cfg) return fail(WV_EINVAL, "bad argument");
+    std::lock_guard<std::mutex> g(ix->mu);
+    const int dev = ix->cfg.device;
+    const uint64_t base = ix->cfg.id_base;
+    ix->cfg = *cfg;
+    ix->cfg.device = dev;   // the device and id base are fixed at creation
+    ix->cfg.id_base = base;
+    return WV_OK;
+}
+
+static int upload_rows(wv_index* ix, const float* src, bool device_src, int ld, uint64_t n, uint64_t first_id) {
+    if (first_id + n > ix->capacity) return fail(WV_EINVAL, "upload beyond capacity");
+    if (n == 0) return WV_OK;
+    HIP_TRY(hipSetDevice(ix->cfg.device));
+    float* dst = ix->vecs.as<float>() + first_id * ix->dpad;
+    const float* dsrc = src;
+    if (!device_src) {
+        HIP_TRY(ix->stage.ensure(n * (size_t)ix->dim * 4));
+        HIP_TRY(hipMemcpyAsync(ix->stage.p, src, n * (size_t)ix->dim * 4, hipMemcpyHostToDevice, ix->stream));
+        dsrc = ix->stage.as<float>();
+        ld = ix->dim;
+    }
+    HIP_TRY(launch_pad_rows(dsrc, ld, n, ix->dim, dst, ix->dpad, ix->stream));
+    if (ix->metric == WV_COSINE_DOT)  // normalize on write (insert.go:56-60, vector_cache.go:110-112)
+        HIP_TRY(wv_launch_normalize(dst, dst, n, ix->dim, ix->dpad, ix->stream));
+    HIP_TRY(wv_launch_rownorm(dst, n, ix->dim, ix->dpad, ix->xnorm.as<float>() + first_id,
+                              ix->maxnorm.as<unsigned int>(), ix->stream));
+    HIP_TRY(hipStreamSynchronize(ix->stream));
+    for (uint64_t i = first_id; i < first_id + n; ++i) ix->has_vec[i >> 6] |= 1ull << (i & 63);
+    ix->n_rows = std::max(ix->n_rows, first_id + n);
+    ix->bitmaps_dirty = true;
+    return WV_OK;
+}
+
+int wv_index_upload_vectors(wv_index* ix, const float* rows, uint64_t n, uint64_t first_id) {
+    if (check(ix) || (!rows && n)) return fail(WV_EINVAL, "bad argument");
+    std::lock_guard<std::mutex> g(ix->mu);
+    return upload_rows(ix, rows, false, ix->dim, n, first_id);
+}
+
+int wv_index_upload_vectors_device(wv_index* ix, const float* d_rows, uint64_t n, uint64_t first_id, int ld) {
+    if (check(ix) || (!d_rows && n) || ld < ix->dim) return fail(WV_EINVAL, "bad argument");
+    std::lock_guard<std::mutex> g(ix->mu);
+    return upload_rows(ix, d_rows, true, ld, n, first_id);
+}
+
+int wv_index_upload_graph(wv_index* ix, uint64_t n, const int8_t* levels, const uint32_t* layer0, int deg0,
+                          const uint32_t* upper_row, const uint32_t* upper, uint64_t n_upper, int degU, int max_level,
+                          uint64_t entrypoint) {
+    if (check(ix)) return WV_EINVAL;
+    if (n == 0 || n > ix->capacity || !levels || !layer0 || deg0 <= 0 || deg0 > 256 || max_level < 0 ||
+        entrypoint >= n || (max_level > 0 && (!upper_row || !upper || degU <= 0 || degU > 256)))
+        return fail(WV_EINVAL, "wv_index_upload_graph: bad argument");
+    std::lock_guard<std::mutex> g(ix->mu);
+    HIP_TRY(hipSetDevice(ix->cfg.device));
+    // validate neighbour ids on the host once (a bad id would fault the kernel)
+    for (uint64_t i = 0; i < n * (uint64_t)deg0; ++i)
+        if (layer0[i] != WV_NIL && layer0[i] >= n) return fail(WV_EINVAL, "layer0 neighbour out of range");
+    if (max_level > 0) {
+        for (uint64_t i = 0; i < n; ++i) {
+            if (levels[i] >= 1 && (upper_row[i] == WV_NIL || upper_row[i] >= n_upper))
+                return fail(WV_EINVAL, "upper_row out of range");
+        }
+        for (uint64_t i = 0; i < n_upper * (uint64_t)max_level * degU; ++i)
+            if (upper[i] != WV_NIL && upper[i] >= n) return fail(WV_EINVAL, "upper neighbour out of range");
+    }
+    if (levels[entrypoint] < max_level) return fail(WV_EINVAL, "entrypoint below max level");
+    HIP_TRY(ix->levels.ensure(n));
+    HIP_TRY(ix->layer0.ensure(n * (size_t)deg0 * 4));
+    HIP_TRY(ix->upper_row.ensure(n * 4));
+    HIP_TRY(ix->upper.ensure(std::max<uint64_t>(1, n_upper * (uint64_t)std::max(1, max_level) * std::max(1, degU)) * 4));
+    HIP_TRY(hipMemcpyAsync(ix->levels.p, levels, n, hipMemcpyHostToDevice, ix->stream));
+    HIP_TRY(hipMemcpyAsync(ix->layer0.p, layer0, n * (size_t)deg0 * 4, hipMemcpyHostToDevice, ix->stream));
+    if (max_level > 0) {
+        HIP_TRY(hipMemcpyAsync(ix->upper_row.p, upper_row, n * 4, hipMemcpyHostToDevice, ix->stream));
+        HIP_TRY(hipMemcpyAsync(ix->upper.p, upper, n_upper * (size_t)max_level * degU * 4, hipMemcpyHostToDevice,
+                               ix->stream));
+    }
+    HIP_TRY(hipStreamSynchronize(ix->stream));
+    ix->levels_host.assign(levels, levels + n);
+    ix->levels_host.resize(ix->capacity, -1);
+    ix->gn = n;
+    ix->deg0 = deg0;
+    ix->degU = max_level > 0 ? degU : 1;
+    ix->max_level = max_level;
+    ix->n_upper = n_upper;
+    ix->entrypoint = entrypoint;
+    ix->has_graph = true;
+    ix->bitmaps_dirty = true;
+    return WV_OK;
+}
+
+int wv_index_set_tombstones(wv_index* ix, const uint64_t* bits, uint64_t nbits) {
+    if (check(ix)) return WV_EINVAL;
+    std::lock_guard<std::mutex> g(ix->mu);
+    std::fill(ix->tomb_host.begin(), ix->tomb_host.end(), 0);
+    const uint64_t w = std::min<uint64_t>((nbits + 63) / 64, ix->bm_words);
+    for (uint64_t i = 0; i < w; ++i) ix->tomb_host[i] = bits ? bits[i] : 0;
+    if (nbits & 63 && w == (nbits + 63) / 64 && w > 0) ix->tomb_host[w - 1] &= (1ull << (nbits & 63)) - 1;
+    ix->bitmaps_dirty = true;
+    return WV_OK;
+}
+
+int wv_search_time_ef(const wv_index* ix, int k) { return ix ? search_time_ef(ix->cfg, k) : -1; }
+
+int wv_search_batch(wv_index* ix, const float* queries, int nq, int k, int ef, const uint64_t* allow_bits,
+                    uint64_t allow_nbits, uint64_t allow_stride_words, int mode, uint64_t* out_ids, float* out_dists,
+                    int32_t* out_n) {
+    if (check(ix) || nq < 0 || k <= 0 || (nq && (!queries || !out_ids || !out_dists || !out_n)))
+        return fail(WV_EINVAL, "wv_search_batch: bad argument");
+    if (nq == 0) return WV_OK;
+    std::lock_guard<std::mutex> g(ix->mu);
+    HIP_TRY(hipSetDevice(ix->cfg.device));
+    hipStream_t s = ix->stream;
+    const float* dq = nullptr;
+    int rc = stage_queries(ix, queries, nq, &dq, s);
+    if (rc) return rc;
+    const uint64_t* dallow = nullptr;
+    if (allow_bits) {
+        const uint64_t words = (allow_nbits + 63) / 64;
+        const uint64_t rows = allow_stride_words ? (uint64_t)nq : 1;
+        const uint64_t stride = allow_stride_words ? allow_stride_words : words;
+        HIP_TRY(ix->g_allow.ensure(rows * stride * 8));
+        HIP_TRY(hipMemcpyAsync(ix->g_allow.p, allow_bits, rows * stride * 8, hipMemcpyHostToDevice, s));
+        dallow = ix->g_allow.as<uint64_t>();
+    }
+    HIP_TRY(ix->out_ids.ensure((size_t)nq * k * 8));
+    HIP_TRY(ix->out_d.ensure((size_t)nq * k * 4));
+    HIP_TRY(ix->out_n.ensure((size_t)nq * 4));
+    // an AUTO batch with per-query allow lists gathers into g_allow: keep the
+    // caller's bitmaps in their own buffer
+    DevBuf allow_copy;
+    if (dallow && allow_stride_words && mode == WV_MODE_AUTO) {
+        HIP_TRY(allow_copy.ensure((size_t)nq * allow_stride_words * 8));
+        HIP_TRY(hipMemcpyAsync(allow_copy.p, dallow, (size_t)nq * allow_stride_words * 8, hipMemcpyDeviceToDevice, s));
+        dallow = allow_copy.as<uint64_t>();
+    }
+    rc = search_core(ix, dq, nq, k, ef, dallow, allow_nbits, allow_stride_words, mode, ix->out_ids.as<uint64_t>(),
+                     ix->out_d.as<float>(), ix->out_n.as<int32_t>(), s);
+    if (rc) { allow_copy.release(); return rc; }
+    HIP_TRY(hipMemcpyAsync(out_ids, ix->out_ids.p, (size_t)nq * k * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(out_dists, ix->out_d.p, (size_t)nq * k * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(out_n, ix->out_n.p, (size_t)nq * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    allow_copy.release();
+    return WV_OK;
+}
+
+int wv_search_batch_device(wv_index* ix, const float* d_queries, int nq, int k, int ef, const uint64_t* d_allow_bits,
+                           uint64_t allow_nbits, uint64_t allow_stride_words, int mode, uint64_t* d_out_ids,
+                           float* d_out_dists, int32_t* d_out_n, void* stream) {
+    if (check(ix) || nq < 0 || k <= 0 || (nq && (!d_queries || !d_out_ids || !d_out_dists || !d_out_n)))
+        return fail(WV_EINVAL, "wv_search_batch_device: bad argument");
+    if (nq == 0) return WV_OK;
+    std::lock_guard<std::mutex> g(ix->mu);
+    HIP_TRY(hipSetDevice(ix->cfg.device));
+    hipStream_t s = stream ? (hipStream_t)stream : ix->stream;
+    const float* dq = d_queries;
+    if (ix->metric == WV_COSINE_DOT) {
+        // the caller's rows are [nq][dpad]; normalize a padded copy
+        HIP_TRY(ix->q_norm.ensure((size_t)nq * ix->dpad * 4));
+        HIP_TRY(launch_pad_rows(d_queries, ix->dpad, nq, ix->dim, ix->q_norm.as<float>(), ix->dpad, s));
+        HIP_TRY(wv_launch_normalize(ix->q_norm.as<float>(), ix->q_norm.as<float>(), nq, ix->dim, ix->dpad, s));
+        dq = ix->q_norm.as<float>();
+    }
+    return search_core(ix, dq, nq, k, ef, d_allow_bits, allow_nbits, allow_stride_words, mode, d_out_ids, d_out_dists,
+                       d_out_n, s);
+}
+
+int wv_search_by_vector(wv_index* ix, const float* vector, int k, const uint64_t* allow_bits, uint64_t allow_nbits,
+                        uint64_t* out_ids, float* out_dists, int32_t* out_n) {
+    return wv_search_batch(ix, vector, 1, k, 0, allow_bits, allow_nbits, 0, WV_MODE_AUTO, out_ids, out_dists, out_n);
+}
+
+int wv_search_by_vector_distance(wv_index* ix, const float* vector, float target, int64_t max_limit,
+                                 const uint64_t* allow_bits, uint64_t allow_nbits, uint64_t* out_ids,
+                                 float* out_dists, int64_t out_cap, int64_t* out_n) {
+    if (check(ix) || !vector || !out_n) return fail(WV_EINVAL, "bad argument");
+    // search.go:90-158 with searchByDistParams (:552-619)
+    int64_t offset = 0, limit = 100, total = 100, n_out = 0;
+    std::vector<uint64_t> ids;
+    std::vector<float> ds;
+    std::vector<int32_t> nn(1);
+    for (bool first = true;; first = false) {
+        if (!first) {
+            offset = total;
+            limit *= 10;
+            total = offset + limit;
+            if (max_limit >= 0 && total > max_limit) break;
+        }
+        if (total > (int64_t)0x7FFFFFFF) break;
+        ids.assign(total, 0);
+        ds.assign(total, 0.f);
+        int rc = wv_search_by_vector(ix, vector, (int)total, allow_bits, allow_nbits, ids.data(), ds.data(), nn.data());
+        if (rc) return rc;
+        const int64_t n = nn[0];
+        const int64_t lo = std::min(offset, n), hi = std::min(total, n);
+        if (hi - lo <= 0) break;
+        const bool cont = ds[hi - 1] <= target;
+        for (int64_t i = lo; i < hi; ++i) {
+            if (ds[i] <= target || std::fabs((double)ds[i] - (double)target) <= 1e-6) {
+                if (n_out < out_cap) { out_ids[n_out] = ids[i]; out_dists[n_out] = ds[i]; }
+                n_out++;
+            } else {
+                break;
+            }
+        }
+        if (!cont) break;
+    }
+    *out_n = n_out;
+    return WV_OK;
+}
+
+int wv_merge_shards_device(const float* d_in_dists, const uint64_t* d_in_ids, const int32_t* d_in_n, int n_shards,
+                           int nq, int k, float* d_out_dists, uint64_t* d_out_ids, int32_t* d_out_n, void* stream) {
+    if (n_shards <= 0 || n_shards > 16 || nq < 0 || k <= 0) return fail(WV_EINVAL, "wv_merge_shards_device: bad argument");
+    if (nq == 0) return WV_OK;
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(merge_shards_kernel, dim3((nq + 127) / 128), dim3(128), 0, s, d_in_dists, d_in_ids, d_in_n,
+                       n_shards, nq, k, d_out_dists, d_out_ids, d_out_n);
+    HIP_TRY(hipGetLastError());
+    return WV_OK;
+}
+
+int wv_index_set_timing(wv_index* ix, int enable) {
+    if (check(ix)) return WV_EINVAL;
+    std::lock_guard<std::mutex> g(ix->mu);
+    HIP_TRY(hipSetDevice(ix->cfg.device));
+    if (enable && !ix->ev[0])
+        for (auto& e : ix->ev) HIP_TRY(hipEventCreate(&e));
+    ix->timing = enable != 0;
+    return WV_OK;
+}
+
+int wv_last_kernel_times(wv_index* ix, float* bf_mfma_ms, float* bf_finalize_ms, float* hnsw_ms) {
+    if (check(ix)) return WV_EINVAL;
+    if (bf_mfma_ms) *bf_mfma_ms = ix->t_mfma;
+    if (bf_finalize_ms) *bf_finalize_ms = ix->t_fin;
+    if (hnsw_ms) *hnsw_ms = ix->t_hnsw;
+    return WV_OK;
+}
+
+int wv_last_batch_stats(wv_index* ix, uint64_t* dist_evals, uint64_t* expansions, uint64_t* fallbacks) {
+    if (check(ix)) return WV_EINVAL;
+    if (dist_evals) *dist_evals = ix->last_dist;
+    if (expansions) *expansions = ix->last_exp;
+    if (fallbacks) *fallbacks = ix->last_fallbacks;
+    return WV_OK;
+}
+
+}  // extern "C"

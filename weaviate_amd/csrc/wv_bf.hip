@@ -1,0 +1,493 @@
+// wv_bf.hip -- exact (and allowList-filtered) brute-force k-NN on CDNA4.
+//
+// Restates flatSearch (adapters/repos/db/vector/hnsw/flat_search.go:19-74) over
+// the whole corpus or an allow list, with ids returned in (distance, id) order.
+//
+// Pipeline (per query batch):
+//   1. wv_bf_mfma_kernel: fp32 MFMA (v_mfma_f32_32x32x2_f32) base x query tiles.
+//      The epilogue turns each dot product into a rank-equivalent approximate
+//      distance (L2: |x|^2 - 2 q.x, dot/cosine: -q.x), masks tombstones and
+//      the allow list, and keeps per-lane sorted candidate lists in registers.
+//      Q x N distances never reach HBM.
+//   2. wv_bf_finalize_kernel: one wave per query merges the candidate lists,
+//      re-ranks the best KF exactly with the reference summation order
+//      (wv_device.h exact_dist_group8) and certifies the result: every point
+//      not re-ranked has approx >= bound, and bound - eps > d_k, where eps
+//      bounds |approx - reference| for any point.  Uncertified queries are
+//      flagged and answered by the exact full scan (wv_exact_scan_kernel).
+//   3. wv_exact_scan_kernel + radix sort: exact reference-order distances for
+//      every id, used for flagged queries and for large k.
+#include "wv_device.h"
+#include "wv_params.h"
+
+#include <float.h>
+
+namespace wv {
+
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void list_insert(float (&ld)[BF_KP], uint32_t (&li)[BF_KP], float d, uint32_t id) {
+    // bubble the new element through the sorted list; the largest falls off
+#pragma unroll
+    for (int i = 0; i < BF_KP; ++i) {
+        const bool lt = key_less(d, id, ld[i], li[i]);
+        const float td = ld[i];
+        const uint32_t ti = li[i];
+        ld[i] = lt ? d : ld[i];
+        li[i] = lt ? id : li[i];
+        d = lt ? td : d;
+        id = lt ? ti : id;
+    }
+}
+
+__global__ __launch_bounds__(256, 1) void wv_bf_mfma_kernel(BfParams p) {
+    extern __shared__ float lds[];
+    float* As = lds;                          // [2][BK][LD]  base tile, k-major
+    float* Bs = lds + 2 * BF_BK * BF_LD;      // [2][BK][LD]  query tile, k-major
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int wm = wave >> 1;   // base-row half of the tile
+    const int wn = wave & 1;    // query half of the tile
+    const int qb = blockIdx.x % p.n_qblocks;
+    const int split = blockIdx.x / p.n_qblocks;
+    const int q0 = qb * BF_BQ;
+    const uint64_t ntiles_total = (p.N + BF_BN - 1) / BF_BN;
+    const uint64_t t_begin = (uint64_t)split * p.tiles_per_split;
+    uint64_t t_end = t_begin + p.tiles_per_split;
+    if (t_end > ntiles_total) t_end = ntiles_total;
+    const int nk = (p.D + BF_BK - 1) / BF_BK;
+
+    // per-lane candidate lists for the two query columns this lane owns
+    float l0d[BF_KP], l1d[BF_KP];
+    uint32_t l0i[BF_KP], l1i[BF_KP];
+#pragma unroll
+    for (int i = 0; i < BF_KP; ++i) {
+        l0d[i] = FLT_MAX; l1d[i] = FLT_MAX;
+        l0i[i] = WV_NIL; l1i[i] = WV_NIL;
+    }
+
+    floatx16 acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+    // global -> register staging: 4 float4 of the base tile and 4 of the query tile
+    float4 ra[4], rb[4];
+    const int total = (int)((t_end > t_begin ? t_end - t_begin : 0) * nk);
+
+    auto load_chunk = [&](int c) {
+        const uint64_t tile = t_begin + (uint64_t)(c / nk);
+        const int kc = c % nk;
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+            const int e = tid + 256 * it;
+            const int row = e >> 3, f4 = e & 7;
+            const int k = kc * BF_BK + 4 * f4;
+            const uint64_t xr = tile * BF_BN + row;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (xr < p.N && k < p.D) v = ld4(p.X + xr * (uint64_t)p.ldx + k);
+            ra[it] = v;
+            const int qr = q0 + row;
+            float4 w = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (qr < p.nq && k < p.D) w = ld4(p.Q + (uint64_t)qr * p.ldq + k);
+            rb[it] = w;
+        }
+    };
+    auto store_chunk = [&](int buf) {
+        float* a = As + buf * BF_BK * BF_LD;
+        float* b = Bs + buf * BF_BK * BF_LD;
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+            const int e = tid + 256 * it;
+            const int row = e >> 3, f4 = e & 7;
+            a[(4 * f4 + 0) * BF_LD + row] = ra[it].x;
+            a[(4 * f4 + 1) * BF_LD + row] = ra[it].y;
+            a[(4 * f4 + 2) * BF_LD + row] = ra[it].z;
+            a[(4 * f4 + 3) * BF_LD + row] = ra[it].w;
+            b[(4 * f4 + 0) * BF_LD + row] = rb[it].x;
+            b[(4 * f4 + 1) * BF_LD + row] = rb[it].y;
+            b[(4 * f4 + 2) * BF_LD + row] = rb[it].z;
+            b[(4 * f4 + 3) * BF_LD + row] = rb[it].w;
+        }
+    };
+
+    if (total > 0) {
+        load_chunk(0);
+        store_chunk(0);
+    }
+    __syncthreads();
+
+    const int khalf = lane >> 5;
+    const int l31 = lane & 31;
+    for (int c = 0; c < total; ++c) {
+        if (c + 1 < total) load_chunk(c + 1);
+        const float* a = As + (c & 1) * BF_BK * BF_LD;
+        const float* b = Bs + (c & 1) * BF_BK * BF_LD;
+#pragma unroll 4
+        for (int ks = 0; ks < BF_BK / 2; ++ks) {
+            const int kr = (2 * ks + khalf) * BF_LD;
+            const float a0 = a[kr + wm * 64 + l31];
+            const float a1 = a[kr + wm * 64 + 32 + l31];
+            const float b0 = b[kr + wn * 64 + l31];
+            const float b1 = b[kr + wn * 64 + 32 + l31];
+            acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+            acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+            acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+            acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+        }
+        if ((c % nk) == nk - 1) {
+            // ---- epilogue of one 128x128 tile ----
+            const uint64_t tile = t_begin + (uint64_t)(c / nk);
+            const int jq0 = q0 + wn * 64 + l31;        // query of list 0
+            const int jq1 = jq0 + 32;                  // query of list 1
+            const uint64_t* al0 = p.allow ? p.allow + (p.allow_stride ? (uint64_t)min(jq0, p.nq - 1) * p.allow_stride : 0) : nullptr;
+            const uint64_t* al1 = p.allow ? p.allow + (p.allow_stride ? (uint64_t)min(jq1, p.nq - 1) * p.allow_stride : 0) : nullptr;
+#pragma unroll
+            for (int rbk = 0; rbk < 2; ++rbk) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int i = wm * 64 + rbk * 32 + (r & 3) + 8 * (r >> 2) + 4 * khalf;
+                    const uint64_t xid = tile * BF_BN + i;
+                    bool ok = xid < p.N;
+                    if (ok && p.tomb) ok = !bit_test(p.tomb, p.tomb_nbits, xid);
+                    float xn = 0.f;
+                    if (p.metric == WV_METRIC_L2 && ok) xn = p.xnorm[xid];
+                    const float d0 = p.metric == WV_METRIC_L2 ? __builtin_fmaf(-2.f, acc[rbk][0][r], xn) : -acc[rbk][0][r];
+                    const float d1 = p.metric == WV_METRIC_L2 ? __builtin_fmaf(-2.f, acc[rbk][1][r], xn) : -acc[rbk][1][r];
+                    bool ok0 = ok && jq0 < p.nq, ok1 = ok && jq1 < p.nq;
+                    if (al0 && ok0) ok0 = bit_test(al0, p.allow_nbits, xid);
+                    if (al1 && ok1) ok1 = bit_test(al1, p.allow_nbits, xid);
+                    const uint32_t id32 = (uint32_t)xid;
+                    const bool in0 = ok0 && key_less(d0, id32, l0d[BF_KP - 1], l0i[BF_KP - 1]);
+                    const bool in1 = ok1 && key_less(d1, id32, l1d[BF_KP - 1], l1i[BF_KP - 1]);
+                    if (__any(in0)) {
+                        if (in0) list_insert(l0d, l0i, d0, id32);
+                    }
+                    if (__any(in1)) {
+                        if (in1) list_insert(l1d, l1i, d1, id32);
+                    }
+                }
+            }
+#pragma unroll
+            for (int a2 = 0; a2 < 2; ++a2)
+#pragma unroll
+                for (int b2 = 0; b2 < 2; ++b2)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) acc[a2][b2][r] = 0.f;
+        }
+        if (c + 1 < total) store_chunk((c + 1) & 1);
+        __syncthreads();
+    }
+
+    // write this lane's two lists: out[q][split][producer][KP]
+    const int prod = wm * 2 + khalf;
+    const int jq0 = q0 + wn * 64 + l31;
+    const int jq1 = jq0 + 32;
+    const size_t per_q = (size_t)p.n_splits * BF_PROD * BF_KP;
+    if (jq0 < p.nq) {
+        const size_t base = (size_t)jq0 * per_q + ((size_t)split * BF_PROD + prod) * BF_KP;
+#pragma unroll
+        for (int i = 0; i < BF_KP; ++i) { p.out_d[base + i] = l0d[i]; p.out_id[base + i] = l0i[i]; }
+    }
+    if (jq1 < p.nq) {
+        const size_t base = (size_t)jq1 * per_q + ((size_t)split * BF_PROD + prod) * BF_KP;
+#pragma unroll
+        for (int i = 0; i < BF_KP; ++i) { p.out_d[base + i] = l1d[i]; p.out_id[base + i] = l1i[i]; }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Finalize: one wave per query.
+
+template <int METRIC>
+__device__ void finalize_one(const BfFinParams& p, int q, float* sd, uint32_t* si, float* qv) {
+    const int lane = threadIdx.x & 63;
+    const int n_ent = p.n_lists * BF_KP;
+    const float* cd = p.cand_d + (size_t)q * n_ent;
+    const uint32_t* ci = p.cand_id + (size_t)q * n_ent;
+
+    // bound from the producers' last entries: anything a producer dropped is >= its KP-th key
+    float bound = FLT_MAX;
+    uint32_t bound_id = WV_NIL;
+    for (int l = lane; l < p.n_lists; l += 64) {
+        const float d = cd[l * BF_KP + BF_KP - 1];
+        const uint32_t i = ci[l * BF_KP + BF_KP - 1];
+        if (key_less(d, i, bound, bound_id)) { bound = d; bound_id = i; }
+    }
+    for (int m = 32; m >= 1; m >>= 1) {
+        const float od = __shfl_xor(bound, m, 64);
+        const uint32_t oi = __shfl_xor(bound_id, m, 64);
+        if (key_less(od, oi, bound, bound_id)) { bound = od; bound_id = oi; }
+    }
+
+    // select the FIN_KF smallest keys among all entries: repeated wave-wide
+    // tournament over per-lane sorted runs would be faster; this keeps a
+    // sorted top-KF list in LDS, one candidate per lane per round.
+    if (lane < FIN_KF) { sd[lane] = FLT_MAX; si[lane] = WV_NIL; }
+    __builtin_amdgcn_wave_barrier();
+    // each lane scans its share and keeps a private top-KF in LDS-free registers
+    float td[FIN_KF];
+    uint32_t ti[FIN_KF];
+#pragma unroll
+    for (int i = 0; i < FIN_KF; ++i) { td[i] = FLT_MAX; ti[i] = WV_NIL; }
+    for (int e = lane; e < n_ent; e += 64) {
+        float d = cd[e];
+        uint32_t id = ci[e];
+        if (id == WV_NIL) continue;
+        if (!key_less(d, id, td[FIN_KF - 1], ti[FIN_KF - 1])) continue;
+#pragma unroll
+        for (int i = 0; i < FIN_KF; ++i) {
+            const bool lt = key_less(d, id, td[i], ti[i]);
+            const float a = td[i];
+            const uint32_t b = ti[i];
+            td[i] = lt ? d : td[i];
+            ti[i] = lt ? id : ti[i];
+            d = lt ? a : d;
+            id = lt ? b : id;
+        }
+    }
+    // wave merge: FIN_KF rounds of argmin over the lane heads
+    int head = 0;
+    for (int r = 0; r < FIN_KF; ++r) {
+        float hd = FLT_MAX;
+        uint32_t hi = WV_NIL;
+#pragma unroll
+        for (int i = 0; i < FIN_KF; ++i)
+            if (i == head) { hd = td[i]; hi = ti[i]; }
+        float md = hd;
+        uint32_t mi = hi;
+        for (int m = 32; m >= 1; m >>= 1) {
+            const float od = __shfl_xor(md, m, 64);
+            const uint32_t oi = __shfl_xor(mi, m, 64);
+            if (key_less(od, oi, md, mi)) { md = od; mi = oi; }
+        }
+        if (hi == mi && hd == md && mi != WV_NIL) head++;
+        if (lane == 0) { sd[r] = md; si[r] = mi; }
+    }
+    __builtin_amdgcn_wave_barrier();
+    // the KF-th approx key bounds every entry not selected
+    {
+        const float dk = sd[FIN_KF - 1];
+        const uint32_t ik = si[FIN_KF - 1];
+        if (key_less(dk, ik, bound, bound_id)) { bound = dk; bound_id = ik; }
+    }
+
+    // query into LDS for the exact distance
+    for (int i = lane; i < ((p.D + 3) & ~3); i += 64) qv[i] = i < p.D ? p.Q[(size_t)q * p.ldq + i] : 0.f;
+    __builtin_amdgcn_wave_barrier();
+
+    // exact re-rank of the FIN_KF candidates: 8 lanes per row
+    const int g = lane & 7, grp = lane >> 3;
+    float ex[FIN_KF / 8];
+#pragma unroll
+    for (int pass = 0; pass < FIN_KF / 8; ++pass) {
+        const int c = pass * 8 + grp;
+        const uint32_t id = si[c];
+        float d = FLT_MAX;
+        if (id != WV_NIL) d = exact_dist_group8<METRIC>(qv, p.X + (size_t)id * p.ldx, p.D, g);
+        ex[pass] = d;
+    }
+    __builtin_amdgcn_wave_barrier();
+    // write exact distances back (group leader)
+#pragma unroll
+    for (int pass = 0; pass < FIN_KF / 8; ++pass)
+        if (g == 0) sd[pass * 8 + grp] = ex[pass];
+    __builtin_amdgcn_wave_barrier();
+    // sort the FIN_KF exact keys (rank by counting: lane c < FIN_KF)
+    float myd = FLT_MAX;
+    uint32_t myi = WV_NIL;
+    int rank = 0;
+    if (lane < FIN_KF) {
+        myd = sd[lane];
+        myi = si[lane];
+        for (int j = 0; j < FIN_KF; ++j)
+            if (key_less(sd[j], si[j], myd, myi)) rank++;
+    }
+    __builtin_amdgcn_wave_barrier();
+    const int k = p.k;
+    int nvalid = 0;
+    for (int j = 0; j < FIN_KF; ++j) nvalid += (si[j] != WV_NIL);
+    if (lane < FIN_KF && myi != WV_NIL && rank < k) {
+        p.out_ids[(size_t)q * k + rank] = p.id_base + myi;
+        p.out_d[(size_t)q * k + rank] = myd;
+    }
+    // k-th exact distance
+    float dk = -FLT_MAX;
+    const int nk = nvalid < k ? nvalid : k;
+    if (lane < FIN_KF && myi != WV_NIL && rank == nk - 1) dk = myd;
+    for (int m = 32; m >= 1; m >>= 1) dk = fmaxf(dk, __shfl_xor(dk, m, 64));
+
+    // certificate: eps bounds |approx - reference| for every point
+    const float u = 5.9604645e-08f;  // 2^-24
+    const float D4 = (float)(p.D + 4);
+    float eps, bfull;
+    if (METRIC == WV_METRIC_L2) {
+        const float qn = sqrtf(p.qnorm[q]);
+        const float s = qn + p.xnorm_max;
+        eps = 4.f * D4 * u * s * s;
+        bfull = bound + p.qnorm[q];
+    } else {
+        const float qn = p.qnorm[q];
+        eps = 4.f * D4 * u * qn * p.xnorm_max + 4.f * u;
+        bfull = METRIC == WV_METRIC_DOT ? bound : 1.0f + bound;
+    }
+    bool certified;
+    if (nvalid < k) certified = bound == FLT_MAX;     // everything eligible was seen
+    else certified = (bound == FLT_MAX) || (bfull - eps > dk);
+    if (lane == 0) {
+        p.out_n[q] = nk;
+        p.fail[q] = certified ? 0 : 1;
+    }
+}
+
+__global__ __launch_bounds__(64) void wv_bf_finalize_kernel(BfFinParams p) {
+    // one dynamic region: query (16-byte aligned base), then the KF keys
+    extern __shared__ float qv[];
+    const int dpad = (p.D + 3) & ~3;
+    float* sd = qv + dpad;
+    uint32_t* si = reinterpret_cast<uint32_t*>(sd + FIN_KF);
+    const int q = blockIdx.x;
+    if (q >= p.nq) return;
+    if (p.metric == WV_METRIC_L2) finalize_one<WV_METRIC_L2>(p, q, sd, si, qv);
+    else if (p.metric == WV_METRIC_DOT) finalize_one<WV_METRIC_DOT>(p, q, sd, si, qv);
+    else finalize_one<WV_METRIC_COSINE>(p, q, sd, si, qv);
+}
+
+// ---------------------------------------------------------------------------
+// Exact full scan for one query: dist[i] = reference-order distance, or +inf
+// when ineligible.  8 lanes per row, 32 rows per 256-thread block pass.
+
+template <int METRIC>
+__device__ void scan_rows(const ScanParams& p, const float* qv) {
+    const int g = threadIdx.x & 7;
+    const uint64_t grp = (uint64_t)blockIdx.x * (blockDim.x >> 3) + (threadIdx.x >> 3);
+    const uint64_t stride = (uint64_t)gridDim.x * (blockDim.x >> 3);
+    for (uint64_t r = grp; r < p.N; r += stride) {
+        const float d = exact_dist_group8<METRIC>(qv, p.X + r * p.ldx, p.D, g);
+        bool ok = true;
+        if (p.tomb) ok = !bit_test(p.tomb, p.tomb_nbits, r);
+        if (p.allow && ok) ok = bit_test(p.allow, p.allow_nbits, r);
+        if (g == 0) {
+            p.dist[r] = ok ? d : __builtin_inff();
+            p.ids[r] = (uint32_t)r;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void wv_exact_scan_kernel(ScanParams p) {
+    extern __shared__ float qv[];
+    // the tail reads whole float4s: zero-fill up to the padded length
+    for (int i = threadIdx.x; i < ((p.D + 3) & ~3); i += blockDim.x) qv[i] = i < p.D ? p.q[i] : 0.f;
+    __syncthreads();
+    if (p.metric == WV_METRIC_L2) scan_rows<WV_METRIC_L2>(p, qv);
+    else if (p.metric == WV_METRIC_DOT) scan_rows<WV_METRIC_DOT>(p, qv);
+    else scan_rows<WV_METRIC_COSINE>(p, qv);
+}
+
+// ---------------------------------------------------------------------------
+// |x|^2 (fp32, any order: only feeds the approximate distance) and max |x|.
+__global__ void wv_rownorm_kernel(const float* X, uint64_t N, int D, int ldx, float* norm2,
+                                  unsigned int* max_norm_bits) {
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= N) return;
+    const float* row = X + r * ldx;
+    float s = 0.f;
+    for (int i = 0; i < D; i += 4) {
+        const float4 v = ld4(row + i);
+        s = __builtin_fmaf(v.x, v.x, s);
+        s = __builtin_fmaf(v.y, v.y, s);
+        s = __builtin_fmaf(v.z, v.z, s);
+        s = __builtin_fmaf(v.w, v.w, s);
+    }
+    if (norm2) norm2[r] = s;
+    // slightly inflated |x| (covers the rounding of s and sqrt)
+    const float n = sqrtf(s) * (1.0f + 1e-6f);
+    atomicMax(max_norm_bits, __float_as_uint(n));
+}
+
+// Normalize (distancer/normalize.go:16-32): sequential, unfused sum of squares,
+// sqrt in double, IEEE division.  One thread per row, in place or out of place.
+__global__ void wv_normalize_kernel(const float* in, float* out, uint64_t n, int D, int ld) {
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const float* v = in + r * ld;
+    float* o = out + r * ld;
+    float norm = 0.f;
+    for (int i = 0; i < D; ++i) {
+        const float sq = __fmul_rn(v[i], v[i]);
+        norm = __fadd_rn(norm, sq);
+    }
+    if (norm == 0.f) {
+        for (int i = 0; i < D; ++i) o[i] = 0.f;
+        return;
+    }
+    const float nn = (float)sqrt((double)norm);
+    for (int i = 0; i < D; ++i) o[i] = __fdiv_rn(v[i], nn);
+}
+
+// |q|^2 for L2, |q| for dot/cosine (feeds eps only)
+__global__ void wv_qnorm_kernel(const float* Q, int nq, int D, int ldq, int metric, float* out) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nq) return;
+    float s = 0.f;
+    for (int i = 0; i < D; ++i) s = __builtin_fmaf(Q[(size_t)r * ldq + i], Q[(size_t)r * ldq + i], s);
+    // L2: |q|^2 enters the bound additively (no inflation; eps covers its
+    // rounding).  dot/cosine: |q| only scales eps, so it is rounded up.
+    out[r] = metric == WV_METRIC_L2 ? s : sqrtf(s * (1.0f + 1e-6f)) * (1.0f + 1e-6f);
+}
+
+}  // namespace wv
+
+// ---- launch wrappers (host side of this TU) --------------------------------
+extern "C" {
+
+hipError_t wv_launch_bf_mfma(const wv::BfParams* p, hipStream_t s) {
+    const size_t lds = 4 * wv::BF_BK * wv::BF_LD * sizeof(float);
+    hipLaunchKernelGGL(wv::wv_bf_mfma_kernel, dim3(p->n_qblocks * p->n_splits), dim3(256), lds, s, *p);
+    return hipGetLastError();
+}
+
+hipError_t wv_launch_bf_finalize(const wv::BfFinParams* p, hipStream_t s) {
+    const size_t lds = (((p->D + 3) & ~3) + 2 * wv::FIN_KF) * sizeof(float);
+    hipLaunchKernelGGL(wv::wv_bf_finalize_kernel, dim3(p->nq), dim3(64), lds, s, *p);
+    return hipGetLastError();
+}
+
+hipError_t wv_launch_exact_scan(const wv::ScanParams* p, hipStream_t s) {
+    uint64_t blocks = (p->N + 31) / 32;
+    if (blocks > 8192) blocks = 8192;
+    if (blocks == 0) blocks = 1;
+    hipLaunchKernelGGL(wv::wv_exact_scan_kernel, dim3((unsigned)blocks), dim3(256), p->D * sizeof(float), s, *p);
+    return hipGetLastError();
+}
+
+hipError_t wv_launch_rownorm(const float* X, uint64_t N, int D, int ldx, float* norm2, unsigned int* maxbits,
+                             hipStream_t s) {
+    if (N == 0) return hipSuccess;
+    hipLaunchKernelGGL(wv::wv_rownorm_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, X, N, D, ldx,
+                       norm2, maxbits);
+    return hipGetLastError();
+}
+
+hipError_t wv_launch_normalize(const float* in, float* out, uint64_t n, int D, int ld, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(wv::wv_normalize_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, in, out, n, D,
+                       ld);
+    return hipGetLastError();
+}
+
+hipError_t wv_launch_qnorm(const float* Q, int nq, int D, int ldq, int metric, float* out, hipStream_t s) {
+    if (nq == 0) return hipSuccess;
+    hipLaunchKernelGGL(wv::wv_qnorm_kernel, dim3((nq + 255) / 256), dim3(256), 0, s, Q, nq, D, ldq, metric, out);
+    return hipGetLastError();
+}
+
+}  // extern "C"

@@ -1,0 +1,102 @@
+// wv_device.h -- device helpers shared by the CDNA4 (gfx950) kernels.
+//
+// The exact distance here reproduces the reference's AVX2 assembly bit for bit
+// (adapters/repos/db/vector/hnsw/distancer/asm/l2_amd64.s:7-64 and
+// dot_amd64.s:7-55): 32 independent FMA chains (4 accumulators x 8 lanes) over
+// 32-float blocks, a sequential FMA tail, then the fixed reduction tree.  On
+// the GPU the 32 chains are spread over a group of 8 lanes, each lane owning
+// one float4 slice (4 chains) of every 32-float block, so a group reads a row
+// as fully coalesced 128-byte pieces.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define WV_NIL 0xFFFFFFFFu
+#define WV_FLAG 0x80000000u   // "expanded" flag carried in bit 31 of a local id
+#define WV_IDMASK 0x7FFFFFFFu
+
+enum { WV_METRIC_L2 = 0, WV_METRIC_DOT = 1, WV_METRIC_COSINE = 2 };
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+__device__ __forceinline__ float shfl_xor_f(float v, int m) { return __shfl_xor(v, m, 64); }
+
+// Exact reference-order distance of one stored row against the query, computed
+// by the 8-lane group that contains this lane (g = lane & 7).  Every lane of
+// the group returns the result.  q and row are 16-byte aligned, D % 4 == 0.
+template <int METRIC>
+__device__ __forceinline__ float exact_dist_group8(const float* __restrict__ q,
+                                                   const float* __restrict__ row,
+                                                   int D, int g) {
+    const int nb = D >> 5;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    for (int b = 0; b < nb; ++b) {
+        const float4 x = ld4(q + 32 * b + 4 * g);
+        const float4 y = ld4(row + 32 * b + 4 * g);
+        if (METRIC == WV_METRIC_L2) {
+            const float d0 = x.x - y.x, d1 = x.y - y.y, d2 = x.z - y.z, d3 = x.w - y.w;
+            a0 = __builtin_fmaf(d0, d0, a0);
+            a1 = __builtin_fmaf(d1, d1, a1);
+            a2 = __builtin_fmaf(d2, d2, a2);
+            a3 = __builtin_fmaf(d3, d3, a3);
+        } else {
+            a0 = __builtin_fmaf(x.x, y.x, a0);
+            a1 = __builtin_fmaf(x.y, y.y, a1);
+            a2 = __builtin_fmaf(x.z, y.z, a2);
+            a3 = __builtin_fmaf(x.w, y.w, a3);
+        }
+    }
+    // tail (l2_amd64.s:40-52 / dot_amd64.s:36-43): one sequential chain
+    float t = 0.f;
+    for (int i = nb * 32; i < D; i += 4) {
+        const float4 x = ld4(q + i);
+        const float4 y = ld4(row + i);
+        if (METRIC == WV_METRIC_L2) {
+            float d = x.x - y.x; t = __builtin_fmaf(d, d, t);
+            d = x.y - y.y;       t = __builtin_fmaf(d, d, t);
+            d = x.z - y.z;       t = __builtin_fmaf(d, d, t);
+            d = x.w - y.w;       t = __builtin_fmaf(d, d, t);
+        } else {
+            t = __builtin_fmaf(x.x, y.x, t);
+            t = __builtin_fmaf(x.y, y.y, t);
+            t = __builtin_fmaf(x.z, y.z, t);
+            t = __builtin_fmaf(x.w, y.w, t);
+        }
+    }
+    // reduction tree (l2_amd64.s:54-64): lane g holds accumulator j = g>>1,
+    // lanes l = 4*(g&1) .. +3.  (acc0+acc1), (acc2+acc3): xor 2
+    a0 = a0 + shfl_xor_f(a0, 2); a1 = a1 + shfl_xor_f(a1, 2);
+    a2 = a2 + shfl_xor_f(a2, 2); a3 = a3 + shfl_xor_f(a3, 2);
+    // (acc0+acc1)+(acc2+acc3): xor 4
+    a0 = a0 + shfl_xor_f(a0, 4); a1 = a1 + shfl_xor_f(a1, 4);
+    a2 = a2 + shfl_xor_f(a2, 4); a3 = a3 + shfl_xor_f(a3, 4);
+    // VEXTRACTF128 + VADDPS: v[l] = s[l] + s[l+4]: xor 1
+    a0 = a0 + shfl_xor_f(a0, 1); a1 = a1 + shfl_xor_f(a1, 1);
+    a2 = a2 + shfl_xor_f(a2, 1); a3 = a3 + shfl_xor_f(a3, 1);
+    // VADDPS X1: v += [t, 0, 0, 0]; two VHADDPS: (v0+v1)+(v2+v3)
+    a0 = t + a0;
+    a1 = 0.0f + a1;
+    a2 = 0.0f + a2;
+    a3 = 0.0f + a3;
+    const float r = (a0 + a1) + (a2 + a3);
+    if (METRIC == WV_METRIC_L2) return r;
+    if (METRIC == WV_METRIC_DOT) return -r;
+    return 1.0f - r;
+}
+
+// Key order used for ids: (dist, id) ascending.
+__device__ __forceinline__ bool key_less(float da, uint32_t ia, float db, uint32_t ib) {
+    return da < db || (da == db && (ia & WV_IDMASK) < (ib & WV_IDMASK));
+}
+
+__device__ __forceinline__ bool bit_test(const uint64_t* __restrict__ bits, uint64_t nbits, uint64_t id) {
+    return id < nbits && ((bits[id >> 6] >> (id & 63)) & 1ull);
+}
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+// exclusive prefix count of set bits below this lane
+__device__ __forceinline__ int mbcnt64(uint64_t mask) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                     __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
+}

@@ -1,0 +1,415 @@
+// wv_hnsw.hip -- HNSW search (knnSearchByVector) with one wavefront per query.
+//
+// Restates adapters/repos/db/vector/hnsw/search.go:
+//   knnSearchByVector (:460-550): entry point, greedy ef=1 descent over the
+//   upper layers, then the layer-0 beam search with ef and the allow list;
+//   searchLayerByVector (:160-327).
+//
+// Graph layout in HBM (a fixed-degree CSR re-layout):
+//   levels[N] int8 (-1 = nil node), layer0[N][deg0] u32 (pad 0xFFFFFFFF),
+//   upper_row[N] u32, upper[n_upper][max_level][degU] u32, vectors[N][ldx] f32.
+//
+// Exactness.  The reference processes the neighbours of a popped candidate one
+// by one; a neighbour is accepted when d < worst || |results| < ef, and worst
+// only moves when an allowed, untombstoned neighbour enters the results.  On
+// tie-free distances that sequential loop ends in the same state as
+//   R' = the ef smallest of R u {eligible neighbours},
+//   S' = S u {ineligible neighbours with d <= worst(R')} (all of them while R'
+//        is not full),
+// where R holds the results (a candidate is exactly an unexpanded member of R)
+// and S holds the traversed-but-ineligible candidates (filtered-out or
+// tombstoned, search.go:282-298).  Candidates with d > worst can never be
+// expanded (the loop breaks on them, :213-215), so they are not stored.  The
+// wave therefore computes all neighbour distances in parallel (bit-identical
+// to the reference distancer), sorts them, and merges the batch into R and S.
+// The visited list (:256-264) is a lossy LDS cache: a node it forgets is
+// re-evaluated, and re-evaluating a visited node cannot change R or S (its
+// key is already in R/S, was evicted with d > worst, or it was expanded from S,
+// which the exact set X records), so pruning with any subset of the visited
+// set is exact.
+#include "wv_device.h"
+#include "wv_params.h"
+
+#include <float.h>
+
+namespace wv {
+
+
+constexpr int BATCH = 128;
+constexpr int MAX_LOCAL_TOMB = 4;
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+struct WaveState {
+    float* qv;
+    float* Rd; uint32_t* Ri;
+    float* Rd2; uint32_t* Ri2;
+    float* Sd; uint32_t* Si;
+    float* Sd2; uint32_t* Si2;
+    float* Bd; uint32_t* Bi;    // raw batch (distance by batch slot)
+    float* Cd; uint32_t* Ci;    // sorted batch
+    uint32_t* vc;
+    uint32_t* xs;
+    uint32_t* ltomb;
+};
+
+__device__ __forceinline__ uint32_t hash32(uint32_t x) { return x * 2654435761u; }
+
+// lower bound: number of entries of a sorted (d,id) array with key < (d,id)
+__device__ __forceinline__ int lower_bound(const float* ad, const uint32_t* ai, int n, float d, uint32_t id) {
+    int lo = 0, len = n;
+    while (len > 0) {
+        const int half = len >> 1;
+        const int mid = lo + half;
+        if (key_less(ad[mid], ai[mid], d, id)) {
+            lo = mid + 1;
+            len = len - half - 1;
+        } else {
+            len = half;
+        }
+    }
+    return lo;
+}
+
+// composite order for the batch sort: eligible first, then (d, id)
+__device__ __forceinline__ bool ckey_less(uint32_t ca, float da, uint32_t ia, uint32_t cb, float db, uint32_t ib) {
+    return ca < cb || (ca == cb && key_less(da, ia, db, ib));
+}
+
+template <int METRIC>
+__device__ void search_layer(const HnswParams& p, WaveState& w, int level, int ef, uint32_t ep, float epd,
+                             const uint64_t* allow, int& Rl, int& Sh, int& Sl, int& status, int nlt,
+                             uint32_t& n_dist, uint32_t& n_exp) {
+    const int lane = threadIdx.x & 63;
+    const int g = lane & 7, grp = lane >> 3;
+    const int VC = 1 << p.vc_log2;
+    const int XS = 1 << p.xs_log2;
+    for (int i = lane; i < VC; i += 64) w.vc[i] = WV_NIL;
+    for (int i = lane; i < XS; i += 64) w.xs[i] = WV_NIL;
+    wave_sync();
+
+    auto eligible = [&](uint32_t id) -> bool {
+        if (p.tomb && bit_test(p.tomb, p.tomb_nbits, id)) return false;
+        for (int t = 0; t < nlt; ++t)
+            if (w.ltomb[t] == id) return false;
+        if (level == 0 && allow && !bit_test(allow, p.allow_nbits, id)) return false;
+        return true;
+    };
+
+    // insertViableEntrypointsAsCandidatesAndResults (search.go:329-353)
+    if (lane == 0) w.vc[hash32(ep) >> (32 - p.vc_log2)] = ep;
+    Rl = 0; Sh = 0; Sl = 0;
+    if (eligible(ep)) {
+        if (lane == 0) { w.Rd[0] = epd; w.Ri[0] = ep; }
+        Rl = 1;
+    } else {
+        if (lane == 0) { w.Sd[0] = epd; w.Si[0] = ep; }
+        Sl = 1;
+    }
+    wave_sync();
+    // currentWorstResultDistanceToFloat (:355-377)
+    float worst = Rl > 0 ? w.Rd[Rl - 1] : FLT_MAX;
+
+    const uint32_t* nbr_base;
+    int deg;
+    for (;;) {
+        // ---- pop the best live candidate: first unexpanded R entry vs S head ----
+        int ridx = Rl;
+        for (int base = 0; base < Rl; base += 64) {
+            const int i = base + lane;
+            const bool unexp = i < Rl && !(w.Ri[i] & WV_FLAG);
+            const uint64_t m = __ballot(unexp);
+            if (m) { ridx = base + __builtin_ctzll(m); break; }
+        }
+        const bool haveR = ridx < Rl;
+        const bool haveS = Sl > 0;
+        if (!haveR && !haveS) break;
+        float cd; uint32_t cid; bool fromR;
+        if (haveR && (!haveS || key_less(w.Rd[ridx], w.Ri[ridx], w.Sd[Sh], w.Si[Sh]))) {
+            cd = w.Rd[ridx]; cid = w.Ri[ridx] & WV_IDMASK; fromR = true;
+        } else {
+            cd = w.Sd[Sh]; cid = w.Si[Sh]; fromR = false;
+        }
+        if (cd > worst) break;  // :213-215
+        wave_sync();
+        if (fromR) {
+            if (lane == 0) w.Ri[ridx] = cid | WV_FLAG;
+        } else {
+            Sh++; Sl--;
+            // record the expansion in X (exact open-addressing set)
+            if (lane == 0) {
+                uint32_t h = hash32(cid) >> (32 - p.xs_log2);
+                int probes = 0;
+                while (w.xs[h] != WV_NIL && w.xs[h] != cid && probes < XS) { h = (h + 1) & (XS - 1); probes++; }
+                if (probes >= XS) status |= 2;
+                else w.xs[h] = cid;
+            }
+            status = __shfl(status, 0, 64);
+        }
+        wave_sync();
+        // :217-234 nil node / level check
+        const int lvl = p.levels[cid];
+        if (lvl < level) continue;
+        if (level == 0) {
+            nbr_base = p.layer0 + (uint64_t)cid * p.deg0;
+            deg = p.deg0;
+        } else {
+            const uint32_t row = p.upper_row[cid];
+            nbr_base = p.upper + ((uint64_t)row * p.max_level + (level - 1)) * p.degU;
+            deg = p.degU;
+        }
+        n_exp++;
+
+        for (int c0 = 0; c0 < deg; c0 += BATCH) {
+            // ---- neighbour ids, visited-cache filter, compaction ----
+            uint32_t id0 = WV_NIL, id1 = WV_NIL;
+            if (c0 + lane < deg) id0 = nbr_base[c0 + lane];
+            if (c0 + 64 + lane < deg) id1 = nbr_base[c0 + 64 + lane];
+            bool v0 = id0 != WV_NIL && id0 < p.N;
+            bool v1 = id1 != WV_NIL && id1 < p.N;
+            const uint32_t h0 = v0 ? hash32(id0) >> (32 - p.vc_log2) : 0;
+            const uint32_t h1 = v1 ? hash32(id1) >> (32 - p.vc_log2) : 0;
+            if (v0 && w.vc[h0] == id0) v0 = false;
+            if (v1 && w.vc[h1] == id1) v1 = false;
+            wave_sync();
+            if (v0) w.vc[h0] = id0;
+            if (v1) w.vc[h1] = id1;
+            const uint64_t m0 = __ballot(v0), m1 = __ballot(v1);
+            const int n0 = __popcll(m0);
+            const int nb = n0 + __popcll(m1);
+            if (v0) w.Bi[mbcnt64(m0)] = id0;
+            if (v1) w.Bi[n0 + mbcnt64(m1)] = id1;
+            wave_sync();
+            if (nb == 0) continue;
+
+            // ---- exact distances, 8 lanes per row (search.go:265-271) ----
+            for (int base = 0; base < nb; base += 8) {
+                const int c = base + grp;
+                float d = FLT_MAX;
+                if (c < nb) d = exact_dist_group8<METRIC>(w.qv, p.X + (uint64_t)w.Bi[c] * p.ldx, p.D, g);
+                if (c < nb && g == 0) w.Bd[c] = d;
+            }
+            n_dist += nb;
+            wave_sync();
+
+            // ---- classify + dedupe (lanes hold slots lane, lane+64) ----
+            uint32_t cls[2]; float bd[2]; uint32_t bi[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int e = lane + 64 * h;
+                cls[h] = 2; bd[h] = FLT_MAX; bi[h] = WV_NIL;
+                if (e < nb) {
+                    const uint32_t id = w.Bi[e];
+                    const float d = w.Bd[e];
+                    const bool el = eligible(id);
+                    bool dup;
+                    if (el) {
+                        const int pos = lower_bound(w.Rd, w.Ri, Rl, d, id);
+                        dup = pos < Rl && w.Rd[pos] == d && (w.Ri[pos] & WV_IDMASK) == id;
+                    } else {
+                        const int pos = lower_bound(w.Sd + Sh, w.Si + Sh, Sl, d, id);
+                        dup = pos < Sl && w.Sd[Sh + pos] == d && w.Si[Sh + pos] == id;
+                        if (!dup) {
+                            uint32_t hh = hash32(id) >> (32 - p.xs_log2);
+                            for (int pr = 0; pr < XS; ++pr) {
+                                const uint32_t v = w.xs[hh];
+                                if (v == id) { dup = true; break; }
+                                if (v == WV_NIL) break;
+                                hh = (hh + 1) & (XS - 1);
+                            }
+                        }
+                    }
+                    if (!dup) { cls[h] = el ? 0 : 1; bd[h] = d; bi[h] = id; }
+                }
+            }
+            // ---- bitonic sort of 128 (cls, d, id) keys, 2 per lane ----
+            for (int kk = 2; kk <= 128; kk <<= 1) {
+                for (int j = kk >> 1; j > 0; j >>= 1) {
+                    if (j == 64) {
+                        // partner is the other slot of this lane; element e = lane, asc if (e & kk)==0
+                        const bool asc = ((lane & kk) == 0);
+                        const bool sw = asc ? ckey_less(cls[1], bd[1], bi[1], cls[0], bd[0], bi[0])
+                                            : ckey_less(cls[0], bd[0], bi[0], cls[1], bd[1], bi[1]);
+                        if (sw) {
+                            uint32_t tc = cls[0]; cls[0] = cls[1]; cls[1] = tc;
+                            float td = bd[0]; bd[0] = bd[1]; bd[1] = td;
+                            uint32_t ti = bi[0]; bi[0] = bi[1]; bi[1] = ti;
+                        }
+                    } else {
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) {
+                            const int e = lane + 64 * h;
+                            const uint32_t oc = __shfl_xor(cls[h], j, 64);
+                            const float od = __shfl_xor(bd[h], j, 64);
+                            const uint32_t oi = __shfl_xor(bi[h], j, 64);
+                            const bool asc = ((e & kk) == 0);
+                            const bool lower = (e & j) == 0;
+                            const bool other_less = ckey_less(oc, od, oi, cls[h], bd[h], bi[h]);
+                            const bool self_less = ckey_less(cls[h], bd[h], bi[h], oc, od, oi);
+                            // lower element keeps min when ascending
+                            const bool take = (lower == asc) ? other_less : self_less;
+                            if (take) { cls[h] = oc; bd[h] = od; bi[h] = oi; }
+                        }
+                    }
+                }
+            }
+            const int ne = __popcll(__ballot(cls[0] == 0)) + __popcll(__ballot(cls[1] == 0));
+            const int ns = __popcll(__ballot(cls[0] == 1)) + __popcll(__ballot(cls[1] == 1));
+            w.Cd[lane] = bd[0]; w.Ci[lane] = bi[0];
+            w.Cd[lane + 64] = bd[1]; w.Ci[lane + 64] = bi[1];
+            wave_sync();
+
+            // ---- merge eligible [0, ne) into R (cap ef) ----
+            if (ne > 0) {
+                const int newRl = min(ef, Rl + ne);
+                for (int i = lane; i < Rl; i += 64) {
+                    const float d = w.Rd[i];
+                    const uint32_t id = w.Ri[i];
+                    const int pos = i + lower_bound(w.Cd, w.Ci, ne, d, id);
+                    if (pos < newRl) { w.Rd2[pos] = d; w.Ri2[pos] = id; }
+                }
+                for (int j = lane; j < ne; j += 64) {
+                    const float d = w.Cd[j];
+                    const uint32_t id = w.Ci[j];
+                    const int pos = j + lower_bound(w.Rd, w.Ri, Rl, d, id);
+                    if (pos < newRl) { w.Rd2[pos] = d; w.Ri2[pos] = id; }
+                }
+                wave_sync();
+                float* td = w.Rd; w.Rd = w.Rd2; w.Rd2 = td;
+                uint32_t* ti = w.Ri; w.Ri = w.Ri2; w.Ri2 = ti;
+                Rl = newRl;
+                worst = w.Rd[Rl - 1];
+            }
+            // ---- side candidates: keep live ones, prune S by worst ----
+            int nsk = ns;
+            if (Rl >= ef) {
+                // live iff d <= worst; the ineligible run [ne, ne+ns) is sorted
+                nsk = lower_bound(w.Cd + ne, w.Ci + ne, ns, worst, 0xFFFFFFFFu) ;
+                // entries equal to worst with any id are live: lower_bound with id max
+                // counts keys < (worst, max id) -> all d < worst and d == worst
+                const int sl_live = lower_bound(w.Sd + Sh, w.Si + Sh, Sl, worst, 0xFFFFFFFFu);
+                Sl = sl_live;
+            }
+            if (nsk > 0) {
+                int newSl = Sl + nsk;
+                if (newSl > p.sc) { newSl = p.sc; status |= 1; }
+                for (int i = lane; i < Sl; i += 64) {
+                    const float d = w.Sd[Sh + i];
+                    const uint32_t id = w.Si[Sh + i];
+                    const int pos = i + lower_bound(w.Cd + ne, w.Ci + ne, nsk, d, id);
+                    if (pos < newSl) { w.Sd2[pos] = d; w.Si2[pos] = id; }
+                }
+                for (int j = lane; j < nsk; j += 64) {
+                    const float d = w.Cd[ne + j];
+                    const uint32_t id = w.Ci[ne + j];
+                    const int pos = j + lower_bound(w.Sd + Sh, w.Si + Sh, Sl, d, id);
+                    if (pos < newSl) { w.Sd2[pos] = d; w.Si2[pos] = id; }
+                }
+                wave_sync();
+                float* td = w.Sd; w.Sd = w.Sd2; w.Sd2 = td;
+                uint32_t* ti = w.Si; w.Si = w.Si2; w.Si2 = ti;
+                Sh = 0;
+                Sl = newSl;
+            }
+            wave_sync();
+        }
+    }
+}
+
+template <int METRIC>
+__device__ void knn_one(const HnswParams& p, WaveState& w, int q) {
+    const int lane = threadIdx.x & 63;
+    const int g = lane & 7;
+    // query -> LDS
+    for (int i = lane; i < p.dpad; i += 64) w.qv[i] = i < p.D ? p.Q[(uint64_t)q * p.ldq + i] : 0.f;
+    wave_sync();
+    const uint64_t* allow = p.allow ? p.allow + (p.allow_stride ? (uint64_t)q * p.allow_stride : 0) : nullptr;
+    int status = 0;
+    uint32_t n_dist = 0, n_exp = 0;
+    int nlt = 0;
+
+    // entry point distance (search.go:467-476)
+    uint32_t ep = p.entrypoint;
+    float epd = exact_dist_group8<METRIC>(w.qv, p.X + (uint64_t)ep * p.ldx, p.D, g);
+    epd = __shfl(epd, 0, 64);
+    n_dist++;
+    int Rl, Sh, Sl;
+    // greedy descent, levels max..1 with ef = 1 (:479-521)
+    for (int level = p.max_level; level >= 1; --level) {
+        search_layer<METRIC>(p, w, level, 1, ep, epd, nullptr, Rl, Sh, Sl, status, nlt, n_dist, n_exp);
+        if (Rl > 0) {
+            const uint32_t cid = w.Ri[0] & WV_IDMASK;
+            if (p.levels[cid] < 0) {
+                // nil node in the results: tombstoned by the reference (:496-507)
+                if (nlt < MAX_LOCAL_TOMB) {
+                    if (lane == 0) w.ltomb[nlt] = cid;
+                    nlt++;
+                }
+                wave_sync();
+            } else {
+                ep = cid;
+                epd = w.Rd[0];
+            }
+        }
+    }
+    // layer 0 with ef and the allow list (:523-528)
+    search_layer<METRIC>(p, w, 0, p.ef, ep, epd, allow, Rl, Sh, Sl, status, nlt, n_dist, n_exp);
+    const int n = min(Rl, p.k);
+    for (int i = lane; i < n; i += 64) {
+        p.out_ids[(uint64_t)q * p.k + i] = p.id_base + (w.Ri[i] & WV_IDMASK);
+        p.out_d[(uint64_t)q * p.k + i] = w.Rd[i];
+    }
+    if (lane == 0) {
+        p.out_n[q] = n;
+        p.status[q] = status;
+        if (p.counters) { p.counters[2 * q] = n_dist; p.counters[2 * q + 1] = n_exp; }
+    }
+}
+
+__global__ __launch_bounds__(256) void wv_hnsw_kernel(HnswParams p) {
+    extern __shared__ float lds[];
+    const int wave = threadIdx.x >> 6;
+    const int q = blockIdx.x * (blockDim.x >> 6) + wave;
+    if (q >= p.nq) return;
+    float* base = lds + (uint64_t)wave * p.per_wave_words;
+    WaveState w;
+    float* cur = base;
+    w.qv = cur; cur += p.dpad;
+    w.Rd = cur; cur += p.efc; w.Ri = reinterpret_cast<uint32_t*>(cur); cur += p.efc;
+    w.Rd2 = cur; cur += p.efc; w.Ri2 = reinterpret_cast<uint32_t*>(cur); cur += p.efc;
+    w.Sd = cur; cur += p.sc; w.Si = reinterpret_cast<uint32_t*>(cur); cur += p.sc;
+    w.Sd2 = cur; cur += p.sc; w.Si2 = reinterpret_cast<uint32_t*>(cur); cur += p.sc;
+    w.Bd = cur; cur += BATCH; w.Bi = reinterpret_cast<uint32_t*>(cur); cur += BATCH;
+    w.Cd = cur; cur += BATCH; w.Ci = reinterpret_cast<uint32_t*>(cur); cur += BATCH;
+    w.vc = reinterpret_cast<uint32_t*>(cur); cur += (1 << p.vc_log2);
+    w.xs = reinterpret_cast<uint32_t*>(cur); cur += (1 << p.xs_log2);
+    w.ltomb = reinterpret_cast<uint32_t*>(cur); cur += MAX_LOCAL_TOMB;
+    if (p.metric == WV_METRIC_L2) knn_one<WV_METRIC_L2>(p, w, q);
+    else if (p.metric == WV_METRIC_DOT) knn_one<WV_METRIC_DOT>(p, w, q);
+    else knn_one<WV_METRIC_COSINE>(p, w, q);
+}
+
+int hnsw_per_wave_words(int dpad, int efc, int sc, int vc_log2, int xs_log2) {
+    return dpad + 4 * efc + 4 * sc + 4 * BATCH + (1 << vc_log2) + (1 << xs_log2) + MAX_LOCAL_TOMB;
+}
+
+}  // namespace wv
+
+extern "C" {
+
+int wv_hnsw_per_wave_words(int dpad, int efc, int sc, int vc_log2, int xs_log2) {
+    return wv::hnsw_per_wave_words(dpad, efc, sc, vc_log2, xs_log2);
+}
+
+hipError_t wv_launch_hnsw(const wv::HnswParams* p, int waves_per_block, hipStream_t s) {
+    const size_t lds = (size_t)waves_per_block * p->per_wave_words * sizeof(float);
+    const unsigned blocks = (unsigned)((p->nq + waves_per_block - 1) / waves_per_block);
+    if (blocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(wv::wv_hnsw_kernel, dim3(blocks), dim3(64 * waves_per_block), lds, s, *p);
+    return hipGetLastError();
+}
+
+}  // extern "C"

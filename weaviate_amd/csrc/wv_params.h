@@ -1,0 +1,80 @@
+// wv_params.h -- kernel parameter blocks shared by the kernels and the host API.
+#pragma once
+#include <stdint.h>
+
+namespace wv {
+
+constexpr int BF_BQ = 128;   // queries per workgroup tile
+constexpr int BF_BN = 128;   // base rows per workgroup tile
+constexpr int BF_BK = 32;    // k-chunk staged through LDS
+constexpr int BF_LD = 129;   // padded LDS row (conflict-free transposed writes)
+constexpr int BF_KP = 16;    // candidates kept per producer lane
+constexpr int BF_PROD = 4;   // producers per query: 2 base-row waves x 2 lane halves
+constexpr int FIN_KF = 32;   // candidates re-ranked exactly per query
+constexpr int BF_FAST_KMAX = 32;   // k served by the MFMA + finalize pipeline
+constexpr int HNSW_EF_MAX = 512;   // largest ef the LDS beam holds
+
+struct BfParams {
+    const float* X;         // base rows [N][ldx]
+    const float* Q;         // queries [nq][ldq]
+    const float* xnorm;     // |x|^2 per row (L2 only)
+    const uint64_t* tomb;   // excluded ids (tombstones, nil nodes, missing rows)
+    const uint64_t* allow;  // allow bits (nullable)
+    uint64_t tomb_nbits, allow_nbits, allow_stride;  // stride in words (0 = shared)
+    uint64_t N;
+    int nq, D, ldx, ldq, metric;
+    int n_qblocks, n_splits, tiles_per_split;
+    float* out_d;           // [nq][n_splits][BF_PROD*BF_KP]
+    uint32_t* out_id;
+};
+
+struct BfFinParams {
+    const float* X;
+    const float* Q;
+    const float* cand_d;
+    const uint32_t* cand_id;
+    const float* qnorm;     // |q|^2 (L2) or |q| (dot, cosine)
+    float xnorm_max;        // max |x| over the corpus (rounded up)
+    int n_lists;            // n_splits * BF_PROD
+    int nq, D, ldx, ldq, metric, k;
+    uint64_t id_base;       // global id of local id 0
+    uint64_t* out_ids;      // [nq][k]
+    float* out_d;
+    int32_t* out_n;
+    int32_t* fail;          // per query: 1 = uncertified
+};
+
+struct ScanParams {
+    const float* X;
+    const float* q;          // one query (device)
+    const uint64_t* tomb;
+    const uint64_t* allow;
+    uint64_t tomb_nbits, allow_nbits;
+    uint64_t N;
+    int D, ldx, metric;
+    float* dist;             // [N]
+    uint32_t* ids;           // [N] iota
+};
+
+struct HnswParams {
+    const float* X;
+    const int8_t* levels;
+    const uint32_t* layer0;
+    const uint32_t* upper_row;
+    const uint32_t* upper;
+    const uint64_t* tomb;
+    const uint64_t* allow;
+    const float* Q;
+    uint64_t N, tomb_nbits, allow_nbits, allow_stride, id_base;
+    uint32_t entrypoint;
+    int D, ldx, ldq, metric, deg0, degU, max_level;
+    int nq, k, ef;
+    int efc, sc, vc_log2, xs_log2, dpad, per_wave_words;
+    uint64_t* out_ids;   // [nq][k]
+    float* out_d;
+    int32_t* out_n;
+    int32_t* status;     // bit0 side overflow, bit1 expanded-set overflow
+    uint32_t* counters;  // [nq][2]: distance evaluations, expansions (nullable)
+};
+
+}  // namespace wv

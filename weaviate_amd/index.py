@@ -1,0 +1,217 @@
+"""Host-side mirror of the reference VectorIndex search interface.
+
+adapters/repos/db/vector_index.go:23-40 declares the interface; the hnsw
+package implements the search half in adapters/repos/db/vector/hnsw/search.go.
+`GPUVectorIndex` exposes the same operations with the same argument meaning
+and error behaviour (errors raise `WvError` where Go returns an error), backed
+by libwvgpu.so.  Every search runs on the GPU; there is no CPU path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Iterable, Optional
+
+import numpy as np
+
+from ._lib import MODE_AUTO, MODE_EXACT, MODE_HNSW, METRICS, WvConfig, WvError, check, lib
+
+_MODES = {"auto": MODE_AUTO, "exact": MODE_EXACT, "hnsw": MODE_HNSW}
+
+
+def _ptr(a):
+    return None if a is None else C.c_void_p(a.ctypes.data)
+
+
+class AllowList:
+    """helpers.AllowList (adapters/repos/db/helpers/allow_list.go:19-118) as a
+    dense bitmap over docIDs: Insert / Contains / Len / ascending Iterator."""
+
+    def __init__(self, *ids: int, nbits: int = 0):
+        self.nbits = max(nbits, (max(ids) + 1) if ids else 0)
+        self.words = np.zeros((self.nbits + 63) // 64, dtype=np.uint64)
+        if ids:
+            self.insert(*ids)
+
+    @classmethod
+    def from_ids(cls, ids: Iterable[int], nbits: int) -> "AllowList":
+        al = cls(nbits=nbits)
+        ids = np.asarray(list(ids) if not isinstance(ids, np.ndarray) else ids, dtype=np.uint64)
+        al.insert_array(ids)
+        return al
+
+    def _grow(self, nbits):
+        if nbits > self.nbits:
+            w = np.zeros((nbits + 63) // 64, dtype=np.uint64)
+            w[: self.words.size] = self.words
+            self.words, self.nbits = w, nbits
+
+    def insert_array(self, ids: np.ndarray):
+        if ids.size == 0:
+            return
+        self._grow(int(ids.max()) + 1)
+        np.bitwise_or.at(self.words, (ids >> np.uint64(6)).astype(np.int64), np.uint64(1) << (ids & np.uint64(63)))
+
+    def insert(self, *ids: int):
+        self.insert_array(np.asarray(ids, dtype=np.uint64))
+
+    def contains(self, id_: int) -> bool:
+        return id_ < self.nbits and bool((int(self.words[id_ >> 6]) >> (id_ & 63)) & 1)
+
+    def __len__(self):
+        return int(sum(bin(int(w)).count("1") for w in self.words)) if self.words.size < 4096 else int(
+            np.unpackbits(self.words.view(np.uint8)).sum())
+
+    def iterator(self):
+        for wi, w in enumerate(self.words.tolist()):
+            while w:
+                b = (w & -w).bit_length() - 1
+                yield wi * 64 + b
+                w &= w - 1
+
+
+class GPUVectorIndex:
+    """The GPU mirror of one shard's `hnsw` index (search side)."""
+
+    def __init__(self, dim: int, distance: str = "cosine-dot", capacity: int = 1 << 20, *, device: int = 0,
+                 max_connections: int = 64, ef: int = -1, dynamic_ef_min: int = 100, dynamic_ef_max: int = 500,
+                 dynamic_ef_factor: int = 8, flat_search_cutoff: int = 40000, forbid_flat: bool = False,
+                 id_base: int = 0):
+        if distance not in METRICS:
+            raise WvError(1, f"unsupported distance {distance!r} (l2-squared, dot, cosine-dot)")
+        self.dim, self.distance, self.capacity = dim, distance, capacity
+        self.cfg = WvConfig()
+        lib().wv_config_default(C.byref(self.cfg))
+        self.cfg.device, self.cfg.max_connections = device, max_connections
+        self.cfg.ef, self.cfg.dynamic_ef_min, self.cfg.dynamic_ef_max = ef, dynamic_ef_min, dynamic_ef_max
+        self.cfg.dynamic_ef_factor, self.cfg.flat_search_cutoff = dynamic_ef_factor, flat_search_cutoff
+        self.cfg.forbid_flat, self.cfg.id_base = int(forbid_flat), id_base
+        h = C.c_void_p()
+        check(lib().wv_index_create(dim, METRICS[distance], C.byref(self.cfg), capacity, C.byref(h)))
+        self._h = h
+
+    # -- lifecycle -----------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().wv_index_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def update_user_config(self, **kw):
+        """UpdateUserConfig (config_update.go:79-128): ef / dynamic ef / cutoff."""
+        for k, v in kw.items():
+            setattr(self.cfg, k, int(v))
+        check(lib().wv_index_update_config(self._h, C.byref(self.cfg)))
+
+    # -- state upload ----------------------------------------------------------
+    def upload_vectors(self, rows: np.ndarray, first_id: int = 0):
+        rows = np.ascontiguousarray(rows, dtype=np.float32)
+        if rows.ndim != 2 or rows.shape[1] != self.dim:
+            raise WvError(1, f"vector lengths don't match: {rows.shape[-1]} vs {self.dim}")
+        check(lib().wv_index_upload_vectors(self._h, _ptr(rows), rows.shape[0], first_id))
+
+    def upload_vectors_device(self, ptr: int, n: int, first_id: int = 0, ld: Optional[int] = None):
+        check(lib().wv_index_upload_vectors_device(self._h, C.c_void_p(ptr), n, first_id, ld or self.dim))
+
+    def upload_graph(self, g: dict):
+        """g: the fixed-degree CSR of oracle.pyoracle.Index.export_graph()."""
+        levels = np.ascontiguousarray(g["levels"], dtype=np.int8)
+        layer0 = np.ascontiguousarray(g["layer0"], dtype=np.uint32)
+        upper_row = np.ascontiguousarray(g["upper_row"], dtype=np.uint32)
+        upper = np.ascontiguousarray(g["upper"], dtype=np.uint32)
+        check(lib().wv_index_upload_graph(self._h, g["n"], _ptr(levels), _ptr(layer0), layer0.shape[1],
+                                          _ptr(upper_row), _ptr(upper), upper.shape[0], upper.shape[2],
+                                          g["max_level"], g["entrypoint"]))
+
+    def set_tombstones(self, ids: Iterable[int]):
+        al = AllowList.from_ids(ids, self.capacity)
+        check(lib().wv_index_set_tombstones(self._h, _ptr(al.words), al.nbits))
+
+    def search_time_ef(self, k: int) -> int:
+        return lib().wv_search_time_ef(self._h, k)
+
+    # -- search ----------------------------------------------------------------
+    @staticmethod
+    def _allow_args(allow):
+        if allow is None:
+            return None, 0, 0
+        if isinstance(allow, AllowList):
+            return allow.words, allow.nbits, 0
+        if isinstance(allow, list) and allow and isinstance(allow[0], AllowList):
+            nb = max(a.nbits for a in allow)
+            stride = (nb + 63) // 64
+            m = np.zeros((len(allow), stride), dtype=np.uint64)
+            for i, a in enumerate(allow):
+                m[i, : a.words.size] = a.words
+            return m, nb, stride
+        raise WvError(1, "allow must be an AllowList or a list of AllowList (one per query)")
+
+    def search_by_vector(self, vector, k: int, allow: Optional[AllowList] = None):
+        """SearchByVector (search.go:64-79) -> (ids uint64[n], dists float32[n])."""
+        q = np.ascontiguousarray(vector, dtype=np.float32)
+        if q.size != self.dim:
+            raise WvError(1, f"vector lengths don't match: {q.size} vs {self.dim}")
+        bits, nb, _ = self._allow_args(allow)
+        ids = np.zeros(k, np.uint64)
+        ds = np.zeros(k, np.float32)
+        n = np.zeros(1, np.int32)
+        check(lib().wv_search_by_vector(self._h, _ptr(q), k, _ptr(bits), nb, _ptr(ids), _ptr(ds), _ptr(n)))
+        return ids[: n[0]], ds[: n[0]]
+
+    def search_by_vector_distance(self, vector, target_distance: float, max_limit: int = -1,
+                                  allow: Optional[AllowList] = None, cap: int = 1 << 20):
+        """SearchByVectorDistance (search.go:90-158)."""
+        q = np.ascontiguousarray(vector, dtype=np.float32)
+        bits, nb, _ = self._allow_args(allow)
+        ids = np.zeros(cap, np.uint64)
+        ds = np.zeros(cap, np.float32)
+        n = C.c_int64(0)
+        check(lib().wv_search_by_vector_distance(self._h, _ptr(q), float(target_distance), max_limit, _ptr(bits), nb,
+                                                 _ptr(ids), _ptr(ds), cap, C.byref(n)))
+        m = min(n.value, cap)
+        return ids[:m], ds[:m]
+
+    def search_batch(self, queries, k: int, ef: int = 0, allow=None, mode: str = "auto"):
+        """Batched search: (ids [nq,k] uint64, dists [nq,k] f32, n [nq] i32)."""
+        qs = np.ascontiguousarray(queries, dtype=np.float32).reshape(-1, self.dim)
+        nq = qs.shape[0]
+        bits, nb, stride = self._allow_args(allow)
+        ids = np.zeros((nq, k), np.uint64)
+        ds = np.zeros((nq, k), np.float32)
+        n = np.zeros(nq, np.int32)
+        check(lib().wv_search_batch(self._h, _ptr(qs), nq, k, ef, _ptr(bits), nb, stride, _MODES[mode], _ptr(ids),
+                                    _ptr(ds), _ptr(n)))
+        return ids, ds, n
+
+    def search_batch_device(self, q_ptr: int, nq: int, k: int, out_ids_ptr: int, out_d_ptr: int, out_n_ptr: int,
+                            ef: int = 0, allow_ptr: int = 0, allow_nbits: int = 0, allow_stride: int = 0,
+                            mode: str = "exact", stream: int = 0):
+        """Device-resident batch (pointers from torch tensors on this device)."""
+        check(lib().wv_search_batch_device(self._h, C.c_void_p(q_ptr), nq, k, ef,
+                                           C.c_void_p(allow_ptr) if allow_ptr else None, allow_nbits, allow_stride,
+                                           _MODES[mode], C.c_void_p(out_ids_ptr), C.c_void_p(out_d_ptr),
+                                           C.c_void_p(out_n_ptr), C.c_void_p(stream) if stream else None))
+
+    def set_timing(self, enable: bool = True):
+        check(lib().wv_index_set_timing(self._h, int(enable)))
+
+    def last_kernel_times(self):
+        a, b, c = C.c_float(), C.c_float(), C.c_float()
+        check(lib().wv_last_kernel_times(self._h, C.byref(a), C.byref(b), C.byref(c)))
+        return {"bf_mfma_ms": a.value, "bf_finalize_ms": b.value, "hnsw_ms": c.value}
+
+    def last_batch_stats(self):
+        a, b, c = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        check(lib().wv_last_batch_stats(self._h, C.byref(a), C.byref(b), C.byref(c)))
+        return {"dist_evals": a.value, "expansions": b.value, "fallbacks": c.value}
+
+
+def merge_shards_device(in_d_ptr, in_ids_ptr, in_n_ptr, n_shards, nq, k, out_d_ptr, out_ids_ptr, out_n_ptr, stream=0):
+    """Merge per-shard (dist, id) lists on the device (after the RCCL all-gather)."""
+    check(lib().wv_merge_shards_device(C.c_void_p(in_d_ptr), C.c_void_p(in_ids_ptr), C.c_void_p(in_n_ptr), n_shards,
+                                       nq, k, C.c_void_p(out_d_ptr), C.c_void_p(out_ids_ptr), C.c_void_p(out_n_ptr),
+                                       C.c_void_p(stream) if stream else None))
