@@ -43,10 +43,17 @@ __device__ __forceinline__ void list_insert(float (&ld)[BF_KP], uint32_t (&li)[B
     }
 }
 
-__global__ __launch_bounds__(256, 1) void wv_bf_mfma_kernel(BfParams p) {
+// LDS: two stages of {base tile [128][LDT], query tile [128][LDT]} plus the
+// |x|^2 of the tile's rows (two tile parities).  Rows are k-contiguous; the
+// MFMA k order is permuted so each lane streams 16 consecutive k of its row
+// with ds_read_b128 (lane half h takes k = 16h .. 16h+15 of the chunk; A and
+// B use the same permutation, so the dot products are unchanged).
+constexpr int BF_STAGE = 2 * BF_BQ * BF_LDT;     // floats per stage (A + B)
+constexpr size_t BF_LDS_BYTES = (2 * BF_STAGE + 2 * BF_BN) * sizeof(float);
+
+__global__ __launch_bounds__(256, 2) void wv_bf_mfma_kernel(BfParams p) {
     extern __shared__ float lds[];
-    float* As = lds;                          // [2][BK][LD]  base tile, k-major
-    float* Bs = lds + 2 * BF_BK * BF_LD;      // [2][BK][LD]  query tile, k-major
+    float* xnb = lds + 2 * BF_STAGE;          // [2][BN] |x|^2 per tile parity
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -61,8 +68,10 @@ __global__ __launch_bounds__(256, 1) void wv_bf_mfma_kernel(BfParams p) {
     uint64_t t_end = t_begin + p.tiles_per_split;
     if (t_end > ntiles_total) t_end = ntiles_total;
     const int nk = (p.D + BF_BK - 1) / BF_BK;
+    const int khalf = lane >> 5;
+    const int l31 = lane & 31;
 
-    // per-lane candidate lists for the two query columns this lane owns
+    // per-lane candidate lists (sorted, BF_KP entries) for its two query columns
     float l0d[BF_KP], l1d[BF_KP];
     uint32_t l0i[BF_KP], l1i[BF_KP];
 #pragma unroll
@@ -70,17 +79,12 @@ __global__ __launch_bounds__(256, 1) void wv_bf_mfma_kernel(BfParams p) {
         l0d[i] = FLT_MAX; l1d[i] = FLT_MAX;
         l0i[i] = WV_NIL; l1i[i] = WV_NIL;
     }
+    floatx16 acc00, acc01, acc10, acc11;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { acc00[r] = 0.f; acc01[r] = 0.f; acc10[r] = 0.f; acc11[r] = 0.f; }
 
-    floatx16 acc[2][2];
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int b = 0; b < 2; ++b)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
-
-    // global -> register staging: 4 float4 of the base tile and 4 of the query tile
     float4 ra[4], rb[4];
+    float rxn = 0.f;
     const int total = (int)((t_end > t_begin ? t_end - t_begin : 0) * nk);
 
     auto load_chunk = [&](int c) {
@@ -100,23 +104,21 @@ __global__ __launch_bounds__(256, 1) void wv_bf_mfma_kernel(BfParams p) {
             if (qr < p.nq && k < p.D) w = ld4(p.Q + (uint64_t)qr * p.ldq + k);
             rb[it] = w;
         }
+        if (kc == 0 && tid < BF_BN) {
+            const uint64_t xr = tile * BF_BN + tid;
+            rxn = (p.metric == WV_METRIC_L2 && xr < p.N) ? p.xnorm[xr] : 0.f;
+        }
     };
-    auto store_chunk = [&](int buf) {
-        float* a = As + buf * BF_BK * BF_LD;
-        float* b = Bs + buf * BF_BK * BF_LD;
+    auto store_chunk = [&](int c) {
+        float* st = lds + (c & 1) * BF_STAGE;
 #pragma unroll
         for (int it = 0; it < 4; ++it) {
             const int e = tid + 256 * it;
             const int row = e >> 3, f4 = e & 7;
-            a[(4 * f4 + 0) * BF_LD + row] = ra[it].x;
-            a[(4 * f4 + 1) * BF_LD + row] = ra[it].y;
-            a[(4 * f4 + 2) * BF_LD + row] = ra[it].z;
-            a[(4 * f4 + 3) * BF_LD + row] = ra[it].w;
-            b[(4 * f4 + 0) * BF_LD + row] = rb[it].x;
-            b[(4 * f4 + 1) * BF_LD + row] = rb[it].y;
-            b[(4 * f4 + 2) * BF_LD + row] = rb[it].z;
-            b[(4 * f4 + 3) * BF_LD + row] = rb[it].w;
+            *reinterpret_cast<float4*>(st + row * BF_LDT + 4 * f4) = ra[it];
+            *reinterpret_cast<float4*>(st + BF_BQ * BF_LDT + row * BF_LDT + 4 * f4) = rb[it];
         }
+        if ((c % nk) == 0 && tid < BF_BN) xnb[((c / nk) & 1) * BF_BN + tid] = rxn;
     };
 
     if (total > 0) {
@@ -125,65 +127,78 @@ __global__ __launch_bounds__(256, 1) void wv_bf_mfma_kernel(BfParams p) {
     }
     __syncthreads();
 
-    const int khalf = lane >> 5;
-    const int l31 = lane & 31;
+    const int arow = (wm * 64 + l31) * BF_LDT + 16 * khalf;
+    const int brow = BF_BQ * BF_LDT + (wn * 64 + l31) * BF_LDT + 16 * khalf;
     for (int c = 0; c < total; ++c) {
         if (c + 1 < total) load_chunk(c + 1);
-        const float* a = As + (c & 1) * BF_BK * BF_LD;
-        const float* b = Bs + (c & 1) * BF_BK * BF_LD;
-#pragma unroll 4
-        for (int ks = 0; ks < BF_BK / 2; ++ks) {
-            const int kr = (2 * ks + khalf) * BF_LD;
-            const float a0 = a[kr + wm * 64 + l31];
-            const float a1 = a[kr + wm * 64 + 32 + l31];
-            const float b0 = b[kr + wn * 64 + l31];
-            const float b1 = b[kr + wn * 64 + 32 + l31];
-            acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-            acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-            acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-            acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+        const float* st = lds + (c & 1) * BF_STAGE;
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+            const float4 a0 = *reinterpret_cast<const float4*>(st + arow + 4 * s4);
+            const float4 a1 = *reinterpret_cast<const float4*>(st + arow + 32 * BF_LDT + 4 * s4);
+            const float4 b0 = *reinterpret_cast<const float4*>(st + brow + 4 * s4);
+            const float4 b1 = *reinterpret_cast<const float4*>(st + brow + 32 * BF_LDT + 4 * s4);
+#define WV_MF(C) \
+    acc00 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.C, b0.C, acc00, 0, 0, 0); \
+    acc01 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.C, b1.C, acc01, 0, 0, 0); \
+    acc10 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.C, b0.C, acc10, 0, 0, 0); \
+    acc11 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.C, b1.C, acc11, 0, 0, 0);
+            WV_MF(x) WV_MF(y) WV_MF(z) WV_MF(w)
+#undef WV_MF
         }
         if ((c % nk) == nk - 1) {
             // ---- epilogue of one 128x128 tile ----
             const uint64_t tile = t_begin + (uint64_t)(c / nk);
-            const int jq0 = q0 + wn * 64 + l31;        // query of list 0
-            const int jq1 = jq0 + 32;                  // query of list 1
-            const uint64_t* al0 = p.allow ? p.allow + (p.allow_stride ? (uint64_t)min(jq0, p.nq - 1) * p.allow_stride : 0) : nullptr;
-            const uint64_t* al1 = p.allow ? p.allow + (p.allow_stride ? (uint64_t)min(jq1, p.nq - 1) * p.allow_stride : 0) : nullptr;
+            const uint64_t row0 = tile * BF_BN + wm * 64;     // this wave's 64 base rows
+            const uint64_t word = row0 >> 6;                  // their bitmap word
+            // eligibility of the 64 rows: not excluded, < N, allowed (shared list)
+            uint64_t ok_bits = ~0ull;
+            if (row0 + 64 > p.N) ok_bits = p.N > row0 ? ((1ull << (p.N - row0)) - 1) : 0ull;
+            if (p.tomb && word < (p.tomb_nbits + 63) / 64) ok_bits &= ~p.tomb[word];
+            uint64_t ok0 = ok_bits, ok1 = ok_bits;
+            const int jq0 = q0 + wn * 64 + l31;
+            const int jq1 = jq0 + 32;
+            if (p.allow) {
+                const uint64_t aw = (p.allow_nbits + 63) / 64;
+                if (p.allow_stride) {
+                    ok0 &= (jq0 < p.nq && word < aw) ? p.allow[(uint64_t)jq0 * p.allow_stride + word] : 0ull;
+                    ok1 &= (jq1 < p.nq && word < aw) ? p.allow[(uint64_t)jq1 * p.allow_stride + word] : 0ull;
+                } else {
+                    const uint64_t a = word < aw ? p.allow[word] : 0ull;
+                    ok0 &= a;
+                    ok1 &= a;
+                }
+            }
+            if (jq0 >= p.nq) ok0 = 0;
+            if (jq1 >= p.nq) ok1 = 0;
+            const float* xn = xnb + ((c / nk) & 1) * BF_BN + wm * 64;   // parity of store_chunk
 #pragma unroll
             for (int rbk = 0; rbk < 2; ++rbk) {
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int i = wm * 64 + rbk * 32 + (r & 3) + 8 * (r >> 2) + 4 * khalf;
-                    const uint64_t xid = tile * BF_BN + i;
-                    bool ok = xid < p.N;
-                    if (ok && p.tomb) ok = !bit_test(p.tomb, p.tomb_nbits, xid);
-                    float xn = 0.f;
-                    if (p.metric == WV_METRIC_L2 && ok) xn = p.xnorm[xid];
-                    const float d0 = p.metric == WV_METRIC_L2 ? __builtin_fmaf(-2.f, acc[rbk][0][r], xn) : -acc[rbk][0][r];
-                    const float d1 = p.metric == WV_METRIC_L2 ? __builtin_fmaf(-2.f, acc[rbk][1][r], xn) : -acc[rbk][1][r];
-                    bool ok0 = ok && jq0 < p.nq, ok1 = ok && jq1 < p.nq;
-                    if (al0 && ok0) ok0 = bit_test(al0, p.allow_nbits, xid);
-                    if (al1 && ok1) ok1 = bit_test(al1, p.allow_nbits, xid);
-                    const uint32_t id32 = (uint32_t)xid;
-                    const bool in0 = ok0 && key_less(d0, id32, l0d[BF_KP - 1], l0i[BF_KP - 1]);
-                    const bool in1 = ok1 && key_less(d1, id32, l1d[BF_KP - 1], l1i[BF_KP - 1]);
-                    if (__any(in0)) {
+                for (int g4 = 0; g4 < 4; ++g4) {
+                    const int ib = rbk * 32 + 8 * g4 + 4 * khalf;   // row within the wave's 64
+                    const float4 x4 = *reinterpret_cast<const float4*>(xn + ib);
+                    const float xs[4] = {x4.x, x4.y, x4.z, x4.w};
+#pragma unroll
+                    for (int r3 = 0; r3 < 4; ++r3) {
+                        const int r = 4 * g4 + r3;
+                        const int ir = ib + r3;
+                        const uint32_t id32 = (uint32_t)(row0 + ir);
+                        const float v0 = rbk ? acc10[r] : acc00[r];
+                        const float v1 = rbk ? acc11[r] : acc01[r];
+                        const float d0 = p.metric == WV_METRIC_L2 ? __builtin_fmaf(-2.f, v0, xs[r3]) : -v0;
+                        const float d1 = p.metric == WV_METRIC_L2 ? __builtin_fmaf(-2.f, v1, xs[r3]) : -v1;
+                        const bool in0 = ((ok0 >> ir) & 1ull) && key_less(d0, id32, l0d[BF_KP - 1], l0i[BF_KP - 1]);
+                        const bool in1 = ((ok1 >> ir) & 1ull) && key_less(d1, id32, l1d[BF_KP - 1], l1i[BF_KP - 1]);
                         if (in0) list_insert(l0d, l0i, d0, id32);
-                    }
-                    if (__any(in1)) {
                         if (in1) list_insert(l1d, l1i, d1, id32);
                     }
                 }
             }
 #pragma unroll
-            for (int a2 = 0; a2 < 2; ++a2)
-#pragma unroll
-                for (int b2 = 0; b2 < 2; ++b2)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) acc[a2][b2][r] = 0.f;
+            for (int r = 0; r < 16; ++r) { acc00[r] = 0.f; acc01[r] = 0.f; acc10[r] = 0.f; acc11[r] = 0.f; }
         }
-        if (c + 1 < total) store_chunk((c + 1) & 1);
+        if (c + 1 < total) store_chunk(c + 1);
         __syncthreads();
     }
 
@@ -450,7 +465,7 @@ __global__ void wv_qnorm_kernel(const float* Q, int nq, int D, int ldq, int metr
 extern "C" {
 
 hipError_t wv_launch_bf_mfma(const wv::BfParams* p, hipStream_t s) {
-    const size_t lds = 4 * wv::BF_BK * wv::BF_LD * sizeof(float);
+    const size_t lds = wv::BF_LDS_BYTES;
     hipLaunchKernelGGL(wv::wv_bf_mfma_kernel, dim3(p->n_qblocks * p->n_splits), dim3(256), lds, s, *p);
     return hipGetLastError();
 }
