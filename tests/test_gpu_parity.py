@@ -82,6 +82,27 @@ def test_bruteforce_mfma_ids_identical(metric):
     ix.close()
 
 
+def test_bruteforce_integer_data_with_ties_uses_exact_fallback():
+    """SIFT-shaped integer data (many equal distances): the certificate cannot
+    separate ties at the boundary, so the batched exact fallback answers; the
+    result must equal the restatement up to the order among equal distances."""
+    rng = np.random.default_rng(21)
+    base = rng.integers(0, 3, (20000, 16)).astype(np.float32)
+    qs = rng.integers(0, 3, (200, 16)).astype(np.float32)
+    ix = W.GPUVectorIndex(16, "l2-squared", capacity=20000)
+    ix.upload_vectors(base)
+    ids, ds, n = ix.search_batch(qs, 10, mode="exact")
+    oi, od, on = O.flat_scan(O.L2, base, qs, 10)
+    assert ix.last_batch_stats()["fallbacks"] > 0
+    for i in range(len(qs)):
+        _same_tie_aware(ids[i], ds[i], oi[i], od[i])
+        # (dist, id) order: among equal distances the smallest ids win
+        full = ((base.astype(np.float64) - qs[i].astype(np.float64)) ** 2).sum(1)
+        order = np.lexsort((np.arange(len(base)), full))[:10]
+        assert ids[i].tolist() == order.tolist()
+    ix.close()
+
+
 def test_bruteforce_ragged_sizes_and_small_batches():
     for n_base, nq, k in [(1, 1, 10), (5, 3, 10), (129, 1, 1), (1000, 7, 32), (3001, 129, 10)]:
         base, qs = _data(n_base, 96, nq, seed=n_base)

@@ -1,0 +1,40 @@
+// Standalone timing harness for wv_bf_mfma_kernel variants (tools/bf_ablate.sh).
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include "../weaviate_amd/csrc/wv_params.h"
+extern "C" hipError_t wv_launch_bf_mfma(const wv::BfParams* p, hipStream_t s);
+int main(int argc, char** argv) {
+    const uint64_t N = argc > 1 ? atoll(argv[1]) : 1000000;
+    const int nq = argc > 2 ? atoi(argv[2]) : 10000, D = 128;
+    std::vector<float> hx(N * D), hq((size_t)nq * D), hn(N);
+    srand(1);
+    for (auto& v : hx) v = rand() / (float)RAND_MAX;
+    for (auto& v : hq) v = -2.f * rand() / (float)RAND_MAX;  // pre-scaled B operand (-2q)
+    for (uint64_t i = 0; i < N; ++i) { float s = 0; for (int k = 0; k < D; ++k) s += hx[i * D + k] * hx[i * D + k]; hn[i] = s; }
+    float *X, *Q, *xn, *od; uint32_t* oi;
+    hipMalloc(&X, N * D * 4); hipMalloc(&Q, (size_t)nq * D * 4); hipMalloc(&xn, N * 4);
+    hipMemcpy(X, hx.data(), N * D * 4, hipMemcpyHostToDevice);
+    hipMemcpy(Q, hq.data(), (size_t)nq * D * 4, hipMemcpyHostToDevice);
+    hipMemcpy(xn, hn.data(), N * 4, hipMemcpyHostToDevice);
+    wv::BfParams p{};
+    const int nqb = (nq + 127) / 128;
+    const uint64_t ntiles = (N + 127) / 128;
+    int ns = std::max(1, (1024 + nqb - 1) / nqb);
+    const int tps = (int)((ntiles + ns - 1) / ns);
+    ns = (int)((ntiles + tps - 1) / tps);
+    hipMalloc(&od, (size_t)nq * ns * 4 * wv::BF_KP * 4); hipMalloc(&oi, (size_t)nq * ns * 4 * wv::BF_KP * 4);
+    p.X = X; p.Q = Q; p.xnorm = xn; p.N = N; p.nq = nq; p.D = D; p.ldx = D; p.ldq = D; p.metric = 0;
+    p.n_qblocks = nqb; p.n_splits = ns; p.tiles_per_split = tps; p.out_d = od; p.out_id = oi;
+    hipEvent_t a, b; hipEventCreate(&a); hipEventCreate(&b);
+    wv_launch_bf_mfma(&p, 0); hipDeviceSynchronize();
+    float best = 1e9;
+    for (int it = 0; it < 5; ++it) {
+        hipEventRecord(a, 0); wv_launch_bf_mfma(&p, 0); hipEventRecord(b, 0); hipEventSynchronize(b);
+        float ms; hipEventElapsedTime(&ms, a, b); if (ms < best) best = ms;
+    }
+    printf("%s N=%llu nq=%d: %.3f ms  %.1f TF/s  (%.1f%% of 157.3)\n", argc > 3 ? argv[3] : "variant",
+           (unsigned long long)N, nq, best, 2.0 * D * N * nq / best / 1e9, 100 * 2.0 * D * N * nq / best / 1e9 / 157.3);
+    return 0;
+}

@@ -25,9 +25,11 @@ extern "C" {
 hipError_t wv_launch_bf_mfma(const wv::BfParams* p, hipStream_t s);
 hipError_t wv_launch_bf_finalize(const wv::BfFinParams* p, hipStream_t s);
 hipError_t wv_launch_exact_scan(const wv::ScanParams* p, hipStream_t s);
+hipError_t wv_launch_fb(const wv::FbParams* p, hipStream_t s);
 hipError_t wv_launch_rownorm(const float* X, uint64_t N, int D, int ldx, float* norm2, unsigned int* maxbits,
                              hipStream_t s);
 hipError_t wv_launch_normalize(const float* in, float* out, uint64_t n, int D, int ld, hipStream_t s);
+hipError_t wv_launch_scale(const float* in, float* out, uint64_t n, float scale, hipStream_t s);
 hipError_t wv_launch_qnorm(const float* Q, int nq, int D, int ldq, int metric, float* out, hipStream_t s);
 hipError_t wv_launch_hnsw(const wv::HnswParams* p, int waves_per_block, hipStream_t s);
 int wv_hnsw_per_wave_words(int dpad, int efc, int sc, int vc_log2, int xs_log2);
@@ -194,10 +196,11 @@ struct wv_index {
     bool bitmaps_dirty = true;
     // scratch
     DevBuf stage;           // contiguous host->device staging
-    DevBuf q_in, q_norm, q_nrm2, cand_d, cand_id, fail, status, counters;
+    DevBuf q_in, q_norm, q_nrm2, q_scaled, cand_d, cand_id, fail, status, counters;
     DevBuf scan_d, scan_i, sort_d, sort_i, sort_tmp;
     DevBuf g_idx, g_q, g_allow, g_ids, g_d, g_n, g_cnt;
     DevBuf out_ids, out_d, out_n;
+    DevBuf fail_thr, fb_idx, fb_d, fb_i, fb_n, fb_of;
     // stats of the last batch
     uint64_t last_dist = 0, last_exp = 0, last_fallbacks = 0;
     // optional kernel timing (hipEvents on the launch stream)
@@ -308,9 +311,12 @@ int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
         HIP_TRY(ix->q_nrm2.ensure((size_t)nq * 4));
         HIP_TRY(ix->fail.ensure((size_t)nq * 4));
         HIP_TRY(wv_launch_qnorm(d_q, nq, ix->dim, ix->dpad, ix->metric, ix->q_nrm2.as<float>(), s));
+        HIP_TRY(ix->q_scaled.ensure((size_t)nq * ix->dpad * 4));
+        HIP_TRY(wv_launch_scale(d_q, ix->q_scaled.as<float>(), (uint64_t)nq * ix->dpad,
+                                ix->metric == WV_L2_SQUARED ? -2.f : -1.f, s));
         wv::BfParams bp{};
         bp.X = ix->vecs.as<float>();
-        bp.Q = d_q;
+        bp.Q = ix->q_scaled.as<float>();
         bp.xnorm = ix->xnorm.as<float>();
         bp.tomb = ix->excl.as<uint64_t>();
         bp.tomb_nbits = ix->capacity;
@@ -355,6 +361,8 @@ int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
         fp.out_d = d_out_d;
         fp.out_n = d_out_n;
         fp.fail = ix->fail.as<int32_t>();
+        HIP_TRY(ix->fail_thr.ensure((size_t)nq * 4));
+        fp.fail_thr = ix->fail_thr.as<float>();
         if (ix->timing) HIP_TRY(hipEventRecord(ix->ev[2], s));
         HIP_TRY(wv_launch_bf_finalize(&fp, s));
         if (ix->timing) HIP_TRY(hipEventRecord(ix->ev[3], s));
@@ -374,6 +382,52 @@ int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
         for (int i = 0; i < nq; ++i) fails.push_back(i);
     }
     ix->last_fallbacks += fails.size();
+    if (!fails.empty() && k <= wv::BF_FAST_KMAX) {
+        // batched threshold filter over the corpus for every failed query
+        std::vector<int32_t> rest;
+        for (size_t b0 = 0; b0 < fails.size(); b0 += 256) {
+            const int nf = (int)std::min<size_t>(256, fails.size() - b0);
+            HIP_TRY(ix->fb_idx.ensure((size_t)nf * 4));
+            HIP_TRY(ix->fb_d.ensure((size_t)nf * wv::FB_CAP * 4));
+            HIP_TRY(ix->fb_i.ensure((size_t)nf * wv::FB_CAP * 4));
+            HIP_TRY(ix->fb_n.ensure((size_t)nf * 4));
+            HIP_TRY(ix->fb_of.ensure((size_t)nf * 4));
+            HIP_TRY(hipMemcpyAsync(ix->fb_idx.p, fails.data() + b0, 4 * (size_t)nf, hipMemcpyHostToDevice, s));
+            HIP_TRY(hipMemsetAsync(ix->fb_n.p, 0, 4 * (size_t)nf, s));
+            wv::FbParams bp{};
+            bp.X = ix->vecs.as<float>();
+            bp.Q = d_q;
+            bp.qidx = ix->fb_idx.as<int32_t>();
+            bp.thr = ix->fail_thr.as<float>();
+            bp.tomb = ix->excl.as<uint64_t>();
+            bp.tomb_nbits = ix->capacity;
+            bp.allow = d_allow;
+            bp.allow_nbits = allow_nbits;
+            bp.allow_stride = allow_stride;
+            bp.N = N;
+            bp.nf = nf;
+            bp.D = ix->dim;
+            bp.ldx = ix->dpad;
+            bp.ldq = ix->dpad;
+            bp.metric = ix->metric;
+            bp.k = k;
+            bp.id_base = ix->cfg.id_base;
+            bp.cand_d = ix->fb_d.as<float>();
+            bp.cand_id = ix->fb_i.as<uint32_t>();
+            bp.cand_n = ix->fb_n.as<uint32_t>();
+            bp.out_ids = d_out_ids;
+            bp.out_d = d_out_d;
+            bp.out_n = d_out_n;
+            bp.overflow = ix->fb_of.as<int32_t>();
+            HIP_TRY(wv_launch_fb(&bp, s));
+            std::vector<int32_t> of(nf);
+            HIP_TRY(hipMemcpyAsync(of.data(), ix->fb_of.p, 4 * (size_t)nf, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipStreamSynchronize(s));
+            for (int i = 0; i < nf; ++i)
+                if (of[i]) rest.push_back(fails[b0 + i]);
+        }
+        fails.swap(rest);   // survivors overflowed: full scan + sort below
+    }
     for (int q : fails) {
         const uint64_t* al = d_allow ? d_allow + (allow_stride ? (uint64_t)q * allow_stride : 0) : nullptr;
         int rc = exact_full(ix, d_q + (size_t)q * ix->dpad, k, al, allow_nbits, d_out_ids + (size_t)q * k,
@@ -627,10 +681,10 @@ int wv_index_destroy(wv_index* ix) {
     if (!ix) return WV_OK;
     (void)hipSetDevice(ix->cfg.device);
     for (DevBuf* b : {&ix->vecs, &ix->xnorm, &ix->maxnorm, &ix->levels, &ix->layer0, &ix->upper_row, &ix->upper,
-                      &ix->tomb, &ix->excl, &ix->q_in, &ix->q_norm, &ix->q_nrm2, &ix->cand_d, &ix->cand_id,
+                      &ix->tomb, &ix->excl, &ix->q_in, &ix->q_norm, &ix->q_nrm2, &ix->q_scaled, &ix->cand_d, &ix->cand_id,
                       &ix->fail, &ix->status, &ix->counters, &ix->scan_d, &ix->scan_i, &ix->sort_d, &ix->sort_i,
                       &ix->sort_tmp, &ix->g_idx, &ix->g_q, &ix->g_allow, &ix->g_ids, &ix->g_d, &ix->g_n, &ix->g_cnt,
-                      &ix->out_ids, &ix->out_d, &ix->out_n, &ix->stage})
+                      &ix->out_ids, &ix->out_d, &ix->out_n, &ix->stage, &ix->fail_thr, &ix->fb_idx, &ix->fb_d, &ix->fb_i, &ix->fb_n, &ix->fb_of})
         b->release();
     for (auto& e : ix->ev)
         if (e) (void)hipEventDestroy(e);

@@ -48,10 +48,13 @@ __device__ __forceinline__ void list_insert(float (&ld)[BF_KP], uint32_t (&li)[B
 // MFMA k order is permuted so each lane streams 16 consecutive k of its row
 // with ds_read_b128 (lane half h takes k = 16h .. 16h+15 of the chunk; A and
 // B use the same permutation, so the dot products are unchanged).
+#ifndef WV_BF_WAVES_PER_SIMD
+#define WV_BF_WAVES_PER_SIMD 2
+#endif
 constexpr int BF_STAGE = 2 * BF_BQ * BF_LDT;     // floats per stage (A + B)
 constexpr size_t BF_LDS_BYTES = (2 * BF_STAGE + 2 * BF_BN) * sizeof(float);
 
-__global__ __launch_bounds__(256, 2) void wv_bf_mfma_kernel(BfParams p) {
+__global__ __launch_bounds__(256, WV_BF_WAVES_PER_SIMD) void wv_bf_mfma_kernel(BfParams p) {
     extern __shared__ float lds[];
     float* xnb = lds + 2 * BF_STAGE;          // [2][BN] |x|^2 per tile parity
 
@@ -79,15 +82,14 @@ __global__ __launch_bounds__(256, 2) void wv_bf_mfma_kernel(BfParams p) {
         l0d[i] = FLT_MAX; l1d[i] = FLT_MAX;
         l0i[i] = WV_NIL; l1i[i] = WV_NIL;
     }
-    floatx16 acc00, acc01, acc10, acc11;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) { acc00[r] = 0.f; acc01[r] = 0.f; acc10[r] = 0.f; acc11[r] = 0.f; }
-
     float4 ra[4], rb[4];
     float rxn = 0.f;
-    const int total = (int)((t_end > t_begin ? t_end - t_begin : 0) * nk);
+    const int total = (int)((t_end > t_begin ? t_end - t_begin : 0) * nk);   // chunks
 
     auto load_chunk = [&](int c) {
+#ifdef WV_BF_ABLATE_NO_LOADS
+        if (c > 1) return;
+#endif
         const uint64_t tile = t_begin + (uint64_t)(c / nk);
         const int kc = c % nk;
 #pragma unroll
@@ -129,77 +131,129 @@ __global__ __launch_bounds__(256, 2) void wv_bf_mfma_kernel(BfParams p) {
 
     const int arow = (wm * 64 + l31) * BF_LDT + 16 * khalf;
     const int brow = BF_BQ * BF_LDT + (wn * 64 + l31) * BF_LDT + 16 * khalf;
-    for (int c = 0; c < total; ++c) {
-        if (c + 1 < total) load_chunk(c + 1);
-        const float* st = lds + (c & 1) * BF_STAGE;
+    const int ntile = total / (nk > 0 ? nk : 1);
+    int c = 0;   // global chunk counter: stage c & 1 holds chunk c
+    for (int t = 0; t < ntile; ++t) {
+        const uint64_t tile = t_begin + (uint64_t)t;
+        // C-in of the tile = |x|^2 of the row (L2) or 0: with B = -2q (L2) or
+        // -q (dot, cosine) the accumulator ends as the approximate key
+        floatx16 acc00, acc01, acc10, acc11;
+        {
+            const float* xn = xnb + (t & 1) * BF_BN + wm * 64;
 #pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) {
-            const float4 a0 = *reinterpret_cast<const float4*>(st + arow + 4 * s4);
-            const float4 a1 = *reinterpret_cast<const float4*>(st + arow + 32 * BF_LDT + 4 * s4);
-            const float4 b0 = *reinterpret_cast<const float4*>(st + brow + 4 * s4);
-            const float4 b1 = *reinterpret_cast<const float4*>(st + brow + 32 * BF_LDT + 4 * s4);
+            for (int g4 = 0; g4 < 4; ++g4) {
+                float4 x0 = make_float4(0.f, 0.f, 0.f, 0.f), x1 = x0;
+                if (p.metric == WV_METRIC_L2) {
+                    x0 = *reinterpret_cast<const float4*>(xn + 8 * g4 + 4 * khalf);
+                    x1 = *reinterpret_cast<const float4*>(xn + 32 + 8 * g4 + 4 * khalf);
+                }
+                const float a0s[4] = {x0.x, x0.y, x0.z, x0.w}, a1s[4] = {x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+                for (int r3 = 0; r3 < 4; ++r3) {
+                    acc00[4 * g4 + r3] = a0s[r3]; acc01[4 * g4 + r3] = a0s[r3];
+                    acc10[4 * g4 + r3] = a1s[r3]; acc11[4 * g4 + r3] = a1s[r3];
+                }
+            }
+        }
+        for (int kc = 0; kc < nk; ++kc, ++c) {
+            if (c + 1 < total) load_chunk(c + 1);
+            const float* st = lds + (c & 1) * BF_STAGE;
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4) {
+                const float4 a0 = *reinterpret_cast<const float4*>(st + arow + 4 * s4);
+                const float4 a1 = *reinterpret_cast<const float4*>(st + arow + 32 * BF_LDT + 4 * s4);
+                const float4 b0 = *reinterpret_cast<const float4*>(st + brow + 4 * s4);
+                const float4 b1 = *reinterpret_cast<const float4*>(st + brow + 32 * BF_LDT + 4 * s4);
 #define WV_MF(C) \
     acc00 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.C, b0.C, acc00, 0, 0, 0); \
     acc01 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.C, b1.C, acc01, 0, 0, 0); \
     acc10 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.C, b0.C, acc10, 0, 0, 0); \
     acc11 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.C, b1.C, acc11, 0, 0, 0);
-            WV_MF(x) WV_MF(y) WV_MF(z) WV_MF(w)
+                WV_MF(x) WV_MF(y) WV_MF(z) WV_MF(w)
 #undef WV_MF
-        }
-        if ((c % nk) == nk - 1) {
-            // ---- epilogue of one 128x128 tile ----
-            const uint64_t tile = t_begin + (uint64_t)(c / nk);
-            const uint64_t row0 = tile * BF_BN + wm * 64;     // this wave's 64 base rows
-            const uint64_t word = row0 >> 6;                  // their bitmap word
-            // eligibility of the 64 rows: not excluded, < N, allowed (shared list)
-            uint64_t ok_bits = ~0ull;
-            if (row0 + 64 > p.N) ok_bits = p.N > row0 ? ((1ull << (p.N - row0)) - 1) : 0ull;
-            if (p.tomb && word < (p.tomb_nbits + 63) / 64) ok_bits &= ~p.tomb[word];
-            uint64_t ok0 = ok_bits, ok1 = ok_bits;
-            const int jq0 = q0 + wn * 64 + l31;
-            const int jq1 = jq0 + 32;
-            if (p.allow) {
-                const uint64_t aw = (p.allow_nbits + 63) / 64;
-                if (p.allow_stride) {
-                    ok0 &= (jq0 < p.nq && word < aw) ? p.allow[(uint64_t)jq0 * p.allow_stride + word] : 0ull;
-                    ok1 &= (jq1 < p.nq && word < aw) ? p.allow[(uint64_t)jq1 * p.allow_stride + word] : 0ull;
-                } else {
-                    const uint64_t a = word < aw ? p.allow[word] : 0ull;
-                    ok0 &= a;
-                    ok1 &= a;
-                }
             }
-            if (jq0 >= p.nq) ok0 = 0;
-            if (jq1 >= p.nq) ok1 = 0;
-            const float* xn = xnb + ((c / nk) & 1) * BF_BN + wm * 64;   // parity of store_chunk
-#pragma unroll
-            for (int rbk = 0; rbk < 2; ++rbk) {
-#pragma unroll
-                for (int g4 = 0; g4 < 4; ++g4) {
-                    const int ib = rbk * 32 + 8 * g4 + 4 * khalf;   // row within the wave's 64
-                    const float4 x4 = *reinterpret_cast<const float4*>(xn + ib);
-                    const float xs[4] = {x4.x, x4.y, x4.z, x4.w};
-#pragma unroll
-                    for (int r3 = 0; r3 < 4; ++r3) {
-                        const int r = 4 * g4 + r3;
-                        const int ir = ib + r3;
-                        const uint32_t id32 = (uint32_t)(row0 + ir);
-                        const float v0 = rbk ? acc10[r] : acc00[r];
-                        const float v1 = rbk ? acc11[r] : acc01[r];
-                        const float d0 = p.metric == WV_METRIC_L2 ? __builtin_fmaf(-2.f, v0, xs[r3]) : -v0;
-                        const float d1 = p.metric == WV_METRIC_L2 ? __builtin_fmaf(-2.f, v1, xs[r3]) : -v1;
-                        const bool in0 = ((ok0 >> ir) & 1ull) && key_less(d0, id32, l0d[BF_KP - 1], l0i[BF_KP - 1]);
-                        const bool in1 = ((ok1 >> ir) & 1ull) && key_less(d1, id32, l1d[BF_KP - 1], l1i[BF_KP - 1]);
-                        if (in0) list_insert(l0d, l0i, d0, id32);
-                        if (in1) list_insert(l1d, l1i, d1, id32);
+            if (kc == nk - 1) {
+                // the stage of the last chunk is read by every wave before the
+                // next tile's first chunk overwrites the other stage below
+            }
+            if (c + 1 < total) store_chunk(c + 1);
+            __syncthreads();
+        }
+#ifdef WV_BF_ABLATE_NO_EPILOGUE
+        asm volatile("" ::"v"(acc00[0]), "v"(acc01[0]), "v"(acc10[0]), "v"(acc11[0]));
+        if (acc00[3] == 1234.5f) l0d[0] = acc01[5];
+        continue;
+#endif
+                    // ---- epilogue of one 128x128 tile ----
+                    const uint64_t row0 = tile * BF_BN + wm * 64;     // this wave's 64 base rows
+                    const uint64_t word = row0 >> 6;                  // their bitmap word
+                    // eligibility of the 64 rows: not excluded, < N, allowed (shared list)
+                    uint64_t ok_bits = ~0ull;
+                    if (row0 + 64 > p.N) ok_bits = p.N > row0 ? ((1ull << (p.N - row0)) - 1) : 0ull;
+                    if (p.tomb && word < (p.tomb_nbits + 63) / 64) ok_bits &= ~p.tomb[word];
+                    uint64_t ok0 = ok_bits, ok1 = ok_bits;
+                    const int jq0 = q0 + wn * 64 + l31;
+                    const int jq1 = jq0 + 32;
+                    if (p.allow) {
+                        const uint64_t aw = (p.allow_nbits + 63) / 64;
+                        if (p.allow_stride) {
+                            ok0 &= (jq0 < p.nq && word < aw) ? p.allow[(uint64_t)jq0 * p.allow_stride + word] : 0ull;
+                            ok1 &= (jq1 < p.nq && word < aw) ? p.allow[(uint64_t)jq1 * p.allow_stride + word] : 0ull;
+                        } else {
+                            const uint64_t a = word < aw ? p.allow[word] : 0ull;
+                            ok0 &= a;
+                            ok1 &= a;
+                        }
                     }
-                }
-            }
-#pragma unroll
-            for (int r = 0; r < 16; ++r) { acc00[r] = 0.f; acc01[r] = 0.f; acc10[r] = 0.f; acc11[r] = 0.f; }
-        }
-        if (c + 1 < total) store_chunk(c + 1);
-        __syncthreads();
+                    if (jq0 >= p.nq) ok0 = 0;
+                    if (jq1 >= p.nq) ok1 = 0;
+                    // pass 1: the accumulators already hold the approximate keys;
+                    // mask ineligible rows to +inf and take the per-query minimum.
+                    // Almost every tile stops here.
+                    const float INF = __builtin_inff();
+                    float m0 = INF, m1 = INF;
+                    if (__all(ok0 == ~0ull && ok1 == ~0ull)) {
+        #pragma unroll
+                        for (int r = 0; r < 16; ++r) {
+                            m0 = fminf(m0, fminf(acc00[r], acc10[r]));
+                            m1 = fminf(m1, fminf(acc01[r], acc11[r]));
+                        }
+                    } else {
+        #pragma unroll
+                        for (int r = 0; r < 16; ++r) {
+                            const int ir = (r & 3) + 8 * (r >> 2) + 4 * khalf;
+                            if (!((ok0 >> ir) & 1ull)) acc00[r] = INF;
+                            if (!((ok0 >> (ir + 32)) & 1ull)) acc10[r] = INF;
+                            if (!((ok1 >> ir) & 1ull)) acc01[r] = INF;
+                            if (!((ok1 >> (ir + 32)) & 1ull)) acc11[r] = INF;
+                            m0 = fminf(m0, fminf(acc00[r], acc10[r]));
+                            m1 = fminf(m1, fminf(acc01[r], acc11[r]));
+                        }
+                    }
+                    // pass 2 (rare after the first tiles): extract the minimum while it
+                    // beats the list tail; rows are scanned in ascending id, so among
+                    // equal keys the smallest id is taken first
+        #define WV_EXTRACT(M, A0, A1, LD, LI)                                                        \
+                    while (M <= LD[BF_KP - 1]) {                                                    \
+                        uint32_t idm = WV_NIL;                                                      \
+                        _Pragma("unroll") for (int r = 0; r < 16; ++r) {                            \
+                            const bool hit = idm == WV_NIL && A0[r] == M;                           \
+                            idm = hit ? (uint32_t)(row0 + (r & 3) + 8 * (r >> 2) + 4 * khalf) : idm;\
+                            A0[r] = hit ? INF : A0[r];                                              \
+                        }                                                                           \
+                        _Pragma("unroll") for (int r = 0; r < 16; ++r) {                            \
+                            const bool hit = idm == WV_NIL && A1[r] == M;                           \
+                            idm = hit ? (uint32_t)(row0 + 32 + (r & 3) + 8 * (r >> 2) + 4 * khalf) : idm; \
+                            A1[r] = hit ? INF : A1[r];                                              \
+                        }                                                                           \
+                        if (!key_less(M, idm, LD[BF_KP - 1], LI[BF_KP - 1])) break;                 \
+                        list_insert(LD, LI, M, idm);                                                \
+                        M = INF;                                                                    \
+                        _Pragma("unroll") for (int r = 0; r < 16; ++r) M = fminf(M, fminf(A0[r], A1[r])); \
+                    }
+                    WV_EXTRACT(m0, acc00, acc10, l0d, l0i)
+                    WV_EXTRACT(m1, acc01, acc11, l1d, l1i)
+        #undef WV_EXTRACT
     }
 
     // write this lane's two lists: out[q][split][producer][KP]
@@ -360,6 +414,9 @@ __device__ void finalize_one(const BfFinParams& p, int q, float* sd, uint32_t* s
     if (lane == 0) {
         p.out_n[q] = nk;
         p.fail[q] = certified ? 0 : 1;
+        // the re-ranked set holds nk real points with exact distance <= dk:
+        // dk bounds the true k-th distance from above (all when nvalid < k)
+        p.fail_thr[q] = nvalid < k ? __builtin_inff() : dk;
     }
 }
 
@@ -408,6 +465,87 @@ __global__ __launch_bounds__(256) void wv_exact_scan_kernel(ScanParams p) {
 }
 
 // ---------------------------------------------------------------------------
+// Certificate fallback, batched over failed queries (see FbParams).
+template <int METRIC>
+__device__ void fb_filter(const FbParams& p, const float* qv, int f) {
+    const int g = threadIdx.x & 7;
+    const uint64_t grp = (uint64_t)blockIdx.x * (blockDim.x >> 3) + (threadIdx.x >> 3);
+    const uint64_t stride = (uint64_t)gridDim.x * (blockDim.x >> 3);
+    const int q = p.qidx[f];
+    const float thr = p.thr[q];
+    const uint64_t* al = p.allow ? p.allow + (p.allow_stride ? (uint64_t)q * p.allow_stride : 0) : nullptr;
+    for (uint64_t r = grp; r < p.N; r += stride) {
+        const float d = exact_dist_group8<METRIC>(qv, p.X + r * p.ldx, p.D, g);
+        if (g == 0 && d <= thr) {
+            bool ok = true;
+            if (p.tomb) ok = !bit_test(p.tomb, p.tomb_nbits, r);
+            if (al && ok) ok = bit_test(al, p.allow_nbits, r);
+            if (ok) {
+                const uint32_t pos = atomicAdd(&p.cand_n[f], 1u);
+                if (pos < FB_CAP) {
+                    p.cand_d[(size_t)f * FB_CAP + pos] = d;
+                    p.cand_id[(size_t)f * FB_CAP + pos] = (uint32_t)r;
+                }
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void wv_fb_filter_kernel(FbParams p) {
+    extern __shared__ float qv[];
+    const int f = blockIdx.y;
+    const int dpad = (p.D + 3) & ~3;
+    for (int i = threadIdx.x; i < dpad; i += blockDim.x)
+        qv[i] = i < p.D ? p.Q[(size_t)p.qidx[f] * p.ldq + i] : 0.f;
+    __syncthreads();
+    if (p.metric == WV_METRIC_L2) fb_filter<WV_METRIC_L2>(p, qv, f);
+    else if (p.metric == WV_METRIC_DOT) fb_filter<WV_METRIC_DOT>(p, qv, f);
+    else fb_filter<WV_METRIC_COSINE>(p, qv, f);
+}
+
+// one workgroup per failed query: bitonic sort of the survivors by (d, id)
+__global__ __launch_bounds__(1024) void wv_fb_select_kernel(FbParams p) {
+    __shared__ float sd[FB_CAP];
+    __shared__ uint32_t si[FB_CAP];
+    const int f = blockIdx.x;
+    const uint32_t n_all = p.cand_n[f];
+    const int n = (int)(n_all < (uint32_t)FB_CAP ? n_all : (uint32_t)FB_CAP);
+    int len = 1;
+    while (len < n) len <<= 1;
+    for (int i = threadIdx.x; i < len; i += blockDim.x) {
+        sd[i] = i < n ? p.cand_d[(size_t)f * FB_CAP + i] : __builtin_inff();
+        si[i] = i < n ? p.cand_id[(size_t)f * FB_CAP + i] : WV_NIL;
+    }
+    __syncthreads();
+    for (int kk = 2; kk <= len; kk <<= 1) {
+        for (int j = kk >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < len; i += blockDim.x) {
+                const int o = i ^ j;
+                if (o > i) {
+                    const bool asc = (i & kk) == 0;
+                    const bool gt = key_less(sd[o], si[o], sd[i], si[i]);
+                    if (gt == asc) {
+                        const float td = sd[i]; sd[i] = sd[o]; sd[o] = td;
+                        const uint32_t ti = si[i]; si[i] = si[o]; si[o] = ti;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    const int q = p.qidx[f];
+    const int m = n < p.k ? n : p.k;
+    for (int i = threadIdx.x; i < m; i += blockDim.x) {
+        p.out_ids[(size_t)q * p.k + i] = p.id_base + si[i];
+        p.out_d[(size_t)q * p.k + i] = sd[i];
+    }
+    if (threadIdx.x == 0) {
+        p.out_n[q] = m;
+        p.overflow[f] = n_all > (uint32_t)FB_CAP ? 1 : 0;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // |x|^2 (fp32, any order: only feeds the approximate distance) and max |x|.
 __global__ void wv_rownorm_kernel(const float* X, uint64_t N, int D, int ldx, float* norm2,
                                   unsigned int* max_norm_bits) {
@@ -448,6 +586,12 @@ __global__ void wv_normalize_kernel(const float* in, float* out, uint64_t n, int
     for (int i = 0; i < D; ++i) o[i] = __fdiv_rn(v[i], nn);
 }
 
+// B operand of the MFMA pass: -2q (L2) or -q (dot, cosine); exact scalings
+__global__ void wv_scale_rows_kernel(const float* in, float* out, uint64_t n, float s) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = s * in[i];
+}
+
 // |q|^2 for L2, |q| for dot/cosine (feeds eps only)
 __global__ void wv_qnorm_kernel(const float* Q, int nq, int D, int ldq, int metric, float* out) {
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
@@ -476,6 +620,20 @@ hipError_t wv_launch_bf_finalize(const wv::BfFinParams* p, hipStream_t s) {
     return hipGetLastError();
 }
 
+hipError_t wv_launch_fb(const wv::FbParams* p, hipStream_t s) {
+    if (p->nf == 0) return hipSuccess;
+    uint64_t blocks = (p->N + 255) / 256;
+    const uint64_t cap = (uint64_t)(2048 / (p->nf > 0 ? p->nf : 1)) + 64;
+    if (blocks > cap) blocks = cap;
+    if (blocks == 0) blocks = 1;
+    const size_t lds = ((p->D + 3) & ~3) * sizeof(float);
+    hipLaunchKernelGGL(wv::wv_fb_filter_kernel, dim3((unsigned)blocks, p->nf), dim3(256), lds, s, *p);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(wv::wv_fb_select_kernel, dim3(p->nf), dim3(1024), 0, s, *p);
+    return hipGetLastError();
+}
+
 hipError_t wv_launch_exact_scan(const wv::ScanParams* p, hipStream_t s) {
     uint64_t blocks = (p->N + 31) / 32;
     if (blocks > 8192) blocks = 8192;
@@ -496,6 +654,13 @@ hipError_t wv_launch_normalize(const float* in, float* out, uint64_t n, int D, i
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(wv::wv_normalize_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, in, out, n, D,
                        ld);
+    return hipGetLastError();
+}
+
+hipError_t wv_launch_scale(const float* in, float* out, uint64_t n, float scale, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(wv::wv_scale_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, in, out, n,
+                       scale);
     return hipGetLastError();
 }
 

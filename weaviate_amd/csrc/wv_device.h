@@ -84,6 +84,95 @@ __device__ __forceinline__ float exact_dist_group8(const float* __restrict__ q,
     return 1.0f - r;
 }
 
+// Exact reference-order distances of up to 32 rows at once (4 per 8-lane
+// group), all row loads of a 4-block (128-float) slab issued before any FMA so
+// one memory round trip serves 32 rows.  ids/out live in LDS; rows >= n are
+// skipped.  Same arithmetic, in the same order, as exact_dist_group8.
+template <int METRIC>
+__device__ __forceinline__ void exact_dist_rows32(const float* __restrict__ q, const float* __restrict__ X,
+                                                  int ldx, int D, const uint32_t* ids, int n, float* out,
+                                                  int lane) {
+    const int g = lane & 7, grp = lane >> 3;
+    const int nb = D >> 5;
+    const float* row[4];
+    bool ok[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int c = grp + 8 * j;
+        ok[j] = c < n;
+        row[j] = X + (uint64_t)(ok[j] ? ids[c] : ids[0]) * ldx;
+    }
+    float a[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) a[j][0] = a[j][1] = a[j][2] = a[j][3] = 0.f;
+    for (int b0 = 0; b0 < nb; b0 += 4) {
+        float4 y[4][4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int bb = 0; bb < 4; ++bb)
+                if (ok[j] && b0 + bb < nb) y[j][bb] = ld4(row[j] + 32 * (b0 + bb) + 4 * g);
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb) {
+            if (b0 + bb >= nb) break;
+            const float4 x = ld4(q + 32 * (b0 + bb) + 4 * g);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (!ok[j]) continue;
+                const float4 yy = y[j][bb];
+                if (METRIC == WV_METRIC_L2) {
+                    const float d0 = x.x - yy.x, d1 = x.y - yy.y, d2 = x.z - yy.z, d3 = x.w - yy.w;
+                    a[j][0] = __builtin_fmaf(d0, d0, a[j][0]);
+                    a[j][1] = __builtin_fmaf(d1, d1, a[j][1]);
+                    a[j][2] = __builtin_fmaf(d2, d2, a[j][2]);
+                    a[j][3] = __builtin_fmaf(d3, d3, a[j][3]);
+                } else {
+                    a[j][0] = __builtin_fmaf(x.x, yy.x, a[j][0]);
+                    a[j][1] = __builtin_fmaf(x.y, yy.y, a[j][1]);
+                    a[j][2] = __builtin_fmaf(x.z, yy.z, a[j][2]);
+                    a[j][3] = __builtin_fmaf(x.w, yy.w, a[j][3]);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        float t = 0.f;
+        if (ok[j]) {
+            for (int i = nb * 32; i < D; i += 4) {
+                const float4 x = ld4(q + i);
+                const float4 yy = ld4(row[j] + i);
+                if (METRIC == WV_METRIC_L2) {
+                    float d = x.x - yy.x; t = __builtin_fmaf(d, d, t);
+                    d = x.y - yy.y;       t = __builtin_fmaf(d, d, t);
+                    d = x.z - yy.z;       t = __builtin_fmaf(d, d, t);
+                    d = x.w - yy.w;       t = __builtin_fmaf(d, d, t);
+                } else {
+                    t = __builtin_fmaf(x.x, yy.x, t);
+                    t = __builtin_fmaf(x.y, yy.y, t);
+                    t = __builtin_fmaf(x.z, yy.z, t);
+                    t = __builtin_fmaf(x.w, yy.w, t);
+                }
+            }
+        }
+        float a0 = a[j][0], a1 = a[j][1], a2 = a[j][2], a3 = a[j][3];
+        a0 = a0 + shfl_xor_f(a0, 2); a1 = a1 + shfl_xor_f(a1, 2);
+        a2 = a2 + shfl_xor_f(a2, 2); a3 = a3 + shfl_xor_f(a3, 2);
+        a0 = a0 + shfl_xor_f(a0, 4); a1 = a1 + shfl_xor_f(a1, 4);
+        a2 = a2 + shfl_xor_f(a2, 4); a3 = a3 + shfl_xor_f(a3, 4);
+        a0 = a0 + shfl_xor_f(a0, 1); a1 = a1 + shfl_xor_f(a1, 1);
+        a2 = a2 + shfl_xor_f(a2, 1); a3 = a3 + shfl_xor_f(a3, 1);
+        a0 = t + a0;
+        a1 = 0.0f + a1;
+        a2 = 0.0f + a2;
+        a3 = 0.0f + a3;
+        float r = (a0 + a1) + (a2 + a3);
+        if (METRIC == WV_METRIC_DOT) r = -r;
+        else if (METRIC == WV_METRIC_COSINE) r = 1.0f - r;
+        if (ok[j] && g == 0) out[grp + 8 * j] = r;
+    }
+}
+
 // Key order used for ids: (dist, id) ascending.
 __device__ __forceinline__ bool key_less(float da, uint32_t ia, float db, uint32_t ib) {
     return da < db || (da == db && (ia & WV_IDMASK) < (ib & WV_IDMASK));

@@ -80,7 +80,7 @@ __device__ __forceinline__ bool ckey_less(uint32_t ca, float da, uint32_t ia, ui
 }
 
 template <int METRIC>
-__device__ void search_layer(const HnswParams& p, WaveState& w, int level, int ef, uint32_t ep, float epd,
+__device__ __forceinline__ void search_layer(const HnswParams& p, WaveState& w, int level, int ef, uint32_t ep, float epd,
                              const uint64_t* allow, int& Rl, int& Sh, int& Sl, int& status, int nlt,
                              uint32_t& n_dist, uint32_t& n_exp) {
     const int lane = threadIdx.x & 63;
@@ -186,12 +186,8 @@ __device__ void search_layer(const HnswParams& p, WaveState& w, int level, int e
             if (nb == 0) continue;
 
             // ---- exact distances, 8 lanes per row (search.go:265-271) ----
-            for (int base = 0; base < nb; base += 8) {
-                const int c = base + grp;
-                float d = FLT_MAX;
-                if (c < nb) d = exact_dist_group8<METRIC>(w.qv, p.X + (uint64_t)w.Bi[c] * p.ldx, p.D, g);
-                if (c < nb && g == 0) w.Bd[c] = d;
-            }
+            for (int base = 0; base < nb; base += 32)
+                exact_dist_rows32<METRIC>(w.qv, p.X, p.ldx, p.D, w.Bi + base, nb - base, w.Bd + base, lane);
             n_dist += nb;
             wave_sync();
 
@@ -320,7 +316,7 @@ __device__ void search_layer(const HnswParams& p, WaveState& w, int level, int e
 }
 
 template <int METRIC>
-__device__ void knn_one(const HnswParams& p, WaveState& w, int q) {
+__device__ __forceinline__ void knn_one(const HnswParams& p, WaveState& w, int q) {
     const int lane = threadIdx.x & 63;
     const int g = lane & 7;
     // query -> LDS

@@ -42,6 +42,31 @@ struct BfFinParams {
     float* out_d;
     int32_t* out_n;
     int32_t* fail;          // per query: 1 = uncertified
+    float* fail_thr;        // per query: exact d_k of the re-ranked set (upper bound of the true d_k)
+};
+
+// Certificate fallback: exact distances of every row for a batch of failed
+// queries, keeping the rows with d <= thr[f] (thr = an upper bound of the
+// true k-th distance), then a per-query sort of the survivors.
+constexpr int FB_CAP = 2048;       // survivors kept per failed query
+struct FbParams {
+    const float* X;
+    const float* Q;          // all queries [nq][ldq]
+    const int32_t* qidx;     // [nf] query index of each failed query
+    const float* thr;        // [nq] threshold per query
+    const uint64_t* tomb;
+    const uint64_t* allow;
+    uint64_t tomb_nbits, allow_nbits, allow_stride;
+    uint64_t N;
+    int nf, D, ldx, ldq, metric, k;
+    uint64_t id_base;
+    float* cand_d;           // [nf][FB_CAP]
+    uint32_t* cand_id;
+    uint32_t* cand_n;        // [nf] (may exceed FB_CAP: overflow)
+    uint64_t* out_ids;       // [nq][k]
+    float* out_d;
+    int32_t* out_n;
+    int32_t* overflow;       // [nf] 1 = more than FB_CAP survivors
 };
 
 struct ScanParams {
