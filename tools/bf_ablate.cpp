@@ -20,13 +20,12 @@ int main(int argc, char** argv) {
     hipMemcpy(xn, hn.data(), N * 4, hipMemcpyHostToDevice);
     wv::BfParams p{};
     const int nqb = (nq + 127) / 128;
-    const uint64_t ntiles = (N + 127) / 128;
-    int ns = std::max(1, (1024 + nqb - 1) / nqb);
-    const int tps = (int)((ntiles + ns - 1) / ns);
-    ns = (int)((ntiles + tps - 1) / tps);
+    const int target = getenv("BLOCKS") ? atoi(getenv("BLOCKS")) : 512;
+    const wv::BfSchedule sch = wv::bf_schedule(nq, N, target);
+    const int ns = sch.n_slots;
     hipMalloc(&od, (size_t)nq * ns * 4 * wv::BF_KP * 4); hipMalloc(&oi, (size_t)nq * ns * 4 * wv::BF_KP * 4);
     p.X = X; p.Q = Q; p.xnorm = xn; p.N = N; p.nq = nq; p.D = D; p.ldx = D; p.ldq = D; p.metric = 0;
-    p.n_qblocks = nqb; p.n_splits = ns; p.tiles_per_split = tps; p.out_d = od; p.out_id = oi;
+    p.n_qblocks = nqb; p.n_slots = ns; p.ntiles = sch.ntiles; p.units_per_block = sch.units_per_block; p.out_d = od; p.out_id = oi;
     hipEvent_t a, b; hipEventCreate(&a); hipEventCreate(&b);
     wv_launch_bf_mfma(&p, 0); hipDeviceSynchronize();
     float best = 1e9;
@@ -34,7 +33,7 @@ int main(int argc, char** argv) {
         hipEventRecord(a, 0); wv_launch_bf_mfma(&p, 0); hipEventRecord(b, 0); hipEventSynchronize(b);
         float ms; hipEventElapsedTime(&ms, a, b); if (ms < best) best = ms;
     }
-    printf("%s N=%llu nq=%d: %.3f ms  %.1f TF/s  (%.1f%% of 157.3)\n", argc > 3 ? argv[3] : "variant",
+    printf("%s blocks=%d N=%llu nq=%d: %.3f ms  %.1f TF/s  (%.1f%% of 157.3)\n", argc > 3 ? argv[3] : "variant", sch.n_blocks,
            (unsigned long long)N, nq, best, 2.0 * D * N * nq / best / 1e9, 100 * 2.0 * D * N * nq / best / 1e9 / 157.3);
     return 0;
 }

@@ -15,4 +15,8 @@ if [ "$1" == "build" ]; then
   done
   exit 0
 fi
-for f in $B/ablate_*; do timeout -k 5 120 $f ${N:-1000000} ${NQ:-10000} ${f##*/ablate_}; done
+for f in $B/ablate_*; do
+  for nb in ${BLOCKS_LIST:-512}; do
+    BLOCKS=$nb timeout -k 5 120 $f ${N:-1000000} ${NQ:-10000} ${f##*/ablate_} || exit $?
+  done
+done

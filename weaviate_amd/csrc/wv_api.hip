@@ -11,6 +11,7 @@
 #include <atomic>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -207,6 +208,9 @@ struct wv_index {
     bool timing = false;
     hipEvent_t ev[6] = {};
     float t_mfma = 0.f, t_fin = 0.f, t_hnsw = 0.f;
+    // brute-force workgroups per launch: a whole number of resident waves of
+    // workgroups (CUs x 2 per CU x WV_BF_ROUNDS)
+    int bf_blocks = 512;
 };
 
 namespace {
@@ -300,12 +304,8 @@ int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
     std::vector<int32_t> fails;
     if (k <= wv::BF_FAST_KMAX) {
         const int n_qblocks = (nq + wv::BF_BQ - 1) / wv::BF_BQ;
-        const uint64_t ntiles = (N + wv::BF_BN - 1) / wv::BF_BN;
-        int n_splits = std::max(1, (1024 + n_qblocks - 1) / n_qblocks);
-        if ((uint64_t)n_splits > ntiles) n_splits = (int)ntiles;
-        const int tps = (int)((ntiles + n_splits - 1) / n_splits);
-        n_splits = (int)((ntiles + tps - 1) / tps);
-        const size_t n_lists = (size_t)n_splits * wv::BF_PROD;
+        const wv::BfSchedule sch = wv::bf_schedule(nq, N, ix->bf_blocks);
+        const size_t n_lists = (size_t)sch.n_slots * wv::BF_PROD;
         HIP_TRY(ix->cand_d.ensure((size_t)nq * n_lists * wv::BF_KP * 4));
         HIP_TRY(ix->cand_id.ensure((size_t)nq * n_lists * wv::BF_KP * 4));
         HIP_TRY(ix->q_nrm2.ensure((size_t)nq * 4));
@@ -330,8 +330,9 @@ int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
         bp.ldq = ix->dpad;
         bp.metric = ix->metric;
         bp.n_qblocks = n_qblocks;
-        bp.n_splits = n_splits;
-        bp.tiles_per_split = tps;
+        bp.n_slots = sch.n_slots;
+        bp.ntiles = sch.ntiles;
+        bp.units_per_block = sch.units_per_block;
         bp.out_d = ix->cand_d.as<float>();
         bp.out_id = ix->cand_id.as<uint32_t>();
         if (ix->timing) HIP_TRY(hipEventRecord(ix->ev[0], s));
@@ -349,7 +350,9 @@ int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
         fp.cand_id = ix->cand_id.as<uint32_t>();
         fp.qnorm = ix->q_nrm2.as<float>();
         fp.xnorm_max = maxn;
-        fp.n_lists = (int)n_lists;
+        fp.n_slots = sch.n_slots;
+        fp.ntiles = sch.ntiles;
+        fp.units_per_block = sch.units_per_block;
         fp.nq = nq;
         fp.D = ix->dim;
         fp.ldx = ix->dpad;
@@ -660,6 +663,14 @@ int wv_index_create(int dim, int metric, const wv_config* cfg, uint64_t capacity
     if (e != hipSuccess) { delete ix; return fail(WV_EDEVICE, std::string("hipSetDevice: ") + hipGetErrorString(e)); }
     e = hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking);
     if (e != hipSuccess) { delete ix; return fail(WV_EDEVICE, std::string("hipStreamCreate: ") + hipGetErrorString(e)); }
+    {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ix->cfg.device) != hipSuccess || cus <= 0)
+            cus = 256;
+        int rounds = 1;
+        if (const char* r = std::getenv("WV_BF_ROUNDS")) rounds = std::max(1, std::atoi(r));
+        ix->bf_blocks = cus * 2 * rounds;
+    }
     ix->bm_words = (capacity + 63) / 64;
     const size_t vbytes = capacity * (size_t)ix->dpad * 4;
     if (ix->vecs.ensure(vbytes) != hipSuccess || ix->xnorm.ensure(capacity * 4) != hipSuccess ||

@@ -63,16 +63,22 @@ __global__ __launch_bounds__(256, WV_BF_WAVES_PER_SIMD) void wv_bf_mfma_kernel(B
     const int wave = tid >> 6;
     const int wm = wave >> 1;   // base-row half of the tile
     const int wn = wave & 1;    // query half of the tile
-    const int qb = blockIdx.x % p.n_qblocks;
-    const int split = blockIdx.x / p.n_qblocks;
-    const int q0 = qb * BF_BQ;
-    const uint64_t ntiles_total = (p.N + BF_BN - 1) / BF_BN;
-    const uint64_t t_begin = (uint64_t)split * p.tiles_per_split;
-    uint64_t t_end = t_begin + p.tiles_per_split;
-    if (t_end > ntiles_total) t_end = ntiles_total;
     const int nk = (p.D + BF_BK - 1) / BF_BK;
     const int khalf = lane >> 5;
     const int l31 = lane & 31;
+    const uint64_t u_first = (uint64_t)blockIdx.x * p.units_per_block;
+    uint64_t u_last = u_first + p.units_per_block;
+    if (u_last > (uint64_t)p.n_qblocks * p.ntiles) u_last = (uint64_t)p.n_qblocks * p.ntiles;
+
+    // one segment per query block touched by this block's run of units
+    for (uint64_t u = u_first; u < u_last;) {
+    const int qb = (int)(u / p.ntiles);
+    const uint64_t t_begin = u % p.ntiles;
+    uint64_t t_end = t_begin + (u_last - u);
+    if (t_end > p.ntiles) t_end = p.ntiles;
+    u += t_end - t_begin;
+    const int slot = (int)blockIdx.x - bf_first_block(qb, p.ntiles, p.units_per_block);
+    const int q0 = qb * BF_BQ;
 
     // per-lane candidate lists (sorted, BF_KP entries) for its two query columns
     float l0d[BF_KP], l1d[BF_KP];
@@ -256,21 +262,22 @@ __global__ __launch_bounds__(256, WV_BF_WAVES_PER_SIMD) void wv_bf_mfma_kernel(B
         #undef WV_EXTRACT
     }
 
-    // write this lane's two lists: out[q][split][producer][KP]
+    // write this lane's two lists: out[q][slot][producer][KP]
     const int prod = wm * 2 + khalf;
     const int jq0 = q0 + wn * 64 + l31;
     const int jq1 = jq0 + 32;
-    const size_t per_q = (size_t)p.n_splits * BF_PROD * BF_KP;
+    const size_t per_q = (size_t)p.n_slots * BF_PROD * BF_KP;
     if (jq0 < p.nq) {
-        const size_t base = (size_t)jq0 * per_q + ((size_t)split * BF_PROD + prod) * BF_KP;
+        const size_t base = (size_t)jq0 * per_q + ((size_t)slot * BF_PROD + prod) * BF_KP;
 #pragma unroll
         for (int i = 0; i < BF_KP; ++i) { p.out_d[base + i] = l0d[i]; p.out_id[base + i] = l0i[i]; }
     }
     if (jq1 < p.nq) {
-        const size_t base = (size_t)jq1 * per_q + ((size_t)split * BF_PROD + prod) * BF_KP;
+        const size_t base = (size_t)jq1 * per_q + ((size_t)slot * BF_PROD + prod) * BF_KP;
 #pragma unroll
         for (int i = 0; i < BF_KP; ++i) { p.out_d[base + i] = l1d[i]; p.out_id[base + i] = l1i[i]; }
     }
+    }   // segments
 }
 
 // ---------------------------------------------------------------------------
@@ -279,14 +286,15 @@ __global__ __launch_bounds__(256, WV_BF_WAVES_PER_SIMD) void wv_bf_mfma_kernel(B
 template <int METRIC>
 __device__ void finalize_one(const BfFinParams& p, int q, float* sd, uint32_t* si, float* qv) {
     const int lane = threadIdx.x & 63;
-    const int n_ent = p.n_lists * BF_KP;
-    const float* cd = p.cand_d + (size_t)q * n_ent;
-    const uint32_t* ci = p.cand_id + (size_t)q * n_ent;
+    const int n_lists = bf_slots_of((uint64_t)(q / BF_BQ), p.ntiles, p.units_per_block) * BF_PROD;
+    const int n_ent = n_lists * BF_KP;
+    const float* cd = p.cand_d + (size_t)q * p.n_slots * BF_PROD * BF_KP;
+    const uint32_t* ci = p.cand_id + (size_t)q * p.n_slots * BF_PROD * BF_KP;
 
     // bound from the producers' last entries: anything a producer dropped is >= its KP-th key
     float bound = FLT_MAX;
     uint32_t bound_id = WV_NIL;
-    for (int l = lane; l < p.n_lists; l += 64) {
+    for (int l = lane; l < n_lists; l += 64) {
         const float d = cd[l * BF_KP + BF_KP - 1];
         const uint32_t i = ci[l * BF_KP + BF_KP - 1];
         if (key_less(d, i, bound, bound_id)) { bound = d; bound_id = i; }
@@ -610,7 +618,10 @@ extern "C" {
 
 hipError_t wv_launch_bf_mfma(const wv::BfParams* p, hipStream_t s) {
     const size_t lds = wv::BF_LDS_BYTES;
-    hipLaunchKernelGGL(wv::wv_bf_mfma_kernel, dim3(p->n_qblocks * p->n_splits), dim3(256), lds, s, *p);
+    const uint64_t total = (uint64_t)p->n_qblocks * p->ntiles;
+    const unsigned nb = (unsigned)((total + p->units_per_block - 1) / p->units_per_block);
+    if (nb == 0) return hipSuccess;
+    hipLaunchKernelGGL(wv::wv_bf_mfma_kernel, dim3(nb), dim3(256), lds, s, *p);
     return hipGetLastError();
 }
 

@@ -84,7 +84,6 @@ __device__ __forceinline__ void search_layer(const HnswParams& p, WaveState& w, 
                              const uint64_t* allow, int& Rl, int& Sh, int& Sl, int& status, int nlt,
                              uint32_t& n_dist, uint32_t& n_exp) {
     const int lane = threadIdx.x & 63;
-    const int g = lane & 7, grp = lane >> 3;
     const int VC = 1 << p.vc_log2;
     const int XS = 1 << p.xs_log2;
     for (int i = lane; i < VC; i += 64) w.vc[i] = WV_NIL;

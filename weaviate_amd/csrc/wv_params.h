@@ -23,10 +23,45 @@ struct BfParams {
     uint64_t tomb_nbits, allow_nbits, allow_stride;  // stride in words (0 = shared)
     uint64_t N;
     int nq, D, ldx, ldq, metric;
-    int n_qblocks, n_splits, tiles_per_split;
-    float* out_d;           // [nq][n_splits][BF_PROD*BF_KP]
+    // flattened schedule (bf_schedule): the (query block, base tile) units are
+    // numbered qb * ntiles + tile and cut into n_blocks equal contiguous runs
+    int n_qblocks, n_slots;
+    uint64_t ntiles, units_per_block;
+    float* out_d;           // [nq][n_slots][BF_PROD*BF_KP]
     uint32_t* out_id;
 };
+
+// Equal-work schedule for wv_bf_mfma_kernel: exactly n_blocks workgroups
+// (a multiple of the resident slots) so no partial last wave of workgroups.
+// A block's run of units crosses at most a few query blocks; the lists it
+// produces for query block qb go to slot (block - first block of qb).
+struct BfSchedule {
+    int n_blocks, n_slots;
+    uint64_t ntiles, units_per_block;
+};
+inline BfSchedule bf_schedule(int nq, uint64_t N, int target_blocks) {
+    BfSchedule s{};
+    const uint64_t nqb = (uint64_t)(nq + BF_BQ - 1) / BF_BQ;
+    s.ntiles = (N + BF_BN - 1) / BF_BN;
+    const uint64_t total = nqb * s.ntiles;
+    uint64_t nb = target_blocks > 0 ? (uint64_t)target_blocks : 1;
+    if (nb > total) nb = total;
+    s.units_per_block = (total + nb - 1) / nb;
+    s.n_blocks = (int)((total + s.units_per_block - 1) / s.units_per_block);
+    // slots touched by one query block: ceil(ntiles / U) + 1 at most
+    s.n_slots = (int)((s.ntiles + s.units_per_block - 1) / s.units_per_block) + 1;
+    return s;
+}
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+inline int bf_first_block(uint64_t qb, uint64_t ntiles, uint64_t upb) { return (int)(qb * ntiles / upb); }
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+inline int bf_slots_of(uint64_t qb, uint64_t ntiles, uint64_t upb) {
+    return (int)(((qb + 1) * ntiles - 1) / upb) - bf_first_block(qb, ntiles, upb) + 1;
+}
 
 struct BfFinParams {
     const float* X;
@@ -35,7 +70,8 @@ struct BfFinParams {
     const uint32_t* cand_id;
     const float* qnorm;     // |q|^2 (L2) or |q| (dot, cosine)
     float xnorm_max;        // max |x| over the corpus (rounded up)
-    int n_lists;            // n_splits * BF_PROD
+    int n_slots;            // list slots per query (BfParams.n_slots)
+    uint64_t ntiles, units_per_block;
     int nq, D, ldx, ldq, metric, k;
     uint64_t id_base;       // global id of local id 0
     uint64_t* out_ids;      // [nq][k]
