@@ -14,7 +14,9 @@ int main(int argc, char** argv) {
     for (auto& v : hq) v = -2.f * rand() / (float)RAND_MAX;  // pre-scaled B operand (-2q)
     for (uint64_t i = 0; i < N; ++i) { float s = 0; for (int k = 0; k < D; ++k) s += hx[i * D + k] * hx[i * D + k]; hn[i] = s; }
     float *X, *Q, *xn, *od; uint32_t* oi;
-    hipMalloc(&X, N * D * 4); hipMalloc(&Q, (size_t)nq * D * 4); hipMalloc(&xn, N * 4);
+    const uint64_t Np = (N + 127) / 128 * 128; const size_t nqp = (nq + 127) / 128 * 128;
+    hipMalloc(&X, Np * D * 4); hipMalloc(&Q, nqp * D * 4); hipMalloc(&xn, Np * 4);
+    hipMemset(X, 0, Np * D * 4); hipMemset(Q, 0, nqp * D * 4); hipMemset(xn, 0, Np * 4);
     hipMemcpy(X, hx.data(), N * D * 4, hipMemcpyHostToDevice);
     hipMemcpy(Q, hq.data(), (size_t)nq * D * 4, hipMemcpyHostToDevice);
     hipMemcpy(xn, hn.data(), N * 4, hipMemcpyHostToDevice);

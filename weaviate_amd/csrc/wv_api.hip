@@ -311,7 +311,12 @@ int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
         HIP_TRY(ix->q_nrm2.ensure((size_t)nq * 4));
         HIP_TRY(ix->fail.ensure((size_t)nq * 4));
         HIP_TRY(wv_launch_qnorm(d_q, nq, ix->dim, ix->dpad, ix->metric, ix->q_nrm2.as<float>(), s));
-        HIP_TRY(ix->q_scaled.ensure((size_t)nq * ix->dpad * 4));
+        // B operand in whole BF_BQ-row query blocks, zero rows past nq
+        const size_t nq_pad = (size_t)n_qblocks * wv::BF_BQ;
+        HIP_TRY(ix->q_scaled.ensure(nq_pad * ix->dpad * 4));
+        if (nq_pad > (size_t)nq)
+            HIP_TRY(hipMemsetAsync(ix->q_scaled.as<float>() + (size_t)nq * ix->dpad, 0,
+                                   (nq_pad - nq) * ix->dpad * 4, s));
         HIP_TRY(wv_launch_scale(d_q, ix->q_scaled.as<float>(), (uint64_t)nq * ix->dpad,
                                 ix->metric == WV_L2_SQUARED ? -2.f : -1.f, s));
         wv::BfParams bp{};
@@ -672,14 +677,17 @@ int wv_index_create(int dim, int metric, const wv_config* cfg, uint64_t capacity
         ix->bf_blocks = cus * 2 * rounds;
     }
     ix->bm_words = (capacity + 63) / 64;
-    const size_t vbytes = capacity * (size_t)ix->dpad * 4;
-    if (ix->vecs.ensure(vbytes) != hipSuccess || ix->xnorm.ensure(capacity * 4) != hipSuccess ||
+    // whole brute-force tiles (wv_bf.hip layout contract): zero rows past capacity
+    const uint64_t cap_rows = (capacity + wv::BF_BN - 1) / wv::BF_BN * wv::BF_BN;
+    const size_t vbytes = cap_rows * (size_t)ix->dpad * 4;
+    if (ix->vecs.ensure(vbytes) != hipSuccess || ix->xnorm.ensure(cap_rows * 4) != hipSuccess ||
         ix->maxnorm.ensure(4) != hipSuccess || ix->tomb.ensure(ix->bm_words * 8) != hipSuccess ||
         ix->excl.ensure(ix->bm_words * 8) != hipSuccess) {
         wv_index_destroy(ix);
         return fail(WV_EOOM, "wv_index_create: device allocation failed");
     }
     (void)hipMemsetAsync(ix->vecs.p, 0, vbytes, ix->stream);
+    (void)hipMemsetAsync(ix->xnorm.p, 0, cap_rows * 4, ix->stream);
     (void)hipMemsetAsync(ix->maxnorm.p, 0, 4, ix->stream);
     (void)hipStreamSynchronize(ix->stream);
     ix->has_vec.assign(ix->bm_words, 0);
