@@ -29,6 +29,14 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 
 // ---------------------------------------------------------------------------
+// v_min3_f32 without the IEEE canonicalisation hipcc wraps around fminf of
+// MFMA results (a NaN key never wins a comparison either way)
+__device__ __forceinline__ float min3_raw(float a, float b, float c) {
+    float r;
+    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
 __device__ __forceinline__ void list_insert(float (&ld)[BF_KP], uint32_t (&li)[BF_KP], float d, uint32_t id) {
     // bubble the new element through the sorted list; the largest falls off
 #pragma unroll
@@ -226,30 +234,34 @@ __global__ __launch_bounds__(256, WV_BF_WAVES_PER_SIMD) void wv_bf_mfma_kernel(B
             continue;
 #endif
             // ---- epilogue of one 128x128 tile ----
-            uint64_t ok0 = jq0 < p.nq ? okw & aq0 : 0ull;
-            uint64_t ok1 = jq1 < p.nq ? okw & aq1 : 0ull;
-            // pass 1: the accumulators already hold the approximate keys;
-            // mask ineligible rows to +inf and take the per-query minimum.
-            // Almost every tile stops here.
+            // lane (l31, khalf) holds rows (r & 3) + 8 * (r >> 2) + 4 * khalf of
+            // each 32-row half: shift the eligibility words once so every row
+            // test is a constant-position bit test
+            const uint32_t rb0 = (uint32_t)row0 + 4 * khalf;   // row of acc*0[0]
+            const uint64_t o0 = (jq0 < p.nq ? okw & aq0 : 0ull) >> (4 * khalf);
+            const uint64_t o1 = (jq1 < p.nq ? okw & aq1 : 0ull) >> (4 * khalf);
+            const uint32_t o0lo = (uint32_t)o0, o0hi = (uint32_t)(o0 >> 32);
+            const uint32_t o1lo = (uint32_t)o1, o1hi = (uint32_t)(o1 >> 32);
+            constexpr uint32_t LANE_ROWS = 0x0F0F0F0Fu;   // bits (r&3) + 8*(r>>2), r < 16
             const float INF = __builtin_inff();
+            // pass 1: the accumulators already hold the approximate keys; mask
+            // ineligible rows to +inf and take the per-query minimum.  Almost
+            // every tile stops here.
+            if (!__all((o0lo & o0hi & o1lo & o1hi & LANE_ROWS) == LANE_ROWS)) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int bit = (r & 3) + 8 * (r >> 2);
+                    acc00[r] = (o0lo >> bit) & 1u ? acc00[r] : INF;
+                    acc10[r] = (o0hi >> bit) & 1u ? acc10[r] : INF;
+                    acc01[r] = (o1lo >> bit) & 1u ? acc01[r] : INF;
+                    acc11[r] = (o1hi >> bit) & 1u ? acc11[r] : INF;
+                }
+            }
             float m0 = INF, m1 = INF;
-            if (__all(ok0 == ~0ull && ok1 == ~0ull)) {
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    m0 = fminf(m0, fminf(acc00[r], acc10[r]));
-                    m1 = fminf(m1, fminf(acc01[r], acc11[r]));
-                }
-            } else {
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int ir = (r & 3) + 8 * (r >> 2) + 4 * khalf;
-                    if (!((ok0 >> ir) & 1ull)) acc00[r] = INF;
-                    if (!((ok0 >> (ir + 32)) & 1ull)) acc10[r] = INF;
-                    if (!((ok1 >> ir) & 1ull)) acc01[r] = INF;
-                    if (!((ok1 >> (ir + 32)) & 1ull)) acc11[r] = INF;
-                    m0 = fminf(m0, fminf(acc00[r], acc10[r]));
-                    m1 = fminf(m1, fminf(acc01[r], acc11[r]));
-                }
+            for (int r = 0; r < 16; ++r) {
+                m0 = min3_raw(m0, acc00[r], acc10[r]);
+                m1 = min3_raw(m1, acc01[r], acc11[r]);
             }
             // pass 2 (rare after the first tiles): extract the minimum while it
             // beats the list tail; rows are scanned in ascending id, so among
@@ -259,18 +271,18 @@ __global__ __launch_bounds__(256, WV_BF_WAVES_PER_SIMD) void wv_bf_mfma_kernel(B
                 uint32_t idm = WV_NIL;                                                          \
                 _Pragma("unroll") for (int r = 0; r < 16; ++r) {                                \
                     const bool hit = idm == WV_NIL && A0[r] == M;                               \
-                    idm = hit ? (uint32_t)(row0 + (r & 3) + 8 * (r >> 2) + 4 * khalf) : idm;    \
+                    idm = hit ? rb0 + (r & 3) + 8 * (r >> 2) : idm;                             \
                     A0[r] = hit ? INF : A0[r];                                                  \
                 }                                                                               \
                 _Pragma("unroll") for (int r = 0; r < 16; ++r) {                                \
                     const bool hit = idm == WV_NIL && A1[r] == M;                               \
-                    idm = hit ? (uint32_t)(row0 + 32 + (r & 3) + 8 * (r >> 2) + 4 * khalf) : idm; \
+                    idm = hit ? rb0 + 32 + (r & 3) + 8 * (r >> 2) : idm;                        \
                     A1[r] = hit ? INF : A1[r];                                                  \
                 }                                                                               \
                 if (!key_less(M, idm, LD[BF_KP - 1], LI[BF_KP - 1])) break;                     \
                 list_insert(LD, LI, M, idm);                                                    \
                 M = INF;                                                                        \
-                _Pragma("unroll") for (int r = 0; r < 16; ++r) M = fminf(M, fminf(A0[r], A1[r])); \
+                _Pragma("unroll") for (int r = 0; r < 16; ++r) M = min3_raw(M, A0[r], A1[r]);   \
             }
             WV_EXTRACT(m0, acc00, acc10, l0d, l0i)
             WV_EXTRACT(m1, acc01, acc11, l1d, l1i)
