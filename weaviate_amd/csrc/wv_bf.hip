@@ -207,12 +207,23 @@ __global__ __launch_bounds__(256, WV_BF_WAVES_PER_SIMD) void wv_bf_mfma_kernel(B
             for (int kc = 0; kc < nk; ++kc, ++c) {
                 if (c + 1 < total) load_chunk(c + 1);
                 const float* st = lds + (c & 1) * BF_STAGE;
+                // operands of k-step group s4+1 are read from LDS while the 16
+                // MFMAs of group s4 run (register double buffer)
+                float4 fa0[2], fa1[2], fb0[2], fb1[2];
+                fa0[0] = *reinterpret_cast<const float4*>(st + arow);
+                fa1[0] = *reinterpret_cast<const float4*>(st + arow + 32 * BF_LDT);
+                fb0[0] = *reinterpret_cast<const float4*>(st + brow);
+                fb1[0] = *reinterpret_cast<const float4*>(st + brow + 32 * BF_LDT);
 #pragma unroll
                 for (int s4 = 0; s4 < 4; ++s4) {
-                    const float4 a0 = *reinterpret_cast<const float4*>(st + arow + 4 * s4);
-                    const float4 a1 = *reinterpret_cast<const float4*>(st + arow + 32 * BF_LDT + 4 * s4);
-                    const float4 b0 = *reinterpret_cast<const float4*>(st + brow + 4 * s4);
-                    const float4 b1 = *reinterpret_cast<const float4*>(st + brow + 32 * BF_LDT + 4 * s4);
+                    const int cur = s4 & 1, nxt = cur ^ 1;
+                    if (s4 < 3) {
+                        fa0[nxt] = *reinterpret_cast<const float4*>(st + arow + 4 * (s4 + 1));
+                        fa1[nxt] = *reinterpret_cast<const float4*>(st + arow + 32 * BF_LDT + 4 * (s4 + 1));
+                        fb0[nxt] = *reinterpret_cast<const float4*>(st + brow + 4 * (s4 + 1));
+                        fb1[nxt] = *reinterpret_cast<const float4*>(st + brow + 32 * BF_LDT + 4 * (s4 + 1));
+                    }
+                    const float4 a0 = fa0[cur], a1 = fa1[cur], b0 = fb0[cur], b1 = fb1[cur];
 #define WV_MF(C) \
     acc00 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.C, b0.C, acc00, 0, 0, 0); \
     acc01 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.C, b1.C, acc01, 0, 0, 0); \
@@ -220,6 +231,9 @@ __global__ __launch_bounds__(256, WV_BF_WAVES_PER_SIMD) void wv_bf_mfma_kernel(B
     acc11 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.C, b1.C, acc11, 0, 0, 0);
                     WV_MF(x) WV_MF(y) WV_MF(z) WV_MF(w)
 #undef WV_MF
+                    // 4 LDS reads first, then the 16 MFMAs of this group
+                    __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
                 }
                 // the stage of the last chunk is read by every wave before the
                 // next tile's first chunk overwrites the other stage below

@@ -8,7 +8,7 @@ constexpr int BF_BQ = 128;   // queries per workgroup tile
 constexpr int BF_BN = 128;   // base rows per workgroup tile
 constexpr int BF_BK = 32;    // k-chunk staged through LDS
 constexpr int BF_LDT = 36;   // LDS row: 32 k + 4 pad floats (odd 16-byte stride: conflict-free b128)
-constexpr int BF_KP = 4;     // candidates kept per producer lane (register list)
+constexpr int BF_KP = 8;     // candidates kept per producer lane (register list)
 constexpr int BF_PROD = 4;   // producers per query: 2 base-row waves x 2 lane halves
 constexpr int FIN_KF = 32;   // candidates re-ranked exactly per query
 constexpr int BF_FAST_KMAX = 32;   // k served by the MFMA + finalize pipeline
