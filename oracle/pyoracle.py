@@ -67,6 +67,8 @@ def lib():
             "wvo_remove_tombstone": (C.c_int, [vp, C.c_uint64]),
             "wvo_import_node": (C.c_int, [vp, C.c_uint64, C.c_int, u64p, i32p]),
             "wvo_set_entrypoint": (None, [vp, C.c_uint64, C.c_int]),
+            "wvo_import_csr": (C.c_int, [vp, C.c_uint64, fp, vp, vp, C.c_int, vp, vp, C.c_int, C.c_int,
+                                         C.c_uint64]),
             "wvo_graph_info": (None, [vp, u64p, u64p, i32p, u64p]),
             "wvo_export_layer0": (C.c_int, [vp, C.c_int, vp, vp, vp]),
             "wvo_export_upper": (C.c_int, [vp, C.c_int, C.c_int, vp, vp, C.c_uint64]),
@@ -184,6 +186,18 @@ class Index:
             flat = np.zeros(1, np.uint64)
         counts = np.array([len(lvl) for lvl in conns_per_level], dtype=np.int32)
         assert lib().wvo_import_node(self.h, id_, level, _u64(flat), _i32(counts)) == 0
+
+    def import_graph(self, vecs, g):
+        """Restore vectors + graph from export_graph()'s CSR (inverse of export)."""
+        vecs = f32(vecs)
+        lv = np.ascontiguousarray(g["levels"], np.int8)
+        l0 = np.ascontiguousarray(g["layer0"], np.uint32)
+        ur = np.ascontiguousarray(g["upper_row"], np.uint32)
+        up = np.ascontiguousarray(g["upper"], np.uint32)
+        rc = lib().wvo_import_csr(self.h, int(g["n"]), _f(vecs), lv.ctypes.data, l0.ctypes.data, l0.shape[1],
+                                  ur.ctypes.data, up.ctypes.data, up.shape[2], int(g["max_level"]),
+                                  int(g["entrypoint"]))
+        assert rc == 0, rc
 
     def set_entrypoint(self, ep, max_level):
         lib().wvo_set_entrypoint(self.h, ep, max_level)

@@ -1096,6 +1096,45 @@ int wvo_import_node(wvo_index *h, uint64_t id, int level, const uint64_t *conns,
     return 0;
 }
 
+/* Bulk restore from the fixed-degree CSR of wvo_export_layer0/_upper (the
+ * bench's graph cache): vectors rows [0, n) and every node's lists in stored
+ * order (NIL_ID pads dropped).  Equivalent to import_node per node. */
+int wvo_import_csr(wvo_index *h, uint64_t n, const float *vecs, const int8_t *levels, const uint32_t *layer0,
+                   int deg0, const uint32_t *upper_row, const uint32_t *upper, int degU, int max_level,
+                   uint64_t entrypoint) {
+    if (n > h->cap) return -1;
+    uint64_t *buf = (uint64_t *)malloc(sizeof(uint64_t) * ((size_t)deg0 + (size_t)degU * (max_level + 1) + 1));
+    int *counts = (int *)malloc(sizeof(int) * ((size_t)max_level + 2));
+    for (uint64_t i = 0; i < n; i++) {
+        wvo_set_vector(h, i, vecs + i * (uint64_t)h->dim);
+        if (levels[i] < 0) continue;
+        size_t off = 0;
+        int c = 0;
+        for (int j = 0; j < deg0; j++) {
+            uint32_t v = layer0[i * (uint64_t)deg0 + j];
+            if (v == NIL_ID) break;
+            buf[off++] = v;
+            c++;
+        }
+        counts[0] = c;
+        for (int l = 1; l <= levels[i]; l++) {
+            const uint32_t *row = upper + ((uint64_t)upper_row[i] * max_level + (l - 1)) * degU;
+            c = 0;
+            for (int j = 0; j < degU; j++) {
+                if (row[j] == NIL_ID) break;
+                buf[off++] = row[j];
+                c++;
+            }
+            counts[l] = c;
+        }
+        wvo_import_node(h, i, levels[i], buf, counts);
+    }
+    free(buf);
+    free(counts);
+    wvo_set_entrypoint(h, entrypoint, max_level);
+    return 0;
+}
+
 void wvo_set_entrypoint(wvo_index *h, uint64_t ep, int max_level) {
     h->ep = ep;
     h->max_layer = max_level;

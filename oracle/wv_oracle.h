@@ -88,6 +88,9 @@ int wvo_remove_tombstone(wvo_index *h, uint64_t id);
 /* graph import (debug.go:108-175 NewFromJSONDump*) */
 int wvo_import_node(wvo_index *h, uint64_t id, int level,
                     const uint64_t *conns, const int *counts /* level+1 */);
+int wvo_import_csr(wvo_index *h, uint64_t n, const float *vecs, const int8_t *levels, const uint32_t *layer0,
+                   int deg0, const uint32_t *upper_row, const uint32_t *upper, int degU, int max_level,
+                   uint64_t entrypoint);
 void wvo_set_entrypoint(wvo_index *h, uint64_t ep, int max_level);
 
 /* graph export for the GPU CSR upload */

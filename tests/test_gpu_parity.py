@@ -303,3 +303,45 @@ def test_merge_shards_device():
     for q in range(nq):
         cand = sorted((float(d[s, q, j]), int(ids[s, q, j])) for s in range(S) for j in range(n[s, q]))[:k]
         assert [c[1] for c in cand] == oi[q].cpu().numpy().view(np.uint64).tolist()
+
+
+@pytest.mark.parametrize("sel", [0.01, 0.10, 0.50])
+def test_c4_shape_dot_768_allow_list_sharded(sel):
+    """BASELINE configs[3] scaled down: 768-d dot with a shared allow list at
+    1/10/50% selectivity, the corpus split into two id-range shards (id_base)
+    whose per-shard top-k are merged on the device -- identical to one flat
+    search of the whole corpus (flat_search.go:19-74, index.go:967-1044)."""
+    import torch
+    n, d, nq, k = 12000, 768, 40, 10
+    rng = np.random.default_rng(int(sel * 100))
+    base = (rng.standard_normal((n, d)) / np.sqrt(d)).astype(np.float32)
+    qs = (rng.standard_normal((nq, d)) / np.sqrt(d)).astype(np.float32)
+    allow_ids = np.nonzero(rng.random(n) < sel)[0]
+    al = W.AllowList.from_ids(allow_ids, n)
+    oi, od, on = O.flat_scan(O.DOT, base, qs, k, allow_bits=al.words)
+    # one index over everything
+    ix = W.GPUVectorIndex(d, "dot", capacity=n)
+    ix.upload_vectors(base)
+    ids, ds, cnt = ix.search_batch(qs, k, allow=al, mode="exact")
+    _same(ids, ds, oi, od)
+    ix.close()
+    # two shards (global ids = id_base + local), allow list sliced per shard
+    dev = torch.device("cuda:0")
+    parts = []
+    for lo, hi in ((0, n // 2), (n // 2, n)):
+        sh = W.GPUVectorIndex(d, "dot", capacity=hi - lo, id_base=lo)
+        sh.upload_vectors(base[lo:hi])
+        sal = W.AllowList.from_ids(allow_ids[(allow_ids >= lo) & (allow_ids < hi)] - lo, hi - lo)
+        parts.append(sh.search_batch(qs, k, allow=sal, mode="exact"))
+        sh.close()
+    g_i = torch.from_numpy(np.stack([p[0] for p in parts]).view(np.int64)).to(dev)
+    g_d = torch.from_numpy(np.stack([p[1] for p in parts])).to(dev)
+    g_n = torch.from_numpy(np.stack([p[2] for p in parts])).to(dev)
+    m_d = torch.empty((nq, k), dtype=torch.float32, device=dev)
+    m_i = torch.empty((nq, k), dtype=torch.int64, device=dev)
+    m_n = torch.empty(nq, dtype=torch.int32, device=dev)
+    W.merge_shards_device(g_d.data_ptr(), g_i.data_ptr(), g_n.data_ptr(), 2, nq, k, m_d.data_ptr(), m_i.data_ptr(),
+                          m_n.data_ptr())
+    torch.cuda.synchronize()
+    assert m_n.cpu().tolist() == on.tolist()
+    _same(m_i.cpu().numpy().view(np.uint64), m_d.cpu().numpy(), oi, od)

@@ -174,3 +174,21 @@ def test_threaded_build_recall():
     assert recall > 0.95
     g = idx.export_graph()
     assert (g["counts0"] <= 32).all()  # layer-0 degree <= 2M (too_many_links test)
+
+
+def test_csr_export_import_round_trip():
+    """The fixed-degree CSR re-layout (the GPU's graph format) loses nothing:
+    a restatement restored from it searches identically (bench graph cache)."""
+    rng = np.random.default_rng(5)
+    base = rng.random((4000, 24), dtype=np.float32)
+    qs = rng.random((60, 24), dtype=np.float32)
+    a = O.Index(24, "l2-squared", 8, 48, capacity=4000, seed=3)
+    a.add_batch(base, threads=4)
+    g = a.export_graph()
+    b = O.Index(24, "l2-squared", 8, 48, capacity=4000, seed=3)
+    b.import_graph(base, g)
+    ra, rb = a.search_batch(qs, 10, 40), b.search_batch(qs, 10, 40)
+    assert (ra[0] == rb[0]).all() and (ra[1] == rb[1]).all() and ra[3] == rb[3]
+    g2 = b.export_graph()
+    for key in ("levels", "layer0", "upper_row", "upper"):
+        assert np.array_equal(g[key], g2[key]), key
