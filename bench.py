@@ -287,11 +287,27 @@ def main():
                                        "gpu_dist_evals_per_query": result["roofline"]["dist_evals_per_query"]})
             kind_desc = "knnSearchByVector restated in C on the same graph (oracle/)"
             same = float((oi == final_ids[:ns]).mean())
+            # tie-aware: distances bitwise equal, ids equal up to the order among
+            # equal distances (the reference orders ties by heap layout)
+            gd = final_d[:ns]
+            dist_same = float((od.view(np.uint32) == gd.view(np.uint32)).all(axis=1).mean())
+            tie_ok = 0
+            for a_i, a_d, b_i, b_d in zip(final_ids[:ns], gd, oi, od):
+                ok = np.array_equal(a_d.view(np.uint32), b_d.view(np.uint32))
+                if ok:
+                    for v in np.unique(a_d[:-1]):
+                        if v == a_d[-1]:
+                            continue
+                        if set(a_i[a_d == v].tolist()) != set(b_i[b_d == v].tolist()):
+                            ok = False
+                            break
+                tie_ok += ok
             nt = min(NQ, 1000)   # exact truths for recall on a sample
             ti, td, tn = O.flat_scan(metric_id, base, queries[:nt], K, threads=threads)
             rec_gpu = float(np.mean([len(set(a) & set(b)) / K for a, b in zip(final_ids[:nt].tolist(), ti.tolist())]))
             rec_cpu = float(np.mean([len(set(a) & set(b)) / K for a, b in zip(oi[:nt].tolist(), ti.tolist())]))
-            result["parity_sample"] = {"queries": ns, "id_match_frac": same, "recall@10_gpu": rec_gpu,
+            result["parity_sample"] = {"queries": ns, "id_match_frac": same, "dists_bitwise_equal_frac": dist_same,
+                                       "tie_aware_identical_frac": tie_ok / ns, "recall@10_gpu": rec_gpu,
                                        "recall@10_cpu_restatement": rec_cpu, "recall_sample": nt}
         result["cpu_baseline"] = {"value": round(ns / cpu_t, 1), "unit": "queries/s", "cores": threads,
                                   "kind": "port",

@@ -191,6 +191,7 @@ struct wv_index {
     DevBuf levels, layer0, upper_row, upper;
     // bitmaps
     std::vector<uint64_t> tomb_host;
+    bool any_tomb = false, any_nil = false;   // any tombstone / nil node below gn
     DevBuf tomb;            // tombstones (HNSW eligibility)
     DevBuf excl;            // tombstone | nil node | no vector (flatSearch skips)
     uint64_t bm_words = 0;
@@ -455,11 +456,20 @@ int run_hnsw(wv_index* ix, const float* d_q, int nq, int k, int ef, const uint64
              uint64_t allow_stride, uint64_t* d_out_ids, float* d_out_d, int32_t* d_out_n, hipStream_t s) {
     if (!ix->has_graph || ix->gn == 0) return fail(WV_ESTATE, "no graph uploaded");
     const int efc = std::max(64, (ef + 63) / 64 * 64);
-    const int sc = 256;
-    const int xs_log2 = 9;
+    // Side candidates S (traversed but ineligible: search.go:282-298) and the
+    // exact set of expanded side candidates exist only under a filter,
+    // tombstones or nil nodes.  Without them the wave state shrinks and more
+    // queries are in flight (the search is latency-bound on its gathers).  A
+    // stray ineligible node still ends in the exact fallback (status bit 0),
+    // never in a wrong answer.
+    const bool filtered = d_allow != nullptr || ix->any_tomb || ix->any_nil;
+    const int sc = filtered ? 256 : 0;
+    const int xs_log2 = filtered ? 9 : 0;
     const int fixed = wv_hnsw_per_wave_words(ix->dpad, efc, sc, 0, xs_log2) - 1;
-    // 8 waves per CU: 160 KiB / 8 = 20 KiB per wave when possible
-    const int budget = 20 * 1024 / 4;
+    // per-wave LDS budget: 20 KiB filtered (8 waves per CU), 12 KiB otherwise
+    int wave_kb = filtered ? 20 : 12;
+    if (const char* e = std::getenv("WV_HNSW_WAVE_KB")) wave_kb = std::max(4, std::atoi(e));
+    const int budget = wave_kb * 1024 / 4;
     const int vc_log2 = choose_vc_log2(budget, fixed);
     int per_wave = wv_hnsw_per_wave_words(ix->dpad, efc, sc, vc_log2, xs_log2);
     per_wave = (per_wave + 3) & ~3;
@@ -474,7 +484,7 @@ int run_hnsw(wv_index* ix, const float* d_q, int nq, int k, int ef, const uint64
     hp.layer0 = ix->layer0.as<uint32_t>();
     hp.upper_row = ix->upper_row.as<uint32_t>();
     hp.upper = ix->upper.as<uint32_t>();
-    hp.tomb = ix->tomb.as<uint64_t>();
+    hp.tomb = ix->any_tomb ? ix->tomb.as<uint64_t>() : nullptr;
     hp.tomb_nbits = ix->capacity;
     hp.allow = d_allow;
     hp.allow_nbits = allow_nbits;
@@ -793,6 +803,7 @@ int wv_index_upload_graph(wv_index* ix, uint64_t n, const int8_t* levels, const 
     }
     HIP_TRY(hipStreamSynchronize(ix->stream));
     ix->levels_host.assign(levels, levels + n);
+    ix->any_nil = std::any_of(levels, levels + n, [](int8_t l) { return l < 0; });
     ix->levels_host.resize(ix->capacity, -1);
     ix->gn = n;
     ix->deg0 = deg0;
@@ -812,6 +823,9 @@ int wv_index_set_tombstones(wv_index* ix, const uint64_t* bits, uint64_t nbits) 
     const uint64_t w = std::min<uint64_t>((nbits + 63) / 64, ix->bm_words);
     for (uint64_t i = 0; i < w; ++i) ix->tomb_host[i] = bits ? bits[i] : 0;
     if (nbits & 63 && w == (nbits + 63) / 64 && w > 0) ix->tomb_host[w - 1] &= (1ull << (nbits & 63)) - 1;
+    ix->any_tomb = false;
+    for (uint64_t i = 0; i < ix->bm_words; ++i)
+        if (ix->tomb_host[i]) { ix->any_tomb = true; break; }
     ix->bitmaps_dirty = true;
     return WV_OK;
 }

@@ -74,11 +74,6 @@ __device__ __forceinline__ int lower_bound(const float* ad, const uint32_t* ai, 
     return lo;
 }
 
-// composite order for the batch sort: eligible first, then (d, id)
-__device__ __forceinline__ bool ckey_less(uint32_t ca, float da, uint32_t ia, uint32_t cb, float db, uint32_t ib) {
-    return ca < cb || (ca == cb && key_less(da, ia, db, ib));
-}
-
 template <int METRIC>
 __device__ __forceinline__ void search_layer(const HnswParams& p, WaveState& w, int level, int ef, uint32_t ep, float epd,
                              const uint64_t* allow, int& Rl, int& Sh, int& Sl, int& status, int nlt,
@@ -149,13 +144,18 @@ __device__ __forceinline__ void search_layer(const HnswParams& p, WaveState& w, 
             status = __shfl(status, 0, 64);
         }
         wave_sync();
-        // :217-234 nil node / level check
-        const int lvl = p.levels[cid];
-        if (lvl < level) continue;
+        // :217-234 nil node / level check.  Every layer-0 row exists (nil
+        // nodes hold pads), so there the first neighbour ids are fetched in
+        // the same memory round trip as the level.
+        uint32_t pre0 = WV_NIL, pre1 = WV_NIL;
         if (level == 0) {
             nbr_base = p.layer0 + (uint64_t)cid * p.deg0;
             deg = p.deg0;
+            if (lane < deg) pre0 = nbr_base[lane];
+            if (64 + lane < deg) pre1 = nbr_base[64 + lane];
+            if (p.levels[cid] < 0) continue;
         } else {
+            if (p.levels[cid] < level) continue;
             const uint32_t row = p.upper_row[cid];
             nbr_base = p.upper + ((uint64_t)row * p.max_level + (level - 1)) * p.degU;
             deg = p.degU;
@@ -165,8 +165,13 @@ __device__ __forceinline__ void search_layer(const HnswParams& p, WaveState& w, 
         for (int c0 = 0; c0 < deg; c0 += BATCH) {
             // ---- neighbour ids, visited-cache filter, compaction ----
             uint32_t id0 = WV_NIL, id1 = WV_NIL;
-            if (c0 + lane < deg) id0 = nbr_base[c0 + lane];
-            if (c0 + 64 + lane < deg) id1 = nbr_base[c0 + 64 + lane];
+            if (level == 0 && c0 == 0) {
+                id0 = pre0;
+                id1 = pre1;
+            } else {
+                if (c0 + lane < deg) id0 = nbr_base[c0 + lane];
+                if (c0 + 64 + lane < deg) id1 = nbr_base[c0 + 64 + lane];
+            }
             bool v0 = id0 != WV_NIL && id0 < p.N;
             bool v1 = id1 != WV_NIL && id1 < p.N;
             const uint32_t h0 = v0 ? hash32(id0) >> (32 - p.vc_log2) : 0;
@@ -190,7 +195,12 @@ __device__ __forceinline__ void search_layer(const HnswParams& p, WaveState& w, 
             n_dist += nb;
             wave_sync();
 
-            // ---- classify + dedupe (lanes hold slots lane, lane+64) ----
+            // ---- keep test + dedupe (lanes hold batch slots lane, lane+64) ----
+            // Only a neighbour the reference pushes into the candidate heap
+            // matters: d < worst || |results| < ef (search.go:282).  worst only
+            // falls while R is full, so the pre-batch worst keeps a superset;
+            // the merge below settles the rest.  Late in a search most
+            // neighbours fail here and the batch ends without any sorting.
             uint32_t cls[2]; float bd[2]; uint32_t bi[2];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
@@ -199,62 +209,60 @@ __device__ __forceinline__ void search_layer(const HnswParams& p, WaveState& w, 
                 if (e < nb) {
                     const uint32_t id = w.Bi[e];
                     const float d = w.Bd[e];
-                    const bool el = eligible(id);
-                    bool dup;
-                    if (el) {
-                        const int pos = lower_bound(w.Rd, w.Ri, Rl, d, id);
-                        dup = pos < Rl && w.Rd[pos] == d && (w.Ri[pos] & WV_IDMASK) == id;
-                    } else {
-                        const int pos = lower_bound(w.Sd + Sh, w.Si + Sh, Sl, d, id);
-                        dup = pos < Sl && w.Sd[Sh + pos] == d && w.Si[Sh + pos] == id;
-                        if (!dup) {
-                            uint32_t hh = hash32(id) >> (32 - p.xs_log2);
-                            for (int pr = 0; pr < XS; ++pr) {
-                                const uint32_t v = w.xs[hh];
-                                if (v == id) { dup = true; break; }
-                                if (v == WV_NIL) break;
-                                hh = (hh + 1) & (XS - 1);
+                    if (d < worst || Rl < ef) {
+                        const bool el = eligible(id);
+                        bool dup;
+                        if (el) {
+                            const int pos = lower_bound(w.Rd, w.Ri, Rl, d, id);
+                            dup = pos < Rl && w.Rd[pos] == d && (w.Ri[pos] & WV_IDMASK) == id;
+                        } else {
+                            const int pos = lower_bound(w.Sd + Sh, w.Si + Sh, Sl, d, id);
+                            dup = pos < Sl && w.Sd[Sh + pos] == d && w.Si[Sh + pos] == id;
+                            if (!dup) {
+                                uint32_t hh = hash32(id) >> (32 - p.xs_log2);
+                                for (int pr = 0; pr < XS; ++pr) {
+                                    const uint32_t v = w.xs[hh];
+                                    if (v == id) { dup = true; break; }
+                                    if (v == WV_NIL) break;
+                                    hh = (hh + 1) & (XS - 1);
+                                }
                             }
                         }
-                    }
-                    if (!dup) { cls[h] = el ? 0 : 1; bd[h] = d; bi[h] = id; }
-                }
-            }
-            // ---- bitonic sort of 128 (cls, d, id) keys, 2 per lane ----
-            for (int kk = 2; kk <= 128; kk <<= 1) {
-                for (int j = kk >> 1; j > 0; j >>= 1) {
-                    if (j == 64) {
-                        // partner is the other slot of this lane; element e = lane, asc if (e & kk)==0
-                        const bool asc = ((lane & kk) == 0);
-                        const bool sw = asc ? ckey_less(cls[1], bd[1], bi[1], cls[0], bd[0], bi[0])
-                                            : ckey_less(cls[0], bd[0], bi[0], cls[1], bd[1], bi[1]);
-                        if (sw) {
-                            uint32_t tc = cls[0]; cls[0] = cls[1]; cls[1] = tc;
-                            float td = bd[0]; bd[0] = bd[1]; bd[1] = td;
-                            uint32_t ti = bi[0]; bi[0] = bi[1]; bi[1] = ti;
-                        }
-                    } else {
-#pragma unroll
-                        for (int h = 0; h < 2; ++h) {
-                            const int e = lane + 64 * h;
-                            const uint32_t oc = __shfl_xor(cls[h], j, 64);
-                            const float od = __shfl_xor(bd[h], j, 64);
-                            const uint32_t oi = __shfl_xor(bi[h], j, 64);
-                            const bool asc = ((e & kk) == 0);
-                            const bool lower = (e & j) == 0;
-                            const bool other_less = ckey_less(oc, od, oi, cls[h], bd[h], bi[h]);
-                            const bool self_less = ckey_less(cls[h], bd[h], bi[h], oc, od, oi);
-                            // lower element keeps min when ascending
-                            const bool take = (lower == asc) ? other_less : self_less;
-                            if (take) { cls[h] = oc; bd[h] = od; bi[h] = oi; }
-                        }
+                        if (!dup) { cls[h] = el ? 0 : 1; bd[h] = d; bi[h] = id; }
                     }
                 }
             }
-            const int ne = __popcll(__ballot(cls[0] == 0)) + __popcll(__ballot(cls[1] == 0));
-            const int ns = __popcll(__ballot(cls[0] == 1)) + __popcll(__ballot(cls[1] == 1));
-            w.Cd[lane] = bd[0]; w.Ci[lane] = bi[0];
-            w.Cd[lane + 64] = bd[1]; w.Ci[lane + 64] = bi[1];
+            const uint64_t me0 = __ballot(cls[0] == 0), me1 = __ballot(cls[1] == 0);
+            const uint64_t ms0 = __ballot(cls[0] == 1), ms1 = __ballot(cls[1] == 1);
+            const int ne = __popcll(me0) + __popcll(me1);
+            const int ns = __popcll(ms0) + __popcll(ms1);
+            if (ne + ns == 0) {
+                wave_sync();
+                continue;
+            }
+            // compact the kept keys into the (consumed) raw batch: eligible
+            // [0, ne), ineligible [ne, ne + ns)
+            wave_sync();
+            if (cls[0] == 0) { const int u = mbcnt64(me0); w.Bd[u] = bd[0]; w.Bi[u] = bi[0]; }
+            if (cls[1] == 0) { const int u = __popcll(me0) + mbcnt64(me1); w.Bd[u] = bd[1]; w.Bi[u] = bi[1]; }
+            if (cls[0] == 1) { const int u = ne + mbcnt64(ms0); w.Bd[u] = bd[0]; w.Bi[u] = bi[0]; }
+            if (cls[1] == 1) { const int u = ne + __popcll(ms0) + mbcnt64(ms1); w.Bd[u] = bd[1]; w.Bi[u] = bi[1]; }
+            wave_sync();
+            // rank sort inside each class by (d, id); equal keys (a neighbour
+            // listed twice) keep their batch order
+            for (int u = lane; u < ne + ns; u += 64) {
+                const float d = w.Bd[u];
+                const uint32_t id = w.Bi[u];
+                const int lo = u < ne ? 0 : ne, hi = u < ne ? ne : ne + ns;
+                int r = lo;
+                for (int i = lo; i < hi; ++i) {
+                    const float di = w.Bd[i];
+                    const uint32_t ii = w.Bi[i];
+                    r += key_less(di, ii, d, id) || (i < u && di == d && ii == id);
+                }
+                w.Cd[r] = d;
+                w.Ci[r] = id;
+            }
             wave_sync();
 
             // ---- merge eligible [0, ne) into R (cap ef) ----
