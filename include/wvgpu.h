@@ -30,8 +30,9 @@
  *    the boundary as a dense little-endian uint64 bitmap: bit i of word i/64
  *    set <=> docID i allowed.  allow_bits == NULL means "no filter".
  *  - Results are ascending by distance; equal distances are ordered by id.
- *  - Thread safety: an index may be searched from many threads at once; each
- *    call uses its own stream and scratch.  Uploads (vectors, graph,
+ *  - Thread safety: an index may be searched from many threads at once (calls
+ *    on one index are serialised on its stream; wv_batcher coalesces
+ *    concurrent single-query calls into batches).  Uploads (vectors, graph,
  *    tombstones, config) must not race with searches on the same index.
  */
 #ifndef WVGPU_H
@@ -151,6 +152,21 @@ int wv_last_batch_stats(wv_index *ix, uint64_t *dist_evals, uint64_t *expansions
  * beam-search kernel (milliseconds, summed over the launches of the batch). */
 int wv_index_set_timing(wv_index *ix, int enable);
 int wv_last_kernel_times(wv_index *ix, float *bf_mfma_ms, float *bf_finalize_ms, float *hnsw_ms);
+
+/* Micro-batcher (SURVEY 8b "Threading"): SearchByVector is called once per
+ * request from many threads (adapters/repos/db/index.go:988-1028 ->
+ * shard_read.go:246-252).  wv_batcher_search blocks its caller while a
+ * dispatcher thread coalesces up to max_batch waiting requests (or those that
+ * arrived within max_wait_us of the first) into one wv_search_batch with
+ * per-query allow lists, then returns this caller's row: the same result as
+ * wv_search_by_vector(ix, vector, k, allow_bits, allow_nbits, ...).  Destroy
+ * the batcher before the index. */
+typedef struct wv_batcher wv_batcher;
+int wv_batcher_create(wv_index *ix, int dim, int max_batch, int max_wait_us, wv_batcher **out);
+int wv_batcher_search(wv_batcher *b, const float *vector, int k, const uint64_t *allow_bits, uint64_t allow_nbits,
+                      uint64_t *out_ids, float *out_dists, int32_t *out_n);
+int wv_batcher_stats(wv_batcher *b, uint64_t *requests, uint64_t *batches);
+int wv_batcher_destroy(wv_batcher *b);
 
 const char *wv_last_error(void);
 const char *wv_version(void);

@@ -345,3 +345,36 @@ def test_c4_shape_dot_768_allow_list_sharded(sel):
     torch.cuda.synchronize()
     assert m_n.cpu().tolist() == on.tolist()
     _same(m_i.cpu().numpy().view(np.uint64), m_d.cpu().numpy(), oi, od)
+
+
+def test_batcher_concurrent_single_queries_equal_direct_calls():
+    """SearchByVector from many threads (index.go:988-1028 fan-out): the native
+    micro-batcher coalesces the calls and every caller gets exactly the row a
+    direct wv_search_by_vector call returns -- unfiltered and filtered, mixed k."""
+    import threading
+    n, d = 20000, 64
+    base, qs = _data(n, d, 96, seed=12)
+    rng = np.random.default_rng(13)
+    ix = W.GPUVectorIndex(d, "l2-squared", capacity=n)
+    ix.upload_vectors(base)
+    allows = [None if i % 3 else W.AllowList.from_ids(np.nonzero(rng.random(n) < 0.3)[0], n) for i in range(len(qs))]
+    ks = [10 if i % 2 else 5 for i in range(len(qs))]
+    want = [ix.search_by_vector(qs[i], ks[i], allow=allows[i]) for i in range(len(qs))]
+    b = W.Batcher(ix, max_batch=64, max_wait_us=2000)
+    got = [None] * len(qs)
+
+    def worker(t):
+        for i in range(t, len(qs), 8):
+            got[i] = b.search(qs[i], ks[i], allow=allows[i])
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    st = b.stats()
+    b.close()
+    ix.close()
+    for i in range(len(qs)):
+        _same(got[i][0], got[i][1], want[i][0], want[i][1])
+    assert st["requests"] == len(qs) and st["batches"] < len(qs), st

@@ -69,6 +69,10 @@ SIGNATURES = {
     "wv_last_batch_stats": (C.c_int, [_vp, _u64p, _u64p, _u64p]),
     "wv_index_set_timing": (C.c_int, [_vp, C.c_int]),
     "wv_last_kernel_times": (C.c_int, [_vp, _f32p, _f32p, _f32p]),
+    "wv_batcher_create": (C.c_int, [_vp, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p)]),
+    "wv_batcher_search": (C.c_int, [_vp, _vp, C.c_int, _vp, C.c_uint64, _vp, _vp, _vp]),
+    "wv_batcher_stats": (C.c_int, [_vp, _u64p, _u64p]),
+    "wv_batcher_destroy": (C.c_int, [_vp]),
     "wv_last_error": (C.c_char_p, []),
     "wv_version": (C.c_char_p, []),
 }

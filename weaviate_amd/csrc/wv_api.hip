@@ -663,6 +663,8 @@ void wv_config_default(wv_config* c) {
 }
 
 const char* wv_last_error(void) { return g_err.c_str(); }
+// for wv_batcher.cpp: a request's error is reported on its caller's thread
+void wv_internal_set_error(const char* msg) { g_err = msg ? msg : ""; }
 const char* wv_version(void) { return "wvgpu 0.1 (gfx950)"; }
 
 int wv_index_create(int dim, int metric, const wv_config* cfg, uint64_t capacity, wv_index** out) {

@@ -1,0 +1,203 @@
+// wv_batcher.cpp -- native micro-batcher for concurrent single-query searches.
+//
+// The reference calls VectorIndex.SearchByVector once per request, from many
+// goroutines at once: concurrent HTTP/gRPC requests plus the per-shard errgroup
+// of Index.objectVectorSearch (adapters/repos/db/index.go:988-1028) reach
+// Shard.objectVectorSearch -> SearchByVector (shard_read.go:246-252).  One
+// query is far too little work for a GPU launch, so callers hand their query to
+// a dispatcher thread that coalesces up to max_batch waiting requests (or what
+// arrived within max_wait_us of the first) into one wv_search_batch call and
+// fans the rows back out.  Each caller blocks until its own row is written;
+// no caller pointer is kept after its call returns (cgo pointer rules).
+//
+// Requests are grouped by (k, filtered): searchTimeEF depends on k
+// (search.go:30-62), and a filtered group carries one allow bitmap per query
+// (allow_stride_words), so the AUTO dispatch of search.go:64-79 (flat vs HNSW
+// by allowList.Len()) is still decided per query inside the batch.
+#include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/wvgpu.h"
+
+extern "C" void wv_internal_set_error(const char* msg);
+
+namespace {
+
+struct Request {
+    const float* q;
+    int k;
+    const uint64_t* allow;
+    uint64_t allow_nbits;
+    uint64_t* out_ids;
+    float* out_d;
+    int32_t* out_n;
+    int rc = WV_OK;
+    std::string err;
+    bool done = false;
+};
+
+}  // namespace
+
+struct wv_batcher {
+    wv_index* ix = nullptr;
+    int dim = 0;
+    int max_batch = 256;
+    int max_wait_us = 200;
+    std::mutex mu;
+    std::condition_variable cv_work, cv_done;
+    std::deque<Request*> queue;
+    bool stop = false;
+    std::thread th;
+    uint64_t n_requests = 0, n_batches = 0, n_launch_rows = 0;
+
+    void run_group(std::vector<Request*>& g) {
+        const int n = (int)g.size();
+        const int k = g[0]->k;
+        const bool filtered = g[0]->allow != nullptr;
+        std::vector<float> q((size_t)n * dim);
+        for (int i = 0; i < n; ++i) std::memcpy(q.data() + (size_t)i * dim, g[i]->q, sizeof(float) * dim);
+        std::vector<uint64_t> bits;
+        uint64_t nbits = 0, stride = 0;
+        if (filtered) {
+            for (Request* r : g) nbits = std::max(nbits, r->allow_nbits);
+            stride = (nbits + 63) / 64;
+            bits.assign((size_t)n * std::max<uint64_t>(stride, 1), 0);
+            for (int i = 0; i < n; ++i) {
+                const uint64_t w = (g[i]->allow_nbits + 63) / 64;
+                std::memcpy(bits.data() + (size_t)i * stride, g[i]->allow, w * 8);
+                if (g[i]->allow_nbits & 63)   // bits past a request's own nbits are not allowed
+                    bits[(size_t)i * stride + w - 1] &= (1ull << (g[i]->allow_nbits & 63)) - 1;
+            }
+        }
+        std::vector<uint64_t> ids((size_t)n * k);
+        std::vector<float> ds((size_t)n * k);
+        std::vector<int32_t> cnt(n);
+        const int rc = wv_search_batch(ix, q.data(), n, k, 0, filtered ? bits.data() : nullptr, nbits, stride,
+                                       WV_MODE_AUTO, ids.data(), ds.data(), cnt.data());
+        const std::string msg = rc ? wv_last_error() : "";
+        std::lock_guard<std::mutex> l(mu);
+        for (int i = 0; i < n; ++i) {
+            Request* r = g[i];
+            r->rc = rc;
+            if (rc) {
+                r->err = msg;
+            } else {
+                const int m = cnt[i];
+                std::memcpy(r->out_ids, ids.data() + (size_t)i * k, sizeof(uint64_t) * m);
+                std::memcpy(r->out_d, ds.data() + (size_t)i * k, sizeof(float) * m);
+                *r->out_n = m;
+            }
+            r->done = true;
+        }
+        n_batches++;
+        n_launch_rows += n;
+        cv_done.notify_all();
+    }
+
+    void loop() {
+        std::unique_lock<std::mutex> l(mu);
+        for (;;) {
+            cv_work.wait(l, [&] { return stop || !queue.empty(); });
+            if (queue.empty() && stop) return;
+            // the window opens with the first waiting request
+            const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(max_wait_us);
+            cv_work.wait_until(l, deadline, [&] { return stop || (int)queue.size() >= max_batch; });
+            std::vector<Request*> take;
+            while (!queue.empty() && (int)take.size() < max_batch) {
+                take.push_back(queue.front());
+                queue.pop_front();
+            }
+            l.unlock();
+            // group by (k, filtered), keeping arrival order inside a group
+            std::vector<bool> used(take.size(), false);
+            for (size_t i = 0; i < take.size(); ++i) {
+                if (used[i]) continue;
+                std::vector<Request*> g;
+                for (size_t j = i; j < take.size(); ++j) {
+                    if (used[j] || take[j]->k != take[i]->k ||
+                        (take[j]->allow != nullptr) != (take[i]->allow != nullptr))
+                        continue;
+                    used[j] = true;
+                    g.push_back(take[j]);
+                }
+                run_group(g);
+            }
+            l.lock();
+        }
+    }
+};
+
+extern "C" {
+
+int wv_batcher_create(wv_index* ix, int dim, int max_batch, int max_wait_us, wv_batcher** out) {
+    if (!ix || !out || dim <= 0 || max_batch <= 0 || max_wait_us < 0) {
+        wv_internal_set_error("wv_batcher_create: bad argument");
+        return WV_EINVAL;
+    }
+    auto* b = new wv_batcher();
+    b->ix = ix;
+    b->dim = dim;
+    b->max_batch = max_batch;
+    b->max_wait_us = max_wait_us;
+    b->th = std::thread([b] { b->loop(); });
+    *out = b;
+    return WV_OK;
+}
+
+int wv_batcher_search(wv_batcher* b, const float* vector, int k, const uint64_t* allow_bits, uint64_t allow_nbits,
+                      uint64_t* out_ids, float* out_dists, int32_t* out_n) {
+    if (!b || !vector || k <= 0 || !out_ids || !out_dists || !out_n) {
+        wv_internal_set_error("wv_batcher_search: bad argument");
+        return WV_EINVAL;
+    }
+    Request r;
+    r.q = vector;
+    r.k = k;
+    r.allow = allow_bits;
+    r.allow_nbits = allow_bits ? allow_nbits : 0;
+    r.out_ids = out_ids;
+    r.out_d = out_dists;
+    r.out_n = out_n;
+    {
+        std::unique_lock<std::mutex> l(b->mu);
+        if (b->stop) {
+            wv_internal_set_error("wv_batcher_search: batcher is shut down");
+            return WV_ESTATE;
+        }
+        b->queue.push_back(&r);
+        b->n_requests++;
+        b->cv_work.notify_one();
+        b->cv_done.wait(l, [&] { return r.done; });
+    }
+    if (r.rc) wv_internal_set_error(r.err.c_str());
+    return r.rc;
+}
+
+int wv_batcher_stats(wv_batcher* b, uint64_t* requests, uint64_t* batches) {
+    if (!b) return WV_EINVAL;
+    std::lock_guard<std::mutex> l(b->mu);
+    if (requests) *requests = b->n_requests;
+    if (batches) *batches = b->n_batches;
+    return WV_OK;
+}
+
+int wv_batcher_destroy(wv_batcher* b) {
+    if (!b) return WV_OK;
+    {
+        std::lock_guard<std::mutex> l(b->mu);
+        b->stop = true;
+    }
+    b->cv_work.notify_all();
+    if (b->th.joinable()) b->th.join();   // drains the queue before it exits
+    delete b;
+    return WV_OK;
+}
+
+}  // extern "C"

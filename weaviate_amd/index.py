@@ -210,6 +210,45 @@ class GPUVectorIndex:
         return {"dist_evals": a.value, "expansions": b.value, "fallbacks": c.value}
 
 
+class Batcher:
+    """Native micro-batcher over one index (wv_batcher_*): `search` has the
+    signature and result of GPUVectorIndex.search_by_vector and is meant to be
+    called from many threads at once (ctypes releases the GIL for the call)."""
+
+    def __init__(self, index: GPUVectorIndex, max_batch: int = 256, max_wait_us: int = 200):
+        self.index = index
+        h = C.c_void_p()
+        check(lib().wv_batcher_create(index._h, index.dim, max_batch, max_wait_us, C.byref(h)))
+        self._h = h
+
+    def search(self, vector, k: int, allow: Optional[AllowList] = None):
+        q = np.ascontiguousarray(vector, dtype=np.float32)
+        if q.size != self.index.dim:
+            raise WvError(1, f"vector lengths don't match: {q.size} vs {self.index.dim}")
+        bits, nb, _ = GPUVectorIndex._allow_args(allow)
+        ids = np.zeros(k, np.uint64)
+        ds = np.zeros(k, np.float32)
+        n = np.zeros(1, np.int32)
+        check(lib().wv_batcher_search(self._h, _ptr(q), k, _ptr(bits), nb, _ptr(ids), _ptr(ds), _ptr(n)))
+        return ids[: n[0]], ds[: n[0]]
+
+    def stats(self):
+        a, b = C.c_uint64(), C.c_uint64()
+        check(lib().wv_batcher_stats(self._h, C.byref(a), C.byref(b)))
+        return {"requests": a.value, "batches": b.value}
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().wv_batcher_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def merge_shards_device(in_d_ptr, in_ids_ptr, in_n_ptr, n_shards, nq, k, out_d_ptr, out_ids_ptr, out_n_ptr, stream=0):
     """Merge per-shard (dist, id) lists on the device (after the RCCL all-gather)."""
     check(lib().wv_merge_shards_device(C.c_void_p(in_d_ptr), C.c_void_p(in_ids_ptr), C.c_void_p(in_n_ptr), n_shards,
