@@ -75,9 +75,12 @@ __device__ __forceinline__ int lower_bound(const float* ad, const uint32_t* ai, 
 }
 
 template <int METRIC>
-__device__ __forceinline__ void search_layer(const HnswParams& p, WaveState& w, int level, int ef, uint32_t ep, float epd,
-                             const uint64_t* allow, int& Rl, int& Sh, int& Sl, int& status, int nlt,
-                             uint32_t& n_dist, uint32_t& n_exp) {
+__device__ __forceinline__ void search_layer(const HnswParams& p, WaveState& w_io, int level, int ef, uint32_t ep,
+                             float epd, const uint64_t* allow, int& Rl_out, int& Sh_out, int& Sl_out, int& status,
+                             int nlt, uint32_t& n_dist, uint32_t& n_exp) {
+    // the state lives in registers for the whole layer (LDS pointers and the
+    // R / S lengths are wave-uniform); written back once at the end
+    WaveState w = w_io;
     const int lane = threadIdx.x & 63;
     const int VC = 1 << p.vc_log2;
     const int XS = 1 << p.xs_log2;
@@ -95,14 +98,14 @@ __device__ __forceinline__ void search_layer(const HnswParams& p, WaveState& w, 
 
     // insertViableEntrypointsAsCandidatesAndResults (search.go:329-353)
     if (lane == 0) w.vc[hash32(ep) >> (32 - p.vc_log2)] = ep;
-    Rl = 0; Sh = 0; Sl = 0;
-    if (eligible(ep)) {
-        if (lane == 0) { w.Rd[0] = epd; w.Ri[0] = ep; }
-        Rl = 1;
-    } else {
-        if (lane == 0) { w.Sd[0] = epd; w.Si[0] = ep; }
-        Sl = 1;
+    const bool ep_ok = eligible(ep);
+    if (lane == 0) {
+        float* dd = ep_ok ? w.Rd : w.Sd;
+        uint32_t* di = ep_ok ? w.Ri : w.Si;
+        dd[0] = epd;
+        di[0] = ep;
     }
+    int Rl = ep_ok ? 1 : 0, Sh = 0, Sl = ep_ok ? 0 : 1;
     wave_sync();
     // currentWorstResultDistanceToFloat (:355-377)
     float worst = Rl > 0 ? w.Rd[Rl - 1] : FLT_MAX;
@@ -320,6 +323,10 @@ __device__ __forceinline__ void search_layer(const HnswParams& p, WaveState& w, 
             wave_sync();
         }
     }
+    Rl_out = Rl;
+    Sh_out = Sh;
+    Sl_out = Sl;
+    w_io = w;
 }
 
 template <int METRIC>
