@@ -26,6 +26,7 @@ class Stats(C.Structure):
         ("visited", C.c_uint64),
         ("max_cand", C.c_uint64),
         ("layer0_visited_max", C.c_uint64),
+        ("ties", C.c_uint64),
     ]
 
     def asdict(self):

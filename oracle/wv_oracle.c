@@ -575,6 +575,9 @@ static void search_layer(wvo_index *h, ctx_t *c, const float *q, pq_t *eps,
         if (dist > worst) break;
         pq_item candidate = pq_pop(cand);
         uint64_t cid = candidate.id;
+        /* diagnostics only: an equal-distance candidate left on the heap means
+         * the expansion order depends on heap layout */
+        if (cand->len > 0 && cand->it[0].dist == candidate.dist) c->st.ties++;
         /* :217-254 */
         nlock(h, cid);
         if (h->level[cid] < 0 || h->conns[cid] == NULL) { nunlock(h, cid); continue; }
@@ -597,6 +600,7 @@ static void search_layer(wvo_index *h, ctx_t *c, const float *q, pq_t *eps,
             ctx_visit(c, nb);
             float d;
             if (!dist_node_vec(h, c, nb, q, &d)) continue;
+            if (d == worst && (int)results->len >= ef) c->st.ties++;
             if (d < worst || (int)results->len < ef) {
                 pq_insert(cand, nb, d);
                 if (level == 0 && allow && !allow_contains(allow, allow_nbits, nb)) continue;
@@ -1269,6 +1273,7 @@ int wvo_search_batch(wvo_index *h, const float *qs, int nq, int k, int ef,
         tot.expansions += args[t].st.expansions;
         tot.nbr_slots += args[t].st.nbr_slots;
         tot.visited += args[t].st.visited;
+        tot.ties += args[t].st.ties;
         if (args[t].st.max_cand > tot.max_cand) tot.max_cand = args[t].st.max_cand;
         if (args[t].st.layer0_visited_max > tot.layer0_visited_max)
             tot.layer0_visited_max = args[t].st.layer0_visited_max;

@@ -61,6 +61,7 @@ typedef struct {
     uint64_t visited;      /* visited-set insertions                              */
     uint64_t max_cand;     /* high-water mark of the candidate heap               */
     uint64_t layer0_visited_max; /* max visited count of one layer-0 search      */
+    uint64_t ties;         /* decisions taken between equal distances (heap order) */
 } wvo_stats;
 
 wvo_index *wvo_create(int dim, int metric, int max_connections,

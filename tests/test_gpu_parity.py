@@ -378,3 +378,40 @@ def test_batcher_concurrent_single_queries_equal_direct_calls():
     for i in range(len(qs)):
         _same(got[i][0], got[i][1], want[i][0], want[i][1])
     assert st["requests"] == len(qs) and st["batches"] < len(qs), st
+
+
+def test_hnsw_large_batch_parity_modulo_ties():
+    """At scale fp32 distances tie (tens of thousands of evaluations per
+    query): the reference then decides by heap layout, the GPU by (dist, id).
+    Every query must be identical up to the order among equal distances,
+    unless the restatement itself took a decision between equal distances
+    (counted by the oracle); and the lossy LDS visited cache must never change
+    a result, whatever its size."""
+    import os
+    n, d, nq, ef = 50000, 64, 4000, 64
+    rng = np.random.default_rng(31)
+    base = rng.random((n, d), dtype=np.float32)
+    qs = rng.random((nq, d), dtype=np.float32)
+    ref = O.Index(d, "l2-squared", 32, 64, capacity=n, seed=5)
+    ref.add_batch(base, threads=8)
+    ix = W.GPUVectorIndex(d, "l2-squared", capacity=n, max_connections=32)
+    ix.upload_vectors(base)
+    ix.upload_graph(ref.export_graph())
+    gi, gd, gn = ix.search_batch(qs, 10, ef=ef, mode="hnsw")
+    oi, od, on, _ = ref.search_batch(qs, 10, ef, threads=8)
+    unexplained = []
+    for i in range(nq):
+        try:
+            _same_tie_aware(gi[i], gd[i], oi[i], od[i])
+        except AssertionError:
+            if ref.knn_search(qs[i], 10, ef, with_stats=True)[2]["ties"] == 0:
+                unexplained.append(i)
+    assert not unexplained, unexplained[:10]
+    for kb in ("6", "32"):
+        os.environ["WV_HNSW_WAVE_KB"] = kb
+        try:
+            hi, hd, _ = ix.search_batch(qs, 10, ef=ef, mode="hnsw")
+        finally:
+            os.environ.pop("WV_HNSW_WAVE_KB")
+        assert (hi == gi).all() and np.array_equal(hd.view(np.uint32), gd.view(np.uint32))
+    ix.close()
