@@ -66,7 +66,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", choices=["exact", "hnsw"], default="exact")
-    ap.add_argument("--n", type=int, default=1_000_000)
+    ap.add_argument("--rows", type=int, default=1_000_000, help="corpus rows N (all shards)")
     ap.add_argument("--dim", type=int, default=128)
     ap.add_argument("--nq", type=int, default=10_000)
     ap.add_argument("--k", type=int, default=10)
@@ -78,6 +78,9 @@ def main():
     ap.add_argument("--hnsw-build-threads", type=int, default=16)
     ap.add_argument("--M", type=int, default=64, help="hnsw maxConnections (layer-0 degree 2M)")
     ap.add_argument("--efc", type=int, default=128, help="hnsw efConstruction")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (RCCL over xGMI, the product path); gloo only to rehearse N ranks on one GPU")
+    ap.add_argument("--dump-ids", default="", help="rank 0 saves the final ids/dists (npz) for cross-N checks")
     ap.add_argument("--graph-cache", default="", help="npz path: load the hnsw graph if present, else build and save")
     args = ap.parse_args()
 
@@ -87,20 +90,25 @@ def main():
 
     import weaviate_amd as W
 
+    gpu = local % max(torch.cuda.device_count(), 1)
     if ws > 1:
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+        if args.dist_backend == "nccl":
+            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(backend="gloo")
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
+    gloo = ws > 1 and args.dist_backend == "gloo"
 
     # ---- corpus shard of this rank (contiguous id range) ----
-    N, D, NQ, K = args.n, args.dim, args.nq, args.k
+    N, D, NQ, K = args.rows, args.dim, args.nq, args.k
     lo = N * rank // ws
     hi = N * (rank + 1) // ws
     n_local = hi - lo
     base = counter_uniform(1, lo, n_local, D)
     queries = counter_uniform(2, 0, NQ, D)
 
-    ix = W.GPUVectorIndex(D, args.metric, capacity=max(n_local, 1), device=local, id_base=lo,
+    ix = W.GPUVectorIndex(D, args.metric, capacity=max(n_local, 1), device=gpu, id_base=lo,
                           max_connections=args.M)
     ix.upload_vectors(base)
     mode = "exact"
@@ -160,9 +168,15 @@ def main():
         if timed:
             kern_ms.append(ix.last_kernel_times())
         if ws > 1:
-            dist.all_gather_into_tensor(g_ids, out_ids)
-            dist.all_gather_into_tensor(g_d, out_d)
-            dist.all_gather_into_tensor(g_n, out_n)
+            if gloo:   # rehearsal only: the gather goes through host memory
+                for g, o in ((g_ids, out_ids), (g_d, out_d), (g_n, out_n)):
+                    parts = [torch.empty_like(o, device="cpu") for _ in range(ws)]
+                    dist.all_gather(parts, o.cpu())
+                    g.copy_(torch.stack(parts).to(dev))
+            else:
+                dist.all_gather_into_tensor(g_ids, out_ids)
+                dist.all_gather_into_tensor(g_d, out_d)
+                dist.all_gather_into_tensor(g_n, out_n)
             W.merge_shards_device(g_d.data_ptr(), g_ids.data_ptr(), g_n.data_ptr(), ws, NQ, K, m_d.data_ptr(),
                                   m_ids.data_ptr(), m_n.data_ptr(), stream=stream)
 
@@ -182,7 +196,7 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     if ws > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if gloo else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     stats = ix.last_batch_stats()
@@ -190,6 +204,8 @@ def main():
     final_ids = (m_ids if ws > 1 else out_ids).cpu().numpy().view(np.uint64)
     final_d = (m_d if ws > 1 else out_d).cpu().numpy()
 
+    if args.dump_ids and rank == 0:
+        np.savez(args.dump_ids, ids=final_ids, dists=final_d)
     qps = NQ * args.steps / elapsed
     result = {
         "metric": METRIC,

@@ -5,7 +5,7 @@ mkdir -p gpurun_out
 N=${HN:-1000000}
 TAG=${TAG:-r01_hnsw}
 CACHE=/tmp/wv_graph_${N}.npz
-ARGS="--workload hnsw --n $N --ef ${EF:-64} --graph-cache $CACHE"
+ARGS="--workload hnsw --rows $N --ef ${EF:-64} --graph-cache $CACHE"
 timeout -k 10 1000 python -u bench.py $ARGS --steps 3 --warmup 1 --cpu-seconds 10 > gpurun_out/bench_hnsw.log 2>&1
 rc=$?; echo "bench rc=$rc"; tail -1 gpurun_out/bench_hnsw.log | cut -c1-3000
 [ $rc -eq 0 ] || exit $rc
