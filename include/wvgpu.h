@@ -153,6 +153,46 @@ int wv_last_batch_stats(wv_index *ix, uint64_t *dist_evals, uint64_t *expansions
 int wv_index_set_timing(wv_index *ix, int enable);
 int wv_last_kernel_times(wv_index *ix, float *bf_mfma_ms, float *bf_finalize_ms, float *hnsw_ms);
 
+/* HNSW commit log -> CSR.  Replays the write-ahead log a
+ * Weaviate shard persists (adapters/repos/db/vector/hnsw/commitlog/logger.go
+ * record layouts) exactly as Deserializer.Do does at startup
+ * (deserializer.go:80-158, startup.go:56-152), so a GPU mirror can serve an
+ * existing shard without rebuilding its graph.  Never modifies the files: a
+ * record torn at the end of a file is reported (info.truncated) and the state
+ * keeps every complete record, as the reference does before truncating. */
+typedef struct wv_graph wv_graph;
+typedef struct {
+    uint64_t n_slots;        /* highest live node id + 1 */
+    uint64_t entrypoint;
+    uint64_t n_upper;        /* nodes with level >= 1 */
+    uint64_t n_tombstones;
+    uint64_t valid_bytes;    /* bytes of complete records over all files */
+    int max_level;           /* SetEntryPointMaxLevel's level */
+    int max_node_level;      /* highest level field of a live node */
+    int max_deg0, max_degU;  /* longest layer-0 / upper neighbour list */
+    int compressed;          /* an AddPQ record was seen: PQ is not served by the GPU */
+    int truncated;           /* a file ended inside a record */
+} wv_graph_info;
+/* one log held in memory */
+int wv_graph_load_commitlog_buffer(const uint8_t *buf, uint64_t len, wv_graph **out);
+/* log files in the given order */
+int wv_graph_load_commitlogs(const char *const *paths, int n_paths, wv_graph **out);
+/* <root>/<name>.hnsw.commitlog.d: files ordered by timestamp name
+ * (commit_logger.go:121-166), temporaries and hidden files ignored, a
+ * .condensed file whose original still exists skipped
+ * (corrupt_commit_logs_fixer.go:43-70) */
+int wv_graph_load_commitlog_dir(const char *dir, wv_graph **out);
+int wv_graph_get_info(const wv_graph *g, wv_graph_info *info);
+/* one node: *node_level = -1 for a nil node; up to cap links of `level` copied,
+ * *n_links = the list length */
+int wv_graph_node(const wv_graph *g, uint64_t id, int level, int *node_level, uint64_t *links, int cap, int *n_links);
+/* The CSR of wv_index_upload_graph for n = info.n_slots nodes:
+ * levels[n], layer0[n*deg0], upper_row[n], upper[info.n_upper*max(1,info.max_node_level)*degU],
+ * tomb_bits[(n+63)/64] (nullable).  deg0 >= info.max_deg0, degU >= info.max_degU. */
+int wv_graph_export_csr(wv_graph *g, int deg0, int degU, int8_t *levels, uint32_t *layer0, uint32_t *upper_row,
+                        uint32_t *upper, uint64_t *tomb_bits);
+int wv_graph_destroy(wv_graph *g);
+
 /* Micro-batcher (SURVEY 8b "Threading"): SearchByVector is called once per
  * request from many threads (adapters/repos/db/index.go:988-1028 ->
  * shard_read.go:246-252).  wv_batcher_search blocks its caller while a

@@ -68,6 +68,9 @@ def lib():
             "wvo_remove_tombstone": (C.c_int, [vp, C.c_uint64]),
             "wvo_import_node": (C.c_int, [vp, C.c_uint64, C.c_int, u64p, i32p]),
             "wvo_set_entrypoint": (None, [vp, C.c_uint64, C.c_int]),
+            "wvo_log_enable": (None, [vp, C.c_int]),
+            "wvo_log_size": (C.c_uint64, [vp]),
+            "wvo_log_copy": (C.c_uint64, [vp, vp, C.c_uint64]),
             "wvo_import_csr": (C.c_int, [vp, C.c_uint64, fp, vp, vp, C.c_int, vp, vp, C.c_int, C.c_int,
                                          C.c_uint64]),
             "wvo_graph_info": (None, [vp, u64p, u64p, i32p, u64p]),
@@ -187,6 +190,16 @@ class Index:
             flat = np.zeros(1, np.uint64)
         counts = np.array([len(lvl) for lvl in conns_per_level], dtype=np.int32)
         assert lib().wvo_import_node(self.h, id_, level, _u64(flat), _i32(counts)) == 0
+
+    def enable_commit_log(self, on=True):
+        """Record the commit log the reference would write (logger.go)."""
+        lib().wvo_log_enable(self.h, int(on))
+
+    def commit_log(self) -> bytes:
+        n = lib().wvo_log_size(self.h)
+        buf = (C.c_uint8 * max(n, 1))()
+        lib().wvo_log_copy(self.h, buf, n)
+        return bytes(buf[:n])
 
     def import_graph(self, vecs, g):
         """Restore vectors + graph from export_graph()'s CSR (inverse of export)."""

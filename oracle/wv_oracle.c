@@ -383,7 +383,88 @@ struct wvo_index {
     /* search config (index.go:79-87) */
     int64_t ef, ef_min, ef_max, ef_factor, flat_cutoff;
     int forbid_flat;
+    /* commit log (commitlog/logger.go), written where the reference writes it */
+    int log_on;
+    uint8_t *log;
+    size_t log_len, log_cap;
+    pthread_mutex_t log_lock;
 };
+
+/* ---- commit log records -- commitlog/logger.go:28-215 (little endian) ---- */
+enum { CL_ADD_NODE = 0, CL_SET_EP = 1, CL_ADD_LINK = 2, CL_REPLACE_LINKS = 3, CL_ADD_TOMB = 4,
+       CL_REMOVE_TOMB = 5, CL_CLEAR_LINKS = 6, CL_DELETE_NODE = 7, CL_RESET = 8, CL_CLEAR_LINKS_AT_LEVEL = 9,
+       CL_ADD_LINKS = 10 };
+
+static void log_bytes(wvo_index *h, const uint8_t *b, size_t n) {
+    if (h->log_len + n > h->log_cap) {
+        size_t c = h->log_cap ? h->log_cap * 2 : 1 << 16;
+        while (c < h->log_len + n) c *= 2;
+        h->log = (uint8_t *)realloc(h->log, c);
+        h->log_cap = c;
+    }
+    memcpy(h->log + h->log_len, b, n);
+    h->log_len += n;
+}
+static void put64(uint8_t *p, uint64_t v) { for (int i = 0; i < 8; i++) p[i] = (uint8_t)(v >> (8 * i)); }
+static void put16(uint8_t *p, uint16_t v) { p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); }
+
+/* AddNode / SetEntryPointWithMaxLayer / AddLinkAtLevel / AddTombstone /
+ * ClearLinksAtLevel (logger.go:59-75,98-106,170-176,194-201) */
+static void log_id_level(wvo_index *h, int type, uint64_t id, int level) {
+    if (!h->log_on) return;
+    uint8_t b[11];
+    b[0] = (uint8_t)type;
+    put64(b + 1, id);
+    put16(b + 9, (uint16_t)level);
+    pthread_mutex_lock(&h->log_lock);
+    log_bytes(h, b, 11);
+    pthread_mutex_unlock(&h->log_lock);
+}
+static void log_add_link(wvo_index *h, uint64_t id, int level, uint64_t target) {
+    if (!h->log_on) return;
+    uint8_t b[19];
+    b[0] = CL_ADD_LINK;
+    put64(b + 1, id);
+    put16(b + 9, (uint16_t)level);
+    put64(b + 11, target);
+    pthread_mutex_lock(&h->log_lock);
+    log_bytes(h, b, 19);
+    pthread_mutex_unlock(&h->log_lock);
+}
+/* ReplaceLinksAtLevel (logger.go:125-168): 13-byte header + 8 bytes per target */
+static void log_replace_links(wvo_index *h, uint64_t id, int level, const uint32_t *t, uint32_t n) {
+    if (!h->log_on) return;
+    uint8_t hd[13];
+    hd[0] = CL_REPLACE_LINKS;
+    put64(hd + 1, id);
+    put16(hd + 9, (uint16_t)level);
+    put16(hd + 11, (uint16_t)n);
+    pthread_mutex_lock(&h->log_lock);
+    log_bytes(h, hd, 13);
+    for (uint32_t i = 0; i < n; i++) {
+        uint8_t v[8];
+        put64(v, t[i]);
+        log_bytes(h, v, 8);
+    }
+    pthread_mutex_unlock(&h->log_lock);
+}
+static void log_id(wvo_index *h, int type, uint64_t id) {
+    if (!h->log_on) return;
+    uint8_t b[9];
+    b[0] = (uint8_t)type;
+    put64(b + 1, id);
+    pthread_mutex_lock(&h->log_lock);
+    log_bytes(h, b, 9);
+    pthread_mutex_unlock(&h->log_lock);
+}
+
+void wvo_log_enable(wvo_index *h, int on) { h->log_on = on; }
+uint64_t wvo_log_size(wvo_index *h) { return h->log_len; }
+uint64_t wvo_log_copy(wvo_index *h, uint8_t *out, uint64_t cap) {
+    uint64_t n = h->log_len < cap ? h->log_len : cap;
+    if (n) memcpy(out, h->log, n);
+    return n;
+}
 
 /* per-thread search context: the visited.ListSet (visited/list_set.go:23-64)
  * restated as an epoch array; a fresh epoch == a freshly borrowed list. */
@@ -452,6 +533,7 @@ wvo_index *wvo_create(int dim, int metric, int max_connections,
     for (uint64_t i = 0; i < capacity; i++) pthread_mutex_init(&h->node_lock[i], NULL);
     pthread_rwlock_init(&h->glock, NULL);
     pthread_mutex_init(&h->init_lock, NULL);
+    pthread_mutex_init(&h->log_lock, NULL);
     h->next_level = -1;
     /* entities/vectorindex/hnsw/config.go:33-50 defaults */
     h->ef = -1; h->ef_min = 100; h->ef_max = 500; h->ef_factor = 8;
@@ -469,7 +551,7 @@ void wvo_destroy(wvo_index *h) {
         pthread_mutex_destroy(&h->node_lock[i]);
     }
     free(h->conns); free(h->vecs); free(h->has_vec); free(h->level);
-    free(h->maint); free(h->tomb); free(h->node_lock);
+    free(h->maint); free(h->tomb); free(h->node_lock); free(h->log);
     free(h);
 }
 
@@ -856,6 +938,7 @@ static void connect_neighbor(wvo_index *h, uint64_t node, uint64_t nb, int level
     int maxc = level == 0 ? h->M0 : h->M;
     if ((int)cl->len < maxc) {
         conn_append(cl, (uint32_t)node);
+        log_add_link(h, nb, level, node);                 /* :155 */
     } else {
         float d = metric_dist(h->metric, vec_of(h, node), vec_of(h, nb), h->dim);
         pq_t cands;
@@ -869,7 +952,12 @@ static void connect_neighbor(wvo_index *h, uint64_t node, uint64_t nb, int level
         }
         select_neighbors_heuristic(h, &cands, maxc);
         cl->len = 0;
-        while (cands.len > 0) conn_append(cl, (uint32_t)pq_pop(&cands).id);
+        log_id_level(h, CL_CLEAR_LINKS_AT_LEVEL, nb, level);   /* :194-197 */
+        while (cands.len > 0) {
+            uint64_t id = pq_pop(&cands).id;
+            conn_append(cl, (uint32_t)id);
+            log_add_link(h, nb, level, id);                   /* :199-205 */
+        }
         pq_free(&cands);
     }
     nunlock(h, nb);
@@ -925,6 +1013,7 @@ static void find_and_connect(wvo_index *h, ctx_t *c, uint64_t node, uint64_t ep,
         while (res.len > 0) nbrs[nn++] = (uint32_t)pq_pop(&res).id;
         nlock(h, node);
         conn_set(&h->conns[node][level], nbrs, (uint32_t)nn); /* setConnectionsAtLevel */
+        log_replace_links(h, node, level, nbrs, (uint32_t)nn); /* :111 */
         nunlock(h, node);
         for (int i = 0; i < nn; i++) connect_neighbor(h, node, nbrs[i], level);
         if (nn > 0) {
@@ -954,8 +1043,10 @@ static int insert_node(wvo_index *h, ctx_t *c, uint64_t id, int forced_level) {
         h->initial_done = 1;
         if (atomic_load(&h->n_nodes) == 0) {
             was_first = 1;
+            log_id_level(h, CL_SET_EP, id, 0);                /* insertInitialElement :71 */
             h->conns[id] = alloc_levels(0, h->M, h->M0);
             h->level[id] = 0;
+            log_id_level(h, CL_ADD_NODE, id, 0);              /* :81 */
             if (h->threaded) pthread_rwlock_wrlock(&h->glock);
             h->ep = id;
             h->max_layer = 0;
@@ -987,6 +1078,7 @@ static int insert_node(wvo_index *h, ctx_t *c, uint64_t id, int forced_level) {
     h->conns[id] = cl;
     h->level[id] = (int8_t)target;
     nunlock(h, id);
+    log_id_level(h, CL_ADD_NODE, id, target);             /* insert.go:148 */
     atomic_fetch_add(&h->n_nodes, 1);
 
     ep = find_best_entrypoint(h, c, cur_max, target, ep, vec);
@@ -995,6 +1087,7 @@ static int insert_node(wvo_index *h, ctx_t *c, uint64_t id, int forced_level) {
 
     if (h->threaded) pthread_rwlock_wrlock(&h->glock);
     if (target > h->max_layer) {
+        log_id_level(h, CL_SET_EP, id, target);           /* insert.go:206 */
         h->ep = id;
         h->max_layer = target;
     }
@@ -1070,6 +1163,7 @@ int wvo_add_batch(wvo_index *h, uint64_t first_id, const float *vecs, uint64_t n
 int wvo_add_tombstone(wvo_index *h, uint64_t id) {
     if (id >= h->cap) return -1;
     h->tomb[id] = 1;
+    log_id(h, CL_ADD_TOMB, id);                           /* delete.go -> AddTombstone */
     return 0;
 }
 int wvo_remove_tombstone(wvo_index *h, uint64_t id) {

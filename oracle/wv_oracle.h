@@ -92,6 +92,10 @@ int wvo_import_node(wvo_index *h, uint64_t id, int level,
 int wvo_import_csr(wvo_index *h, uint64_t n, const float *vecs, const int8_t *levels, const uint32_t *layer0,
                    int deg0, const uint32_t *upper_row, const uint32_t *upper, int degU, int max_level,
                    uint64_t entrypoint);
+/* commit log written during builds (commitlog/logger.go record layouts) */
+void wvo_log_enable(wvo_index *h, int on);
+uint64_t wvo_log_size(wvo_index *h);
+uint64_t wvo_log_copy(wvo_index *h, uint8_t *out, uint64_t cap);
 void wvo_set_entrypoint(wvo_index *h, uint64_t ep, int max_level);
 
 /* graph export for the GPU CSR upload */

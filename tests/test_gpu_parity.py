@@ -415,3 +415,29 @@ def test_hnsw_large_batch_parity_modulo_ties():
             os.environ.pop("WV_HNSW_WAVE_KB")
         assert (hi == gi).all() and np.array_equal(hd.view(np.uint32), gd.view(np.uint32))
     ix.close()
+
+
+def test_graph_replayed_from_commit_log_serves_identical_searches():
+    """a shard's persisted commit log (written by the
+    restatement exactly where insert.go / neighbor_connections.go write it)
+    replayed into the GPU index answers like the in-memory index, tombstones
+    included."""
+    n, d = 5000, 32
+    rng = np.random.default_rng(41)
+    base = rng.random((n, d), dtype=np.float32)
+    qs = rng.random((200, d), dtype=np.float32)
+    ref = O.Index(d, "l2-squared", 16, 64, capacity=n, seed=9)
+    ref.enable_commit_log()
+    ref.add_batch(base, threads=1)
+    tomb = np.nonzero(rng.random(n) < 0.02)[0]
+    for t in tomb:
+        ref.add_tombstone(int(t))
+    g = W.CommitLogGraph(ref.commit_log())
+    ix = W.GPUVectorIndex(d, "l2-squared", capacity=n, max_connections=16)
+    ix.upload_vectors(base)
+    ix.upload_graph_from_commitlog(g)
+    ids, ds, cnt = ix.search_batch(qs, 10, ef=64, mode="hnsw")
+    oi, od, on, _ = ref.search_batch(qs, 10, 64)
+    assert not set(ids.ravel().tolist()) & set(tomb.tolist())
+    _same(ids, ds, oi, od)
+    ix.close()

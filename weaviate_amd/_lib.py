@@ -33,6 +33,25 @@ class WvConfig(C.Structure):
     ]
 
 
+class WvGraphInfo(C.Structure):
+    _fields_ = [
+        ("n_slots", C.c_uint64),
+        ("entrypoint", C.c_uint64),
+        ("n_upper", C.c_uint64),
+        ("n_tombstones", C.c_uint64),
+        ("valid_bytes", C.c_uint64),
+        ("max_level", C.c_int),
+        ("max_node_level", C.c_int),
+        ("max_deg0", C.c_int),
+        ("max_degU", C.c_int),
+        ("compressed", C.c_int),
+        ("truncated", C.c_int),
+    ]
+
+    def asdict(self):
+        return {f: int(getattr(self, f)) for f, _ in self._fields_}
+
+
 class WvError(RuntimeError):
     def __init__(self, code, msg):
         super().__init__(f"wvgpu error {code}: {msg}")
@@ -69,6 +88,13 @@ SIGNATURES = {
     "wv_last_batch_stats": (C.c_int, [_vp, _u64p, _u64p, _u64p]),
     "wv_index_set_timing": (C.c_int, [_vp, C.c_int]),
     "wv_last_kernel_times": (C.c_int, [_vp, _f32p, _f32p, _f32p]),
+    "wv_graph_load_commitlog_buffer": (C.c_int, [_vp, C.c_uint64, C.POINTER(C.c_void_p)]),
+    "wv_graph_load_commitlogs": (C.c_int, [C.POINTER(C.c_char_p), C.c_int, C.POINTER(C.c_void_p)]),
+    "wv_graph_load_commitlog_dir": (C.c_int, [C.c_char_p, C.POINTER(C.c_void_p)]),
+    "wv_graph_get_info": (C.c_int, [_vp, C.POINTER(WvGraphInfo)]),
+    "wv_graph_node": (C.c_int, [_vp, C.c_uint64, C.c_int, C.POINTER(C.c_int), _vp, C.c_int, C.POINTER(C.c_int)]),
+    "wv_graph_export_csr": (C.c_int, [_vp, C.c_int, C.c_int, _vp, _vp, _vp, _vp, _vp]),
+    "wv_graph_destroy": (C.c_int, [_vp]),
     "wv_batcher_create": (C.c_int, [_vp, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p)]),
     "wv_batcher_search": (C.c_int, [_vp, _vp, C.c_int, _vp, C.c_uint64, _vp, _vp, _vp]),
     "wv_batcher_stats": (C.c_int, [_vp, _u64p, _u64p]),

@@ -13,7 +13,7 @@ from typing import Iterable, Optional
 
 import numpy as np
 
-from ._lib import MODE_AUTO, MODE_EXACT, MODE_HNSW, METRICS, WvConfig, WvError, check, lib
+from ._lib import MODE_AUTO, MODE_EXACT, MODE_HNSW, METRICS, WvConfig, WvError, WvGraphInfo, check, lib
 
 _MODES = {"auto": MODE_AUTO, "exact": MODE_EXACT, "hnsw": MODE_HNSW}
 
@@ -127,6 +127,19 @@ class GPUVectorIndex:
                                           _ptr(upper_row), _ptr(upper), upper.shape[0], upper.shape[2],
                                           g["max_level"], g["entrypoint"]))
 
+    def upload_graph_from_commitlog(self, graph: "CommitLogGraph"):
+        """Serve a graph replayed from a shard's commit log: the CSR degree is
+        the configured 2M / M or the longest list the log holds (legacy
+        oversize lists, search.go:236-251), and the log's tombstones replace
+        the index's."""
+        info = graph.info()
+        if info["compressed"]:
+            raise WvError(4, "commit log holds a PQ-compressed index; the GPU path serves uncompressed vectors")
+        m = self.cfg.max_connections
+        g = graph.export_csr(max(2 * m, info["max_deg0"]), max(m, info["max_degU"], 1))
+        self.upload_graph(g)
+        check(lib().wv_index_set_tombstones(self._h, _ptr(g["tomb_bits"]), g["n"]))
+
     def set_tombstones(self, ids: Iterable[int]):
         al = AllowList.from_ids(ids, self.capacity)
         check(lib().wv_index_set_tombstones(self._h, _ptr(al.words), al.nbits))
@@ -208,6 +221,63 @@ class GPUVectorIndex:
         a, b, c = C.c_uint64(), C.c_uint64(), C.c_uint64()
         check(lib().wv_last_batch_stats(self._h, C.byref(a), C.byref(b), C.byref(c)))
         return {"dist_evals": a.value, "expansions": b.value, "fallbacks": c.value}
+
+
+class CommitLogGraph:
+    """A graph replayed from HNSW commit logs (wv_graph_*, deserializer.go:80-158).
+    `source`: bytes (one log), a directory (<name>.hnsw.commitlog.d) or a list of
+    log file paths in replay order."""
+
+    def __init__(self, source):
+        h = C.c_void_p()
+        if isinstance(source, (bytes, bytearray)):
+            buf = (C.c_uint8 * max(len(source), 1)).from_buffer_copy(bytes(source) or b"\0")
+            check(lib().wv_graph_load_commitlog_buffer(buf, len(source), C.byref(h)))
+        elif isinstance(source, str):
+            check(lib().wv_graph_load_commitlog_dir(source.encode(), C.byref(h)))
+        else:
+            paths = [str(p).encode() for p in source]
+            arr = (C.c_char_p * max(len(paths), 1))(*paths)
+            check(lib().wv_graph_load_commitlogs(arr, len(paths), C.byref(h)))
+        self._h = h
+
+    def info(self) -> dict:
+        i = WvGraphInfo()
+        check(lib().wv_graph_get_info(self._h, C.byref(i)))
+        return i.asdict()
+
+    def node(self, id_: int, level: int = 0):
+        """(level, links at `level`) of one node; level -1 = nil node."""
+        lv, n = C.c_int(), C.c_int()
+        check(lib().wv_graph_node(self._h, id_, level, C.byref(lv), None, 0, C.byref(n)))
+        out = np.zeros(max(n.value, 1), np.uint64)
+        check(lib().wv_graph_node(self._h, id_, level, C.byref(lv), _ptr(out), n.value, C.byref(n)))
+        return lv.value, out[: n.value].tolist()
+
+    def export_csr(self, deg0: int, degU: int) -> dict:
+        """The fixed-degree CSR of GPUVectorIndex.upload_graph (+ tombstone bits)."""
+        i = self.info()
+        n, ml = i["n_slots"], max(1, i["max_node_level"])
+        levels = np.zeros(n, np.int8)
+        layer0 = np.zeros((n, deg0), np.uint32)
+        upper_row = np.zeros(n, np.uint32)
+        upper = np.zeros((max(i["n_upper"], 1), ml, degU), np.uint32)
+        tomb = np.zeros((n + 63) // 64 or 1, np.uint64)
+        check(lib().wv_graph_export_csr(self._h, deg0, degU, _ptr(levels), _ptr(layer0), _ptr(upper_row), _ptr(upper),
+                                        _ptr(tomb)))
+        return dict(n=n, entrypoint=i["entrypoint"], max_level=i["max_level"], levels=levels, layer0=layer0,
+                    upper_row=upper_row, upper=upper, deg0=deg0, degU=degU, tomb_bits=tomb)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().wv_graph_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class Batcher:
