@@ -72,6 +72,8 @@ def main():
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--ef", type=int, default=64)
     ap.add_argument("--metric", default="l2-squared")
+    ap.add_argument("--allow-frac", type=float, default=0.0,
+                    help="exact mode: shared allow list, Bernoulli(p) over ids (seed 3, BASELINE configs[3])")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample time")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -159,12 +161,21 @@ def main():
         m_d = torch.empty((NQ, K), dtype=torch.float32, device=dev)
         m_n = torch.empty((NQ,), dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
+    allow_ptr, allow_bits, n_allowed = 0, 0, n_local
+    if args.allow_frac > 0:
+        keep = counter_uniform(3, lo, n_local, 1)[:, 0] < args.allow_frac
+        words = np.zeros((n_local + 63) // 64, np.uint64)
+        idx = np.nonzero(keep)[0].astype(np.uint64)
+        np.bitwise_or.at(words, (idx >> np.uint64(6)).astype(np.int64), np.uint64(1) << (idx & np.uint64(63)))
+        allow_t = torch.from_numpy(words.view(np.int64)).to(dev)
+        allow_ptr, allow_bits, n_allowed = allow_t.data_ptr(), n_local, int(keep.sum())
 
     kern_ms = []
 
     def step(timed=False):
         ix.search_batch_device(qt.data_ptr(), NQ, K, out_ids.data_ptr(), out_d.data_ptr(), out_n.data_ptr(),
-                               ef=args.ef if mode == "hnsw" else 0, mode=mode, stream=stream)
+                               ef=args.ef if mode == "hnsw" else 0, mode=mode, stream=stream,
+                               allow_ptr=allow_ptr, allow_nbits=allow_bits)
         if timed:
             kern_ms.append(ix.last_kernel_times())
         if ws > 1:
@@ -221,8 +232,11 @@ def main():
         "dtype": "f32",
         "data": "synthetic: counter-based U[0,1) float32 corpus (seed 1) and queries (seed 2)",
         "config": {
-            "workload": ("exact brute-force %d-NN, %s x %d-d %s, %d-query batch (BASELINE configs[1])"
-                         % (K, f"{N:,}", D, args.metric, NQ)) if mode == "exact" else
+            "workload": ("exact brute-force %d-NN, %s x %d-d %s, %d-query batch%s"
+                         % (K, f"{N:,}", D, args.metric, NQ,
+                            " (BASELINE configs[1])" if args.allow_frac <= 0 else
+                            f", shared allow list p={args.allow_frac} ({n_allowed:,} rows on rank 0)"))
+                        if mode == "exact" else
                         ("hnsw layer-0 beam search ef=%d, %s x %d-d %s, %d-query batch" % (args.ef, f"{N:,}", D,
                                                                                          args.metric, NQ)),
             "N": N, "dim": D, "nq": NQ, "k": K, "metric": args.metric, "mode": mode,
@@ -234,7 +248,7 @@ def main():
     # ---- roofline of the dominant kernel (HIP events on its launch stream) ----
     if mode == "exact":
         mfma_ms = float(np.mean([k["bf_mfma_ms"] for k in kern_ms]))
-        flops = 2.0 * D * n_local * NQ    # algorithmic: 2*D*N per query
+        flops = 2.0 * D * n_allowed * NQ    # algorithmic: 2*D*N_eff per query
         achieved = flops / (mfma_ms * 1e-3) / 1e12
         result["roofline"] = {"bound": "mfma", "kernel": "wv_bf_mfma_kernel", "achieved": round(achieved, 2),
                               "peak": FP32_MFMA_PEAK_TF, "unit": "TFLOP/s",
@@ -268,11 +282,12 @@ def main():
         if mode == "exact":
             probe = 32
             t0 = time.perf_counter()
-            oi, od, on = O.flat_scan(metric_id, base, queries[:probe], K, threads=threads)
+            cpu_allow = words if args.allow_frac > 0 else None
+            oi, od, on = O.flat_scan(metric_id, base, queries[:probe], K, allow_bits=cpu_allow, threads=threads)
             per_q = (time.perf_counter() - t0) / probe
             ns = int(min(NQ, max(probe, args.cpu_seconds / max(per_q, 1e-9))))
             t0 = time.perf_counter()
-            oi, od, on = O.flat_scan(metric_id, base, queries[:ns], K, threads=threads)
+            oi, od, on = O.flat_scan(metric_id, base, queries[:ns], K, allow_bits=cpu_allow, threads=threads)
             cpu_t = time.perf_counter() - t0
             kind_desc = "flatSearch restated in C (AVX2 asm-order distancer, oracle/)"
             parity = bool((oi == final_ids[:ns]).all() and np.array_equal(od.view(np.uint32),

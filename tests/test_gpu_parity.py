@@ -441,3 +441,30 @@ def test_graph_replayed_from_commit_log_serves_identical_searches():
     assert not set(ids.ravel().tolist()) & set(tomb.tolist())
     _same(ids, ds, oi, od)
     ix.close()
+
+
+def test_allow_list_compaction_equals_masking():
+    """A shared allow list under half the corpus is compacted into a row list
+    (contraction over |allow| rows); the masked full scan must agree bit for
+    bit, with tombstones on top."""
+    import os
+    n, d = 30000, 96
+    base, qs = _data(n, d, 150, seed=17)
+    rng = np.random.default_rng(18)
+    ix = W.GPUVectorIndex(d, "l2-squared", capacity=n)
+    ix.upload_vectors(base)
+    ix.set_tombstones(np.nonzero(rng.random(n) < 0.05)[0])
+    for sel in (0.001, 0.03, 0.3):
+        al = W.AllowList.from_ids(np.nonzero(rng.random(n) < sel)[0], n)
+        a = ix.search_batch(qs, 10, allow=al, mode="exact")
+        os.environ["WV_BF_NO_COMPACT"] = "1"
+        try:
+            b = ix.search_batch(qs, 10, allow=al, mode="exact")
+        finally:
+            os.environ.pop("WV_BF_NO_COMPACT")
+        assert a[2].tolist() == b[2].tolist()
+        for i in range(len(qs)):
+            _same(a[0][i, : a[2][i]], a[1][i, : a[2][i]], b[0][i, : b[2][i]], b[1][i, : b[2][i]])
+    empty = W.AllowList(nbits=n)
+    assert (ix.search_batch(qs, 10, allow=empty, mode="exact")[2] == 0).all()
+    ix.close()

@@ -203,6 +203,7 @@ struct wv_index {
     DevBuf g_idx, g_q, g_allow, g_ids, g_d, g_n, g_cnt;
     DevBuf out_ids, out_d, out_n;
     DevBuf fail_thr, fb_idx, fb_d, fb_i, fb_n, fb_of;
+    DevBuf ac_cnt, ac_off, rowidx;   // allow-list compaction
     // stats of the last batch
     uint64_t last_dist = 0, last_exp = 0, last_fallbacks = 0;
     // optional kernel timing (hipEvents on the launch stream)
@@ -294,6 +295,71 @@ int exact_full(wv_index* ix, const float* d_q, int k, const uint64_t* d_allow, u
     return WV_OK;
 }
 
+__global__ void allowed_count_kernel(const uint64_t* allow, uint64_t allow_words, const uint64_t* excl, uint64_t N,
+                                     uint32_t* cnt) {
+    const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t words = (N + 63) / 64;
+    if (w >= words) return;
+    uint64_t b = w < allow_words ? allow[w] & ~excl[w] : 0ull;
+    if (w == words - 1 && (N & 63)) b &= (1ull << (N & 63)) - 1;
+    cnt[w] = (uint32_t)__popcll(b);
+}
+
+__global__ void allowed_scatter_kernel(const uint64_t* allow, uint64_t allow_words, const uint64_t* excl, uint64_t N,
+                                       const uint32_t* off, uint32_t* rowidx) {
+    const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t words = (N + 63) / 64;
+    if (w >= words) return;
+    uint64_t b = w < allow_words ? allow[w] & ~excl[w] : 0ull;
+    if (w == words - 1 && (N & 63)) b &= (1ull << (N & 63)) - 1;
+    uint32_t o = off[w];
+    while (b) {
+        rowidx[o++] = (uint32_t)(w * 64 + __builtin_ctzll(b));
+        b &= b - 1;
+    }
+}
+
+__global__ void pad_rowidx_kernel(uint32_t* rowidx, uint64_t from, uint64_t to) {
+    const uint64_t i = from + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < to) rowidx[i] = 0;   // padded tile rows read row 0 and are masked by the row count
+}
+
+// Ascending list of the rows a shared allow list keeps (allowed, not excluded,
+// < N) into ix->rowidx, padded to whole tiles; *n_ok = its length.
+int compact_allowed(wv_index* ix, const uint64_t* d_allow, uint64_t allow_nbits, uint64_t N, uint64_t* n_ok,
+                    hipStream_t s) {
+    const uint64_t words = (N + 63) / 64;
+    const uint64_t allow_words = (allow_nbits + 63) / 64;
+    HIP_TRY(ix->ac_cnt.ensure((words + 1) * 4));
+    HIP_TRY(ix->ac_off.ensure((words + 1) * 4));
+    const unsigned blocks = (unsigned)((words + 255) / 256);
+    hipLaunchKernelGGL(allowed_count_kernel, dim3(blocks), dim3(256), 0, s, d_allow, allow_words,
+                       ix->excl.as<uint64_t>(), N, ix->ac_cnt.as<uint32_t>());
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemsetAsync(ix->ac_cnt.as<uint32_t>() + words, 0, 4, s));
+    size_t tmp = 0;
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, ix->ac_cnt.as<uint32_t>(), ix->ac_off.as<uint32_t>(),
+                                             (int)(words + 1), s));
+    HIP_TRY(ix->sort_tmp.ensure(tmp));
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(ix->sort_tmp.p, tmp, ix->ac_cnt.as<uint32_t>(), ix->ac_off.as<uint32_t>(),
+                                             (int)(words + 1), s));
+    uint32_t total = 0;
+    HIP_TRY(hipMemcpyAsync(&total, ix->ac_off.as<uint32_t>() + words, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    *n_ok = total;
+    if (total == 0 || 2 * (uint64_t)total >= N) return WV_OK;
+    const uint64_t padded = (total + wv::BF_BN - 1) / wv::BF_BN * wv::BF_BN;
+    HIP_TRY(ix->rowidx.ensure(padded * 4));
+    hipLaunchKernelGGL(allowed_scatter_kernel, dim3(blocks), dim3(256), 0, s, d_allow, allow_words,
+                       ix->excl.as<uint64_t>(), N, ix->ac_off.as<uint32_t>(), ix->rowidx.as<uint32_t>());
+    HIP_TRY(hipGetLastError());
+    if (padded > total)
+        hipLaunchKernelGGL(pad_rowidx_kernel, dim3(1), dim3(256), 0, s, ix->rowidx.as<uint32_t>(), (uint64_t)total,
+                           padded);
+    HIP_TRY(hipGetLastError());
+    return WV_OK;
+}
+
 // Brute force (flatSearch semantics) over a device batch of prepared queries.
 int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_allow, uint64_t allow_nbits,
               uint64_t allow_stride, uint64_t* d_out_ids, float* d_out_d, int32_t* d_out_n, hipStream_t s) {
@@ -305,7 +371,26 @@ int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
     std::vector<int32_t> fails;
     if (k <= wv::BF_FAST_KMAX) {
         const int n_qblocks = (nq + wv::BF_BQ - 1) / wv::BF_BQ;
-        const wv::BfSchedule sch = wv::bf_schedule(nq, N, ix->bf_blocks);
+        // A shared allow list that keeps under half the corpus is compacted
+        // into a row list first: the contraction then runs over |allow| rows
+        // (the reference's flatSearch also walks only the allow list,
+        // flat_search.go:25-58) instead of masking N.
+        uint64_t n_scan = N;
+        const uint32_t* d_rowidx = nullptr;
+        if (d_allow && !allow_stride) {
+            uint64_t n_ok = 0;
+            int rc = compact_allowed(ix, d_allow, allow_nbits, N, &n_ok, s);
+            if (rc) return rc;
+            if (n_ok == 0) {
+                HIP_TRY(hipMemsetAsync(d_out_n, 0, sizeof(int32_t) * nq, s));
+                return WV_OK;
+            }
+            if (2 * n_ok < N && !std::getenv("WV_BF_NO_COMPACT")) {
+                n_scan = n_ok;
+                d_rowidx = ix->rowidx.as<uint32_t>();
+            }
+        }
+        const wv::BfSchedule sch = wv::bf_schedule(nq, n_scan, ix->bf_blocks);
         const size_t n_lists = (size_t)sch.n_slots * wv::BF_PROD;
         HIP_TRY(ix->cand_d.ensure((size_t)nq * n_lists * wv::BF_KP * 4));
         HIP_TRY(ix->cand_id.ensure((size_t)nq * n_lists * wv::BF_KP * 4));
@@ -324,12 +409,13 @@ int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
         bp.X = ix->vecs.as<float>();
         bp.Q = ix->q_scaled.as<float>();
         bp.xnorm = ix->xnorm.as<float>();
-        bp.tomb = ix->excl.as<uint64_t>();
+        bp.tomb = d_rowidx ? nullptr : ix->excl.as<uint64_t>();
         bp.tomb_nbits = ix->capacity;
-        bp.allow = d_allow;
+        bp.allow = d_rowidx ? nullptr : d_allow;
         bp.allow_nbits = allow_nbits;
         bp.allow_stride = allow_stride;
-        bp.N = N;
+        bp.rowidx = d_rowidx;
+        bp.N = n_scan;
         bp.nq = nq;
         bp.D = ix->dim;
         bp.ldx = ix->dpad;
@@ -715,7 +801,8 @@ int wv_index_destroy(wv_index* ix) {
                       &ix->tomb, &ix->excl, &ix->q_in, &ix->q_norm, &ix->q_nrm2, &ix->q_scaled, &ix->cand_d, &ix->cand_id,
                       &ix->fail, &ix->status, &ix->counters, &ix->scan_d, &ix->scan_i, &ix->sort_d, &ix->sort_i,
                       &ix->sort_tmp, &ix->g_idx, &ix->g_q, &ix->g_allow, &ix->g_ids, &ix->g_d, &ix->g_n, &ix->g_cnt,
-                      &ix->out_ids, &ix->out_d, &ix->out_n, &ix->stage, &ix->fail_thr, &ix->fb_idx, &ix->fb_d, &ix->fb_i, &ix->fb_n, &ix->fb_of})
+                      &ix->out_ids, &ix->out_d, &ix->out_n, &ix->stage, &ix->fail_thr, &ix->fb_idx, &ix->fb_d, &ix->fb_i, &ix->fb_n, &ix->fb_of,
+                      &ix->ac_cnt, &ix->ac_off, &ix->rowidx})
         b->release();
     for (auto& e : ix->ev)
         if (e) (void)hipEventDestroy(e);

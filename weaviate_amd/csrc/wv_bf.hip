@@ -85,6 +85,9 @@ __global__ __launch_bounds__(256, WV_BF_WAVES_PER_SIMD) void wv_bf_mfma_kernel(B
     const uint64_t allow_words = (p.allow_nbits + 63) / 64;
     const uint64_t* __restrict__ tomb = p.tomb;
     const uint64_t* __restrict__ allow = p.allow;
+    // compacted rows (shared allow list below half the corpus): tile row r is
+    // corpus row rowidx[r]; p.N counts compacted rows, no bitmap is applied
+    const uint32_t* __restrict__ rowidx = p.rowidx;
     // this thread's slice of a chunk load: rows lrow + 32*it, floats 4*lf4..+3
     const int lrow = tid >> 3, lf4 = tid & 7;
     const uint32_t xoff = (uint32_t)lrow * p.ldx + 4 * lf4;
@@ -135,14 +138,20 @@ __global__ __launch_bounds__(256, WV_BF_WAVES_PER_SIMD) void wv_bf_mfma_kernel(B
             for (int it = 0; it < 4; ++it) {
                 const uint32_t ro = (uint32_t)(32 * it);
                 if (kin) {
-                    ra[it] = ld4(xt + xoff + ro * p.ldx);
+                    if (rowidx) {   // compacted allow list: row gather
+                        const uint64_t g = rowidx[tile * BF_BN + lrow + ro];
+                        ra[it] = ld4(p.X + g * p.ldx + kc * BF_BK + 4 * lf4);
+                    } else {
+                        ra[it] = ld4(xt + xoff + ro * p.ldx);
+                    }
                     rb[it] = ld4(qt + qoff + ro * p.ldq);
                 } else {
                     ra[it] = make_float4(0.f, 0.f, 0.f, 0.f);
                     rb[it] = ra[it];
                 }
             }
-            if (kc == 0 && tid < BF_BN && p.metric == WV_METRIC_L2) rxn = p.xnorm[tile * BF_BN + tid];
+            if (kc == 0 && tid < BF_BN && p.metric == WV_METRIC_L2)
+                rxn = p.xnorm[rowidx ? (uint64_t)rowidx[tile * BF_BN + tid] : tile * BF_BN + tid];
         };
         auto store_chunk = [&](int c) {
             float* st = lds + (c & 1) * BF_STAGE;
@@ -293,6 +302,7 @@ __global__ __launch_bounds__(256, WV_BF_WAVES_PER_SIMD) void wv_bf_mfma_kernel(B
                     idm = hit ? rb0 + 32 + (r & 3) + 8 * (r >> 2) : idm;                        \
                     A1[r] = hit ? INF : A1[r];                                                  \
                 }                                                                               \
+                if (rowidx) idm = rowidx[idm];   /* corpus id; the map is increasing */      \
                 if (!key_less(M, idm, LD[BF_KP - 1], LI[BF_KP - 1])) break;                     \
                 list_insert(LD, LI, M, idm);                                                    \
                 M = INF;                                                                        \

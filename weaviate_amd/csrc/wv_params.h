@@ -20,6 +20,7 @@ struct BfParams {
     const float* xnorm;     // |x|^2 per row (L2 only)
     const uint64_t* tomb;   // excluded ids (tombstones, nil nodes, missing rows)
     const uint64_t* allow;  // allow bits (nullable)
+    const uint32_t* rowidx; // compacted rows (nullable): tile row r = corpus row rowidx[r], N = their count
     uint64_t tomb_nbits, allow_nbits, allow_stride;  // stride in words (0 = shared)
     uint64_t N;
     int nq, D, ldx, ldq, metric;
