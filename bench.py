@@ -53,6 +53,15 @@ def counter_uniform(seed: int, row0: int, nrows: int, dim: int) -> np.ndarray:
     return out
 
 
+def counter_gauss(seed: int, row0: int, nrows: int, dim: int) -> np.ndarray:
+    """N(0,1)/sqrt(dim) float32 by Box-Muller over two counter-based streams
+    (GloVe / Deep / C4-shaped data)."""
+    u1 = counter_uniform(seed, row0, nrows, dim).astype(np.float64)
+    u2 = counter_uniform(seed + 1000, row0, nrows, dim).astype(np.float64)
+    z = np.sqrt(-2.0 * np.log(u1 + 2.0 ** -25)) * np.cos(2.0 * np.pi * u2)
+    return (z / np.sqrt(dim)).astype(np.float32)
+
+
 def dist_env():
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -72,6 +81,8 @@ def main():
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--ef", type=int, default=64)
     ap.add_argument("--metric", default="l2-squared")
+    ap.add_argument("--data", choices=["uniform", "gauss"], default="uniform",
+                    help="uniform: U[0,1) (tie-free, configs[1]); gauss: N(0,1)/sqrt(D) (GloVe/Deep/C4-shaped)")
     ap.add_argument("--allow-frac", type=float, default=0.0,
                     help="exact mode: shared allow list, Bernoulli(p) over ids (seed 3, BASELINE configs[3])")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample time")
@@ -107,8 +118,9 @@ def main():
     lo = N * rank // ws
     hi = N * (rank + 1) // ws
     n_local = hi - lo
-    base = counter_uniform(1, lo, n_local, D)
-    queries = counter_uniform(2, 0, NQ, D)
+    gen = counter_gauss if args.data == "gauss" else counter_uniform
+    base = gen(1, lo, n_local, D)
+    queries = gen(2, 0, NQ, D)
 
     ix = W.GPUVectorIndex(D, args.metric, capacity=max(n_local, 1), device=gpu, id_base=lo,
                           max_connections=args.M)
@@ -230,7 +242,8 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic: counter-based U[0,1) float32 corpus (seed 1) and queries (seed 2)",
+        "data": ("synthetic: counter-based U[0,1) float32 corpus (seed 1) and queries (seed 2)" if args.data == "uniform"
+                 else "synthetic: counter-based N(0,1)/sqrt(D) float32 corpus (seed 1) and queries (seed 2)"),
         "config": {
             "workload": ("exact brute-force %d-NN, %s x %d-d %s, %d-query batch%s"
                          % (K, f"{N:,}", D, args.metric, NQ,

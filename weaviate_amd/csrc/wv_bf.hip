@@ -119,6 +119,7 @@ __global__ __launch_bounds__(256, WV_BF_WAVES_PER_SIMD) void wv_bf_mfma_kernel(B
         }
         float4 ra[4], rb[4];
         float rxn = 0.f;
+        uint32_t gidx[4] = {0, 0, 0, 0};   // compacted path: corpus rows of the tile being loaded
         const int total = (int)(t_end - t_begin) * nk;   // chunks of this segment
 
         auto load_chunk = [&](int c) {
@@ -137,10 +138,10 @@ __global__ __launch_bounds__(256, WV_BF_WAVES_PER_SIMD) void wv_bf_mfma_kernel(B
 #pragma unroll
             for (int it = 0; it < 4; ++it) {
                 const uint32_t ro = (uint32_t)(32 * it);
+                if (rowidx && kc == 0) gidx[it] = rowidx[tile * BF_BN + lrow + ro];   // once per tile
                 if (kin) {
                     if (rowidx) {   // compacted allow list: row gather
-                        const uint64_t g = rowidx[tile * BF_BN + lrow + ro];
-                        ra[it] = ld4(p.X + g * p.ldx + kc * BF_BK + 4 * lf4);
+                        ra[it] = ld4(p.X + (uint64_t)gidx[it] * p.ldx + kc * BF_BK + 4 * lf4);
                     } else {
                         ra[it] = ld4(xt + xoff + ro * p.ldx);
                     }
