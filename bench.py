@@ -296,6 +296,9 @@ def main():
             probe = 32
             t0 = time.perf_counter()
             cpu_allow = words if args.allow_frac > 0 else None
+            if args.metric == "cosine-dot":   # stored vectors normalized on insert (insert.go:56-60), queries per search
+                base = O.normalize_rows(base)
+                queries = O.normalize_rows(queries)
             oi, od, on = O.flat_scan(metric_id, base, queries[:probe], K, allow_bits=cpu_allow, threads=threads)
             per_q = (time.perf_counter() - t0) / probe
             ns = int(min(NQ, max(probe, args.cpu_seconds / max(per_q, 1e-9))))

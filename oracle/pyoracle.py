@@ -55,6 +55,7 @@ def lib():
             "wvo_asm_l2": (C.c_float, [fp, fp, C.c_int]),
             "wvo_asm_dot": (C.c_float, [fp, fp, C.c_int]),
             "wvo_normalize": (None, [fp, fp, C.c_int]),
+            "wvo_normalize_rows": (None, [fp, fp, C.c_uint64, C.c_int]),
             "wvo_pq_script": (C.c_int, [C.c_int, C.c_int, i32p, u64p, fp, u64p, fp]),
             "wvo_search_time_ef": (C.c_int, [C.c_int64] * 4 + [C.c_int]),
             "wvo_create": (vp, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_uint64]),
@@ -117,6 +118,14 @@ def normalize(v):
     v = f32(v)
     out = np.empty_like(v)
     lib().wvo_normalize(_f(v), _f(out), len(v))
+    return out
+
+
+def normalize_rows(a):
+    """Normalize (distancer/normalize.go:16-32) applied to every row."""
+    a = f32(a)
+    out = np.empty_like(a)
+    lib().wvo_normalize_rows(_f(a), _f(out), a.shape[0], a.shape[1])
     return out
 
 

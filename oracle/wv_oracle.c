@@ -236,6 +236,10 @@ void wvo_normalize(const float *in, float *out, int n) {
     for (int i = 0; i < n; i++) out[i] = in[i] / norm;
 }
 
+void wvo_normalize_rows(const float *in, float *out, uint64_t rows, int dim) {
+    for (uint64_t r = 0; r < rows; r++) wvo_normalize(in + r * (uint64_t)dim, out + r * (uint64_t)dim, dim);
+}
+
 /* ======================================================================== */
 /* priorityqueue.Queue clone -- priorityqueue/queue.go:14-111               */
 /* ======================================================================== */

@@ -40,6 +40,7 @@ float wvo_asm_l2(const float *x, const float *y, int n);
 float wvo_asm_dot(const float *x, const float *y, int n);
 /* distancer/normalize.go:16-32 */
 void wvo_normalize(const float *in, float *out, int n);
+void wvo_normalize_rows(const float *in, float *out, uint64_t rows, int dim);
 
 /* ---- binary heap clone (priorityqueue/queue.go) for the heap-order KAT -- */
 /* Runs a script of ops on a fresh Min (is_max=0) or Max (is_max=1) queue.

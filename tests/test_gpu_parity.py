@@ -468,3 +468,23 @@ def test_allow_list_compaction_equals_masking():
     empty = W.AllowList(nbits=n)
     assert (ix.search_batch(qs, 10, allow=empty, mode="exact")[2] == 0).all()
     ix.close()
+
+
+@pytest.mark.parametrize("dim", [7, 33, 100, 130, 200])
+@pytest.mark.parametrize("metric", [O.L2, O.COSINE])
+def test_bruteforce_mfma_ragged_dims(dim, metric):
+    """D not a multiple of the 32-float k-chunk: padded corpus stride, k test
+    in the tile loads, zero k-groups of the last chunk skipped -- still the
+    reference's ids and distances (GloVe-100-shaped: D=100, cosine)."""
+    rng = np.random.default_rng(dim)
+    base = rng.standard_normal((12000, dim)).astype(np.float32)
+    qs = rng.standard_normal((200, dim)).astype(np.float32)
+    ix = W.GPUVectorIndex(dim, METRIC_NAMES[metric], capacity=12000)
+    ix.upload_vectors(base)
+    ids, ds, n = ix.search_batch(qs, 10, mode="exact")
+    b = O.normalize_rows(base) if metric == O.COSINE else base
+    q = O.normalize_rows(qs) if metric == O.COSINE else qs
+    oi, od, on = O.flat_scan(metric, b, q, 10)
+    for i in range(len(qs)):
+        _same_tie_aware(ids[i], ds[i], oi[i], od[i])
+    ix.close()

@@ -172,12 +172,13 @@ __global__ void popcount_rows_kernel(const uint64_t* bits, uint64_t words, uint6
 
 struct wv_index {
     int dim = 0, dpad = 0, metric = 0;
+    int ldx = 0;            // corpus row stride: D rounded up to 32 floats (whole 128-B lines, whole MFMA k-chunks) when D >= 32
     wv_config cfg{};
     uint64_t capacity = 0;
     hipStream_t stream = nullptr;
     std::mutex mu;
     // corpus
-    DevBuf vecs;            // [capacity][dpad]
+    DevBuf vecs;            // [capacity rounded to 128][ldx]
     DevBuf xnorm;           // [capacity]
     DevBuf maxnorm;         // unsigned bits of max |x|
     std::vector<uint64_t> has_vec;   // host copy of uploaded rows
@@ -276,7 +277,7 @@ int exact_full(wv_index* ix, const float* d_q, int k, const uint64_t* d_allow, u
     sp.allow_nbits = allow_nbits;
     sp.N = N;
     sp.D = ix->dim;
-    sp.ldx = ix->dpad;
+    sp.ldx = ix->ldx;
     sp.metric = ix->metric;
     sp.dist = ix->scan_d.as<float>();
     sp.ids = ix->scan_i.as<uint32_t>();
@@ -418,7 +419,7 @@ int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
         bp.N = n_scan;
         bp.nq = nq;
         bp.D = ix->dim;
-        bp.ldx = ix->dpad;
+        bp.ldx = ix->ldx;
         bp.ldq = ix->dpad;
         bp.metric = ix->metric;
         bp.n_qblocks = n_qblocks;
@@ -447,7 +448,7 @@ int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
         fp.units_per_block = sch.units_per_block;
         fp.nq = nq;
         fp.D = ix->dim;
-        fp.ldx = ix->dpad;
+        fp.ldx = ix->ldx;
         fp.ldq = ix->dpad;
         fp.metric = ix->metric;
         fp.k = k;
@@ -502,7 +503,7 @@ int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
             bp.N = N;
             bp.nf = nf;
             bp.D = ix->dim;
-            bp.ldx = ix->dpad;
+            bp.ldx = ix->ldx;
             bp.ldq = ix->dpad;
             bp.metric = ix->metric;
             bp.k = k;
@@ -580,7 +581,7 @@ int run_hnsw(wv_index* ix, const float* d_q, int nq, int k, int ef, const uint64
     hp.id_base = ix->cfg.id_base;
     hp.entrypoint = (uint32_t)ix->entrypoint;
     hp.D = ix->dim;
-    hp.ldx = ix->dpad;
+    hp.ldx = ix->ldx;
     hp.ldq = ix->dpad;
     hp.metric = ix->metric;
     hp.deg0 = ix->deg0;
@@ -759,6 +760,7 @@ int wv_index_create(int dim, int metric, const wv_config* cfg, uint64_t capacity
     auto* ix = new wv_index();
     ix->dim = dim;
     ix->dpad = (dim + 3) & ~3;
+    ix->ldx = dim >= 32 ? (dim + 31) & ~31 : ix->dpad;
     ix->metric = metric;
     if (cfg) ix->cfg = *cfg; else wv_config_default(&ix->cfg);
     ix->capacity = capacity;
@@ -777,7 +779,7 @@ int wv_index_create(int dim, int metric, const wv_config* cfg, uint64_t capacity
     ix->bm_words = (capacity + 63) / 64;
     // whole brute-force tiles (wv_bf.hip layout contract): zero rows past capacity
     const uint64_t cap_rows = (capacity + wv::BF_BN - 1) / wv::BF_BN * wv::BF_BN;
-    const size_t vbytes = cap_rows * (size_t)ix->dpad * 4;
+    const size_t vbytes = cap_rows * (size_t)ix->ldx * 4;
     if (ix->vecs.ensure(vbytes) != hipSuccess || ix->xnorm.ensure(cap_rows * 4) != hipSuccess ||
         ix->maxnorm.ensure(4) != hipSuccess || ix->tomb.ensure(ix->bm_words * 8) != hipSuccess ||
         ix->excl.ensure(ix->bm_words * 8) != hipSuccess) {
@@ -826,7 +828,7 @@ static int upload_rows(wv_index* ix, const float* src, bool device_src, int ld, 
     if (first_id + n > ix->capacity) return fail(WV_EINVAL, "upload beyond capacity");
     if (n == 0) return WV_OK;
     HIP_TRY(hipSetDevice(ix->cfg.device));
-    float* dst = ix->vecs.as<float>() + first_id * ix->dpad;
+    float* dst = ix->vecs.as<float>() + first_id * ix->ldx;
     const float* dsrc = src;
     if (!device_src) {
         HIP_TRY(ix->stage.ensure(n * (size_t)ix->dim * 4));
@@ -834,10 +836,10 @@ static int upload_rows(wv_index* ix, const float* src, bool device_src, int ld, 
         dsrc = ix->stage.as<float>();
         ld = ix->dim;
     }
-    HIP_TRY(launch_pad_rows(dsrc, ld, n, ix->dim, dst, ix->dpad, ix->stream));
+    HIP_TRY(launch_pad_rows(dsrc, ld, n, ix->dim, dst, ix->ldx, ix->stream));
     if (ix->metric == WV_COSINE_DOT)  // normalize on write (insert.go:56-60, vector_cache.go:110-112)
-        HIP_TRY(wv_launch_normalize(dst, dst, n, ix->dim, ix->dpad, ix->stream));
-    HIP_TRY(wv_launch_rownorm(dst, n, ix->dim, ix->dpad, ix->xnorm.as<float>() + first_id,
+        HIP_TRY(wv_launch_normalize(dst, dst, n, ix->dim, ix->ldx, ix->stream));
+    HIP_TRY(wv_launch_rownorm(dst, n, ix->dim, ix->ldx, ix->xnorm.as<float>() + first_id,
                               ix->maxnorm.as<unsigned int>(), ix->stream));
     HIP_TRY(hipStreamSynchronize(ix->stream));
     for (uint64_t i = first_id; i < first_id + n; ++i) ix->has_vec[i >> 6] |= 1ull << (i & 63);

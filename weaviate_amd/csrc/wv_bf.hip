@@ -220,12 +220,16 @@ __global__ __launch_bounds__(256, WV_BF_WAVES_PER_SIMD) void wv_bf_mfma_kernel(B
                 // operands of k-step group s4+1 are read from LDS while the 16
                 // MFMAs of group s4 run (register double buffer)
                 float4 fa0[2], fa1[2], fb0[2], fb1[2];
+                // valid k of this chunk: a k-group whose both lane halves lie past
+                // D (the last chunk when D mod 32 <= 16) carries only zeros
+                const int kvalid = KFULL ? BF_BK : min(BF_BK, p.D - kc * BF_BK);
                 fa0[0] = *reinterpret_cast<const float4*>(st + arow);
                 fa1[0] = *reinterpret_cast<const float4*>(st + arow + 32 * BF_LDT);
                 fb0[0] = *reinterpret_cast<const float4*>(st + brow);
                 fb1[0] = *reinterpret_cast<const float4*>(st + brow + 32 * BF_LDT);
 #pragma unroll
                 for (int s4 = 0; s4 < 4; ++s4) {
+                    if (!KFULL && 4 * s4 >= kvalid) break;
                     const int cur = s4 & 1, nxt = cur ^ 1;
                     if (s4 < 3) {
                         fa0[nxt] = *reinterpret_cast<const float4*>(st + arow + 4 * (s4 + 1));
