@@ -106,6 +106,18 @@ int wv_index_upload_graph(wv_index *ix, uint64_t n, const int8_t *levels, const 
 /* Tombstones (delete.go:546-566) as a bitmap over local ids (replaces the set). */
 int wv_index_set_tombstones(wv_index *ix, const uint64_t *bits, uint64_t nbits);
 
+/* Incremental writes while serving.  wv_index_add mirrors
+ * hnsw.Add (insert.go:43-65): rows for arbitrary local ids, normalized for
+ * cosine; an id the uploaded graph does not hold joins the delta set, which
+ * every HNSW search also scans exactly and merges by (dist, id) -- the row is
+ * findable at once, as after the reference's insert -- until a later
+ * wv_index_upload_graph snapshot contains it.  Tombstones are added / removed
+ * one by one (delete.go:29-84 AddTombstone, tombstone cleanup). */
+int wv_index_add(wv_index *ix, const uint64_t *ids, const float *rows, uint64_t n);
+int wv_index_add_tombstones(wv_index *ix, const uint64_t *ids, uint64_t n);
+int wv_index_remove_tombstones(wv_index *ix, const uint64_t *ids, uint64_t n);
+int wv_index_delta_size(wv_index *ix, uint64_t *n);
+
 /* searchTimeEF (search.go:30-62) for the current config. */
 int wv_search_time_ef(const wv_index *ix, int k);
 

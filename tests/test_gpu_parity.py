@@ -488,3 +488,78 @@ def test_bruteforce_mfma_ragged_dims(dim, metric):
     for i in range(len(qs)):
         _same_tie_aware(ids[i], ds[i], oi[i], od[i])
     ix.close()
+
+
+def _merge_topk(a_ids, a_d, b_ids, b_d, k):
+    out_i, out_d = [], []
+    for ai, ad, bi, bd in zip(a_ids, a_d, b_ids, b_d):
+        c = sorted(list(zip(ad.tolist(), ai.tolist())) + list(zip(bd.tolist(), bi.tolist())))[:k]
+        out_d.append([x[0] for x in c])
+        out_i.append([x[1] for x in c])
+    return np.array(out_i, np.uint64), np.array(out_d, np.float32)
+
+
+def test_mutable_index_added_rows_are_searchable_until_the_next_snapshot():
+    """rows added after the graph snapshot (hnsw.Add,
+    insert.go:43-65) are found at once -- HNSW over the snapshot merged with an
+    exact pass over the delta -- tombstones apply to both, and a new snapshot
+    that holds them empties the delta."""
+    n0, n1, d, k, ef = 4000, 5000, 32, 10, 64
+    rng = np.random.default_rng(51)
+    base = rng.random((n1, d), dtype=np.float32)
+    qs = rng.random((150, d), dtype=np.float32)
+    ref = O.Index(d, "l2-squared", 16, 64, capacity=n1, seed=4)
+    ref.add_batch(base[:n0], threads=4)
+    ix = W.GPUVectorIndex(d, "l2-squared", capacity=n1, max_connections=16)
+    ix.upload_vectors(base[:n0])
+    ix.upload_graph(ref.export_graph())
+    g_old = ref.search_batch(qs, k, ef)          # the snapshot's own answer
+    ix.add(np.arange(n0, n1), base[n0:])
+    assert ix.delta_size() == n1 - n0
+    ids, ds, cnt = ix.search_batch(qs, k, ef=ef, mode="hnsw")
+    fi, fd, fn = O.flat_scan(O.L2, base[n0:], qs, k)
+    want_i, want_d = _merge_topk(g_old[0], g_old[1], fi + np.uint64(n0), fd, k)
+    _same(ids, ds, want_i, want_d)
+    # exact mode covers every row with a vector
+    ei, ed, en = ix.search_batch(qs, k, mode="exact")
+    oi, od, on = O.flat_scan(O.L2, base, qs, k)
+    _same(ei, ed, oi, od)
+    # tombstones on old and added rows
+    dead = np.concatenate([want_i[:5, 0], want_i[5:10, 1]]).astype(np.uint64)
+    ix.add_tombstones(dead)
+    ids2, _, _ = ix.search_batch(qs, k, ef=ef, mode="hnsw")
+    assert not set(ids2.ravel().tolist()) & set(dead.tolist())
+    ix.remove_tombstones(dead)
+    # a snapshot holding the added rows empties the delta
+    for i in range(n0, n1):
+        ref.add(i, base[i])
+    ix.upload_graph(ref.export_graph())
+    assert ix.delta_size() == 0
+    ids3, ds3, _ = ix.search_batch(qs, k, ef=ef, mode="hnsw")
+    ri, rd, rn, _ = ref.search_batch(qs, k, ef)
+    _same(ids3, ds3, ri, rd)
+    ix.close()
+
+
+def test_mutable_index_delta_with_per_query_allow_lists():
+    n0, n1, d, k = 3000, 3600, 24, 10
+    rng = np.random.default_rng(52)
+    base = rng.random((n1, d), dtype=np.float32)
+    qs = rng.random((64, d), dtype=np.float32)
+    ref = O.Index(d, "l2-squared", 16, 64, capacity=n1, seed=6)
+    ref.add_batch(base[:n0], threads=4)
+    ix = W.GPUVectorIndex(d, "l2-squared", capacity=n1, max_connections=16, forbid_flat=True)
+    ix.upload_vectors(base[:n0])
+    ix.upload_graph(ref.export_graph())
+    ix.add(np.arange(n0, n1), base[n0:])
+    per = [W.AllowList.from_ids(np.nonzero(rng.random(n1) < 0.5)[0], n1) for _ in range(len(qs))]
+    ids, ds, cnt = ix.search_batch(qs, k, ef=64, allow=per, mode="hnsw")
+    for i in range(len(qs)):
+        gi, gd, _, _ = ref.search_batch(qs[i:i + 1], k, 64, allow=per[i].words)
+        fi, fd, fn = O.flat_scan(O.L2, base[n0:], qs[i:i + 1], k, allow_bits=per[i].words[n0 // 64:] if n0 % 64 == 0
+                                 else None)
+        sel = np.array([j for j in range(n0, n1) if per[i].contains(j)], np.int64)
+        fi, fd, fn = O.flat_scan(O.L2, base[sel], qs[i:i + 1], k)
+        wi, wd = _merge_topk(gi, gd, sel[fi.astype(np.int64)].astype(np.uint64), fd, k)
+        _same(ids[i, : cnt[i]], ds[i, : cnt[i]], wi[0], wd[0])
+    ix.close()

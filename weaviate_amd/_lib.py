@@ -77,6 +77,10 @@ SIGNATURES = {
                                         C.c_uint64]),
     "wv_index_set_tombstones": (C.c_int, [_vp, _vp, C.c_uint64]),
     "wv_search_time_ef": (C.c_int, [_vp, C.c_int]),
+    "wv_index_add": (C.c_int, [_vp, _vp, _vp, C.c_uint64]),
+    "wv_index_add_tombstones": (C.c_int, [_vp, _vp, C.c_uint64]),
+    "wv_index_remove_tombstones": (C.c_int, [_vp, _vp, C.c_uint64]),
+    "wv_index_delta_size": (C.c_int, [_vp, _u64p]),
     "wv_search_by_vector": (C.c_int, [_vp, _vp, C.c_int, _vp, C.c_uint64, _vp, _vp, _vp]),
     "wv_search_by_vector_distance": (C.c_int, [_vp, _vp, C.c_float, C.c_int64, _vp, C.c_uint64, _vp, _vp, C.c_int64,
                                                C.POINTER(C.c_int64)]),

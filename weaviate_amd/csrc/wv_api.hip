@@ -205,6 +205,12 @@ struct wv_index {
     DevBuf out_ids, out_d, out_n;
     DevBuf fail_thr, fb_idx, fb_d, fb_i, fb_n, fb_of;
     DevBuf ac_cnt, ac_off, rowidx;   // allow-list compaction
+    // mutable-index sync: rows added since the last graph
+    // upload are "pending"; those the graph does not hold are the delta set,
+    // searched exactly beside the graph
+    std::vector<uint64_t> pending_host;
+    uint64_t delta_count = 0;
+    DevBuf delta, dmask, dl_ids, dl_d, dl_n, dq_tmp;
     // stats of the last batch
     uint64_t last_dist = 0, last_exp = 0, last_fallbacks = 0;
     // optional kernel timing (hipEvents on the launch stream)
@@ -227,11 +233,26 @@ int refresh_bitmaps(wv_index* ix) {
         if (w < ix->tomb_host.size()) v |= ix->tomb_host[w];
         ex[w] = v;
     }
+    std::vector<uint64_t> dl(words, 0);
+    uint64_t dcount = 0;
     if (ix->has_graph) {
         for (uint64_t i = 0; i < ix->capacity; ++i) {
             const bool nil = i >= ix->gn || ix->levels_host[i] < 0;
-            if (nil) ex[i >> 6] |= 1ull << (i & 63);
+            const uint64_t bit = 1ull << (i & 63);
+            const bool pend = ix->pending_host[i >> 6] & bit;
+            // a nil node is skipped by flatSearch (flat_search.go:29-40) unless
+            // it was added after the graph snapshot: then it is live (delta)
+            if (nil && !pend) ex[i >> 6] |= bit;
+            if (nil && pend && (ix->has_vec[i >> 6] & bit) && !(ex[i >> 6] & bit)) {
+                dl[i >> 6] |= bit;
+                dcount++;
+            }
         }
+    }
+    ix->delta_count = dcount;
+    if (dcount) {
+        HIP_TRY(ix->delta.ensure(words * 8));
+        HIP_TRY(hipMemcpyAsync(ix->delta.p, dl.data(), words * 8, hipMemcpyHostToDevice, ix->stream));
     }
     std::vector<uint64_t> tb(words, 0);
     for (uint64_t w = 0; w < words && w < ix->tomb_host.size(); ++w) tb[w] = ix->tomb_host[w];
@@ -328,7 +349,7 @@ __global__ void pad_rowidx_kernel(uint32_t* rowidx, uint64_t from, uint64_t to) 
 // Ascending list of the rows a shared allow list keeps (allowed, not excluded,
 // < N) into ix->rowidx, padded to whole tiles; *n_ok = its length.
 int compact_allowed(wv_index* ix, const uint64_t* d_allow, uint64_t allow_nbits, uint64_t N, uint64_t* n_ok,
-                    hipStream_t s) {
+                    hipStream_t s, bool always = false) {
     const uint64_t words = (N + 63) / 64;
     const uint64_t allow_words = (allow_nbits + 63) / 64;
     HIP_TRY(ix->ac_cnt.ensure((words + 1) * 4));
@@ -348,7 +369,7 @@ int compact_allowed(wv_index* ix, const uint64_t* d_allow, uint64_t allow_nbits,
     HIP_TRY(hipMemcpyAsync(&total, ix->ac_off.as<uint32_t>() + words, 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     *n_ok = total;
-    if (total == 0 || 2 * (uint64_t)total >= N) return WV_OK;
+    if (total == 0 || (2 * (uint64_t)total >= N && !always)) return WV_OK;
     const uint64_t padded = (total + wv::BF_BN - 1) / wv::BF_BN * wv::BF_BN;
     HIP_TRY(ix->rowidx.ensure(padded * 4));
     hipLaunchKernelGGL(allowed_scatter_kernel, dim3(blocks), dim3(256), 0, s, d_allow, allow_words,
@@ -362,8 +383,12 @@ int compact_allowed(wv_index* ix, const uint64_t* d_allow, uint64_t allow_nbits,
 }
 
 // Brute force (flatSearch semantics) over a device batch of prepared queries.
+// d_rowmask (nullable, with per-query allow lists only): a shared bitmap that
+// contains every row any query may return (the delta set of wv_index_add);
+// its rows are compacted and each query's own list is tested per row.
 int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_allow, uint64_t allow_nbits,
-              uint64_t allow_stride, uint64_t* d_out_ids, float* d_out_d, int32_t* d_out_n, hipStream_t s) {
+              uint64_t allow_stride, uint64_t* d_out_ids, float* d_out_d, int32_t* d_out_n, hipStream_t s,
+              const uint64_t* d_rowmask = nullptr, uint64_t rowmask_nbits = 0) {
     const uint64_t N = ix->n_rows;
     if (N == 0 || nq == 0) {
         if (nq) HIP_TRY(hipMemsetAsync(d_out_n, 0, sizeof(int32_t) * nq, s));
@@ -378,15 +403,17 @@ int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
         // flat_search.go:25-58) instead of masking N.
         uint64_t n_scan = N;
         const uint32_t* d_rowidx = nullptr;
-        if (d_allow && !allow_stride) {
+        const uint64_t* cmask = d_allow && !allow_stride ? d_allow : d_rowmask;
+        const uint64_t cbits = d_allow && !allow_stride ? allow_nbits : rowmask_nbits;
+        if (cmask) {
             uint64_t n_ok = 0;
-            int rc = compact_allowed(ix, d_allow, allow_nbits, N, &n_ok, s);
+            int rc = compact_allowed(ix, cmask, cbits, N, &n_ok, s, d_rowmask != nullptr);
             if (rc) return rc;
             if (n_ok == 0) {
                 HIP_TRY(hipMemsetAsync(d_out_n, 0, sizeof(int32_t) * nq, s));
                 return WV_OK;
             }
-            if (2 * n_ok < N && !std::getenv("WV_BF_NO_COMPACT")) {
+            if ((2 * n_ok < N && !std::getenv("WV_BF_NO_COMPACT")) || d_rowmask) {
                 n_scan = n_ok;
                 d_rowidx = ix->rowidx.as<uint32_t>();
             }
@@ -412,7 +439,9 @@ int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
         bp.xnorm = ix->xnorm.as<float>();
         bp.tomb = d_rowidx ? nullptr : ix->excl.as<uint64_t>();
         bp.tomb_nbits = ix->capacity;
-        bp.allow = d_rowidx ? nullptr : d_allow;
+        // compacted rows carry the shared list already; per-query lists are
+        // still tested (per gathered row)
+        bp.allow = d_rowidx && !allow_stride ? nullptr : d_allow;
         bp.allow_nbits = allow_nbits;
         bp.allow_stride = allow_stride;
         bp.rowidx = d_rowidx;
@@ -631,6 +660,58 @@ int run_hnsw(wv_index* ix, const float* d_q, int nq, int k, int ef, const uint64
     return WV_OK;
 }
 
+// out[r][w] = a[r or 0][w] & b[w]  (rows x words; a_stride 0 = one shared row)
+__global__ void and_bits_kernel(const uint64_t* a, uint64_t a_words, uint64_t a_stride, const uint64_t* b,
+                                uint64_t words, int rows, uint64_t* out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= words * (uint64_t)rows) return;
+    const uint64_t r = i / words, w = i % words;
+    const uint64_t av = a ? (w < a_words ? a[r * a_stride + w] : 0ull) : ~0ull;
+    out[i] = av & b[w];
+}
+
+// knnSearchByVector over the uploaded graph, plus an exact pass over the
+// delta set (rows added since the graph snapshot), merged by
+// (dist, id): added rows are findable at once, as in the reference where
+// Add inserts into the live graph (insert.go:43-65).  Exact over the delta is
+// a superset in quality of a graph search.
+int run_hnsw_delta(wv_index* ix, const float* d_q, int nq, int k, int ef, const uint64_t* d_allow,
+                   uint64_t allow_nbits, uint64_t allow_stride, uint64_t* d_out_ids, float* d_out_d,
+                   int32_t* d_out_n, hipStream_t s) {
+    if (ix->delta_count == 0 || nq == 0)
+        return run_hnsw(ix, d_q, nq, k, ef, d_allow, allow_nbits, allow_stride, d_out_ids, d_out_d, d_out_n, s);
+    const size_t nk = (size_t)nq * k;
+    HIP_TRY(ix->dl_ids.ensure(2 * nk * 8));
+    HIP_TRY(ix->dl_d.ensure(2 * nk * 4));
+    HIP_TRY(ix->dl_n.ensure(2 * (size_t)nq * 4));
+    uint64_t* ids = ix->dl_ids.as<uint64_t>();
+    float* ds = ix->dl_d.as<float>();
+    int32_t* ns = ix->dl_n.as<int32_t>();
+    int rc = run_hnsw(ix, d_q, nq, k, ef, d_allow, allow_nbits, allow_stride, ids, ds, ns, s);
+    if (rc) return rc;
+    const uint64_t words = ix->bm_words;
+    const int rows = d_allow && allow_stride ? nq : 1;
+    HIP_TRY(ix->dmask.ensure((size_t)rows * words * 8));
+    hipLaunchKernelGGL(and_bits_kernel, dim3((unsigned)((rows * words + 255) / 256)), dim3(256), 0, s, d_allow,
+                       (allow_nbits + 63) / 64, allow_stride ? allow_stride : 0, ix->delta.as<uint64_t>(), words, rows,
+                       ix->dmask.as<uint64_t>());
+    HIP_TRY(hipGetLastError());
+    const uint64_t st = d_allow && allow_stride ? words : 0;
+    const float t_h = ix->t_hnsw;
+    const uint64_t e = ix->last_dist, x = ix->last_exp, f = ix->last_fallbacks;
+    rc = run_exact(ix, d_q, nq, k, ix->dmask.as<uint64_t>(), ix->capacity, st, ids + nk, ds + nk, ns + nq, s,
+                   st ? ix->delta.as<uint64_t>() : nullptr, ix->capacity);
+    if (rc) return rc;
+    ix->t_hnsw = t_h;
+    ix->last_dist = e;
+    ix->last_exp = x;
+    ix->last_fallbacks += f;
+    hipLaunchKernelGGL(merge_shards_kernel, dim3((nq + 127) / 128), dim3(128), 0, s, ds, ids, ns, 2, nq, k, d_out_d,
+                       d_out_ids, d_out_n);
+    HIP_TRY(hipGetLastError());
+    return WV_OK;
+}
+
 // Core: device queries already padded to dpad and normalized (cosine).
 int search_core(wv_index* ix, const float* d_q, int nq, int k, int ef, const uint64_t* d_allow,
                 uint64_t allow_nbits, uint64_t allow_stride, int mode, uint64_t* d_out_ids, float* d_out_d,
@@ -645,13 +726,13 @@ int search_core(wv_index* ix, const float* d_q, int nq, int k, int ef, const uin
     if (mode == WV_MODE_HNSW) {
         if (ef > wv::HNSW_EF_MAX)
             return run_exact(ix, d_q, nq, k, d_allow, allow_nbits, allow_stride, d_out_ids, d_out_d, d_out_n, s);
-        return run_hnsw(ix, d_q, nq, k, ef, d_allow, allow_nbits, allow_stride, d_out_ids, d_out_d, d_out_n, s);
+        return run_hnsw_delta(ix, d_q, nq, k, ef, d_allow, allow_nbits, allow_stride, d_out_ids, d_out_d, d_out_n, s);
     }
     // AUTO: search.go:74-78
     const bool can_hnsw = ix->has_graph && ef <= wv::HNSW_EF_MAX;
     if (!d_allow || ix->cfg.forbid_flat) {
         if (can_hnsw)
-            return run_hnsw(ix, d_q, nq, k, ef, d_allow, allow_nbits, allow_stride, d_out_ids, d_out_d, d_out_n, s);
+            return run_hnsw_delta(ix, d_q, nq, k, ef, d_allow, allow_nbits, allow_stride, d_out_ids, d_out_d, d_out_n, s);
         return run_exact(ix, d_q, nq, k, d_allow, allow_nbits, allow_stride, d_out_ids, d_out_d, d_out_n, s);
     }
     // allowList.Len() < flatSearchCutoff decides per query
@@ -674,7 +755,7 @@ int search_core(wv_index* ix, const float* d_q, int nq, int k, int ef, const uin
     if (knn.empty())
         return run_exact(ix, d_q, nq, k, d_allow, allow_nbits, allow_stride, d_out_ids, d_out_d, d_out_n, s);
     if (flat.empty())
-        return run_hnsw(ix, d_q, nq, k, ef, d_allow, allow_nbits, allow_stride, d_out_ids, d_out_d, d_out_n, s);
+        return run_hnsw_delta(ix, d_q, nq, k, ef, d_allow, allow_nbits, allow_stride, d_out_ids, d_out_d, d_out_n, s);
     // split the batch: gather each group, run, scatter back
     for (int pass = 0; pass < 2; ++pass) {
         const std::vector<int32_t>& sel = pass == 0 ? flat : knn;
@@ -699,7 +780,7 @@ int search_core(wv_index* ix, const float* d_q, int nq, int k, int ef, const uin
         HIP_TRY(hipGetLastError());
         int rc2 = pass == 0 ? run_exact(ix, ix->g_q.as<float>(), n, k, al, allow_nbits, ast, ix->g_ids.as<uint64_t>(),
                                         ix->g_d.as<float>(), ix->g_n.as<int32_t>(), s)
-                            : run_hnsw(ix, ix->g_q.as<float>(), n, k, ef, al, allow_nbits, ast,
+                            : run_hnsw_delta(ix, ix->g_q.as<float>(), n, k, ef, al, allow_nbits, ast,
                                        ix->g_ids.as<uint64_t>(), ix->g_d.as<float>(), ix->g_n.as<int32_t>(), s);
         if (rc2) return rc2;
         hipLaunchKernelGGL(scatter_results_kernel, dim3(n), dim3(64), 0, s, ix->g_ids.as<uint64_t>(),
@@ -792,6 +873,7 @@ int wv_index_create(int dim, int metric, const wv_config* cfg, uint64_t capacity
     (void)hipStreamSynchronize(ix->stream);
     ix->has_vec.assign(ix->bm_words, 0);
     ix->tomb_host.assign(ix->bm_words, 0);
+    ix->pending_host.assign(ix->bm_words, 0);
     *out = ix;
     return WV_OK;
 }
@@ -895,6 +977,8 @@ int wv_index_upload_graph(wv_index* ix, uint64_t n, const int8_t* levels, const 
     HIP_TRY(hipStreamSynchronize(ix->stream));
     ix->levels_host.assign(levels, levels + n);
     ix->any_nil = std::any_of(levels, levels + n, [](int8_t l) { return l < 0; });
+    for (uint64_t i = 0; i < n; ++i)   // the new snapshot holds these added rows
+        if (levels[i] >= 0) ix->pending_host[i >> 6] &= ~(1ull << (i & 63));
     ix->levels_host.resize(ix->capacity, -1);
     ix->gn = n;
     ix->deg0 = deg0;
@@ -918,6 +1002,78 @@ int wv_index_set_tombstones(wv_index* ix, const uint64_t* bits, uint64_t nbits) 
     for (uint64_t i = 0; i < ix->bm_words; ++i)
         if (ix->tomb_host[i]) { ix->any_tomb = true; break; }
     ix->bitmaps_dirty = true;
+    return WV_OK;
+}
+
+__global__ void scatter_rows_kernel(const float* src, int ld_src, const uint64_t* ids, uint64_t n, int ldx,
+                                    float* X, const float* norms, float* xnorm) {
+    const uint64_t r = blockIdx.x;
+    if (r >= n) return;
+    const uint64_t id = ids[r];
+    for (int i = threadIdx.x; i < ldx; i += blockDim.x) X[id * ldx + i] = src[r * (uint64_t)ld_src + i];
+    if (threadIdx.x == 0) xnorm[id] = norms[r];
+}
+
+int wv_index_add(wv_index* ix, const uint64_t* ids, const float* rows, uint64_t n) {
+    if (check(ix) || (n && (!ids || !rows))) return fail(WV_EINVAL, "wv_index_add: bad argument");
+    if (n == 0) return WV_OK;
+    std::lock_guard<std::mutex> g(ix->mu);
+    for (uint64_t i = 0; i < n; ++i)
+        if (ids[i] >= ix->capacity) return fail(WV_EINVAL, "wv_index_add: id beyond capacity");
+    HIP_TRY(hipSetDevice(ix->cfg.device));
+    hipStream_t s = ix->stream;
+    // rows -> [n][ldx] padded (normalized for cosine, insert.go:56-60), their
+    // |x|^2, then scattered to their ids
+    HIP_TRY(ix->stage.ensure(n * (size_t)ix->dim * 4));
+    HIP_TRY(ix->dq_tmp.ensure(n * (size_t)ix->ldx * 4 + n * 4 + n * 8));
+    float* tmp = ix->dq_tmp.as<float>();
+    float* nrm = tmp + n * (size_t)ix->ldx;
+    uint64_t* d_ids = reinterpret_cast<uint64_t*>(nrm + n + (n & 1));
+    HIP_TRY(hipMemcpyAsync(ix->stage.p, rows, n * (size_t)ix->dim * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d_ids, ids, n * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(launch_pad_rows(ix->stage.as<float>(), ix->dim, n, ix->dim, tmp, ix->ldx, s));
+    if (ix->metric == WV_COSINE_DOT) HIP_TRY(wv_launch_normalize(tmp, tmp, n, ix->dim, ix->ldx, s));
+    HIP_TRY(wv_launch_rownorm(tmp, n, ix->dim, ix->ldx, nrm, ix->maxnorm.as<unsigned int>(), s));
+    hipLaunchKernelGGL(scatter_rows_kernel, dim3((unsigned)n), dim3(128), 0, s, tmp, ix->ldx, d_ids, n, ix->ldx,
+                       ix->vecs.as<float>(), nrm, ix->xnorm.as<float>());
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(s));
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t id = ids[i];
+        ix->has_vec[id >> 6] |= 1ull << (id & 63);
+        ix->pending_host[id >> 6] |= 1ull << (id & 63);
+        ix->n_rows = std::max(ix->n_rows, id + 1);
+    }
+    ix->bitmaps_dirty = true;
+    return WV_OK;
+}
+
+static int edit_tombstones(wv_index* ix, const uint64_t* ids, uint64_t n, bool add) {
+    if (check(ix) || (n && !ids)) return fail(WV_EINVAL, "bad argument");
+    std::lock_guard<std::mutex> g(ix->mu);
+    for (uint64_t i = 0; i < n; ++i) {
+        if (ids[i] >= ix->capacity) return fail(WV_EINVAL, "tombstone id beyond capacity");
+        const uint64_t bit = 1ull << (ids[i] & 63);
+        if (add) ix->tomb_host[ids[i] >> 6] |= bit;
+        else ix->tomb_host[ids[i] >> 6] &= ~bit;
+    }
+    ix->any_tomb = std::any_of(ix->tomb_host.begin(), ix->tomb_host.end(), [](uint64_t w) { return w != 0; });
+    ix->bitmaps_dirty = true;
+    return WV_OK;
+}
+
+int wv_index_add_tombstones(wv_index* ix, const uint64_t* ids, uint64_t n) { return edit_tombstones(ix, ids, n, true); }
+int wv_index_remove_tombstones(wv_index* ix, const uint64_t* ids, uint64_t n) {
+    return edit_tombstones(ix, ids, n, false);
+}
+
+int wv_index_delta_size(wv_index* ix, uint64_t* n) {
+    if (check(ix) || !n) return fail(WV_EINVAL, "bad argument");
+    std::lock_guard<std::mutex> g(ix->mu);
+    HIP_TRY(hipSetDevice(ix->cfg.device));
+    int rc = refresh_bitmaps(ix);
+    if (rc) return rc;
+    *n = ix->delta_count;
     return WV_OK;
 }
 

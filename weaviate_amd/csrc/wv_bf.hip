@@ -187,7 +187,9 @@ __global__ __launch_bounds__(256, WV_BF_WAVES_PER_SIMD) void wv_bf_mfma_kernel(B
             if (tomb && word < tomb_words) okw &= ~tomb[word];
             uint64_t aq0 = ~0ull, aq1 = ~0ull;
             if (allow) {
-                if (p.allow_stride) {
+                if (p.allow_stride && rowidx) {
+                    // compacted rows + per-query lists: tested per row in the epilogue
+                } else if (p.allow_stride) {
                     aq0 = (jq0 < p.nq && word < allow_words) ? allow[(uint64_t)jq0 * p.allow_stride + word] : 0ull;
                     aq1 = (jq1 < p.nq && word < allow_words) ? allow[(uint64_t)jq1 * p.allow_stride + word] : 0ull;
                 } else {
@@ -268,8 +270,25 @@ __global__ __launch_bounds__(256, WV_BF_WAVES_PER_SIMD) void wv_bf_mfma_kernel(B
             const uint32_t rb0 = (uint32_t)row0 + 4 * khalf;   // row of acc*0[0]
             const uint64_t o0 = (jq0 < p.nq ? okw & aq0 : 0ull) >> (4 * khalf);
             const uint64_t o1 = (jq1 < p.nq ? okw & aq1 : 0ull) >> (4 * khalf);
-            const uint32_t o0lo = (uint32_t)o0, o0hi = (uint32_t)(o0 >> 32);
-            const uint32_t o1lo = (uint32_t)o1, o1hi = (uint32_t)(o1 >> 32);
+            uint32_t o0lo = (uint32_t)o0, o0hi = (uint32_t)(o0 >> 32);
+            uint32_t o1lo = (uint32_t)o1, o1hi = (uint32_t)(o1 >> 32);
+            if (rowidx && allow && p.allow_stride) {
+                // per-query lists over gathered rows (the small delta set of
+                // wv_index_add): one bit test per row and query column
+                const uint64_t* a0 = allow + (uint64_t)min(jq0, p.nq - 1) * p.allow_stride;
+                const uint64_t* a1 = allow + (uint64_t)min(jq1, p.nq - 1) * p.allow_stride;
+                uint32_t g0lo = 0, g0hi = 0, g1lo = 0, g1hi = 0;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int bit = (r & 3) + 8 * (r >> 2);
+                    const uint32_t ia = rowidx[rb0 + bit], ib = rowidx[rb0 + 32 + bit];
+                    g0lo |= (uint32_t)bit_test(a0, p.allow_nbits, ia) << bit;
+                    g0hi |= (uint32_t)bit_test(a0, p.allow_nbits, ib) << bit;
+                    g1lo |= (uint32_t)bit_test(a1, p.allow_nbits, ia) << bit;
+                    g1hi |= (uint32_t)bit_test(a1, p.allow_nbits, ib) << bit;
+                }
+                o0lo &= g0lo; o0hi &= g0hi; o1lo &= g1lo; o1hi &= g1hi;
+            }
             constexpr uint32_t LANE_ROWS = 0x0F0F0F0Fu;   // bits (r&3) + 8*(r>>2), r < 16
             const float INF = __builtin_inff();
             // pass 1: the accumulators already hold the approximate keys; mask

@@ -140,6 +140,28 @@ class GPUVectorIndex:
         self.upload_graph(g)
         check(lib().wv_index_set_tombstones(self._h, _ptr(g["tomb_bits"]), g["n"]))
 
+    def add(self, ids, rows):
+        """hnsw.Add (insert.go:43-65) on the GPU mirror: rows at arbitrary ids,
+        searchable at once (delta set, exact) until a graph snapshot holds them."""
+        ids = np.ascontiguousarray(np.atleast_1d(np.asarray(ids, dtype=np.uint64)))
+        rows = np.ascontiguousarray(rows, dtype=np.float32).reshape(len(ids), -1)
+        if rows.shape[1] != self.dim:
+            raise WvError(1, f"vector lengths don't match: {rows.shape[1]} vs {self.dim}")
+        check(lib().wv_index_add(self._h, _ptr(ids), _ptr(rows), len(ids)))
+
+    def add_tombstones(self, ids):
+        ids = np.ascontiguousarray(np.atleast_1d(np.asarray(ids, dtype=np.uint64)))
+        check(lib().wv_index_add_tombstones(self._h, _ptr(ids), len(ids)))
+
+    def remove_tombstones(self, ids):
+        ids = np.ascontiguousarray(np.atleast_1d(np.asarray(ids, dtype=np.uint64)))
+        check(lib().wv_index_remove_tombstones(self._h, _ptr(ids), len(ids)))
+
+    def delta_size(self) -> int:
+        n = C.c_uint64()
+        check(lib().wv_index_delta_size(self._h, C.byref(n)))
+        return n.value
+
     def set_tombstones(self, ids: Iterable[int]):
         al = AllowList.from_ids(ids, self.capacity)
         check(lib().wv_index_set_tombstones(self._h, _ptr(al.words), al.nbits))
