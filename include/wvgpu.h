@@ -103,6 +103,22 @@ int wv_index_upload_graph(wv_index *ix, uint64_t n, const int8_t *levels, const 
                           const uint32_t *upper_row, const uint32_t *upper, uint64_t n_upper, int degU,
                           int max_level, uint64_t entrypoint);
 
+/* GPU graph construction: the graph of rows [0, n_rows),
+ * built on the device with the reference's insert (insert.go:103-217): level
+ * floor(-ln(U)/ln(M)) (U counter-based per id and seed, the same draw as the
+ * CPU restatement), ef=1 descent, efConstruction search per level,
+ * selectNeighborsHeuristic to M (heuristic.go:23-135), bidirectional links
+ * re-pruned at 2M (layer 0) / M (connectNeighborAtLevel,
+ * neighbor_connections.go:134-209).  Nodes are inserted in id order in
+ * batches of max(1, inserted / batch_div) (at most 16384) that search the
+ * graph of all earlier batches.  The result is the index's graph (as after
+ * wv_index_upload_graph, M = cfg.max_connections). */
+int wv_index_build_graph(wv_index *ix, int ef_construction, uint64_t seed, int batch_div);
+/* The index's graph in the wv_index_upload_graph layout (nullable outputs). */
+int wv_index_graph_info(wv_index *ix, uint64_t *n, int *deg0, int *degU, int *max_level, uint64_t *n_upper,
+                        uint64_t *entrypoint);
+int wv_index_download_graph(wv_index *ix, int8_t *levels, uint32_t *layer0, uint32_t *upper_row, uint32_t *upper);
+
 /* Tombstones (delete.go:546-566) as a bitmap over local ids (replaces the set). */
 int wv_index_set_tombstones(wv_index *ix, const uint64_t *bits, uint64_t nbits);
 

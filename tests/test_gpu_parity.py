@@ -563,3 +563,47 @@ def test_mutable_index_delta_with_per_query_allow_lists():
         wi, wd = _merge_topk(gi, gd, sel[fi.astype(np.int64)].astype(np.uint64), fd, k)
         _same(ids[i, : cnt[i]], ds[i, : cnt[i]], wi[0], wd[0])
     ix.close()
+
+
+def _recall(ids, truth, k=10):
+    return float(np.mean([len(set(a[:k]) & set(b[:k])) / k for a, b in zip(ids.tolist(), truth.tolist())]))
+
+
+def test_gpu_graph_build_invariants_and_recall():
+    """the graph built on the GPU (insert.go's algorithm in
+    batches) keeps the reference's invariants -- layer-0 degree <= 2M, upper
+    <= M (index_too_many_links_bug_integration_test.go:127-143), valid ids, no
+    self links, the entrypoint on the top level -- reaches the recall of the
+    restatement's sequential build within 2 points, and the restatement
+    searching the GPU-built graph answers exactly like the GPU does."""
+    n, d, M, efc, ef = 20000, 32, 16, 64, 64
+    rng = np.random.default_rng(61)
+    base = rng.random((n, d), dtype=np.float32)
+    qs = rng.random((300, d), dtype=np.float32)
+    ix = W.GPUVectorIndex(d, "l2-squared", capacity=n, max_connections=M)
+    ix.upload_vectors(base)
+    ix.build_graph(ef_construction=efc, seed=7, batch_div=32)
+    g = ix.download_graph()
+    l0, lv = g["layer0"], g["levels"]
+    assert g["deg0"] == 2 * M and g["degU"] == M
+    valid = l0 != 0xFFFFFFFF
+    assert (l0[valid] < n).all()
+    assert not (l0 == np.arange(n, dtype=np.uint32)[:, None]).any()
+    assert (valid.sum(1) > 0).all()                      # every node reachable from somewhere has links
+    assert lv[g["entrypoint"]] == g["max_level"] == lv.max()
+    up = g["upper"]
+    assert ((up != 0xFFFFFFFF).sum(2) <= M).all()
+    truth, _, _ = O.flat_scan(O.L2, base, qs, 10)
+    gi, gd, gn = ix.search_batch(qs, 10, ef=ef, mode="hnsw")
+    ref = O.Index(d, "l2-squared", M, efc, capacity=n, seed=7)
+    ref.add_batch(base, threads=8)
+    oi, od, on, _ = ref.search_batch(qs, 10, ef, threads=8)
+    r_gpu, r_cpu = _recall(gi, truth), _recall(oi, truth)
+    assert r_gpu >= r_cpu - 0.02, (r_gpu, r_cpu)
+    # the restatement on the GPU-built graph == the GPU on it
+    ref2 = O.Index(d, "l2-squared", M, efc, capacity=n, seed=7)
+    ref2.import_graph(base, g)
+    ri, rd, rn, _ = ref2.search_batch(qs, 10, ef, threads=8)
+    for i in range(len(qs)):
+        _same_tie_aware(gi[i], gd[i], ri[i], rd[i])
+    ix.close()

@@ -78,6 +78,10 @@ SIGNATURES = {
     "wv_index_set_tombstones": (C.c_int, [_vp, _vp, C.c_uint64]),
     "wv_search_time_ef": (C.c_int, [_vp, C.c_int]),
     "wv_index_add": (C.c_int, [_vp, _vp, _vp, C.c_uint64]),
+    "wv_index_build_graph": (C.c_int, [_vp, C.c_int, C.c_uint64, C.c_int]),
+    "wv_index_graph_info": (C.c_int, [_vp, _u64p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int), _u64p,
+                                      _u64p]),
+    "wv_index_download_graph": (C.c_int, [_vp, _vp, _vp, _vp, _vp]),
     "wv_index_add_tombstones": (C.c_int, [_vp, _vp, C.c_uint64]),
     "wv_index_remove_tombstones": (C.c_int, [_vp, _vp, C.c_uint64]),
     "wv_index_delta_size": (C.c_int, [_vp, _u64p]),

@@ -33,6 +33,9 @@ hipError_t wv_launch_normalize(const float* in, float* out, uint64_t n, int D, i
 hipError_t wv_launch_scale(const float* in, float* out, uint64_t n, float scale, hipStream_t s);
 hipError_t wv_launch_qnorm(const float* Q, int nq, int D, int ldq, int metric, float* out, hipStream_t s);
 hipError_t wv_launch_hnsw(const wv::HnswParams* p, int waves_per_block, hipStream_t s);
+hipError_t wv_launch_build_search(const wv::BuildParams* b, int waves_per_block, hipStream_t s);
+hipError_t wv_launch_build_select(const wv::BuildParams* b, hipStream_t s);
+hipError_t wv_launch_build_link(const wv::BuildParams* b, hipStream_t s);
 int wv_hnsw_per_wave_words(int dpad, int efc, int sc, int vc_log2, int xs_log2);
 }
 
@@ -211,6 +214,8 @@ struct wv_index {
     std::vector<uint64_t> pending_host;
     uint64_t delta_count = 0;
     DevBuf delta, dmask, dl_ids, dl_d, dl_n, dq_tmp;
+    // graph construction scratch
+    DevBuf b_tgt, b_ci, b_cd, b_cn, b_cnt0, b_cntu, b_rk, b_rn, b_rk2, b_rn2, b_uk, b_ul, b_uo, b_nr, b_tmp;
     // stats of the last batch
     uint64_t last_dist = 0, last_exp = 0, last_fallbacks = 0;
     // optional kernel timing (hipEvents on the launch stream)
@@ -616,6 +621,7 @@ int run_hnsw(wv_index* ix, const float* d_q, int nq, int k, int ef, const uint64
     hp.deg0 = ix->deg0;
     hp.degU = ix->degU;
     hp.max_level = ix->max_level;
+    hp.upper_levels = ix->max_level;
     hp.nq = nq;
     hp.k = k;
     hp.ef = ef;
@@ -1074,6 +1080,207 @@ int wv_index_delta_size(wv_index* ix, uint64_t* n) {
     int rc = refresh_bitmaps(ix);
     if (rc) return rc;
     *n = ix->delta_count;
+    return WV_OK;
+}
+
+// level draw of the restatement (oracle/wv_oracle.c insert_node): a
+// counter-based U(0,1) per id, targetLevel = floor(-ln(U) * 1/ln(M))
+// (insert.go:132, index.go:226) -- identical levels on the CPU and the GPU
+static int draw_level(uint64_t seed, uint64_t id, double normalizer) {
+    auto mix = [](uint64_t x) {
+        x ^= x >> 30; x *= 0xBF58476D1CE4E5B9ull;
+        x ^= x >> 27; x *= 0x94D049BB133111EBull;
+        x ^= x >> 31;
+        return x;
+    };
+    const uint64_t r = mix(seed * 0xD1B54A32D192ED03ull + id * 0x9E3779B97F4A7C15ull + 1);
+    const double u = ((double)(r >> 11) + 0.5) * (1.0 / 9007199254740992.0);
+    const int t = (int)std::floor(-std::log(u) * normalizer);
+    return t > 126 ? 126 : t;
+}
+
+int wv_index_build_graph(wv_index* ix, int ef_construction, uint64_t seed, int batch_div) {
+    if (check(ix) || ef_construction < 1 || ef_construction > wv::HNSW_EF_MAX || batch_div < 1)
+        return fail(WV_EINVAL, "wv_index_build_graph: bad argument");
+    std::lock_guard<std::mutex> guard(ix->mu);
+    HIP_TRY(hipSetDevice(ix->cfg.device));
+    hipStream_t s = ix->stream;
+    const uint64_t n = ix->n_rows;
+    if (n == 0) return fail(WV_ESTATE, "wv_index_build_graph: no vectors");
+    for (uint64_t i = 0; i < n; ++i)
+        if (!(ix->has_vec[i >> 6] & (1ull << (i & 63)))) return fail(WV_ESTATE, "wv_index_build_graph: a row has no vector");
+    const int M = ix->cfg.max_connections, M0 = 2 * M;
+    if (M < 2 || M0 > 256) return fail(WV_EINVAL, "wv_index_build_graph: maxConnections out of range");
+    // levels: the first node is insertInitialElement's level 0 (insert.go:67-101)
+    std::vector<int8_t> lv(n);
+    const double norm = 1.0 / std::log((double)M);
+    int maxL = 0;
+    uint64_t n_upper = 0;
+    std::vector<uint32_t> urow(n, WV_NIL);
+    for (uint64_t i = 0; i < n; ++i) {
+        lv[i] = (int8_t)(i == 0 ? 0 : draw_level(seed, i, norm));
+        maxL = std::max<int>(maxL, lv[i]);
+        if (lv[i] >= 1) urow[i] = (uint32_t)n_upper++;
+    }
+    const int ul = std::max(1, maxL);
+    HIP_TRY(ix->levels.ensure(n));
+    HIP_TRY(ix->layer0.ensure(n * (size_t)M0 * 4));
+    HIP_TRY(ix->upper_row.ensure(n * 4));
+    HIP_TRY(ix->upper.ensure(std::max<uint64_t>(1, n_upper) * ul * (size_t)M * 4));
+    HIP_TRY(ix->b_cnt0.ensure(n * 4));
+    HIP_TRY(ix->b_cntu.ensure(std::max<uint64_t>(1, n_upper) * ul * 4));
+    HIP_TRY(hipMemsetAsync(ix->levels.p, 0xFF, n, s));   // -1: not inserted yet
+    HIP_TRY(hipMemsetAsync(ix->layer0.p, 0xFF, n * (size_t)M0 * 4, s));
+    HIP_TRY(hipMemsetAsync(ix->upper.p, 0xFF, std::max<uint64_t>(1, n_upper) * ul * (size_t)M * 4, s));
+    HIP_TRY(hipMemsetAsync(ix->b_cnt0.p, 0, n * 4, s));
+    HIP_TRY(hipMemsetAsync(ix->b_cntu.p, 0, std::max<uint64_t>(1, n_upper) * ul * 4, s));
+    HIP_TRY(hipMemcpyAsync(ix->upper_row.p, urow.data(), n * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(ix->levels.p, lv.data(), 1, hipMemcpyHostToDevice, s));   // node 0
+    uint64_t ep = 0;
+    int top = 0;
+    // per-wave search state as in run_hnsw (unfiltered layout)
+    const int efc = std::max(64, (ef_construction + 63) / 64 * 64);
+    const int fixed = wv_hnsw_per_wave_words(ix->dpad, efc, 0, 0, 0) - 1;
+    const int vc_log2 = choose_vc_log2(12 * 1024 / 4, fixed);
+    int per_wave = (wv_hnsw_per_wave_words(ix->dpad, efc, 0, vc_log2, 0) + 3) & ~3;
+    int wpb = 4;
+    while (wpb > 1 && (size_t)wpb * per_wave * 4 > 160 * 1024) --wpb;
+    const int bmax = 16384;
+    uint64_t done = 1;
+    while (done < n) {
+        const int nb = (int)std::min<uint64_t>(n - done, std::max<uint64_t>(1, std::min<uint64_t>(bmax, done / batch_div)));
+        int lb = 1;
+        for (int i = 0; i < nb; ++i) lb = std::max(lb, lv[done + i] + 1);
+        HIP_TRY(ix->b_tgt.ensure(nb));
+        HIP_TRY(ix->b_ci.ensure((size_t)nb * lb * ef_construction * 4));
+        HIP_TRY(ix->b_cd.ensure((size_t)nb * lb * ef_construction * 4));
+        HIP_TRY(ix->b_cn.ensure((size_t)nb * lb * 4));
+        const size_t nreq = (size_t)nb * lb * M;
+        HIP_TRY(ix->b_rk.ensure(nreq * 8));
+        HIP_TRY(ix->b_rn.ensure(nreq * 4));
+        HIP_TRY(ix->b_rk2.ensure(nreq * 8));
+        HIP_TRY(ix->b_rn2.ensure(nreq * 4));
+        HIP_TRY(ix->b_uk.ensure(nreq * 8));
+        HIP_TRY(ix->b_ul.ensure(nreq * 4));
+        HIP_TRY(ix->b_uo.ensure(nreq * 4));
+        HIP_TRY(ix->b_nr.ensure(8));
+        HIP_TRY(hipMemcpyAsync(ix->b_tgt.p, lv.data() + done, nb, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemsetAsync(ix->b_cn.p, 0, (size_t)nb * lb * 4, s));
+        wv::BuildParams b{};
+        wv::HnswParams& h = b.h;
+        h.X = ix->vecs.as<float>();
+        h.levels = ix->levels.as<int8_t>();
+        h.layer0 = ix->layer0.as<uint32_t>();
+        h.upper_row = ix->upper_row.as<uint32_t>();
+        h.upper = ix->upper.as<uint32_t>();
+        h.N = done;
+        h.entrypoint = (uint32_t)ep;
+        h.D = ix->dim;
+        h.ldx = ix->ldx;
+        h.ldq = ix->dpad;
+        h.metric = ix->metric;
+        h.deg0 = M0;
+        h.degU = M;
+        h.max_level = top;
+        h.upper_levels = ul;
+        h.nq = nb;
+        h.ef = ef_construction;
+        h.efc = efc;
+        h.sc = 0;
+        h.vc_log2 = vc_log2;
+        h.xs_log2 = 0;
+        h.dpad = ix->dpad;
+        h.per_wave_words = per_wave;
+        b.first = done;
+        b.nb = nb;
+        b.lb = lb;
+        b.M = M;
+        b.M0 = M0;
+        b.target = ix->b_tgt.as<int8_t>();
+        b.cand_i = ix->b_ci.as<uint32_t>();
+        b.cand_d = ix->b_cd.as<float>();
+        b.cand_n = ix->b_cn.as<int32_t>();
+        b.counts0 = ix->b_cnt0.as<uint32_t>();
+        b.countsU = ix->b_cntu.as<uint32_t>();
+        b.req_key = ix->b_rk.as<uint64_t>();
+        b.req_node = ix->b_rn.as<uint32_t>();
+        HIP_TRY(wv_launch_build_search(&b, wpb, s));
+        HIP_TRY(wv_launch_build_select(&b, s));
+        // reverse links grouped by (level, neighbour), batch order kept (stable)
+        size_t tb = 0, tb2 = 0, tb3 = 0;
+        HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, ix->b_rk.as<uint64_t>(), ix->b_rk2.as<uint64_t>(),
+                                                   ix->b_rn.as<uint32_t>(), ix->b_rn2.as<uint32_t>(), (int)nreq, 0, 64,
+                                                   s));
+        HIP_TRY(hipcub::DeviceRunLengthEncode::Encode(nullptr, tb2, ix->b_rk2.as<uint64_t>(), ix->b_uk.as<uint64_t>(),
+                                                      ix->b_ul.as<uint32_t>(), ix->b_nr.as<uint32_t>(), (int)nreq, s));
+        HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb3, ix->b_ul.as<uint32_t>(), ix->b_uo.as<uint32_t>(),
+                                                 (int)nreq, s));
+        HIP_TRY(ix->b_tmp.ensure(std::max(tb, std::max(tb2, tb3))));
+        HIP_TRY(hipcub::DeviceRadixSort::SortPairs(ix->b_tmp.p, tb, ix->b_rk.as<uint64_t>(), ix->b_rk2.as<uint64_t>(),
+                                                   ix->b_rn.as<uint32_t>(), ix->b_rn2.as<uint32_t>(), (int)nreq, 0, 64,
+                                                   s));
+        HIP_TRY(hipMemsetAsync(ix->b_ul.p, 0, nreq * 4, s));
+        HIP_TRY(hipcub::DeviceRunLengthEncode::Encode(ix->b_tmp.p, tb2, ix->b_rk2.as<uint64_t>(),
+                                                      ix->b_uk.as<uint64_t>(), ix->b_ul.as<uint32_t>(),
+                                                      ix->b_nr.as<uint32_t>(), (int)nreq, s));
+        HIP_TRY(hipcub::DeviceScan::ExclusiveSum(ix->b_tmp.p, tb3, ix->b_ul.as<uint32_t>(), ix->b_uo.as<uint32_t>(),
+                                                 (int)nreq, s));
+        uint32_t n_runs = 0;
+        HIP_TRY(hipMemcpyAsync(&n_runs, ix->b_nr.p, 4, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        b.run_key = ix->b_uk.as<uint64_t>();
+        b.run_off = ix->b_uo.as<uint32_t>();
+        b.run_len = ix->b_ul.as<uint32_t>();
+        b.sorted_node = ix->b_rn2.as<uint32_t>();
+        b.n_runs = (int)n_runs;
+        HIP_TRY(wv_launch_build_link(&b, s));
+        // the batch is in the graph: its levels make it reachable for the next one
+        HIP_TRY(hipMemcpyAsync(ix->levels.as<int8_t>() + done, lv.data() + done, nb, hipMemcpyHostToDevice, s));
+        for (int i = 0; i < nb; ++i)   // insert.go:202-213: a higher node becomes the entrypoint
+            if (lv[done + i] > top) { top = lv[done + i]; ep = done + i; }
+        done += nb;
+    }
+    HIP_TRY(hipStreamSynchronize(s));
+    ix->levels_host.assign(lv.begin(), lv.end());
+    ix->levels_host.resize(ix->capacity, -1);
+    ix->gn = n;
+    ix->deg0 = M0;
+    ix->degU = M;
+    ix->max_level = top;
+    ix->n_upper = n_upper;
+    ix->entrypoint = ep;
+    ix->has_graph = true;
+    ix->any_nil = false;
+    for (uint64_t i = 0; i < n; ++i) ix->pending_host[i >> 6] &= ~(1ull << (i & 63));
+    ix->bitmaps_dirty = true;
+    return WV_OK;
+}
+
+int wv_index_download_graph(wv_index* ix, int8_t* levels, uint32_t* layer0, uint32_t* upper_row, uint32_t* upper) {
+    if (check(ix) || !ix->has_graph) return fail(WV_ESTATE, "wv_index_download_graph: no graph");
+    std::lock_guard<std::mutex> g(ix->mu);
+    HIP_TRY(hipSetDevice(ix->cfg.device));
+    hipStream_t s = ix->stream;
+    const uint64_t n = ix->gn;
+    if (levels) HIP_TRY(hipMemcpyAsync(levels, ix->levels.p, n, hipMemcpyDeviceToHost, s));
+    if (layer0) HIP_TRY(hipMemcpyAsync(layer0, ix->layer0.p, n * (size_t)ix->deg0 * 4, hipMemcpyDeviceToHost, s));
+    if (upper_row) HIP_TRY(hipMemcpyAsync(upper_row, ix->upper_row.p, n * 4, hipMemcpyDeviceToHost, s));
+    if (upper && ix->max_level > 0)
+        HIP_TRY(hipMemcpyAsync(upper, ix->upper.p, ix->n_upper * (size_t)ix->max_level * ix->degU * 4,
+                               hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return WV_OK;
+}
+
+int wv_index_graph_info(wv_index* ix, uint64_t* n, int* deg0, int* degU, int* max_level, uint64_t* n_upper,
+                        uint64_t* entrypoint) {
+    if (check(ix) || !ix->has_graph) return fail(WV_ESTATE, "wv_index_graph_info: no graph");
+    if (n) *n = ix->gn;
+    if (deg0) *deg0 = ix->deg0;
+    if (degU) *degU = ix->degU;
+    if (max_level) *max_level = ix->max_level;
+    if (n_upper) *n_upper = ix->n_upper;
+    if (entrypoint) *entrypoint = ix->entrypoint;
     return WV_OK;
 }
 

@@ -160,7 +160,7 @@ __device__ __forceinline__ void search_layer(const HnswParams& p, WaveState& w_i
         } else {
             if (p.levels[cid] < level) continue;
             const uint32_t row = p.upper_row[cid];
-            nbr_base = p.upper + ((uint64_t)row * p.max_level + (level - 1)) * p.degU;
+            nbr_base = p.upper + ((uint64_t)row * p.upper_levels + (level - 1)) * p.degU;
             deg = p.degU;
         }
         n_exp++;
@@ -402,6 +402,239 @@ __global__ __launch_bounds__(256) void wv_hnsw_kernel(HnswParams p) {
     else knn_one<WV_METRIC_COSINE>(p, w, q);
 }
 
+// ===========================================================================
+// GPU graph construction -- insert.go:103-217 in batches.
+// A batch of new nodes is inserted against the graph of every node before it:
+//   1. wv_build_search_kernel (one wave per node): findBestEntrypointForNode
+//      (ef = 1 descent above the node's level, index.go:371-408), then
+//      searchLayerByVector with efConstruction at each level <= min(level, top)
+//      (neighbor_connections.go:71-84); the next level starts from the closest
+//      result (the last of the selected neighbours, :119-128).
+//   2. wv_build_select_kernel (one wave per node and level):
+//      selectNeighborsHeuristic to M (heuristic.go:23-135), the node's own list
+//      (setConnectionsAtLevel, farthest first as popped from the max-heap) and
+//      one reverse-link request per neighbour.
+//   3. requests sorted by (level, neighbour), stable, so each neighbour sees
+//      its new links in batch order; wv_build_link_kernel (one wave per
+//      neighbour): connectNeighborAtLevel (:134-209) -- append while below
+//      capacity (2M at layer 0, M above), else re-prune the list plus the new
+//      node with the heuristic.
+// Members of one batch do not see each other (the graph they search is the
+// one before the batch); batches grow with the graph (a fixed fraction).
+
+template <int METRIC>
+__device__ void build_search_one(const BuildParams& b, WaveState& w, int slot) {
+    const HnswParams& p = b.h;
+    const int lane = threadIdx.x & 63;
+    const int g = lane & 7;
+    const uint64_t id = b.first + (uint64_t)slot;
+    const int target = b.target[slot];
+    for (int i = lane; i < p.dpad; i += 64) w.qv[i] = i < p.D ? p.X[id * p.ldx + i] : 0.f;
+    wave_sync();
+    int status = 0, nlt = 0;
+    uint32_t n_dist = 0, n_exp = 0;
+    uint32_t ep = p.entrypoint;
+    float epd = __shfl(exact_dist_group8<METRIC>(w.qv, p.X + (uint64_t)ep * p.ldx, p.D, g), 0, 64);
+    int Rl, Sh, Sl;
+    for (int level = p.max_level; level > target; --level) {
+        search_layer<METRIC>(p, w, level, 1, ep, epd, nullptr, Rl, Sh, Sl, status, nlt, n_dist, n_exp);
+        if (Rl > 0) { ep = w.Ri[0] & WV_IDMASK; epd = w.Rd[0]; }
+    }
+    for (int level = min(target, p.max_level); level >= 0; --level) {
+        search_layer<METRIC>(p, w, level, p.ef, ep, epd, nullptr, Rl, Sh, Sl, status, nlt, n_dist, n_exp);
+        const uint64_t o = ((uint64_t)slot * b.lb + level) * p.ef;
+        for (int i = lane; i < Rl; i += 64) {
+            b.cand_i[o + i] = w.Ri[i] & WV_IDMASK;
+            b.cand_d[o + i] = w.Rd[i];
+        }
+        if (lane == 0) b.cand_n[(uint64_t)slot * b.lb + level] = Rl;
+        if (Rl > 0) { ep = w.Ri[0] & WV_IDMASK; epd = w.Rd[0]; }
+        wave_sync();
+    }
+}
+
+__global__ __launch_bounds__(256) void wv_build_search_kernel(BuildParams b) {
+    extern __shared__ float lds[];
+    const int wave = threadIdx.x >> 6;
+    const int slot = blockIdx.x * (blockDim.x >> 6) + wave;
+    if (slot >= b.nb) return;
+    const HnswParams& p = b.h;
+    float* cur = lds + (uint64_t)wave * p.per_wave_words;
+    WaveState w;
+    w.qv = cur; cur += p.dpad;
+    w.Rd = cur; cur += p.efc; w.Ri = reinterpret_cast<uint32_t*>(cur); cur += p.efc;
+    w.Rd2 = cur; cur += p.efc; w.Ri2 = reinterpret_cast<uint32_t*>(cur); cur += p.efc;
+    w.Sd = cur; cur += p.sc; w.Si = reinterpret_cast<uint32_t*>(cur); cur += p.sc;
+    w.Sd2 = cur; cur += p.sc; w.Si2 = reinterpret_cast<uint32_t*>(cur); cur += p.sc;
+    w.Bd = cur; cur += BATCH; w.Bi = reinterpret_cast<uint32_t*>(cur); cur += BATCH;
+    w.Cd = cur; cur += BATCH; w.Ci = reinterpret_cast<uint32_t*>(cur); cur += BATCH;
+    w.vc = reinterpret_cast<uint32_t*>(cur); cur += (1 << p.vc_log2);
+    w.xs = reinterpret_cast<uint32_t*>(cur); cur += (1 << p.xs_log2);
+    w.ltomb = reinterpret_cast<uint32_t*>(cur);
+    if (p.metric == WV_METRIC_L2) build_search_one<WV_METRIC_L2>(b, w, slot);
+    else if (p.metric == WV_METRIC_DOT) build_search_one<WV_METRIC_DOT>(b, w, slot);
+    else build_search_one<WV_METRIC_COSINE>(b, w, slot);
+}
+
+// selectNeighborsHeuristic (heuristic.go:23-135) over n candidates sorted
+// ascending (ci/cd in LDS): keep a candidate unless an already kept one is
+// closer to it than the query is (SingleDist(cand, kept) < dist(cand, query));
+// at most mx kept, in ascending order, into sel.  Returns the count.
+template <int METRIC>
+__device__ int heuristic_select(const HnswParams& p, const uint32_t* ci, const float* cd, int n, int mx,
+                                uint32_t* sel) {
+    const int lane = threadIdx.x & 63;
+    const int g = lane & 7, grp = lane >> 3;
+    if (n < mx) {   // input.Len() < max: every candidate stays
+        for (int i = lane; i < n; i += 64) sel[i] = ci[i];
+        wave_sync();
+        return n;
+    }
+    int ns = 0;
+    for (int i = 0; i < n && ns < mx; ++i) {
+        const uint32_t c = ci[i];
+        const float dq = cd[i];
+        const float* cv = p.X + (uint64_t)c * p.ldx;
+        bool bad = false;
+        for (int j0 = 0; j0 < ns; j0 += 8) {
+            const int j = j0 + grp;
+            float pd = FLT_MAX;
+            if (j < ns) pd = exact_dist_group8<METRIC>(cv, p.X + (uint64_t)sel[j] * p.ldx, p.D, g);
+            bad = bad || (j < ns && pd < dq);
+            if (__any(bad)) break;
+        }
+        if (!__any(bad)) {
+            if (lane == 0) sel[ns] = c;
+            ns++;
+            wave_sync();
+        }
+    }
+    return ns;
+}
+
+template <int METRIC>
+__device__ void build_select_one(const BuildParams& b, int slot, int level, uint32_t* ci, float* cd, uint32_t* sel) {
+    const HnswParams& p = b.h;
+    const int lane = threadIdx.x & 63;
+    const int target = b.target[slot];
+    const uint64_t id = b.first + (uint64_t)slot;
+    const uint64_t rq = ((uint64_t)slot * b.lb + level) * b.M;
+    for (int i = lane; i < b.M; i += 64) b.req_key[rq + i] = ~0ull;
+    if (level > min(target, p.max_level)) return;
+    const int n = b.cand_n[(uint64_t)slot * b.lb + level];
+    const uint64_t o = ((uint64_t)slot * b.lb + level) * p.ef;
+    for (int i = lane; i < n; i += 64) { ci[i] = b.cand_i[o + i]; cd[i] = b.cand_d[o + i]; }
+    wave_sync();
+    const int ns = heuristic_select<METRIC>(p, ci, cd, n, b.M, sel);
+    // own list, farthest first (popped from the results max-heap, :101-111)
+    uint32_t* row;
+    if (level == 0) row = const_cast<uint32_t*>(p.layer0) + id * (uint64_t)p.deg0;
+    else row = const_cast<uint32_t*>(p.upper) + ((uint64_t)p.upper_row[id] * p.upper_levels + (level - 1)) * p.degU;
+    for (int i = lane; i < ns; i += 64) {
+        row[i] = sel[ns - 1 - i];
+        b.req_key[rq + i] = ((uint64_t)level << 32) | sel[i];
+        b.req_node[rq + i] = (uint32_t)id;
+    }
+    if (lane == 0) {
+        if (level == 0) b.counts0[id] = ns;
+        else b.countsU[(uint64_t)p.upper_row[id] * p.upper_levels + (level - 1)] = ns;
+    }
+}
+
+__global__ __launch_bounds__(64) void wv_build_select_kernel(BuildParams b) {
+    extern __shared__ float lds[];
+    const int slot = blockIdx.x / b.lb, level = blockIdx.x % b.lb;
+    if (slot >= b.nb) return;
+    uint32_t* ci = reinterpret_cast<uint32_t*>(lds);
+    float* cd = lds + b.h.ef;
+    uint32_t* sel = reinterpret_cast<uint32_t*>(lds + 2 * b.h.ef);
+    if (b.h.metric == WV_METRIC_L2) build_select_one<WV_METRIC_L2>(b, slot, level, ci, cd, sel);
+    else if (b.h.metric == WV_METRIC_DOT) build_select_one<WV_METRIC_DOT>(b, slot, level, ci, cd, sel);
+    else build_select_one<WV_METRIC_COSINE>(b, slot, level, ci, cd, sel);
+}
+
+// connectNeighborAtLevel for every new link of one neighbour, in batch order.
+template <int METRIC>
+__device__ void build_link_one(const BuildParams& b, int r, uint32_t* ci, float* cd, uint32_t* ui, float* ud,
+                               uint32_t* sel, uint32_t* rowl) {
+    const HnswParams& p = b.h;
+    const int lane = threadIdx.x & 63;
+    const int g = lane & 7, grp = lane >> 3;
+    const uint64_t key = b.run_key[r];
+    if (key == ~0ull) return;
+    const int level = (int)(key >> 32);
+    const uint32_t nb = (uint32_t)key;
+    const int maxc = level == 0 ? b.M0 : b.M;
+    uint32_t* row;
+    uint32_t* cnt;
+    if (level == 0) {
+        row = const_cast<uint32_t*>(p.layer0) + (uint64_t)nb * p.deg0;
+        cnt = b.counts0 + nb;
+    } else {
+        const uint64_t u = (uint64_t)p.upper_row[nb] * p.upper_levels + (level - 1);
+        row = const_cast<uint32_t*>(p.upper) + u * p.degU;
+        cnt = b.countsU + u;
+    }
+    const float* nv = p.X + (uint64_t)nb * p.ldx;
+    int c = (int)*cnt;
+    // the neighbour's list lives in LDS while its new links are applied
+    for (int i = lane; i < c; i += 64) rowl[i] = row[i];
+    wave_sync();
+    const uint32_t off = b.run_off[r], len = b.run_len[r];
+    for (uint32_t t = 0; t < len; ++t) {
+        const uint32_t x = b.sorted_node[off + t];
+        if (c < maxc) {   // appendConnectionAtLevelNoLock (:151-157)
+            if (lane == 0) rowl[c] = x;
+            c++;
+            wave_sync();
+            continue;
+        }
+        // re-prune (:158-205): the list plus x, distances to the neighbour
+        const int n = c + 1;
+        for (int i = lane; i < n; i += 64) ui[i] = i < c ? rowl[i] : x;
+        wave_sync();
+        for (int i0 = 0; i0 < n; i0 += 8) {
+            const int i = i0 + grp;
+            float d = 0.f;
+            if (i < n) d = exact_dist_group8<METRIC>(p.X + (uint64_t)ui[i] * p.ldx, nv, p.D, g);
+            if (i < n && g == 0) ud[i] = d;
+        }
+        wave_sync();
+        // ascending by (d, id): rank placement
+        for (int u = lane; u < n; u += 64) {
+            const float d = ud[u];
+            const uint32_t id = ui[u];
+            int rk = 0;
+            for (int i = 0; i < n; ++i) rk += key_less(ud[i], ui[i], d, id) || (i < u && ud[i] == d && ui[i] == id);
+            ci[rk] = id;
+            cd[rk] = d;
+        }
+        wave_sync();
+        const int ns = heuristic_select<METRIC>(p, ci, cd, n, maxc, sel);
+        for (int i = lane; i < ns; i += 64) rowl[i] = sel[ns - 1 - i];   // farthest first (max-heap pops)
+        c = ns;
+        wave_sync();
+    }
+    for (int i = lane; i < maxc; i += 64) row[i] = i < c ? rowl[i] : WV_NIL;
+    if (lane == 0) *cnt = c;
+}
+
+__global__ __launch_bounds__(64) void wv_build_link_kernel(BuildParams b) {
+    extern __shared__ float lds[];
+    const int r = blockIdx.x;
+    if (r >= b.n_runs) return;
+    const int cap = b.M0 + 1;
+    uint32_t* ci = reinterpret_cast<uint32_t*>(lds);
+    float* cd = lds + cap;
+    uint32_t* ui = reinterpret_cast<uint32_t*>(lds + 2 * cap);
+    float* ud = lds + 3 * cap;
+    uint32_t* sel = reinterpret_cast<uint32_t*>(lds + 4 * cap);
+    uint32_t* rowl = reinterpret_cast<uint32_t*>(lds + 5 * cap);
+    if (b.h.metric == WV_METRIC_L2) build_link_one<WV_METRIC_L2>(b, r, ci, cd, ui, ud, sel, rowl);
+    else if (b.h.metric == WV_METRIC_DOT) build_link_one<WV_METRIC_DOT>(b, r, ci, cd, ui, ud, sel, rowl);
+    else build_link_one<WV_METRIC_COSINE>(b, r, ci, cd, ui, ud, sel, rowl);
+}
+
 int hnsw_per_wave_words(int dpad, int efc, int sc, int vc_log2, int xs_log2) {
     return dpad + 4 * efc + 4 * sc + 4 * BATCH + (1 << vc_log2) + (1 << xs_log2) + MAX_LOCAL_TOMB;
 }
@@ -412,6 +645,28 @@ extern "C" {
 
 int wv_hnsw_per_wave_words(int dpad, int efc, int sc, int vc_log2, int xs_log2) {
     return wv::hnsw_per_wave_words(dpad, efc, sc, vc_log2, xs_log2);
+}
+
+hipError_t wv_launch_build_search(const wv::BuildParams* b, int waves_per_block, hipStream_t s) {
+    const size_t lds = (size_t)waves_per_block * b->h.per_wave_words * sizeof(float);
+    const unsigned blocks = (unsigned)((b->nb + waves_per_block - 1) / waves_per_block);
+    if (blocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(wv::wv_build_search_kernel, dim3(blocks), dim3(64 * waves_per_block), lds, s, *b);
+    return hipGetLastError();
+}
+
+hipError_t wv_launch_build_select(const wv::BuildParams* b, hipStream_t s) {
+    const size_t lds = (2 * (size_t)b->h.ef + b->M) * sizeof(float);
+    if (b->nb == 0) return hipSuccess;
+    hipLaunchKernelGGL(wv::wv_build_select_kernel, dim3((unsigned)(b->nb * b->lb)), dim3(64), lds, s, *b);
+    return hipGetLastError();
+}
+
+hipError_t wv_launch_build_link(const wv::BuildParams* b, hipStream_t s) {
+    const size_t lds = 6 * ((size_t)b->M0 + 1) * sizeof(float);
+    if (b->n_runs == 0) return hipSuccess;
+    hipLaunchKernelGGL(wv::wv_build_link_kernel, dim3((unsigned)b->n_runs), dim3(64), lds, s, *b);
+    return hipGetLastError();
 }
 
 hipError_t wv_launch_hnsw(const wv::HnswParams* p, int waves_per_block, hipStream_t s) {

@@ -130,6 +130,7 @@ struct HnswParams {
     uint64_t N, tomb_nbits, allow_nbits, allow_stride, id_base;
     uint32_t entrypoint;
     int D, ldx, ldq, metric, deg0, degU, max_level;
+    int upper_levels;    // level stride of `upper` (>= max_level)
     int nq, k, ef;
     int efc, sc, vc_log2, xs_log2, dpad, per_wave_words;
     uint64_t* out_ids;   // [nq][k]
@@ -137,6 +138,30 @@ struct HnswParams {
     int32_t* out_n;
     int32_t* status;     // bit0 side overflow, bit1 expanded-set overflow
     uint32_t* counters;  // [nq][2]: distance evaluations, expansions (nullable)
+};
+
+// GPU graph construction: one batch of new nodes
+// [first, first + nb), inserted against the graph of the h.N nodes before it.
+struct BuildParams {
+    HnswParams h;             // graph + search state: h.N inserted rows, h.entrypoint, h.max_level current top
+    uint64_t first;
+    int nb;                   // batch size
+    int lb;                   // level slots per node in the candidate buffers (max target + 1)
+    int M;                    // maximumConnections: selected per level, upper-layer capacity
+    int M0;                   // maximumConnectionsLayerZero = 2M: layer-0 capacity
+    const int8_t* target;     // [nb] drawn level of each batch node
+    uint32_t* cand_i;         // [nb][lb][efc] efConstruction results per level, ascending
+    float* cand_d;
+    int32_t* cand_n;          // [nb][lb]
+    uint32_t* counts0;        // [cap] layer-0 list lengths
+    uint32_t* countsU;        // [n_upper][upper_levels]
+    uint64_t* req_key;        // [nb][lb][M] reverse-link requests: level << 32 | neighbour (~0 = none)
+    uint32_t* req_node;       //   ... the new node that links to it
+    const uint64_t* run_key;  // link phase: one run of equal keys per wave
+    const uint32_t* run_off;
+    const uint32_t* run_len;
+    const uint32_t* sorted_node;
+    int n_runs;
 };
 
 }  // namespace wv

@@ -140,6 +140,24 @@ class GPUVectorIndex:
         self.upload_graph(g)
         check(lib().wv_index_set_tombstones(self._h, _ptr(g["tomb_bits"]), g["n"]))
 
+    def build_graph(self, ef_construction: int = 128, seed: int = 1, batch_div: int = 32):
+        """Build the HNSW graph of the uploaded rows on the GPU (wv_index_build_graph)."""
+        check(lib().wv_index_build_graph(self._h, ef_construction, seed, batch_div))
+
+    def download_graph(self) -> dict:
+        """The index's graph in the upload_graph / export_graph layout."""
+        n, ep, nu = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        d0, du, ml = C.c_int(), C.c_int(), C.c_int()
+        check(lib().wv_index_graph_info(self._h, C.byref(n), C.byref(d0), C.byref(du), C.byref(ml), C.byref(nu),
+                                        C.byref(ep)))
+        levels = np.zeros(n.value, np.int8)
+        layer0 = np.zeros((n.value, d0.value), np.uint32)
+        upper_row = np.zeros(n.value, np.uint32)
+        upper = np.zeros((max(nu.value, 1), max(ml.value, 1), du.value), np.uint32)
+        check(lib().wv_index_download_graph(self._h, _ptr(levels), _ptr(layer0), _ptr(upper_row), _ptr(upper)))
+        return dict(n=n.value, entrypoint=ep.value, max_level=ml.value, levels=levels, layer0=layer0,
+                    upper_row=upper_row, upper=upper, deg0=d0.value, degU=du.value)
+
     def add(self, ids, rows):
         """hnsw.Add (insert.go:43-65) on the GPU mirror: rows at arbitrary ids,
         searchable at once (delta set, exact) until a graph snapshot holds them."""
