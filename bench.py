@@ -11,9 +11,10 @@ shard), the per-shard (dist, id) lists are all-gathered over RCCL/xGMI and
 merged on every rank (index.go:967-1044 restated on device).  Total work is
 fixed, so scaling is "strong"; value = queries/s over the whole corpus.
 
---workload hnsw: layer-0 beam search over a graph built by the CPU
-restatement (oracle/, test infrastructure) on a smaller corpus; reports QPS
-and recall@10.  Not the headline line.
+--workload hnsw (BASELINE configs[0]): beam search over a graph built by the
+CPU restatement (oracle/, test infrastructure; --graph-build gpu builds it
+with wv_index_build_graph instead) on SIFT-shaped data; reports QPS and
+recall@10 next to the restatement's on the same graph.
 """
 from __future__ import annotations
 
@@ -62,6 +63,25 @@ def counter_gauss(seed: int, row0: int, nrows: int, dim: int) -> np.ndarray:
     return (z / np.sqrt(dim)).astype(np.float32)
 
 
+def counter_sift(seed: int, row0: int, nrows: int, dim: int) -> np.ndarray:
+    """SIFT-shaped data (BASELINE configs[0]): non-negative integer-valued
+    features with low intrinsic dimension -- 1024 cluster centres plus a
+    24-d latent spread and a little isotropic noise, rounded and clipped at 0
+    (SIFT descriptors are small non-negative integers).  Corpus and queries
+    share the centres and the latent basis; everything else is counter-based
+    per row like counter_uniform.  Uniform 128-d data has intrinsic dimension
+    128 and no HNSW operating point near recall 0.95 at ef=64; this does
+    (about 0.99 at 100k rows)."""
+    C, L = 1024, 24
+    centres = counter_uniform(77, 0, C, dim) * np.float32(60.0)
+    basis = counter_gauss(78, 0, dim, L) * np.float32(np.sqrt(L))
+    cid = (counter_uniform(seed + 2000, row0, nrows, 1)[:, 0] * C).astype(np.int64)
+    z = counter_gauss(seed + 3000, row0, nrows, L) * np.float32(np.sqrt(L))
+    e = counter_gauss(seed + 4000, row0, nrows, dim) * np.float32(np.sqrt(dim))
+    x = centres[cid] + (z @ basis.T) * np.float32(12.0) + e * np.float32(3.0)
+    return np.maximum(np.rint(x), 0).astype(np.float32)
+
+
 def parity_stats(gi, gd, oi, od):
     """ids position-equal / distances bitwise equal / identical up to the
     order among equal distances (the reference orders ties by heap layout,
@@ -99,8 +119,10 @@ def main():
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--ef", type=int, default=64)
     ap.add_argument("--metric", default="l2-squared")
-    ap.add_argument("--data", choices=["uniform", "gauss"], default="uniform",
-                    help="uniform: U[0,1) (tie-free, configs[1]); gauss: N(0,1)/sqrt(D) (GloVe/Deep/C4-shaped)")
+    ap.add_argument("--data", choices=["auto", "uniform", "gauss", "sift"], default="auto",
+                    help="uniform: U[0,1) (tie-free, configs[1]); gauss: N(0,1)/sqrt(D) (GloVe/Deep/C4-shaped); "
+                         "sift: clustered non-negative integers (SIFT-shaped, configs[0]); "
+                         "auto: uniform for exact, sift for hnsw")
     ap.add_argument("--allow-frac", type=float, default=0.0,
                     help="exact mode: shared allow list, Bernoulli(p) over ids (seed 3, BASELINE configs[3])")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample time")
@@ -112,6 +134,10 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (RCCL over xGMI, the product path); gloo only to rehearse N ranks on one GPU")
     ap.add_argument("--dump-ids", default="", help="rank 0 saves the final ids/dists (npz) for cross-N checks")
+    ap.add_argument("--graph-build", choices=["cpu", "gpu"], default="cpu",
+                    help="hnsw graph: the CPU restatement's sequential build (reference-equivalent) or "
+                         "wv_index_build_graph on the GPU")
+    ap.add_argument("--batch-div", type=int, default=64, help="GPU build: batch = inserted / batch_div")
     ap.add_argument("--graph-cache", default="", help="npz path: load the hnsw graph if present, else build and save")
     args = ap.parse_args()
 
@@ -136,7 +162,9 @@ def main():
     lo = N * rank // ws
     hi = N * (rank + 1) // ws
     n_local = hi - lo
-    gen = counter_gauss if args.data == "gauss" else counter_uniform
+    if args.data == "auto":
+        args.data = "sift" if args.workload == "hnsw" else "uniform"
+    gen = {"uniform": counter_uniform, "gauss": counter_gauss, "sift": counter_sift}[args.data]
     base = gen(1, lo, n_local, D)
     queries = gen(2, 0, NQ, D)
 
@@ -152,7 +180,15 @@ def main():
         t0 = time.time()
         ref = O.Index(D, args.metric, args.M, args.efc, capacity=n_local, seed=1)
         cache = args.graph_cache % {"rank": rank} if args.graph_cache else ""
-        if cache and os.path.exists(cache):
+        if args.graph_build == "gpu":
+            torch.cuda.synchronize(dev)
+            t0 = time.time()
+            ix.build_graph(ef_construction=args.efc, seed=1, batch_div=args.batch_div)
+            g = ix.download_graph()
+            built = f"built on the GPU (wv_index_build_graph, batch = inserted/{args.batch_div})"
+            if rank == 0 and ws == 1 and not args.no_cpu_baseline:
+                ref.import_graph(base, g)   # the restatement searches the same graph
+        elif cache and os.path.exists(cache):
             z = np.load(cache)
             g = {k: (z[k] if z[k].ndim else int(z[k])) for k in z.files}
             ref.import_graph(base, g)   # the restatement searches the same graph
@@ -172,9 +208,11 @@ def main():
             if cache:
                 np.savez(cache, **{k: np.asarray(v) for k, v in g.items()})
             built = "built"
-        ix.upload_graph(g)
-        graph_info = {"build_s": round(time.time() - t0, 1), "M": args.M, "efConstruction": args.efc,
-                      "max_level": int(g["max_level"]), "source": built + " by the CPU restatement (oracle/)"}
+        if args.graph_build != "gpu":
+            ix.upload_graph(g)
+        graph_info = {"build_s": round(time.time() - t0, 2), "M": args.M, "efConstruction": args.efc,
+                      "max_level": int(g["max_level"]), "source": built if args.graph_build == "gpu"
+                      else built + " by the CPU restatement (oracle/)"}
         mode = "hnsw"
 
     dpad = (D + 3) & ~3
@@ -260,8 +298,9 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": ("synthetic: counter-based U[0,1) float32 corpus (seed 1) and queries (seed 2)" if args.data == "uniform"
-                 else "synthetic: counter-based N(0,1)/sqrt(D) float32 corpus (seed 1) and queries (seed 2)"),
+        "data": "synthetic: counter-based %s float32 corpus (seed 1) and queries (seed 2)" % {
+            "uniform": "U[0,1)", "gauss": "N(0,1)/sqrt(D)",
+            "sift": "SIFT-shaped (1024 centres + 24-d latent + noise, non-negative integers)"}[args.data],
         "config": {
             "workload": ("exact brute-force %d-NN, %s x %d-d %s, %d-query batch%s"
                          % (K, f"{N:,}", D, args.metric, NQ,
@@ -301,7 +340,7 @@ def main():
     if os.path.exists(pmc):
         with open(pmc) as f:
             p = json.load(f)
-        if p.get("N") == n_local and p.get("nq") == NQ and p.get("dim") == D:
+        if (p.get("N"), p.get("nq"), p.get("dim"), p.get("data", "uniform")) == (n_local, NQ, D, args.data):
             result["roofline"]["traffic"] = p.get("hbm_bytes_per_launch")
 
     # ---- CPU baseline + parity sample (rank 0, N=1 only) ----
@@ -354,13 +393,18 @@ def main():
             kind_desc = "knnSearchByVector restated in C on the same graph (oracle/)"
             same = float((oi == final_ids[:ns]).mean())
             _, dist_same, tie_ok = parity_stats(final_ids[:ns], final_d[:ns], oi, od)
+            nt = min(NQ, 1000)   # exact truths for recall on a sample
+            ti, td, tn = O.flat_scan(metric_id, base, queries[:nt], K, threads=threads)
+            rec_gpu = float(np.mean([len(set(a) & set(b)) / K for a, b in zip(final_ids[:nt].tolist(), ti.tolist())]))
+            rec_cpu = float(np.mean([len(set(a) & set(b)) / K for a, b in zip(oi[:nt].tolist(), ti.tolist())]))
             result["parity_sample"] = {"queries": ns, "id_match_frac": same, "dists_bitwise_equal_frac": dist_same,
                                        "tie_aware_identical_frac": tie_ok, "recall@10_gpu": rec_gpu,
                                        "recall@10_cpu_restatement": rec_cpu, "recall_sample": nt}
         result["cpu_baseline"] = {"value": round(ns / cpu_t, 1), "unit": "queries/s", "cores": threads,
                                   "kind": "port",
                                   "sample": f"{ns} of the {NQ} queries over the full {N:,}-row corpus "
-                                            f"({cpu_t:.1f} s, {threads} threads, GOMAXPROCS-equivalent); "
+                                            f"({cpu_t:.2f} s per pass{'' if mode == 'exact' else f' x {reps} passes'}, "
+                                            f"{threads} threads, GOMAXPROCS-equivalent); "
                                             + kind_desc}
     if rank == 0:
         print(json.dumps(result), flush=True)

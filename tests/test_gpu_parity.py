@@ -597,6 +597,7 @@ def test_gpu_graph_build_invariants_and_recall():
     gi, gd, gn = ix.search_batch(qs, 10, ef=ef, mode="hnsw")
     ref = O.Index(d, "l2-squared", M, efc, capacity=n, seed=7)
     ref.add_batch(base, threads=8)
+    assert np.array_equal(ref.export_graph()["levels"][1:], lv[1:])   # same level draw (insert.go:132)
     oi, od, on, _ = ref.search_batch(qs, 10, ef, threads=8)
     r_gpu, r_cpu = _recall(gi, truth), _recall(oi, truth)
     assert r_gpu >= r_cpu - 0.02, (r_gpu, r_cpu)

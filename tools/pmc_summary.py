@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--n", type=int, default=1_000_000)
     ap.add_argument("--nq", type=int, default=10_000)
     ap.add_argument("--dim", type=int, default=128)
+    ap.add_argument("--data", default="uniform")
     a = ap.parse_args()
     os.makedirs(os.path.dirname(a.dst) or ".", exist_ok=True)
     stats = os.path.join(a.src, "trace", "run_kernel_stats.csv")
@@ -46,7 +47,7 @@ def main():
     sq = per_kernel(os.path.join(a.src, "pmc_sq", "run_counter_collection.csv"), a.kernel)
     rd = 2 * fetch.get("FETCH_SIZE", 0) * 1024
     wr = write.get("WRITE_SIZE", 0) * 1024
-    out = {"kernel": a.kernel, "N": a.n, "nq": a.nq, "dim": a.dim, "avg_kernel_ns": avg_ns,
+    out = {"kernel": a.kernel, "N": a.n, "nq": a.nq, "dim": a.dim, "data": a.data, "avg_kernel_ns": avg_ns,
            "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
            "hbm_bytes_per_launch": rd + wr, "sq": sq,
            "note": "read = 2*FETCH_SIZE*1024 (gfx950 half-count correction), write = WRITE_SIZE*1024"}
