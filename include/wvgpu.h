@@ -134,6 +134,31 @@ int wv_index_add_tombstones(wv_index *ix, const uint64_t *ids, uint64_t n);
 int wv_index_remove_tombstones(wv_index *ix, const uint64_t *ids, uint64_t n);
 int wv_index_delta_size(wv_index *ix, uint64_t *n);
 
+/* Product quantization (ssdhelpers/product_quantization.go,
+ * hnsw/compress.go:39-89).  The fitted quantizer crosses as its centroid
+ * table, centroid_table[segments][centroids][dims/segments] =
+ * kms[i].Centroid(c) (KMeans centers, or the tile encoder's one-float
+ * centroids), plus encoder = ssdhelpers.Encoder (0 tile, 1 kmeans).
+ * Codes are uploaded in ProductQuantizer.Encode's layout (segments * bytes
+ * per vector, big-endian, bit-packed when use_bits_encoding and bits < 8 *
+ * bytes: wv_pq_code_len), or -- KMeans -- encoded on the device from the
+ * resident vectors (KMeans.Nearest, kmeans.go:78-110).  With the index
+ * compressed (h.compressed) every search ranks by the PQ distance
+ * (DistanceBetweenCompressedAndUncompressedVectors :284-291 = the lookup-table
+ * distance :56-75): flatSearch and knnSearchByVector alike, as the reference
+ * does.  Rows written later are encoded on the device (KMeans, insert.go:91-95)
+ * or wait for their codes (tile encoder). */
+enum { WV_PQ_TILE = 0, WV_PQ_KMEANS = 1 };
+int wv_pq_code_len(int segments, int centroids, int use_bits_encoding);
+int wv_index_set_pq(wv_index *ix, int segments, int centroids, int use_bits_encoding, int encoder,
+                    const float *centroid_table);
+int wv_index_upload_pq_codes(wv_index *ix, const uint8_t *encoded, uint64_t n, uint64_t first_id);
+int wv_index_pq_encode(wv_index *ix);
+/* the device codes of rows first_id.., one uint16 per segment: out[n][segments] */
+int wv_index_download_pq_codes(wv_index *ix, uint16_t *out, uint64_t first_id, uint64_t n);
+/* compressed on/off (h.compressed); on requires a code for every row holding a vector */
+int wv_index_set_compressed(wv_index *ix, int on);
+
 /* searchTimeEF (search.go:30-62) for the current config. */
 int wv_search_time_ef(const wv_index *ix, int k);
 

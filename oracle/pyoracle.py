@@ -83,6 +83,12 @@ def lib():
             "wvo_search_by_vector_distance": (C.c_int, [vp, fp, C.c_float, C.c_int64, u64p, C.c_uint64, u64p, fp, C.c_int64, C.POINTER(C.c_int64)]),
             "wvo_search_batch": (C.c_int, [vp, fp, C.c_int, C.c_int, C.c_int, u64p, C.c_uint64, C.c_int, C.c_int, u64p, fp, i32p, C.POINTER(Stats)]),
             "wvo_flat_scan": (C.c_int, [C.c_int, fp, C.c_uint64, C.c_int, fp, C.c_int, C.c_int, u64p, u64p, C.c_int, u64p, fp, i32p]),
+            "wvo_pq_layout": (C.c_int, [C.c_int, C.c_int, i32p, i32p]),
+            "wvo_pq_extract": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, u64p]),
+            "wvo_pq_put": (C.c_int, [u64p, C.c_int, C.c_int, C.c_int, vp]),
+            "wvo_pq_distance": (C.c_float, [C.c_int, fp, vp, fp, C.c_int, C.c_int, C.c_int, C.c_int]),
+            "wvo_pq_encode_kmeans": (C.c_int, [fp, C.c_uint64, C.c_int, C.c_int, C.c_int, fp, C.c_int, vp]),
+            "wvo_compress": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, fp, vp, vp, C.c_uint64]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -141,6 +147,56 @@ def pq_script(is_max, ops):
     return list(zip(oi[:m].tolist(), od[:m].tolist()))
 
 
+def pq_layout(ks, use_bits=False):
+    """(bits, bytes) of NewProductQuantizer (product_quantization.go:116-179)."""
+    b, y = C.c_int(), C.c_int()
+    assert lib().wvo_pq_layout(ks, int(use_bits), C.byref(b), C.byref(y)) == 0
+    return b.value, y.value
+
+
+def pq_extract(enc, n_codes, ks, use_bits=False):
+    """ProductQuantizer.ExtractCode for indices 0..n_codes-1 (:191-237)."""
+    buf = np.zeros(len(enc) + 8, np.uint8)
+    buf[: len(enc)] = np.frombuffer(bytes(enc), np.uint8)
+    out = np.zeros(n_codes, np.uint64)
+    assert lib().wvo_pq_extract(buf.ctypes.data, n_codes, ks, int(use_bits), _u64(out)) == 0
+    return out.tolist()
+
+
+def pq_put(codes, ks, use_bits=False, length=None):
+    """ProductQuantizer.PutCode for codes[i] at index i (:207-258) into a
+    zeroed buffer of `length` bytes (default m * bytes, as Encode allocates)."""
+    codes = np.asarray(codes, np.uint64)
+    n = len(codes)
+    if length is None:
+        length = n * pq_layout(ks, use_bits)[1]
+    buf = np.zeros(length + 8, np.uint8)
+    assert lib().wvo_pq_put(_u64(codes), n, ks, int(use_bits), buf.ctypes.data) == 0
+    return bytes(buf[:length])
+
+
+def pq_distance(metric, x, enc, cent, ks, use_bits=False):
+    """DistanceBetweenCompressedAndUncompressedVectors (:284-291); cent[m][ks][ds]."""
+    x, cent = f32(x), f32(cent)
+    m = cent.shape[0]
+    buf = np.zeros(len(enc) + 8, np.uint8)
+    buf[: len(enc)] = np.frombuffer(bytes(enc), np.uint8)
+    metric = METRICS[metric] if isinstance(metric, str) else metric
+    return float(np.float32(lib().wvo_pq_distance(metric, _f(x), buf.ctypes.data, _f(cent), m, ks, len(x),
+                                                  int(use_bits))))
+
+
+def pq_encode_kmeans(vecs, cent, use_bits=False):
+    """ProductQuantizer.Encode with KMeans encoders: uint8[n][m * bytes]."""
+    vecs, cent = f32(vecs), f32(cent)
+    m, ks = cent.shape[0], cent.shape[1]
+    n, dim = vecs.shape
+    _, nbytes = pq_layout(ks, use_bits)
+    out = np.zeros((n, m * nbytes), np.uint8)
+    assert lib().wvo_pq_encode_kmeans(_f(vecs), n, dim, m, ks, _f(cent), int(use_bits), out.ctypes.data) == 0
+    return out
+
+
 def search_time_ef(ef, ef_min, ef_max, ef_factor, k):
     return lib().wvo_search_time_ef(ef, ef_min, ef_max, ef_factor, k)
 
@@ -192,6 +248,17 @@ class Index:
 
     def add_tombstone(self, id_):
         lib().wvo_add_tombstone(self.h, id_)
+
+    def compress(self, cent, codes, use_bits=False, has=None):
+        """Compress (compress.go:39-89) with fitted centroids cent[m][ks][ds]
+        and encoded vectors codes[n][m * bytes] for ids 0..n-1."""
+        cent = f32(cent)
+        codes = np.ascontiguousarray(codes, dtype=np.uint8)
+        hs = None if has is None else np.ascontiguousarray(has, dtype=np.uint8)
+        rc = lib().wvo_compress(self.h, cent.shape[0], cent.shape[1], int(use_bits), _f(cent), codes.ctypes.data,
+                                None if hs is None else hs.ctypes.data, codes.shape[0])
+        assert rc == 0, rc
+        self._pq_keep = (cent, codes, hs)
 
     def import_node(self, id_, level, conns_per_level):
         flat = np.array([c for lvl in conns_per_level for c in lvl], dtype=np.uint64)

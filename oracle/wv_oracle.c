@@ -360,6 +360,187 @@ int wvo_search_time_ef(int64_t ef64, int64_t ef_min, int64_t ef_max,
 }
 
 /* ======================================================================== */
+/* Product quantization -- ssdhelpers/product_quantization.go, kmeans.go    */
+/* (paths relative to adapters/repos/db/vector/)                            */
+/* ======================================================================== */
+
+/* NewProductQuantizer (product_quantization.go:116-179): bits = int(log2(ks)),
+ * bytes = int(log2(ks-1))/8 + 1, and the code accessor pair by (bytes, bits,
+ * useBitsEncoding).  kind: 8/16/24/32 = plain big-endian accessor of that
+ * width; 0 = extractBitsCode / putBitsCode over the `inner` accessor. */
+typedef struct { int bits, bytes, kind, inner, sharp; uint64_t mask; } pq_layout;
+
+static int pq_layout_of(int ks, int use_bits, pq_layout *L) {
+    if (ks < 2 || ks > (1 << 24)) return -1;
+    L->bits = (int)log2((double)ks);
+    L->bytes = (int)log2((double)(ks - 1)) / 8 + 1;
+    L->sharp = L->bits % 8 == 0;
+    L->mask = (L->bits >= 64) ? ~0ull : ((1ull << L->bits) - 1);   /* uint64(2^bits) - 1 */
+    switch (L->bytes) {
+    case 1: if (L->bits == 8 || !use_bits) { L->kind = 8; } else { L->kind = 0; L->inner = 16; } break;
+    case 2: if (L->bits == 16 || !use_bits) { L->kind = 16; } else { L->kind = 0; L->inner = 24; } break;
+    case 3: if (L->bits == 32 || !use_bits) { L->kind = 24; } else { L->kind = 0; L->inner = 32; } break;
+    default: return -1;
+    }
+    return 0;
+}
+
+/* extractCode8/16/24/32 (:191-205), big endian */
+static uint64_t pq_get(int width, const uint8_t *p) {
+    switch (width) {
+    case 8: return p[0];
+    case 16: return ((uint64_t)p[0] << 8) | p[1];
+    case 24: return (((uint64_t)p[0] << 24) | ((uint64_t)p[1] << 16) | ((uint64_t)p[2] << 8) | p[3]) >> 8;
+    default: return ((uint64_t)p[0] << 24) | ((uint64_t)p[1] << 16) | ((uint64_t)p[2] << 8) | p[3];
+    }
+}
+
+/* putCode8/16/24/32 (:207-221) */
+static void pq_set(int width, uint64_t code, uint8_t *p) {
+    switch (width) {
+    case 8: p[0] = (uint8_t)code; break;
+    case 16: p[0] = (uint8_t)(code >> 8); p[1] = (uint8_t)code; break;
+    case 24: {
+        uint32_t v = (uint32_t)(code << 8);
+        p[0] = (uint8_t)(v >> 24); p[1] = (uint8_t)(v >> 16); p[2] = (uint8_t)(v >> 8); p[3] = (uint8_t)v;
+        break;
+    }
+    default: {
+        uint32_t v = (uint32_t)code;
+        p[0] = (uint8_t)(v >> 24); p[1] = (uint8_t)(v >> 16); p[2] = (uint8_t)(v >> 8); p[3] = (uint8_t)v;
+    }
+    }
+}
+
+/* ProductQuantizer.ExtractCode: plain accessor or extractBitsCode (:223-237) */
+static uint64_t pq_extract(const pq_layout *L, const uint8_t *enc, int index) {
+    if (L->kind) return pq_get(L->kind, enc + (size_t)index * (L->kind / 8));
+    const int ci = index * L->bits / 8;
+    uint64_t code = pq_get(L->inner, enc + ci);
+    if (L->sharp) return code;
+    const int rest = (index + 1) * L->bits % 8;
+    const int rfs = index * L->bits % 8;
+    if (rfs < rest) code >>= 16 - rest;
+    else code >>= 8 - rest;
+    return code & L->mask;
+}
+
+/* ProductQuantizer.PutCode: plain accessor, putBitsCode (:239-258), or --
+ * for 3-byte codes with bit encoding -- the plain putCode32 (:174) */
+static void pq_put(const pq_layout *L, uint64_t code, uint8_t *enc, int index) {
+    if (L->kind) { pq_set(L->kind, code, enc + (size_t)index * (L->kind / 8)); return; }
+    if (L->inner == 32) { pq_set(32, code, enc + (size_t)index * 4); return; }
+    const int ci = index * L->bits / 8;
+    if (L->sharp) { pq_set(L->inner, code, enc + ci); return; }
+    const int rest = (index + 1) * L->bits % 8;
+    const int rfs = index * L->bits % 8;
+    if (rfs < rest) code <<= 16 - rest;
+    else code <<= 8 - rest;
+    code |= (uint64_t)enc[ci] << (L->bytes * 8);
+    pq_set(L->inner, code, enc + ci);
+}
+
+int wvo_pq_layout(int ks, int use_bits, int *bits, int *bytes) {
+    pq_layout L;
+    if (pq_layout_of(ks, use_bits, &L)) return -1;
+    *bits = L.bits;
+    *bytes = L.bytes;
+    return 0;
+}
+
+int wvo_pq_extract(const uint8_t *enc, int n_codes, int ks, int use_bits, uint64_t *out) {
+    pq_layout L;
+    if (pq_layout_of(ks, use_bits, &L)) return -1;
+    for (int i = 0; i < n_codes; i++) out[i] = pq_extract(&L, enc, i);
+    return 0;
+}
+
+int wvo_pq_put(const uint64_t *codes, int n_codes, int ks, int use_bits, uint8_t *enc) {
+    pq_layout L;
+    if (pq_layout_of(ks, use_bits, &L)) return -1;
+    for (int i = 0; i < n_codes; i++) pq_put(&L, codes[i], enc, i);
+    return 0;
+}
+
+/* L2SquaredProvider.Step / DotProductProvider.Step / CosineDistanceProvider.Step
+ * (distancer/l2.go:63-72, dot_product.go:80-87, cosine_dist.go:57-64): pure Go,
+ * sequential, not fused. */
+static float pq_step(int metric, const float *x, const float *y, int n) {
+    float sum = 0.0f;
+    if (metric == WVO_L2) {
+        for (int i = 0; i < n; i++) {
+            float d = x[i] - y[i];
+            float sq = d * d;
+            sum = sum + sq;
+        }
+    } else {
+        for (int i = 0; i < n; i++) {
+            float p = x[i] * y[i];
+            sum = sum + p;
+        }
+    }
+    return sum;
+}
+
+/* Wrap (l2.go:74-76, dot_product.go:89-91, cosine_dist.go:66-68) */
+static float pq_wrap(int metric, float x) {
+    return metric == WVO_L2 ? x : metric == WVO_DOT ? -x : 1.0f - x;
+}
+
+/* DistanceBetweenCompressedAndUncompressedVectors (:284-291); the lookup
+ * table (:56-75) caches exactly these Step values and sums them in the same
+ * segment order, so PQDistancer.Distance returns the same float. */
+static float pq_distance(int metric, const pq_layout *L, const float *x, const uint8_t *enc,
+                         const float *cent, int m, int ks, int ds) {
+    float dist = 0.0f;
+    for (int i = 0; i < m; i++) {
+        const uint64_t c = pq_extract(L, enc, i);
+        dist = dist + pq_step(metric, x + (size_t)i * ds, cent + ((size_t)i * ks + c) * ds, ds);
+    }
+    return pq_wrap(metric, dist);
+}
+
+float wvo_pq_distance(int metric, const float *x, const uint8_t *enc, const float *cent, int m, int ks, int dim,
+                      int use_bits) {
+    pq_layout L;
+    if (pq_layout_of(ks, use_bits, &L) || m <= 0 || dim % m) return NAN;
+    return pq_distance(metric, &L, x, enc, cent, m, ks, dim / m);
+}
+
+/* KMeans.Nearest / nNearest with n = 1 (kmeans.go:78-110): asm.L2 over the
+ * segment; a candidate replaces the best when best >= d, so among equal
+ * distances the last centroid wins. */
+static uint64_t kmeans_nearest(const float *seg, const float *centers, int ks, int ds) {
+    uint64_t best = 0;
+    float bd = FLT_MAX;
+    for (int c = 0; c < ks; c++) {
+        const float d = raw_l2(seg, centers + (size_t)c * ds, ds);
+        if (!(bd < d)) { bd = d; best = (uint64_t)c; }
+    }
+    return best;
+}
+
+/* ProductQuantizer.Encode (:348-354) with KMeans encoders: enc[n][m*bytes] */
+int wvo_pq_encode_kmeans(const float *vecs, uint64_t n, int dim, int m, int ks, const float *cent, int use_bits,
+                         uint8_t *enc) {
+    pq_layout L;
+    if (pq_layout_of(ks, use_bits, &L) || m <= 0 || dim % m) return -1;
+    have_avx2();
+    const int ds = dim / m;
+    const size_t len = (size_t)m * L.bytes;
+    uint8_t *tmp = (uint8_t *)calloc(len + 8, 1);
+    for (uint64_t r = 0; r < n; r++) {
+        memset(tmp, 0, len + 8);
+        for (int i = 0; i < m; i++)
+            pq_put(&L, kmeans_nearest(vecs + r * (uint64_t)dim + (size_t)i * ds, cent + (size_t)i * ks * ds, ks, ds),
+                   tmp, i);
+        memcpy(enc + r * len, tmp, len);
+    }
+    free(tmp);
+    return 0;
+}
+
+/* ======================================================================== */
 /* Index                                                                    */
 /* ======================================================================== */
 typedef struct { uint32_t len, cap; uint32_t *ids; } conn_list;
@@ -392,6 +573,14 @@ struct wvo_index {
     uint8_t *log;
     size_t log_len, log_cap;
     pthread_mutex_t log_lock;
+    /* product quantization: h.compressed / h.pq / compressedVectorsCache
+     * (compress.go:39-89); codes kept in the reference's encoded layout */
+    int compressed;
+    int pq_m, pq_ks, pq_ds, pq_use_bits;
+    uint64_t pq_code_len;
+    float *pq_cent;      /* [m][ks][ds] = kms[i].Centroid(c) */
+    uint8_t *pq_codes;   /* [cap][code_len] */
+    uint8_t *pq_has;     /* [cap] */
 };
 
 /* ---- commit log records -- commitlog/logger.go:28-215 (little endian) ---- */
@@ -556,6 +745,7 @@ void wvo_destroy(wvo_index *h) {
     }
     free(h->conns); free(h->vecs); free(h->has_vec); free(h->level);
     free(h->maint); free(h->tomb); free(h->node_lock); free(h->log);
+    free(h->pq_cent); free(h->pq_codes); free(h->pq_has);
     free(h);
 }
 
@@ -584,6 +774,21 @@ static inline const float *vec_of(wvo_index *h, uint64_t id) { return h->vecs + 
  * index.go:492-538): ok=0 when the object store has no vector, after which a
  * tombstone is attached (handleDeletedNode, search.go:446-458). */
 static inline int dist_node_vec(wvo_index *h, ctx_t *c, uint64_t id, const float *q, float *out) {
+    if (h->compressed) {
+        /* distanceToByteNode (search.go:403-418) / distBetweenNodeAndVec
+         * compressed branch (index.go:493-511): a node without a code is
+         * handled like a deleted one */
+        if (id >= h->cap || !h->pq_has[id]) {
+            if (id < h->cap) h->tomb[id] = 1;
+            return 0;
+        }
+        if (c) c->st.dist_evals++;
+        pq_layout L;
+        pq_layout_of(h->pq_ks, h->pq_use_bits, &L);
+        *out = pq_distance(h->metric, &L, q, h->pq_codes + id * h->pq_code_len, h->pq_cent, h->pq_m, h->pq_ks,
+                           h->pq_ds);
+        return 1;
+    }
     if (id >= h->cap || !h->has_vec[id]) {
         if (id < h->cap) h->tomb[id] = 1;
         return 0;
@@ -591,6 +796,27 @@ static inline int dist_node_vec(wvo_index *h, ctx_t *c, uint64_t id, const float
     if (c) c->st.dist_evals++;
     *out = metric_dist(h->metric, vec_of(h, id), q, h->dim);
     return 1;
+}
+
+/* Compress (compress.go:39-89) with a fitted quantizer: every later search
+ * uses the PQ distance.  cent = kms[i].Centroid(c) for c < ks, i < m;
+ * codes[n][code_len] in ProductQuantizer.Encode's layout for ids 0..n-1
+ * (has[id] = 0 marks an id with no stored code). */
+int wvo_compress(wvo_index *h, int m, int ks, int use_bits, const float *cent, const uint8_t *codes,
+                 const uint8_t *has, uint64_t n) {
+    pq_layout L;
+    if (pq_layout_of(ks, use_bits, &L) || m <= 0 || h->dim % m || n > h->cap) return -1;
+    h->pq_m = m; h->pq_ks = ks; h->pq_ds = h->dim / m; h->pq_use_bits = use_bits;
+    h->pq_code_len = (uint64_t)m * L.bytes;
+    free(h->pq_cent); free(h->pq_codes); free(h->pq_has);
+    h->pq_cent = (float *)malloc(sizeof(float) * (size_t)m * ks * h->pq_ds);
+    memcpy(h->pq_cent, cent, sizeof(float) * (size_t)m * ks * h->pq_ds);
+    h->pq_codes = (uint8_t *)calloc(h->cap * h->pq_code_len + 8, 1);
+    memcpy(h->pq_codes, codes, n * h->pq_code_len);
+    h->pq_has = (uint8_t *)calloc(h->cap, 1);
+    for (uint64_t i = 0; i < n; i++) h->pq_has[i] = has ? has[i] : 1;
+    h->compressed = 1;
+    return 0;
 }
 
 static conn_list *alloc_levels(int level, int M, int M0) {

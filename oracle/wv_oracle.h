@@ -140,6 +140,23 @@ int wvo_search_batch(wvo_index *h, const float *qs, int nq, int k, int ef,
                      int threads, uint64_t *out_ids, float *out_d, int *out_n,
                      wvo_stats *st);
 
+/* ---- product quantization (ssdhelpers/product_quantization.go, kmeans.go) */
+/* bits / bytes of NewProductQuantizer (:116-179) */
+int wvo_pq_layout(int ks, int use_bits, int *bits, int *bytes);
+/* ExtractCode / PutCode over one encoded vector (:191-258) */
+int wvo_pq_extract(const uint8_t *enc, int n_codes, int ks, int use_bits, uint64_t *out);
+int wvo_pq_put(const uint64_t *codes, int n_codes, int ks, int use_bits, uint8_t *enc);
+/* DistanceBetweenCompressedAndUncompressedVectors (:284-291) = the LUT
+ * distance (:56-75); cent[m][ks][dim/m] */
+float wvo_pq_distance(int metric, const float *x, const uint8_t *enc, const float *cent, int m, int ks, int dim,
+                      int use_bits);
+/* Encode (:348-354) with KMeans encoders (kmeans.go:78-110): enc[n][m*bytes] */
+int wvo_pq_encode_kmeans(const float *vecs, uint64_t n, int dim, int m, int ks, const float *cent, int use_bits,
+                         uint8_t *enc);
+/* Compress (hnsw/compress.go:39-89): all later searches use PQ distances */
+int wvo_compress(wvo_index *h, int m, int ks, int use_bits, const float *cent, const uint8_t *codes,
+                 const uint8_t *has, uint64_t n);
+
 /* ---- standalone exact scan over raw arrays (no index) -------------------- */
 /* flatSearch semantics (flat_search.go:19-74) over ids 0..n-1 of a row-major
  * base[n][dim]; tombstone/allow bitmaps nullable.  Cosine inputs must already

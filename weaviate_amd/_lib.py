@@ -85,6 +85,12 @@ SIGNATURES = {
     "wv_index_add_tombstones": (C.c_int, [_vp, _vp, C.c_uint64]),
     "wv_index_remove_tombstones": (C.c_int, [_vp, _vp, C.c_uint64]),
     "wv_index_delta_size": (C.c_int, [_vp, _u64p]),
+    "wv_pq_code_len": (C.c_int, [C.c_int, C.c_int, C.c_int]),
+    "wv_index_set_pq": (C.c_int, [_vp, C.c_int, C.c_int, C.c_int, C.c_int, _vp]),
+    "wv_index_upload_pq_codes": (C.c_int, [_vp, _vp, C.c_uint64, C.c_uint64]),
+    "wv_index_pq_encode": (C.c_int, [_vp]),
+    "wv_index_download_pq_codes": (C.c_int, [_vp, _vp, C.c_uint64, C.c_uint64]),
+    "wv_index_set_compressed": (C.c_int, [_vp, C.c_int]),
     "wv_search_by_vector": (C.c_int, [_vp, _vp, C.c_int, _vp, C.c_uint64, _vp, _vp, _vp]),
     "wv_search_by_vector_distance": (C.c_int, [_vp, _vp, C.c_float, C.c_int64, _vp, C.c_uint64, _vp, _vp, C.c_int64,
                                                C.POINTER(C.c_int64)]),

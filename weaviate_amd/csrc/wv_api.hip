@@ -37,6 +37,12 @@ hipError_t wv_launch_build_search(const wv::BuildParams* b, int waves_per_block,
 hipError_t wv_launch_build_select(const wv::BuildParams* b, hipStream_t s);
 hipError_t wv_launch_build_link(const wv::BuildParams* b, hipStream_t s);
 int wv_hnsw_per_wave_words(int dpad, int efc, int sc, int vc_log2, int xs_log2);
+hipError_t wv_launch_pq_encode(const float* X, int ldx, const uint64_t* ids, uint64_t n_rows, const wv::PqParams* pq,
+                               uint8_t* codes, hipStream_t s);
+hipError_t wv_launch_pq_scan(const wv::PqScanParams* p, hipStream_t s);
+hipError_t wv_launch_pq_topk(const float* skey, const uint32_t* sval, const float* dist, const uint32_t* rows,
+                             uint64_t nr, int q0, int nqc, int k, uint64_t id_base, uint64_t* out_ids, float* out_d,
+                             int32_t* out_n, hipStream_t s);
 }
 
 namespace {
@@ -216,6 +222,15 @@ struct wv_index {
     DevBuf delta, dmask, dl_ids, dl_d, dl_n, dq_tmp;
     // graph construction scratch
     DevBuf b_tgt, b_ci, b_cd, b_cn, b_cnt0, b_cntu, b_rk, b_rn, b_rk2, b_rn2, b_uk, b_ul, b_uo, b_nr, b_tmp;
+    // product quantization: h.pq / h.compressed
+    // (compress.go:39-89).  Codes live on the device as u8 (ks <= 256) or u16
+    // per segment, rows padded to whole words; has_code marks rows encoded.
+    int pq_m = 0, pq_ks = 0, pq_ds = 0, pq_encoder = 0;
+    bool pq_set = false, pq_on = false, pq_use_bits = false;
+    uint64_t pq_stride = 0;
+    std::vector<uint64_t> has_code;
+    DevBuf pq_cent, pq_codes;
+    DevBuf pk_key, pk_dist, pk_val, pk_skey, pk_sval, pk_off;
     // stats of the last batch
     uint64_t last_dist = 0, last_exp = 0, last_fallbacks = 0;
     // optional kernel timing (hipEvents on the launch stream)
@@ -235,6 +250,9 @@ int refresh_bitmaps(wv_index* ix) {
     std::vector<uint64_t> ex(words, 0);
     for (uint64_t w = 0; w < words; ++w) {
         uint64_t v = ~ix->has_vec[w];
+        // compressed: a node whose code is missing is skipped like a deleted
+        // one (distanceToByteNode, search.go:403-418)
+        if (ix->pq_on) v |= ~ix->has_code[w];
         if (w < ix->tomb_host.size()) v |= ix->tomb_host[w];
         ex[w] = v;
     }
@@ -391,9 +409,16 @@ int compact_allowed(wv_index* ix, const uint64_t* d_allow, uint64_t allow_nbits,
 // d_rowmask (nullable, with per-query allow lists only): a shared bitmap that
 // contains every row any query may return (the delta set of wv_index_add);
 // its rows are compacted and each query's own list is tested per row.
+int run_pq_flat(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_allow, uint64_t allow_nbits,
+                uint64_t allow_stride, uint64_t* d_out_ids, float* d_out_d, int32_t* d_out_n, hipStream_t s,
+                const uint64_t* d_rowmask, uint64_t rowmask_nbits);
+
 int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_allow, uint64_t allow_nbits,
               uint64_t allow_stride, uint64_t* d_out_ids, float* d_out_d, int32_t* d_out_n, hipStream_t s,
               const uint64_t* d_rowmask = nullptr, uint64_t rowmask_nbits = 0) {
+    if (ix->pq_on)   // flatSearch on a compressed index ranks by PQ distance (index.go:493-511)
+        return run_pq_flat(ix, d_q, nq, k, d_allow, allow_nbits, allow_stride, d_out_ids, d_out_d, d_out_n, s,
+                           d_rowmask, rowmask_nbits);
     const uint64_t N = ix->n_rows;
     if (N == 0 || nq == 0) {
         if (nq) HIP_TRY(hipMemsetAsync(d_out_n, 0, sizeof(int32_t) * nq, s));
@@ -560,9 +585,101 @@ int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
     }
     for (int q : fails) {
         const uint64_t* al = d_allow ? d_allow + (allow_stride ? (uint64_t)q * allow_stride : 0) : nullptr;
-        int rc = exact_full(ix, d_q + (size_t)q * ix->dpad, k, al, allow_nbits, d_out_ids + (size_t)q * k,
-                            d_out_d + (size_t)q * k, d_out_n + q, s);
+        int rc = ix->pq_on ? run_pq_flat(ix, d_q + (size_t)q * ix->dpad, 1, k, al, allow_nbits, 0,
+                                         d_out_ids + (size_t)q * k, d_out_d + (size_t)q * k, d_out_n + q, s, nullptr, 0)
+                           : exact_full(ix, d_q + (size_t)q * ix->dpad, k, al, allow_nbits, d_out_ids + (size_t)q * k,
+                                        d_out_d + (size_t)q * k, d_out_n + q, s);
         if (rc) return rc;
+    }
+    return WV_OK;
+}
+
+wv::PqParams pq_params(const wv_index* ix) {
+    wv::PqParams pq{};
+    pq.codes = ix->pq_codes.as<uint8_t>();
+    pq.cent = ix->pq_cent.as<float>();
+    pq.stride = ix->pq_stride;
+    pq.m = ix->pq_m;
+    pq.ks = ix->pq_ks;
+    pq.ds = ix->pq_ds;
+    pq.wide = ix->pq_ks > 256;
+    return pq;
+}
+
+__global__ void iota_stride_kernel(int32_t* off, int n, int64_t stride) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i <= n) off[i] = (int32_t)(i * stride);
+}
+
+// flatSearch over PQ codes: the rows a shared allow list (or the delta mask)
+// keeps are compacted, every (query, row) distance is computed from the codes
+// and a stable segmented radix sort orders each query's row list by
+// (dist, id); queries go in chunks of at most 2^26 (query, row) pairs.
+int run_pq_flat(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_allow, uint64_t allow_nbits,
+                uint64_t allow_stride, uint64_t* d_out_ids, float* d_out_d, int32_t* d_out_n, hipStream_t s,
+                const uint64_t* d_rowmask, uint64_t rowmask_nbits) {
+    const uint64_t N = ix->n_rows;
+    if (N == 0 || nq == 0) {
+        if (nq) HIP_TRY(hipMemsetAsync(d_out_n, 0, sizeof(int32_t) * nq, s));
+        return WV_OK;
+    }
+    const uint64_t* cmask = d_allow && !allow_stride ? d_allow : d_rowmask;
+    const uint64_t cbits = d_allow && !allow_stride ? allow_nbits : rowmask_nbits;
+    uint64_t nr = N;
+    const uint32_t* rows = nullptr;
+    if (cmask) {
+        int rc = compact_allowed(ix, cmask, cbits, N, &nr, s, true);
+        if (rc) return rc;
+        if (nr == 0) {
+            HIP_TRY(hipMemsetAsync(d_out_n, 0, sizeof(int32_t) * nq, s));
+            return WV_OK;
+        }
+        rows = ix->rowidx.as<uint32_t>();
+    }
+    const uint64_t cap = 1ull << 26;
+    const int qc = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)nq, cap / nr));
+    const uint64_t items = (uint64_t)qc * nr;
+    if (items > (uint64_t)INT32_MAX) return fail(WV_EINVAL, "flat PQ search: too many rows per query");
+    HIP_TRY(ix->pk_key.ensure(items * 4));
+    HIP_TRY(ix->pk_dist.ensure(items * 4));
+    HIP_TRY(ix->pk_val.ensure(items * 4));
+    HIP_TRY(ix->pk_skey.ensure(items * 4));
+    HIP_TRY(ix->pk_sval.ensure(items * 4));
+    HIP_TRY(ix->pk_off.ensure(((size_t)qc + 1) * 4));
+    wv::PqScanParams sp{};
+    sp.pq = pq_params(ix);
+    sp.Q = d_q;
+    sp.rows = rows;
+    sp.excl = ix->excl.as<uint64_t>();
+    sp.excl_nbits = ix->capacity;
+    sp.allow = allow_stride ? d_allow : nullptr;   // a shared list is compacted already
+    sp.allow_nbits = allow_nbits;
+    sp.allow_stride = allow_stride;
+    sp.nr = nr;
+    sp.ldq = ix->dpad;
+    sp.metric = ix->metric;
+    sp.key = ix->pk_key.as<float>();
+    sp.dist = ix->pk_dist.as<float>();
+    sp.val = ix->pk_val.as<uint32_t>();
+    for (int q0 = 0; q0 < nq; q0 += qc) {
+        const int nqc = std::min(qc, nq - q0);
+        sp.q0 = q0;
+        sp.nqc = nqc;
+        HIP_TRY(wv_launch_pq_scan(&sp, s));
+        hipLaunchKernelGGL(iota_stride_kernel, dim3((nqc + 256) / 256), dim3(256), 0, s, ix->pk_off.as<int32_t>(), nqc,
+                           (int64_t)nr);
+        HIP_TRY(hipGetLastError());
+        const int n_items = (int)((uint64_t)nqc * nr);
+        size_t tmp = 0;
+        HIP_TRY(hipcub::DeviceSegmentedRadixSort::SortPairs(
+            nullptr, tmp, ix->pk_key.as<float>(), ix->pk_skey.as<float>(), ix->pk_val.as<uint32_t>(),
+            ix->pk_sval.as<uint32_t>(), n_items, nqc, ix->pk_off.as<int32_t>(), ix->pk_off.as<int32_t>() + 1, 0, 32, s));
+        HIP_TRY(ix->sort_tmp.ensure(tmp));
+        HIP_TRY(hipcub::DeviceSegmentedRadixSort::SortPairs(
+            ix->sort_tmp.p, tmp, ix->pk_key.as<float>(), ix->pk_skey.as<float>(), ix->pk_val.as<uint32_t>(),
+            ix->pk_sval.as<uint32_t>(), n_items, nqc, ix->pk_off.as<int32_t>(), ix->pk_off.as<int32_t>() + 1, 0, 32, s));
+        HIP_TRY(wv_launch_pq_topk(ix->pk_skey.as<float>(), ix->pk_sval.as<uint32_t>(), ix->pk_dist.as<float>(), rows,
+                                  nr, q0, nqc, k, ix->cfg.id_base, d_out_ids, d_out_d, d_out_n, s));
     }
     return WV_OK;
 }
@@ -636,6 +753,7 @@ int run_hnsw(wv_index* ix, const float* d_q, int nq, int k, int ef, const uint64
     hp.out_n = d_out_n;
     hp.status = ix->status.as<int32_t>();
     hp.counters = ix->counters.as<uint32_t>();
+    if (ix->pq_on) hp.pq = pq_params(ix);   // compressed: PQ distances (search.go:171-199)
     if (ix->timing) HIP_TRY(hipEventRecord(ix->ev[4], s));
     HIP_TRY(wv_launch_hnsw(&hp, wpb, s));
     if (ix->timing) HIP_TRY(hipEventRecord(ix->ev[5], s));
@@ -659,8 +777,10 @@ int run_hnsw(wv_index* ix, const float* d_q, int nq, int k, int ef, const uint64
         if (!st[q]) continue;
         ix->last_fallbacks++;
         const uint64_t* al = d_allow ? d_allow + (allow_stride ? (uint64_t)q * allow_stride : 0) : nullptr;
-        int rc = exact_full(ix, d_q + (size_t)q * ix->dpad, k, al, allow_nbits, d_out_ids + (size_t)q * k,
-                            d_out_d + (size_t)q * k, d_out_n + q, s);
+        int rc = ix->pq_on ? run_pq_flat(ix, d_q + (size_t)q * ix->dpad, 1, k, al, allow_nbits, 0,
+                                         d_out_ids + (size_t)q * k, d_out_d + (size_t)q * k, d_out_n + q, s, nullptr, 0)
+                           : exact_full(ix, d_q + (size_t)q * ix->dpad, k, al, allow_nbits, d_out_ids + (size_t)q * k,
+                                        d_out_d + (size_t)q * k, d_out_n + q, s);
         if (rc) return rc;
     }
     return WV_OK;
@@ -892,7 +1012,8 @@ int wv_index_destroy(wv_index* ix) {
                       &ix->fail, &ix->status, &ix->counters, &ix->scan_d, &ix->scan_i, &ix->sort_d, &ix->sort_i,
                       &ix->sort_tmp, &ix->g_idx, &ix->g_q, &ix->g_allow, &ix->g_ids, &ix->g_d, &ix->g_n, &ix->g_cnt,
                       &ix->out_ids, &ix->out_d, &ix->out_n, &ix->stage, &ix->fail_thr, &ix->fb_idx, &ix->fb_d, &ix->fb_i, &ix->fb_n, &ix->fb_of,
-                      &ix->ac_cnt, &ix->ac_off, &ix->rowidx})
+                      &ix->ac_cnt, &ix->ac_off, &ix->rowidx, &ix->pq_cent, &ix->pq_codes, &ix->pk_key,
+                      &ix->pk_dist, &ix->pk_val, &ix->pk_skey, &ix->pk_sval, &ix->pk_off})
         b->release();
     for (auto& e : ix->ev)
         if (e) (void)hipEventDestroy(e);
@@ -909,6 +1030,32 @@ int wv_index_update_config(wv_index* ix, const wv_config* cfg) {
     ix->cfg = *cfg;
     ix->cfg.device = dev;   // the device and id base are fixed at creation
     ix->cfg.id_base = base;
+    return WV_OK;
+}
+
+// Rows written while a quantizer is set: with KMeans encoders the device
+// encodes them as hnsw.Add does on a compressed index (insert.go:91-95,
+// 166-170); codes of other encoders come from the host, so the rows are
+// unsearchable on a compressed index until wv_index_upload_pq_codes.
+static int pq_rows_written(wv_index* ix, const uint64_t* d_ids, const uint64_t* ids, uint64_t n, uint64_t first_id) {
+    if (!ix->pq_set || n == 0) return WV_OK;
+    if (ix->pq_encoder == WV_PQ_KMEANS) {
+        wv::PqParams pq = pq_params(ix);
+        if (d_ids) {
+            HIP_TRY(wv_launch_pq_encode(ix->vecs.as<float>(), ix->ldx, d_ids, n, &pq, ix->pq_codes.as<uint8_t>(),
+                                        ix->stream));
+        } else {
+            HIP_TRY(wv_launch_pq_encode(ix->vecs.as<float>() + first_id * ix->ldx, ix->ldx, nullptr, n, &pq,
+                                        ix->pq_codes.as<uint8_t>() + first_id * ix->pq_stride, ix->stream));
+        }
+        HIP_TRY(hipStreamSynchronize(ix->stream));
+    }
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t id = ids ? ids[i] : first_id + i;
+        if (ix->pq_encoder == WV_PQ_KMEANS) ix->has_code[id >> 6] |= 1ull << (id & 63);
+        else ix->has_code[id >> 6] &= ~(1ull << (id & 63));
+    }
+    ix->bitmaps_dirty = true;
     return WV_OK;
 }
 
@@ -933,7 +1080,7 @@ static int upload_rows(wv_index* ix, const float* src, bool device_src, int ld, 
     for (uint64_t i = first_id; i < first_id + n; ++i) ix->has_vec[i >> 6] |= 1ull << (i & 63);
     ix->n_rows = std::max(ix->n_rows, first_id + n);
     ix->bitmaps_dirty = true;
-    return WV_OK;
+    return pq_rows_written(ix, nullptr, nullptr, n, first_id);
 }
 
 int wv_index_upload_vectors(wv_index* ix, const float* rows, uint64_t n, uint64_t first_id) {
@@ -1051,7 +1198,7 @@ int wv_index_add(wv_index* ix, const uint64_t* ids, const float* rows, uint64_t 
         ix->n_rows = std::max(ix->n_rows, id + 1);
     }
     ix->bitmaps_dirty = true;
-    return WV_OK;
+    return pq_rows_written(ix, d_ids, ids, n, 0);
 }
 
 static int edit_tombstones(wv_index* ix, const uint64_t* ids, uint64_t n, bool add) {
@@ -1281,6 +1428,147 @@ int wv_index_graph_info(wv_index* ix, uint64_t* n, int* deg0, int* degU, int* ma
     if (max_level) *max_level = ix->max_level;
     if (n_upper) *n_upper = ix->n_upper;
     if (entrypoint) *entrypoint = ix->entrypoint;
+    return WV_OK;
+}
+
+// ---- product quantization ---------------------------------
+namespace {
+// NewProductQuantizer (ssdhelpers/product_quantization.go:116-179) and
+// ExtractCode (:191-237), read on the host: bits = int(log2 ks), bytes =
+// int(log2(ks-1))/8 + 1; whole-byte codes are big-endian `bytes`-wide fields,
+// bit-packed ones (useBitsEncoding, bits < 8*bytes) are cut from the
+// (bytes+1)-byte big-endian word at index*bits/8.
+struct CodeLayout {
+    int bits = 0, bytes = 0;
+    bool packed = false;
+    bool init(int ks, bool use_bits) {
+        if (ks < 2 || ks > 65536) return false;
+        bits = (int)std::floor(std::log2((double)ks));
+        bytes = (int)std::floor(std::log2((double)(ks - 1))) / 8 + 1;
+        packed = use_bits && bits != 8 * bytes;
+        return true;
+    }
+    static uint64_t be(const uint8_t* p, int nb) {
+        uint64_t v = 0;
+        for (int i = 0; i < nb; ++i) v = (v << 8) | p[i];
+        return v;
+    }
+    uint64_t get(const uint8_t* enc, int index) const {
+        if (!packed) return be(enc + (size_t)index * bytes, bytes);
+        uint64_t code = be(enc + (size_t)index * bits / 8, bytes + 1);
+        const int rest = (index + 1) * bits % 8, from_start = index * bits % 8;
+        code >>= from_start < rest ? 16 - rest : 8 - rest;
+        return code & ((1ull << bits) - 1);
+    }
+};
+}  // namespace
+
+int wv_pq_code_len(int segments, int centroids, int use_bits_encoding) {
+    CodeLayout L;
+    if (segments <= 0 || !L.init(centroids, use_bits_encoding != 0)) return -1;
+    return segments * L.bytes;   // ProductQuantizer.Encode allocates m * bytes (:348-354)
+}
+
+int wv_index_set_pq(wv_index* ix, int segments, int centroids, int use_bits_encoding, int encoder,
+                    const float* centroid_table) {
+    CodeLayout L;
+    if (check(ix) || !centroid_table || segments <= 0 || ix->dim % segments || !L.init(centroids, use_bits_encoding) ||
+        (encoder != WV_PQ_TILE && encoder != WV_PQ_KMEANS))
+        return fail(WV_EINVAL, "wv_index_set_pq: bad argument (segments must divide dims, 2 <= centroids <= 65536)");
+    std::lock_guard<std::mutex> g(ix->mu);
+    HIP_TRY(hipSetDevice(ix->cfg.device));
+    ix->pq_m = segments;
+    ix->pq_ks = centroids;
+    ix->pq_ds = ix->dim / segments;
+    ix->pq_encoder = encoder;
+    ix->pq_use_bits = use_bits_encoding != 0;
+    ix->pq_stride = centroids > 256 ? ((2 * (uint64_t)segments + 7) & ~7ull) : (((uint64_t)segments + 3) & ~3ull);
+    const size_t tbytes = (size_t)segments * centroids * ix->pq_ds * 4;
+    HIP_TRY(ix->pq_cent.ensure(tbytes));
+    HIP_TRY(ix->pq_codes.ensure(ix->capacity * ix->pq_stride));
+    HIP_TRY(hipMemcpyAsync(ix->pq_cent.p, centroid_table, tbytes, hipMemcpyHostToDevice, ix->stream));
+    HIP_TRY(hipMemsetAsync(ix->pq_codes.p, 0, ix->capacity * ix->pq_stride, ix->stream));
+    HIP_TRY(hipStreamSynchronize(ix->stream));
+    ix->has_code.assign(ix->bm_words, 0);
+    ix->pq_set = true;
+    ix->pq_on = false;
+    ix->bitmaps_dirty = true;
+    return WV_OK;
+}
+
+int wv_index_upload_pq_codes(wv_index* ix, const uint8_t* encoded, uint64_t n, uint64_t first_id) {
+    if (check(ix) || (n && !encoded)) return fail(WV_EINVAL, "wv_index_upload_pq_codes: bad argument");
+    std::lock_guard<std::mutex> g(ix->mu);
+    if (!ix->pq_set) return fail(WV_ESTATE, "wv_index_upload_pq_codes: no quantizer (wv_index_set_pq)");
+    if (first_id + n > ix->capacity) return fail(WV_EINVAL, "wv_index_upload_pq_codes: beyond capacity");
+    if (n == 0) return WV_OK;
+    HIP_TRY(hipSetDevice(ix->cfg.device));
+    CodeLayout L;
+    L.init(ix->pq_ks, ix->pq_use_bits);
+    const size_t len = (size_t)ix->pq_m * L.bytes;
+    std::vector<uint8_t> row(len + 8, 0), out(n * ix->pq_stride, 0);
+    for (uint64_t r = 0; r < n; ++r) {
+        std::memcpy(row.data(), encoded + r * len, len);   // zero tail: the packed reader looks one byte ahead
+        uint8_t* dst = out.data() + r * ix->pq_stride;
+        for (int i = 0; i < ix->pq_m; ++i) {
+            const uint64_t c = L.get(row.data(), i);
+            if (c >= (uint64_t)ix->pq_ks) return fail(WV_EINVAL, "wv_index_upload_pq_codes: code out of range");
+            if (ix->pq_ks > 256) reinterpret_cast<uint16_t*>(dst)[i] = (uint16_t)c;
+            else dst[i] = (uint8_t)c;
+        }
+    }
+    HIP_TRY(hipMemcpyAsync(ix->pq_codes.as<uint8_t>() + first_id * ix->pq_stride, out.data(), out.size(),
+                           hipMemcpyHostToDevice, ix->stream));
+    HIP_TRY(hipStreamSynchronize(ix->stream));
+    for (uint64_t i = first_id; i < first_id + n; ++i) ix->has_code[i >> 6] |= 1ull << (i & 63);
+    ix->bitmaps_dirty = true;
+    return WV_OK;
+}
+
+int wv_index_pq_encode(wv_index* ix) {
+    if (check(ix)) return WV_EINVAL;
+    std::lock_guard<std::mutex> g(ix->mu);
+    if (!ix->pq_set || ix->pq_encoder != WV_PQ_KMEANS)
+        return fail(WV_ESTATE, "wv_index_pq_encode: needs a KMeans quantizer (wv_index_set_pq)");
+    HIP_TRY(hipSetDevice(ix->cfg.device));
+    wv::PqParams pq = pq_params(ix);
+    HIP_TRY(wv_launch_pq_encode(ix->vecs.as<float>(), ix->ldx, nullptr, ix->n_rows, &pq, ix->pq_codes.as<uint8_t>(),
+                                ix->stream));
+    HIP_TRY(hipStreamSynchronize(ix->stream));
+    for (uint64_t w = 0; w < ix->bm_words; ++w) ix->has_code[w] |= ix->has_vec[w];
+    ix->bitmaps_dirty = true;
+    return WV_OK;
+}
+
+int wv_index_download_pq_codes(wv_index* ix, uint16_t* out, uint64_t first_id, uint64_t n) {
+    if (check(ix) || (n && !out)) return fail(WV_EINVAL, "wv_index_download_pq_codes: bad argument");
+    std::lock_guard<std::mutex> g(ix->mu);
+    if (!ix->pq_set) return fail(WV_ESTATE, "wv_index_download_pq_codes: no quantizer");
+    if (first_id + n > ix->capacity) return fail(WV_EINVAL, "wv_index_download_pq_codes: beyond capacity");
+    HIP_TRY(hipSetDevice(ix->cfg.device));
+    std::vector<uint8_t> raw(n * ix->pq_stride);
+    HIP_TRY(hipMemcpyAsync(raw.data(), ix->pq_codes.as<uint8_t>() + first_id * ix->pq_stride, raw.size(),
+                           hipMemcpyDeviceToHost, ix->stream));
+    HIP_TRY(hipStreamSynchronize(ix->stream));
+    for (uint64_t r = 0; r < n; ++r)
+        for (int i = 0; i < ix->pq_m; ++i) {
+            const uint8_t* src = raw.data() + r * ix->pq_stride;
+            out[r * ix->pq_m + i] = ix->pq_ks > 256 ? reinterpret_cast<const uint16_t*>(src)[i] : src[i];
+        }
+    return WV_OK;
+}
+
+int wv_index_set_compressed(wv_index* ix, int on) {
+    if (check(ix)) return WV_EINVAL;
+    std::lock_guard<std::mutex> g(ix->mu);
+    if (on) {
+        if (!ix->pq_set) return fail(WV_ESTATE, "wv_index_set_compressed: no quantizer (wv_index_set_pq)");
+        for (uint64_t w = 0; w < ix->bm_words; ++w)
+            if (ix->has_vec[w] & ~ix->has_code[w])
+                return fail(WV_ESTATE, "wv_index_set_compressed: a row with a vector has no code");
+    }
+    ix->pq_on = on != 0;
+    ix->bitmaps_dirty = true;
     return WV_OK;
 }
 

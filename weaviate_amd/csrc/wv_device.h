@@ -173,6 +173,80 @@ __device__ __forceinline__ void exact_dist_rows32(const float* __restrict__ q, c
     }
 }
 
+// Distance of one product-quantized row to the query, computed by ONE lane:
+// DistanceBetweenCompressedAndUncompressedVectors
+// (ssdhelpers/product_quantization.go:284-291), which the lookup table of
+// :56-75 caches value for value.  Step is the pure-Go loop of the provider
+// (distancer/l2.go:63-72, dot_product.go:80-87, cosine_dist.go:57-64): the
+// products are rounded before the add (no FMA: the _rn intrinsics keep the
+// compiler from contracting), segments summed in order, then Wrap.
+template <int METRIC, class PQ>
+__device__ __forceinline__ float pq_dist_row(const float* __restrict__ q, const PQ& pq, uint32_t row) {
+    const uint8_t* cr = pq.codes + (uint64_t)row * pq.stride;
+    float dist = 0.f;
+    for (int i0 = 0; i0 < pq.m; i0 += 4) {
+        // four codes per 32-bit load (rows are padded to whole words)
+        uint32_t w0 = *reinterpret_cast<const uint32_t*>(cr + (pq.wide ? 2 * i0 : i0));
+        uint32_t w1 = pq.wide ? *reinterpret_cast<const uint32_t*>(cr + 2 * i0 + 4) : 0u;
+        const int nseg = min(4, pq.m - i0);
+        for (int t = 0; t < nseg; ++t) {
+            const uint32_t c = pq.wide ? (t < 2 ? (w0 >> (16 * t)) : (w1 >> (16 * (t - 2)))) & 0xFFFFu
+                                       : (w0 >> (8 * t)) & 0xFFu;
+            const int i = i0 + t;
+            const float* cp = pq.cent + ((uint64_t)i * pq.ks + c) * pq.ds;
+            const float* qs = q + i * pq.ds;
+            float s = 0.f;
+            for (int j = 0; j < pq.ds; ++j) {
+                if (METRIC == WV_METRIC_L2) {
+                    const float d = __fsub_rn(qs[j], cp[j]);
+                    s = __fadd_rn(s, __fmul_rn(d, d));
+                } else {
+                    s = __fadd_rn(s, __fmul_rn(qs[j], cp[j]));
+                }
+            }
+            dist = __fadd_rn(dist, s);
+        }
+    }
+    if (METRIC == WV_METRIC_L2) return dist;
+    if (METRIC == WV_METRIC_DOT) return -dist;
+    return __fsub_rn(1.0f, dist);
+}
+
+// asm.L2 (distancer/asm/l2_amd64.s:7-64) of two short rows by ONE lane: the
+// same 4 x 8 accumulators, scalar FMA tail and reduction tree as
+// exact_dist_group8, written serially (KMeans.Nearest, kmeans.go:78-110).
+__device__ __forceinline__ float asm_l2_serial(const float* __restrict__ x, const float* __restrict__ y, int n) {
+    float acc[4][8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int l = 0; l < 8; ++l) acc[j][l] = 0.f;
+    int i = 0;
+    for (; n - i >= 32; i += 32) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int l = 0; l < 8; ++l) {
+                const float d = x[i + 8 * j + l] - y[i + 8 * j + l];
+                acc[j][l] = __builtin_fmaf(d, d, acc[j][l]);
+            }
+    }
+    float t = 0.f;
+    for (; i < n; ++i) {
+        const float d = x[i] - y[i];
+        t = __builtin_fmaf(d, d, t);
+    }
+    float s[8];
+#pragma unroll
+    for (int l = 0; l < 8; ++l) s[l] = (acc[0][l] + acc[1][l]) + (acc[2][l] + acc[3][l]);
+    float v0 = s[0] + s[4], v1 = s[1] + s[5], v2 = s[2] + s[6], v3 = s[3] + s[7];
+    v0 = t + v0;
+    v1 = 0.0f + v1;
+    v2 = 0.0f + v2;
+    v3 = 0.0f + v3;
+    return (v0 + v1) + (v2 + v3);
+}
+
 // Key order used for ids: (dist, id) ascending.
 __device__ __forceinline__ bool key_less(float da, uint32_t ia, float db, uint32_t ib) {
     return da < db || (da == db && (ia & WV_IDMASK) < (ib & WV_IDMASK));

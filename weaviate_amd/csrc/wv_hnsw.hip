@@ -192,9 +192,15 @@ __device__ __forceinline__ void search_layer(const HnswParams& p, WaveState& w_i
             wave_sync();
             if (nb == 0) continue;
 
-            // ---- exact distances, 8 lanes per row (search.go:265-271) ----
-            for (int base = 0; base < nb; base += 32)
-                exact_dist_rows32<METRIC>(w.qv, p.X, p.ldx, p.D, w.Bi + base, nb - base, w.Bd + base, lane);
+            // ---- exact distances, 8 lanes per row (search.go:265-271); on a
+            // compressed index one lane per row from the codes (:196-199) ----
+            if (p.pq.codes) {
+                for (int base = 0; base < nb; base += 64)
+                    if (base + lane < nb) w.Bd[base + lane] = pq_dist_row<METRIC>(w.qv, p.pq, w.Bi[base + lane]);
+            } else {
+                for (int base = 0; base < nb; base += 32)
+                    exact_dist_rows32<METRIC>(w.qv, p.X, p.ldx, p.D, w.Bi + base, nb - base, w.Bd + base, lane);
+            }
             n_dist += nb;
             wave_sync();
 
@@ -343,7 +349,8 @@ __device__ __forceinline__ void knn_one(const HnswParams& p, WaveState& w, int q
 
     // entry point distance (search.go:467-476)
     uint32_t ep = p.entrypoint;
-    float epd = exact_dist_group8<METRIC>(w.qv, p.X + (uint64_t)ep * p.ldx, p.D, g);
+    float epd = p.pq.codes ? pq_dist_row<METRIC>(w.qv, p.pq, ep)   // index.go:493-511
+                           : exact_dist_group8<METRIC>(w.qv, p.X + (uint64_t)ep * p.ldx, p.D, g);
     epd = __shfl(epd, 0, 64);
     n_dist++;
     int Rl, Sh, Sl;

@@ -118,6 +118,16 @@ struct ScanParams {
     uint32_t* ids;           // [N] iota
 };
 
+// Product-quantized rows (ssdhelpers/product_quantization.go): codes[row]
+// holds m codes (u8 when ks <= 256, else u16) at a row stride of `stride`
+// bytes; cent[m][ks][ds] = kms[i].Centroid(c).  codes == nullptr: raw vectors.
+struct PqParams {
+    const uint8_t* codes;
+    const float* cent;
+    uint64_t stride;
+    int m, ks, ds, wide;
+};
+
 struct HnswParams {
     const float* X;
     const int8_t* levels;
@@ -138,6 +148,24 @@ struct HnswParams {
     int32_t* out_n;
     int32_t* status;     // bit0 side overflow, bit1 expanded-set overflow
     uint32_t* counters;  // [nq][2]: distance evaluations, expansions (nullable)
+    PqParams pq;         // compressed index: distances from codes (search.go:171-199)
+};
+
+// Flat search over PQ codes (flat_search.go:19-74 on a compressed index):
+// distances of a chunk of queries against a row list, keyed for a stable
+// segmented sort by (dist, row).
+struct PqScanParams {
+    PqParams pq;
+    const float* Q;          // [nq][ldq] prepared queries (normalized for cosine)
+    const uint32_t* rows;    // [nr] ascending row ids (nullable: rows 0..nr-1)
+    const uint64_t* excl;    // excluded rows (tombstones, nil nodes, rows without a code)
+    const uint64_t* allow;   // allow bits (nullable)
+    uint64_t excl_nbits, allow_nbits, allow_stride;
+    uint64_t nr;
+    int q0, nqc, ldq, metric;
+    float* key;              // [nqc][nr] sort key: the distance (+0 for -0), +inf = excluded
+    float* dist;             // [nqc][nr] the distance as computed
+    uint32_t* val;           // [nqc][nr] j
 };
 
 // GPU graph construction: one batch of new nodes

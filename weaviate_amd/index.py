@@ -180,6 +180,38 @@ class GPUVectorIndex:
         check(lib().wv_index_delta_size(self._h, C.byref(n)))
         return n.value
 
+    # -- product quantization (compress.go:39-89) -------------------------------
+    def set_pq(self, centroids, use_bits_encoding: bool = False, encoder: str = "kmeans"):
+        """The fitted quantizer: centroids[segments][ks][dims/segments] =
+        kms[i].Centroid(c) (product_quantization.go:77-95)."""
+        cent = np.ascontiguousarray(centroids, dtype=np.float32)
+        if cent.ndim != 3 or cent.shape[0] * cent.shape[2] != self.dim:
+            raise WvError(1, f"centroid table must be [segments][centroids][dims/segments], got {cent.shape}")
+        self._pq = (cent.shape[0], cent.shape[1], bool(use_bits_encoding))
+        check(lib().wv_index_set_pq(self._h, cent.shape[0], cent.shape[1], int(use_bits_encoding),
+                                    {"tile": 0, "kmeans": 1}[encoder], _ptr(cent)))
+
+    def upload_pq_codes(self, encoded, first_id: int = 0):
+        """Encoded vectors in ProductQuantizer.Encode's byte layout, uint8[n][code_len]."""
+        enc = np.ascontiguousarray(encoded, dtype=np.uint8)
+        m, ks, ub = self._pq
+        if enc.ndim != 2 or enc.shape[1] != lib().wv_pq_code_len(m, ks, int(ub)):
+            raise WvError(1, f"encoded rows must be [n][{lib().wv_pq_code_len(m, ks, int(ub))}] bytes")
+        check(lib().wv_index_upload_pq_codes(self._h, _ptr(enc), enc.shape[0], first_id))
+
+    def pq_encode(self):
+        """KMeans-encode every resident vector on the device (ProductQuantizer.Encode)."""
+        check(lib().wv_index_pq_encode(self._h))
+
+    def download_pq_codes(self, n: int, first_id: int = 0) -> np.ndarray:
+        out = np.zeros((n, self._pq[0]), np.uint16)
+        check(lib().wv_index_download_pq_codes(self._h, _ptr(out), first_id, n))
+        return out
+
+    def set_compressed(self, on: bool = True):
+        """h.compressed: every search ranks by the PQ distance."""
+        check(lib().wv_index_set_compressed(self._h, int(on)))
+
     def set_tombstones(self, ids: Iterable[int]):
         al = AllowList.from_ids(ids, self.capacity)
         check(lib().wv_index_set_tombstones(self._h, _ptr(al.words), al.nbits))
