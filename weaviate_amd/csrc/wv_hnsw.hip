@@ -74,7 +74,7 @@ __device__ __forceinline__ int lower_bound(const float* ad, const uint32_t* ai, 
     return lo;
 }
 
-template <int METRIC>
+template <int METRIC, bool PQ = false>
 __device__ __forceinline__ void search_layer(const HnswParams& p, WaveState& w_io, int level, int ef, uint32_t ep,
                              float epd, const uint64_t* allow, int& Rl_out, int& Sh_out, int& Sl_out, int& status,
                              int nlt, uint32_t& n_dist, uint32_t& n_exp) {
@@ -194,7 +194,7 @@ __device__ __forceinline__ void search_layer(const HnswParams& p, WaveState& w_i
 
             // ---- exact distances, 8 lanes per row (search.go:265-271); on a
             // compressed index one lane per row from the codes (:196-199) ----
-            if (p.pq.codes) {
+            if (PQ) {
                 for (int base = 0; base < nb; base += 64)
                     if (base + lane < nb) w.Bd[base + lane] = pq_dist_row<METRIC>(w.qv, p.pq, w.Bi[base + lane]);
             } else {
@@ -335,7 +335,7 @@ __device__ __forceinline__ void search_layer(const HnswParams& p, WaveState& w_i
     w_io = w;
 }
 
-template <int METRIC>
+template <int METRIC, bool PQ>
 __device__ __forceinline__ void knn_one(const HnswParams& p, WaveState& w, int q) {
     const int lane = threadIdx.x & 63;
     const int g = lane & 7;
@@ -349,14 +349,14 @@ __device__ __forceinline__ void knn_one(const HnswParams& p, WaveState& w, int q
 
     // entry point distance (search.go:467-476)
     uint32_t ep = p.entrypoint;
-    float epd = p.pq.codes ? pq_dist_row<METRIC>(w.qv, p.pq, ep)   // index.go:493-511
-                           : exact_dist_group8<METRIC>(w.qv, p.X + (uint64_t)ep * p.ldx, p.D, g);
+    float epd = PQ ? pq_dist_row<METRIC>(w.qv, p.pq, ep)   // index.go:493-511
+                   : exact_dist_group8<METRIC>(w.qv, p.X + (uint64_t)ep * p.ldx, p.D, g);
     epd = __shfl(epd, 0, 64);
     n_dist++;
     int Rl, Sh, Sl;
     // greedy descent, levels max..1 with ef = 1 (:479-521)
     for (int level = p.max_level; level >= 1; --level) {
-        search_layer<METRIC>(p, w, level, 1, ep, epd, nullptr, Rl, Sh, Sl, status, nlt, n_dist, n_exp);
+        search_layer<METRIC, PQ>(p, w, level, 1, ep, epd, nullptr, Rl, Sh, Sl, status, nlt, n_dist, n_exp);
         if (Rl > 0) {
             const uint32_t cid = w.Ri[0] & WV_IDMASK;
             if (p.levels[cid] < 0) {
@@ -373,7 +373,7 @@ __device__ __forceinline__ void knn_one(const HnswParams& p, WaveState& w, int q
         }
     }
     // layer 0 with ef and the allow list (:523-528)
-    search_layer<METRIC>(p, w, 0, p.ef, ep, epd, allow, Rl, Sh, Sl, status, nlt, n_dist, n_exp);
+    search_layer<METRIC, PQ>(p, w, 0, p.ef, ep, epd, allow, Rl, Sh, Sl, status, nlt, n_dist, n_exp);
     const int n = min(Rl, p.k);
     for (int i = lane; i < n; i += 64) {
         p.out_ids[(uint64_t)q * p.k + i] = p.id_base + (w.Ri[i] & WV_IDMASK);
@@ -404,9 +404,17 @@ __global__ __launch_bounds__(256) void wv_hnsw_kernel(HnswParams p) {
     w.vc = reinterpret_cast<uint32_t*>(cur); cur += (1 << p.vc_log2);
     w.xs = reinterpret_cast<uint32_t*>(cur); cur += (1 << p.xs_log2);
     w.ltomb = reinterpret_cast<uint32_t*>(cur); cur += MAX_LOCAL_TOMB;
-    if (p.metric == WV_METRIC_L2) knn_one<WV_METRIC_L2>(p, w, q);
-    else if (p.metric == WV_METRIC_DOT) knn_one<WV_METRIC_DOT>(p, w, q);
-    else knn_one<WV_METRIC_COSINE>(p, w, q);
+    // a compressed index (PQ codes) is its own instantiation: the raw-vector
+    // kernel keeps its registers and schedule
+    if (p.pq.codes) {
+        if (p.metric == WV_METRIC_L2) knn_one<WV_METRIC_L2, true>(p, w, q);
+        else if (p.metric == WV_METRIC_DOT) knn_one<WV_METRIC_DOT, true>(p, w, q);
+        else knn_one<WV_METRIC_COSINE, true>(p, w, q);
+    } else {
+        if (p.metric == WV_METRIC_L2) knn_one<WV_METRIC_L2, false>(p, w, q);
+        else if (p.metric == WV_METRIC_DOT) knn_one<WV_METRIC_DOT, false>(p, w, q);
+        else knn_one<WV_METRIC_COSINE, false>(p, w, q);
+    }
 }
 
 // ===========================================================================
