@@ -608,3 +608,36 @@ def test_gpu_graph_build_invariants_and_recall():
     for i in range(len(qs)):
         _same_tie_aware(gi[i], gd[i], ri[i], rd[i])
     ix.close()
+
+
+@pytest.mark.parametrize("metric", [O.L2, O.DOT, O.COSINE])
+def test_split_key_pass_equals_fp32_key_pass(metric):
+    """The bf16x3 key pass (default) and the fp32 MFMA key pass (WV_BF_FP32=1)
+    only rank candidates; both re-rank in the reference's order, so ids and
+    distances agree bit for bit -- also on wide-range data (|x| up to 1e4),
+    where the split error bound of the certificate is largest."""
+    import os
+    rng = np.random.default_rng(31 + metric)
+    n, d = 15000, 128
+    scale = np.exp(rng.uniform(-4, 9, (n, 1))).astype(np.float32)
+    base = (rng.standard_normal((n, d)) * scale).astype(np.float32)
+    qs = (rng.standard_normal((120, d)) * 30).astype(np.float32)
+    out = []
+    for env in (None, "1"):
+        if env:
+            os.environ["WV_BF_FP32"] = env
+        try:
+            ix = W.GPUVectorIndex(d, METRIC_NAMES[metric], capacity=n)
+        finally:
+            os.environ.pop("WV_BF_FP32", None)
+        ix.upload_vectors(base)
+        out.append(ix.search_batch(qs, 10, mode="exact"))
+        ix.close()
+    (ai, ad, an), (bi, bd, bn) = out
+    assert an.tolist() == bn.tolist()
+    _same(ai, ad, bi, bd)
+    b = O.normalize_rows(base) if metric == O.COSINE else base
+    q = O.normalize_rows(qs) if metric == O.COSINE else qs
+    oi, od, on = O.flat_scan(metric, b, q, 10)
+    for i in range(len(qs)):
+        _same_tie_aware(ai[i], ad[i], oi[i], od[i])

@@ -40,6 +40,8 @@ int wv_hnsw_per_wave_words(int dpad, int efc, int sc, int vc_log2, int xs_log2);
 hipError_t wv_launch_pq_encode(const float* X, int ldx, const uint64_t* ids, uint64_t n_rows, const wv::PqParams* pq,
                                uint8_t* codes, hipStream_t s);
 hipError_t wv_launch_pq_scan(const wv::PqScanParams* p, hipStream_t s);
+hipError_t wv_launch_split_rows(const float* in, int ld_in, const uint64_t* ids, uint64_t n, uint64_t n_valid, int D,
+                                float scale, void* out, int ld_out, uint64_t out_row0, hipStream_t s);
 hipError_t wv_launch_pq_topk(const float* skey, const uint32_t* sval, const float* dist, const uint32_t* rows,
                              uint64_t nr, int q0, int nqc, int k, uint64_t id_base, uint64_t* out_ids, float* out_d,
                              int32_t* out_n, hipStream_t s);
@@ -188,6 +190,10 @@ struct wv_index {
     std::mutex mu;
     // corpus
     DevBuf vecs;            // [capacity rounded to 128][ldx]
+    // bf16 hi/lo image of vecs for the brute-force key pass (same bytes, in
+    // the MFMA-native layout of split_hi_index), kept in step with every row write
+    DevBuf xsplit;
+    bool use_split = false;
     DevBuf xnorm;           // [capacity]
     DevBuf maxnorm;         // unsigned bits of max |x|
     std::vector<uint64_t> has_vec;   // host copy of uploaded rows
@@ -455,16 +461,28 @@ int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
         HIP_TRY(ix->q_nrm2.ensure((size_t)nq * 4));
         HIP_TRY(ix->fail.ensure((size_t)nq * 4));
         HIP_TRY(wv_launch_qnorm(d_q, nq, ix->dim, ix->dpad, ix->metric, ix->q_nrm2.as<float>(), s));
-        // B operand in whole BF_BQ-row query blocks, zero rows past nq
+        // B operand in whole BF_BQ-row query blocks, zero rows past nq: -2q
+        // (L2) or -q, as fp32 rows or (split key pass: whole-corpus or shared
+        // allow list scans) as the native bf16 hi/lo image
+        const bool split = ix->use_split && !d_rowidx && !allow_stride;
         const size_t nq_pad = (size_t)n_qblocks * wv::BF_BQ;
-        HIP_TRY(ix->q_scaled.ensure(nq_pad * ix->dpad * 4));
-        if (nq_pad > (size_t)nq)
-            HIP_TRY(hipMemsetAsync(ix->q_scaled.as<float>() + (size_t)nq * ix->dpad, 0,
-                                   (nq_pad - nq) * ix->dpad * 4, s));
-        HIP_TRY(wv_launch_scale(d_q, ix->q_scaled.as<float>(), (uint64_t)nq * ix->dpad,
-                                ix->metric == WV_L2_SQUARED ? -2.f : -1.f, s));
+        const int ldb = split ? ix->ldx : ix->dpad;
+        const float bscale = ix->metric == WV_L2_SQUARED ? -2.f : -1.f;
+        HIP_TRY(ix->q_scaled.ensure(nq_pad * ldb * 4));
+        if (split) {
+            HIP_TRY(wv_launch_split_rows(d_q, ix->dpad, nullptr, nq_pad, nq, ix->dim, bscale, ix->q_scaled.p, ldb, 0, s));
+        } else {
+            if (nq_pad > (size_t)nq)
+                HIP_TRY(hipMemsetAsync(ix->q_scaled.as<float>() + (size_t)nq * ldb, 0, (nq_pad - nq) * ldb * 4, s));
+            HIP_TRY(wv_launch_scale(d_q, ix->q_scaled.as<float>(), (uint64_t)nq * ix->dpad, bscale, s));
+        }
         wv::BfParams bp{};
-        bp.X = ix->vecs.as<float>();
+        bp.split = split ? 1 : 0;
+        {
+            const char* e = std::getenv("WV_BF_LOCALITY");   // ablation: 0..3, default 3
+            bp.locality = e ? std::atoi(e) : 3;
+        }
+        bp.X = split ? ix->xsplit.as<float>() : ix->vecs.as<float>();
         bp.Q = ix->q_scaled.as<float>();
         bp.xnorm = ix->xnorm.as<float>();
         bp.tomb = d_rowidx ? nullptr : ix->excl.as<uint64_t>();
@@ -479,7 +497,7 @@ int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
         bp.nq = nq;
         bp.D = ix->dim;
         bp.ldx = ix->ldx;
-        bp.ldq = ix->dpad;
+        bp.ldq = ldb;
         bp.metric = ix->metric;
         bp.n_qblocks = n_qblocks;
         bp.n_slots = sch.n_slots;
@@ -518,6 +536,7 @@ int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
         fp.fail = ix->fail.as<int32_t>();
         HIP_TRY(ix->fail_thr.ensure((size_t)nq * 4));
         fp.fail_thr = ix->fail_thr.as<float>();
+        fp.split = bp.split;
         if (ix->timing) HIP_TRY(hipEventRecord(ix->ev[2], s));
         HIP_TRY(wv_launch_bf_finalize(&fp, s));
         if (ix->timing) HIP_TRY(hipEventRecord(ix->ev[3], s));
@@ -993,6 +1012,15 @@ int wv_index_create(int dim, int metric, const wv_config* cfg, uint64_t capacity
         wv_index_destroy(ix);
         return fail(WV_EOOM, "wv_index_create: device allocation failed");
     }
+    // bf16x3 key pass (wv_bf_split_kernel): whole 32-float chunks, stride <= 128
+    // (the query block image stays resident in LDS); WV_BF_FP32=1 keeps the
+    // fp32 MFMA pass for every scan
+    ix->use_split = ix->ldx % wv::BF_BK == 0 && ix->ldx <= 128 && !std::getenv("WV_BF_FP32");
+    if (ix->use_split && ix->xsplit.ensure(vbytes) != hipSuccess) {
+        wv_index_destroy(ix);
+        return fail(WV_EOOM, "wv_index_create: device allocation failed");
+    }
+    if (ix->use_split) (void)hipMemsetAsync(ix->xsplit.p, 0, vbytes, ix->stream);
     (void)hipMemsetAsync(ix->vecs.p, 0, vbytes, ix->stream);
     (void)hipMemsetAsync(ix->xnorm.p, 0, cap_rows * 4, ix->stream);
     (void)hipMemsetAsync(ix->maxnorm.p, 0, 4, ix->stream);
@@ -1007,7 +1035,7 @@ int wv_index_create(int dim, int metric, const wv_config* cfg, uint64_t capacity
 int wv_index_destroy(wv_index* ix) {
     if (!ix) return WV_OK;
     (void)hipSetDevice(ix->cfg.device);
-    for (DevBuf* b : {&ix->vecs, &ix->xnorm, &ix->maxnorm, &ix->levels, &ix->layer0, &ix->upper_row, &ix->upper,
+    for (DevBuf* b : {&ix->vecs, &ix->xsplit, &ix->xnorm, &ix->maxnorm, &ix->levels, &ix->layer0, &ix->upper_row, &ix->upper,
                       &ix->tomb, &ix->excl, &ix->q_in, &ix->q_norm, &ix->q_nrm2, &ix->q_scaled, &ix->cand_d, &ix->cand_id,
                       &ix->fail, &ix->status, &ix->counters, &ix->scan_d, &ix->scan_i, &ix->sort_d, &ix->sort_i,
                       &ix->sort_tmp, &ix->g_idx, &ix->g_q, &ix->g_allow, &ix->g_ids, &ix->g_d, &ix->g_n, &ix->g_cnt,
@@ -1076,6 +1104,9 @@ static int upload_rows(wv_index* ix, const float* src, bool device_src, int ld, 
         HIP_TRY(wv_launch_normalize(dst, dst, n, ix->dim, ix->ldx, ix->stream));
     HIP_TRY(wv_launch_rownorm(dst, n, ix->dim, ix->ldx, ix->xnorm.as<float>() + first_id,
                               ix->maxnorm.as<unsigned int>(), ix->stream));
+    if (ix->use_split)
+        HIP_TRY(wv_launch_split_rows(dst, ix->ldx, nullptr, n, n, ix->dim, 1.f, ix->xsplit.p, ix->ldx, first_id,
+                                     ix->stream));
     HIP_TRY(hipStreamSynchronize(ix->stream));
     for (uint64_t i = first_id; i < first_id + n; ++i) ix->has_vec[i >> 6] |= 1ull << (i & 63);
     ix->n_rows = std::max(ix->n_rows, first_id + n);
@@ -1190,6 +1221,9 @@ int wv_index_add(wv_index* ix, const uint64_t* ids, const float* rows, uint64_t 
     hipLaunchKernelGGL(scatter_rows_kernel, dim3((unsigned)n), dim3(128), 0, s, tmp, ix->ldx, d_ids, n, ix->ldx,
                        ix->vecs.as<float>(), nrm, ix->xnorm.as<float>());
     HIP_TRY(hipGetLastError());
+    if (ix->use_split)
+        HIP_TRY(wv_launch_split_rows(ix->vecs.as<float>(), ix->ldx, d_ids, n, n, ix->dim, 1.f, ix->xsplit.p, ix->ldx, 0,
+                                     s));
     HIP_TRY(hipStreamSynchronize(s));
     for (uint64_t i = 0; i < n; ++i) {
         const uint64_t id = ids[i];

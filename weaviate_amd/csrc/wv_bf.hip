@@ -26,6 +26,8 @@ namespace wv {
 
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
 
 
 // ---------------------------------------------------------------------------
@@ -92,7 +94,12 @@ __global__ __launch_bounds__(256, WV_BF_WAVES_PER_SIMD) void wv_bf_mfma_kernel(B
     const int lrow = tid >> 3, lf4 = tid & 7;
     const uint32_t xoff = (uint32_t)lrow * p.ldx + 4 * lf4;
     const uint32_t qoff = (uint32_t)lrow * p.ldq + 4 * lf4;
-    const uint64_t u_first = (uint64_t)blockIdx.x * p.units_per_block;
+    // locality bit 1: logical block ids contiguous per XCD (blocks are dealt
+    // round-robin over the 8 XCDs), so one XCD's L2 serves the query blocks of
+    // ~1/8 of the batch instead of all of them
+    int lb = (int)blockIdx.x;
+    if ((p.locality & 1) && gridDim.x % 8 == 0) lb = (int)(blockIdx.x % 8) * (int)(gridDim.x / 8) + (int)(blockIdx.x / 8);
+    const uint64_t u_first = (uint64_t)lb * p.units_per_block;
     uint64_t u_last = u_first + p.units_per_block;
     if (u_last > (uint64_t)p.n_qblocks * p.ntiles) u_last = (uint64_t)p.n_qblocks * p.ntiles;
 
@@ -103,7 +110,19 @@ __global__ __launch_bounds__(256, WV_BF_WAVES_PER_SIMD) void wv_bf_mfma_kernel(B
         uint64_t t_end = t_begin + (u_last - u);
         if (t_end > p.ntiles) t_end = p.ntiles;
         u += t_end - t_begin;
-        const int slot = (int)blockIdx.x - bf_first_block(qb, p.ntiles, p.units_per_block);
+        const int slot = lb - bf_first_block(qb, p.ntiles, p.units_per_block);
+        // locality bit 2: query block qb visits its tiles rotated by rot(qb) =
+        // the offset of its first block boundary, so every block starts at a
+        // corpus tile that is a multiple of units_per_block and concurrent
+        // blocks of different query blocks stream the same tiles (one L2/MALL
+        // fill serves them all).  A bijection on the tiles of qb; results do
+        // not depend on the visiting order (lists compare (key, id)).
+        uint64_t rt_begin = t_begin;
+        if (p.locality & 2) {
+            const uint64_t rot = ((p.units_per_block - (uint64_t)qb * p.ntiles % p.units_per_block) %
+                                  p.units_per_block) % p.ntiles;
+            rt_begin = t_begin >= rot ? t_begin - rot : t_begin + p.ntiles - rot;
+        }
         const int q0 = qb * BF_BQ;
         const int jq0 = q0 + wn * 64 + l31;   // this lane's two query columns
         const int jq1 = jq0 + 32;
@@ -130,7 +149,8 @@ __global__ __launch_bounds__(256, WV_BF_WAVES_PER_SIMD) void wv_bf_mfma_kernel(B
 #ifdef WV_BF_ABLATE_SAME_TILE
             const uint64_t tile = 0;
 #else
-            const uint64_t tile = t_begin + (uint64_t)(c / nk);
+            uint64_t tile = rt_begin + (uint64_t)(c / nk);
+            if (tile >= p.ntiles) tile -= p.ntiles;
 #endif
             const float* __restrict__ xt = p.X + tile * BF_BN * p.ldx + kc * BF_BK;
             const float* __restrict__ qt = qblk + kc * BF_BK;
@@ -176,7 +196,8 @@ __global__ __launch_bounds__(256, WV_BF_WAVES_PER_SIMD) void wv_bf_mfma_kernel(B
         const int ntile = (int)(t_end - t_begin);
         int c = 0;   // chunk counter: stage c & 1 holds chunk c
         for (int t = 0; t < ntile; ++t) {
-            const uint64_t tile = t_begin + (uint64_t)t;
+            uint64_t tile = rt_begin + (uint64_t)t;
+            if (tile >= p.ntiles) tile -= p.ntiles;
             // eligibility of this wave's 64 base rows, fetched now so the
             // loads complete under the tile's MFMAs: not excluded, < N, and
             // allowed (shared list: wave-uniform; per-query list: per lane)
@@ -354,6 +375,242 @@ __global__ __launch_bounds__(256, WV_BF_WAVES_PER_SIMD) void wv_bf_mfma_kernel(B
 }
 
 // ---------------------------------------------------------------------------
+// Split key pass: bf16x3 on MFMA-native operand images (wv_split_rows_kernel).
+//
+// Each 32-k chunk is two k-steps of v_mfma_f32_32x32x16_bf16 x 3 (hi*hi +
+// hi*lo + lo*hi; the lo*lo term and the rounding of lo are dropped: |error|
+// <= 4 * 2^-16 * |x||b|, which the finalize certificate adds to its eps).  The
+// keys only rank candidates; every reported distance is the exact
+// reference-order re-rank of the finalize.
+//
+// Data movement, chosen for CDNA4:
+//  * the query block's image (128 queries x ldx, NK x 16 KiB) is copied into
+//    LDS once per segment and stays resident while the block streams its
+//    corpus tiles -- no per-tile query reloads;
+//  * corpus operands go global -> registers directly: in the native image one
+//    wave-wide 16-byte load is one contiguous 1 KiB operand block, so there is
+//    no LDS staging, no ds_write and no workgroup barrier inside the tile loop;
+//    the next chunk is prefetched under the current chunk's 24 MFMAs;
+//  * without barriers the two resident workgroups of a CU drift apart, so one
+//    wave's epilogue (VALU) overlaps another wave's MFMAs.
+// Shared allow list / tombstones only, no compacted rows, ldx <= 128 (the host
+// picks the LDS-staged fp32 kernel otherwise).  Wave (wm, wn) owns base rows
+// 64 wm .. +63 and queries 64 wn .. +63 of the 128 x 128 tile, as in
+// wv_bf_mfma_kernel, so the lists and the finalize are shared.
+template <int NK, bool L2>
+__global__ __launch_bounds__(256, 2) void wv_bf_split_kernel(BfParams p) {
+    extern __shared__ uint4 qimg[];            // [4 query groups][NK][2 s][2 part][64 lanes]
+    constexpr int GRP = NK * 4 * 64;           // uint4 per 32-row group of an image
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 1, wn = wave & 1;
+    const int khalf = lane >> 5;
+    const int l31 = lane & 31;
+    const uint64_t tomb_words = (p.tomb_nbits + 63) / 64;
+    const uint64_t allow_words = (p.allow_nbits + 63) / 64;
+    const uint64_t* __restrict__ tomb = p.tomb;
+    const uint64_t* __restrict__ allow = p.allow;
+    const uint4* __restrict__ X = reinterpret_cast<const uint4*>(p.X);
+    const uint4* __restrict__ Qg = reinterpret_cast<const uint4*>(p.Q);
+    int lb = (int)blockIdx.x;
+    if ((p.locality & 1) && gridDim.x % 8 == 0) lb = (int)(blockIdx.x % 8) * (int)(gridDim.x / 8) + (int)(blockIdx.x / 8);
+    const uint64_t u_first = (uint64_t)lb * p.units_per_block;
+    uint64_t u_last = u_first + p.units_per_block;
+    if (u_last > (uint64_t)p.n_qblocks * p.ntiles) u_last = (uint64_t)p.n_qblocks * p.ntiles;
+
+    for (uint64_t u = u_first; u < u_last;) {
+        const int qb = (int)(u / p.ntiles);
+        const uint64_t t_begin = u % p.ntiles;
+        uint64_t t_end = t_begin + (u_last - u);
+        if (t_end > p.ntiles) t_end = p.ntiles;
+        u += t_end - t_begin;
+        const int slot = lb - bf_first_block(qb, p.ntiles, p.units_per_block);
+        uint64_t rt_begin = t_begin;   // aligned rotation, as in wv_bf_mfma_kernel
+        if (p.locality & 2) {
+            const uint64_t rot = ((p.units_per_block - (uint64_t)qb * p.ntiles % p.units_per_block) %
+                                  p.units_per_block) % p.ntiles;
+            rt_begin = t_begin >= rot ? t_begin - rot : t_begin + p.ntiles - rot;
+        }
+        const int jq0 = qb * BF_BQ + wn * 64 + l31;
+        const int jq1 = jq0 + 32;
+
+        __syncthreads();   // the previous segment's reads of qimg are done
+        {
+            const uint4* __restrict__ src = Qg + (uint64_t)qb * 4 * GRP;
+#pragma unroll
+            for (int i = 0; i < 4 * GRP / 256; ++i) qimg[tid + 256 * i] = src[tid + 256 * i];
+        }
+        __syncthreads();
+
+        float l0d[BF_KP], l1d[BF_KP];
+        uint32_t l0i[BF_KP], l1i[BF_KP];
+#pragma unroll
+        for (int i = 0; i < BF_KP; ++i) {
+            l0d[i] = FLT_MAX; l1d[i] = FLT_MAX;
+            l0i[i] = WV_NIL; l1i[i] = WV_NIL;
+        }
+        const uint4* __restrict__ qw = qimg + 2 * wn * GRP + lane;   // query groups 2 wn, 2 wn + 1
+        // corpus operand block of (tile, 32-row half h, chunk c, step s, part)
+        auto xsrc = [&](uint64_t tile, int c) { return X + (tile * 4 + 2 * wm) * GRP + c * 256 + lane; };
+        uint4 cur[8], nxt[8];   // [h][s][part]
+        auto load_x = [&](uint4 (&dst)[8], const uint4* src) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) dst[4 * h + j] = src[h * GRP + 64 * j];
+        };
+        // C-in of a tile's accumulators (L2): |x|^2 of this lane's 32 rows, as
+        // the accumulator layout holds them (rows (r & 3) + 8 (r >> 2) + 4 khalf
+        // of each 32-row half); loaded one tile ahead, during the epilogue
+        float4 xn[8];
+        auto load_xn = [&](uint64_t tile) {
+            const float* xr = p.xnorm + tile * BF_BN + wm * 64 + 4 * khalf;
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) {
+                xn[g4] = ld4(xr + 8 * g4);
+                xn[4 + g4] = ld4(xr + 32 + 8 * g4);
+            }
+        };
+        const int ntile = (int)(t_end - t_begin);
+        if (ntile > 0) {
+            load_x(cur, xsrc(rt_begin, 0));
+            if (L2) load_xn(rt_begin);
+        }
+        for (int t = 0; t < ntile; ++t) {
+            uint64_t tile = rt_begin + (uint64_t)t;
+            if (tile >= p.ntiles) tile -= p.ntiles;
+            uint64_t ntl = tile + 1;
+            if (ntl >= p.ntiles) ntl -= p.ntiles;
+            const uint64_t row0 = tile * BF_BN + wm * 64;
+            const uint64_t word = row0 >> 6;
+            uint64_t okw = ~0ull;
+            if (row0 + 64 > p.N) okw = p.N > row0 ? ((1ull << (p.N - row0)) - 1) : 0ull;
+            if (tomb && word < tomb_words) okw &= ~tomb[word];
+            if (allow) okw &= word < allow_words ? allow[word] : 0ull;
+
+            floatx16 acc00, acc01, acc10, acc11;
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) {
+                const float a0s[4] = {xn[g4].x, xn[g4].y, xn[g4].z, xn[g4].w};
+                const float a1s[4] = {xn[4 + g4].x, xn[4 + g4].y, xn[4 + g4].z, xn[4 + g4].w};
+#pragma unroll
+                for (int r3 = 0; r3 < 4; ++r3) {
+                    acc00[4 * g4 + r3] = L2 ? a0s[r3] : 0.f; acc01[4 * g4 + r3] = L2 ? a0s[r3] : 0.f;
+                    acc10[4 * g4 + r3] = L2 ? a1s[r3] : 0.f; acc11[4 * g4 + r3] = L2 ? a1s[r3] : 0.f;
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < NK; ++c) {
+#ifdef WV_BF_ABLATE_NO_LOADS
+                if (t == 0 && c == 0)
+#endif
+                {
+                    if (c + 1 < NK) load_x(nxt, xsrc(tile, c + 1));
+                    else if (t + 1 < ntile) load_x(nxt, xsrc(ntl, 0));
+                }
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) {
+                    const int qo = c * 256 + s2 * 128;
+                    const bf16x8 bh0 = __builtin_bit_cast(bf16x8, qw[qo]);
+                    const bf16x8 bl0 = __builtin_bit_cast(bf16x8, qw[qo + 64]);
+                    const bf16x8 bh1 = __builtin_bit_cast(bf16x8, qw[GRP + qo]);
+                    const bf16x8 bl1 = __builtin_bit_cast(bf16x8, qw[GRP + qo + 64]);
+                    const bf16x8 ah0 = __builtin_bit_cast(bf16x8, cur[2 * s2]);
+                    const bf16x8 al0 = __builtin_bit_cast(bf16x8, cur[2 * s2 + 1]);
+                    const bf16x8 ah1 = __builtin_bit_cast(bf16x8, cur[4 + 2 * s2]);
+                    const bf16x8 al1 = __builtin_bit_cast(bf16x8, cur[4 + 2 * s2 + 1]);
+#ifdef WV_BF_ABLATE_NO_MFMA
+                    asm volatile("" ::"v"(ah0), "v"(al0), "v"(ah1), "v"(al1), "v"(bh0), "v"(bl0), "v"(bh1), "v"(bl1));
+                    continue;
+#endif
+                    acc00 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al0, bh0, acc00, 0, 0, 0);
+                    acc01 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al0, bh1, acc01, 0, 0, 0);
+                    acc10 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al1, bh0, acc10, 0, 0, 0);
+                    acc11 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al1, bh1, acc11, 0, 0, 0);
+                    acc00 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah0, bl0, acc00, 0, 0, 0);
+                    acc01 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah0, bl1, acc01, 0, 0, 0);
+                    acc10 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah1, bl0, acc10, 0, 0, 0);
+                    acc11 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah1, bl1, acc11, 0, 0, 0);
+                    acc00 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah0, bh0, acc00, 0, 0, 0);
+                    acc01 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah0, bh1, acc01, 0, 0, 0);
+                    acc10 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah1, bh0, acc10, 0, 0, 0);
+                    acc11 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah1, bh1, acc11, 0, 0, 0);
+                }
+#pragma unroll
+                for (int j = 0; j < 8; ++j) cur[j] = nxt[j];
+                // keep each chunk's LDS reads next to its MFMAs (register pressure)
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            if (L2 && t + 1 < ntile) load_xn(ntl);
+#ifdef WV_BF_ABLATE_NO_EPILOGUE
+            asm volatile("" ::"v"(acc00[0]), "v"(acc01[0]), "v"(acc10[0]), "v"(acc11[0]));
+            if (acc00[3] == 1234.5f) l0d[0] = acc01[5] + (float)okw;
+            continue;
+#endif
+            // ---- epilogue of one 128x128 tile (as wv_bf_mfma_kernel) ----
+            const uint32_t rb0 = (uint32_t)row0 + 4 * khalf;
+            const uint64_t o0 = (jq0 < p.nq ? okw : 0ull) >> (4 * khalf);
+            const uint64_t o1 = (jq1 < p.nq ? okw : 0ull) >> (4 * khalf);
+            const uint32_t o0lo = (uint32_t)o0, o0hi = (uint32_t)(o0 >> 32);
+            const uint32_t o1lo = (uint32_t)o1, o1hi = (uint32_t)(o1 >> 32);
+            constexpr uint32_t LANE_ROWS = 0x0F0F0F0Fu;
+            const float INF = __builtin_inff();
+            if (!__all((o0lo & o0hi & o1lo & o1hi & LANE_ROWS) == LANE_ROWS)) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int bit = (r & 3) + 8 * (r >> 2);
+                    acc00[r] = (o0lo >> bit) & 1u ? acc00[r] : INF;
+                    acc10[r] = (o0hi >> bit) & 1u ? acc10[r] : INF;
+                    acc01[r] = (o1lo >> bit) & 1u ? acc01[r] : INF;
+                    acc11[r] = (o1hi >> bit) & 1u ? acc11[r] : INF;
+                }
+            }
+            float m0 = INF, m1 = INF;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                m0 = min3_raw(m0, acc00[r], acc10[r]);
+                m1 = min3_raw(m1, acc01[r], acc11[r]);
+            }
+#define WV_EXTRACT(M, A0, A1, LD, LI)                                                            \
+            while (M <= LD[BF_KP - 1]) {                                                        \
+                uint32_t idm = WV_NIL;                                                          \
+                _Pragma("unroll") for (int r = 0; r < 16; ++r) {                                \
+                    const bool hit = idm == WV_NIL && A0[r] == M;                               \
+                    idm = hit ? rb0 + (r & 3) + 8 * (r >> 2) : idm;                             \
+                    A0[r] = hit ? INF : A0[r];                                                  \
+                }                                                                               \
+                _Pragma("unroll") for (int r = 0; r < 16; ++r) {                                \
+                    const bool hit = idm == WV_NIL && A1[r] == M;                               \
+                    idm = hit ? rb0 + 32 + (r & 3) + 8 * (r >> 2) : idm;                        \
+                    A1[r] = hit ? INF : A1[r];                                                  \
+                }                                                                               \
+                if (!key_less(M, idm, LD[BF_KP - 1], LI[BF_KP - 1])) break;                     \
+                list_insert(LD, LI, M, idm);                                                    \
+                M = INF;                                                                        \
+                _Pragma("unroll") for (int r = 0; r < 16; ++r) M = min3_raw(M, A0[r], A1[r]);   \
+            }
+            WV_EXTRACT(m0, acc00, acc10, l0d, l0i)
+            WV_EXTRACT(m1, acc01, acc11, l1d, l1i)
+#undef WV_EXTRACT
+        }
+
+        const int prod = wm * 2 + khalf;
+        const size_t per_q = (size_t)p.n_slots * BF_PROD * BF_KP;
+        if (jq0 < p.nq) {
+            const size_t base = (size_t)jq0 * per_q + ((size_t)slot * BF_PROD + prod) * BF_KP;
+#pragma unroll
+            for (int i = 0; i < BF_KP; ++i) { p.out_d[base + i] = l0d[i]; p.out_id[base + i] = l0i[i]; }
+        }
+        if (jq1 < p.nq) {
+            const size_t base = (size_t)jq1 * per_q + ((size_t)slot * BF_PROD + prod) * BF_KP;
+#pragma unroll
+            for (int i = 0; i < BF_KP; ++i) { p.out_d[base + i] = l1d[i]; p.out_id[base + i] = l1i[i]; }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Finalize: one wave per query.
 
 template <int METRIC>
@@ -479,16 +736,21 @@ __device__ void finalize_one(const BfFinParams& p, int q, float* sd, uint32_t* s
     const float u = 5.9604645e-08f;  // 2^-24
     const float D4 = (float)(p.D + 4);
     float eps, bfull;
+    // bf16x3 keys: 3x the accumulated terms, plus the split error
+    // 4 * 2^-16 * |x| |b| with b = -2q (L2) or -q
+    const float acc_f = p.split ? 12.f : 4.f;
+    const float split_e = p.split ? 4.f * 1.52587890625e-05f : 0.f;   // 2^-16
     if (METRIC == WV_METRIC_L2) {
         const float qn = sqrtf(p.qnorm[q]);
         const float s = qn + p.xnorm_max;
-        eps = 4.f * D4 * u * s * s;
+        eps = acc_f * D4 * u * s * s + 2.f * split_e * qn * p.xnorm_max;
         bfull = bound + p.qnorm[q];
     } else {
         const float qn = p.qnorm[q];
-        eps = 4.f * D4 * u * qn * p.xnorm_max + 4.f * u;
+        eps = acc_f * D4 * u * qn * p.xnorm_max + 4.f * u + split_e * qn * p.xnorm_max;
         bfull = METRIC == WV_METRIC_DOT ? bound : 1.0f + bound;
     }
+    eps *= 1.0001f;   // the float evaluation of the bound itself
     bool certified;
     if (nvalid < k) certified = bound == FLT_MAX;     // everything eligible was seen
     else certified = (bound == FLT_MAX) || (bfull - eps > dk);
@@ -667,6 +929,30 @@ __global__ void wv_normalize_kernel(const float* in, float* out, uint64_t n, int
     for (int i = 0; i < D; ++i) o[i] = __fdiv_rn(v[i], nn);
 }
 
+// bf16 hi/lo image of rows for the split key pass, in the MFMA-native layout
+// of split_hi_index (wv_params.h): hi = bf16(v), lo = bf16(v - float(hi)),
+// v = scale * in (an exact power-of-two scaling), zero past D and for rows >=
+// n_valid.  Round to nearest even.  Row r of the launch reads in row
+// (ids ? ids[r] : r) and writes image row out_row0 + that.
+__device__ __forceinline__ uint16_t bf16_rn(float v) {
+    const uint32_t b = __float_as_uint(v);
+    return (uint16_t)((b + 0x7FFFu + ((b >> 16) & 1u)) >> 16);
+}
+__global__ void wv_split_rows_kernel(const float* in, int ld_in, const uint64_t* ids, uint64_t n, uint64_t n_valid,
+                                     int D, float scale, uint16_t* out, int ld_out, uint64_t out_row0) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t r = t / (uint64_t)ld_out;
+    const int k = (int)(t % (uint64_t)ld_out);
+    if (r >= n) return;
+    const uint64_t row = ids ? ids[r] : r;
+    const float v = (k < D && r < n_valid) ? scale * in[row * ld_in + k] : 0.f;
+    const uint16_t hi = bf16_rn(v);
+    const uint16_t lo = bf16_rn(v - __uint_as_float((uint32_t)hi << 16));
+    const uint64_t o = split_hi_index(out_row0 + row, k, ld_out / BF_BK);
+    out[o] = hi;
+    out[o + 512] = lo;
+}
+
 // B operand of the MFMA pass: -2q (L2) or -q (dot, cosine); exact scalings
 __global__ void wv_scale_rows_kernel(const float* in, float* out, uint64_t n, float s) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -690,15 +976,41 @@ __global__ void wv_qnorm_kernel(const float* Q, int nq, int D, int ldq, int metr
 extern "C" {
 
 hipError_t wv_launch_bf_mfma(const wv::BfParams* p, hipStream_t s) {
-    const size_t lds = wv::BF_LDS_BYTES;
     if (p->X == nullptr || p->Q == nullptr) return hipErrorInvalidValue;
     const uint64_t total = (uint64_t)p->n_qblocks * p->ntiles;
     const unsigned nb = (unsigned)((total + p->units_per_block - 1) / p->units_per_block);
     if (nb == 0) return hipSuccess;
+    if (p->split) {
+        // native images: whole 32-k chunks, query image stride = corpus stride,
+        // shared lists only (no compacted rows, no per-query lists)
+        const int nk = p->ldx / wv::BF_BK;
+        if (p->ldx % wv::BF_BK || p->ldq != p->ldx || nk < 1 || nk > 4 || p->rowidx || p->allow_stride)
+            return hipErrorInvalidValue;
+        const size_t lds = (size_t)nk * 16384;
+        const bool l2 = p->metric == WV_METRIC_L2;
+        switch (nk) {
+            case 1: if (l2) hipLaunchKernelGGL((wv::wv_bf_split_kernel<1, true>), dim3(nb), dim3(256), lds, s, *p); else hipLaunchKernelGGL((wv::wv_bf_split_kernel<1, false>), dim3(nb), dim3(256), lds, s, *p); break;
+            case 2: if (l2) hipLaunchKernelGGL((wv::wv_bf_split_kernel<2, true>), dim3(nb), dim3(256), lds, s, *p); else hipLaunchKernelGGL((wv::wv_bf_split_kernel<2, false>), dim3(nb), dim3(256), lds, s, *p); break;
+            case 3: if (l2) hipLaunchKernelGGL((wv::wv_bf_split_kernel<3, true>), dim3(nb), dim3(256), lds, s, *p); else hipLaunchKernelGGL((wv::wv_bf_split_kernel<3, false>), dim3(nb), dim3(256), lds, s, *p); break;
+            default: if (l2) hipLaunchKernelGGL((wv::wv_bf_split_kernel<4, true>), dim3(nb), dim3(256), lds, s, *p); else hipLaunchKernelGGL((wv::wv_bf_split_kernel<4, false>), dim3(nb), dim3(256), lds, s, *p); break;
+        }
+        return hipGetLastError();
+    }
+    const size_t lds = wv::BF_LDS_BYTES;
     if (p->D % wv::BF_BK == 0)
-        hipLaunchKernelGGL(wv::wv_bf_mfma_kernel<true>, dim3(nb), dim3(256), lds, s, *p);
+        hipLaunchKernelGGL((wv::wv_bf_mfma_kernel<true>), dim3(nb), dim3(256), lds, s, *p);
     else
-        hipLaunchKernelGGL(wv::wv_bf_mfma_kernel<false>, dim3(nb), dim3(256), lds, s, *p);
+        hipLaunchKernelGGL((wv::wv_bf_mfma_kernel<false>), dim3(nb), dim3(256), lds, s, *p);
+    return hipGetLastError();
+}
+
+hipError_t wv_launch_split_rows(const float* in, int ld_in, const uint64_t* ids, uint64_t n, uint64_t n_valid, int D,
+                                float scale, void* out, int ld_out, uint64_t out_row0, hipStream_t s) {
+    const uint64_t total = n * (uint64_t)ld_out;
+    if (total == 0) return hipSuccess;
+    if (ld_out % wv::BF_BK) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(wv::wv_split_rows_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, in, ld_in,
+                       ids, n, n_valid, D, scale, static_cast<uint16_t*>(out), ld_out, out_row0);
     return hipGetLastError();
 }
 

@@ -30,7 +30,23 @@ struct BfParams {
     uint64_t ntiles, units_per_block;
     float* out_d;           // [nq][n_slots][BF_PROD*BF_KP]
     uint32_t* out_id;
+    int split;              // X and Q are split images (split_hi_index): wv_bf_split_kernel
+    int locality;           // bit 1: XCD-contiguous block ids; bit 2: aligned tile rotation
 };
+
+// MFMA-native bf16 hi/lo image (split key pass): 32-row group g, 32-k chunk c,
+// k-step s (16 k), part (hi = 0, lo = +512): a 1 KiB block of 64 lanes x 8
+// bf16 where lane (h << 5 | r) holds row 32 g + r, k = 32 c + 16 s + 8 h ..
+// +7 -- the A/B operand of v_mfma_f32_32x32x16_bf16.  nk = stride / 32; an
+// image of R rows (R a multiple of 32) takes R * stride * 4 bytes, as fp32.
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+inline uint64_t split_hi_index(uint64_t row, int k, int nk) {
+    const uint64_t g = row >> 5;
+    const int r = (int)(row & 31), c = k >> 5, kk = k & 31, s = kk >> 4, h = (kk >> 3) & 1, e = kk & 7;
+    return ((((g * nk + c) * 2 + s) * 2) * 64 + (h * 32 + r)) * 8 + e;
+}
 
 // Equal-work schedule for wv_bf_mfma_kernel: exactly n_blocks workgroups
 // (a multiple of the resident slots) so no partial last wave of workgroups.
@@ -80,6 +96,7 @@ struct BfFinParams {
     int32_t* out_n;
     int32_t* fail;          // per query: 1 = uncertified
     float* fail_thr;        // per query: exact d_k of the re-ranked set (upper bound of the true d_k)
+    int split;              // approximate keys came from the bf16x3 pass (wider eps)
 };
 
 // Certificate fallback: exact distances of every row for a batch of failed
