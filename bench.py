@@ -325,9 +325,12 @@ def main():
         # v_mfma_f32_32x32x16_bf16, 3 bf16 products per fp32 product, so its
         # fp32-equivalent ceiling is the bf16 dense peak / 3) or as fp32 MFMA
         # (WV_BF_FP32=1).  achieved stays the algorithmic 2*D*N_eff per query.
-        split = not os.environ.get("WV_BF_FP32")
+        # (the library takes the split pass for D <= 128 unless a shared allow
+        # list is compacted into a row list: |allow| < N/2)
+        split = not os.environ.get("WV_BF_FP32") and D <= 128 and 2 * n_allowed >= n_local
         peak = BF16_MFMA_PEAK_TF / 3 if split else FP32_MFMA_PEAK_TF
-        result["roofline"] = {"bound": "mfma", "kernel": "wv_bf_mfma_kernel", "achieved": round(achieved, 2),
+        kname = "wv_bf_split_kernel" if split else "wv_bf_mfma_kernel"
+        result["roofline"] = {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 2),
                               "peak": round(peak, 1), "unit": "TFLOP/s",
                               "frac": round(achieved / peak, 4), "traffic": None,
                               "key_pass": "bf16x3 (peak = bf16 dense / 3)" if split else "fp32 MFMA",

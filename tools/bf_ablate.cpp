@@ -15,14 +15,15 @@ int main(int argc, char** argv) {
     for (auto& v : hq) v = -2.f * rand() / (float)RAND_MAX;  // pre-scaled B operand (-2q)
     for (uint64_t i = 0; i < N; ++i) { float s = 0; for (int k = 0; k < D; ++k) s += hx[i * D + k] * hx[i * D + k]; hn[i] = s; }
     float *X, *Q, *xn, *od; uint32_t* oi;
-    const uint64_t Np = (N + 127) / 128 * 128; const size_t nqp = (nq + 127) / 128 * 128;
+    const bool split = getenv("SPLIT") && atoi(getenv("SPLIT"));
+    const int bq = split ? (getenv("BQ") ? atoi(getenv("BQ")) : 256) : 128;
+    const uint64_t Np = (N + 127) / 128 * 128; const size_t nqp = (nq + bq - 1) / bq * bq;
     hipMalloc(&X, Np * D * 4); hipMalloc(&Q, nqp * D * 4); hipMalloc(&xn, Np * 4);
     hipMemset(X, 0, Np * D * 4); hipMemset(Q, 0, nqp * D * 4); hipMemset(xn, 0, Np * 4);
-    const bool split = getenv("SPLIT") && atoi(getenv("SPLIT"));
     if (split) {   // native bf16 hi/lo images (wv_split_rows_kernel layout)
         auto bf = [](float v) { uint32_t b; memcpy(&b, &v, 4); return (uint16_t)((b + 0x7FFFu + ((b >> 16) & 1u)) >> 16); };
         auto img = [&](std::vector<float>& m, size_t rows) {
-            std::vector<float> o((rows + 127) / 128 * 128 * D, 0.f);
+            std::vector<float> o((rows + bq - 1) / bq * bq * D, 0.f);
             uint16_t* h = reinterpret_cast<uint16_t*>(o.data());
             for (size_t r = 0; r < rows; ++r)
                 for (int k = 0; k < D; ++k) {
@@ -41,14 +42,14 @@ int main(int argc, char** argv) {
     hipMemcpy(Q, hq.data(), (split ? nqp : (size_t)nq) * D * 4, hipMemcpyHostToDevice);
     hipMemcpy(xn, hn.data(), N * 4, hipMemcpyHostToDevice);
     wv::BfParams p{};
-    const int nqb = (nq + 127) / 128;
-    const int target = getenv("BLOCKS") ? atoi(getenv("BLOCKS")) : 512;
-    const wv::BfSchedule sch = wv::bf_schedule(nq, N, target);
+    const int nqb = (nq + bq - 1) / bq;
+    const int target = getenv("BLOCKS") ? atoi(getenv("BLOCKS")) : 512 * 128 / bq;
+    const wv::BfSchedule sch = wv::bf_schedule(nq, N, target, bq);
     const int ns = sch.n_slots;
     hipMalloc(&od, (size_t)nq * ns * 4 * wv::BF_KP * 4); hipMalloc(&oi, (size_t)nq * ns * 4 * wv::BF_KP * 4);
     p.X = X; p.Q = Q; p.xnorm = xn; p.N = N; p.nq = nq; p.D = D; p.ldx = D; p.ldq = D; p.metric = 0;
     p.n_qblocks = nqb; p.n_slots = ns; p.ntiles = sch.ntiles; p.units_per_block = sch.units_per_block; p.out_d = od; p.out_id = oi;
-    p.split = split; p.locality = getenv("LOC") ? atoi(getenv("LOC")) : 3;
+    p.split = split; p.bq = bq; p.locality = getenv("LOC") ? atoi(getenv("LOC")) : 3;
     hipEvent_t a, b; hipEventCreate(&a); hipEventCreate(&b);
     wv_launch_bf_mfma(&p, 0); hipDeviceSynchronize();
     float best = 1e9;

@@ -51,7 +51,7 @@ def main():
            "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
            "hbm_bytes_per_launch": rd + wr, "sq": sq,
            "note": "read = 2*FETCH_SIZE*1024 (gfx950 half-count correction), write = WRITE_SIZE*1024"}
-    if a.kernel == "wv_bf_mfma_kernel":
+    if a.kernel in ("wv_bf_mfma_kernel", "wv_bf_split_kernel"):
         flops = 2.0 * a.dim * a.n * a.nq
         out["algorithmic_tflops"] = flops / avg_ns / 1e3
         if "SQ_VALU_MFMA_BUSY_CYCLES" in sq and "GRBM_GUI_ACTIVE" in sq:

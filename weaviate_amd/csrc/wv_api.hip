@@ -432,7 +432,6 @@ int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
     }
     std::vector<int32_t> fails;
     if (k <= wv::BF_FAST_KMAX) {
-        const int n_qblocks = (nq + wv::BF_BQ - 1) / wv::BF_BQ;
         // A shared allow list that keeps under half the corpus is compacted
         // into a row list first: the contraction then runs over |allow| rows
         // (the reference's flatSearch also walks only the allow list,
@@ -454,18 +453,28 @@ int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
                 d_rowidx = ix->rowidx.as<uint32_t>();
             }
         }
-        const wv::BfSchedule sch = wv::bf_schedule(nq, n_scan, ix->bf_blocks);
+        // bf16x3 key pass on native images (whole-corpus or shared allow list
+        // scans); it runs 256-query blocks, one 512-thread workgroup per CU,
+        // unless WV_BF_BQ=128 (the two-workgroup 128-query variant)
+        const bool split = ix->use_split && !d_rowidx && !allow_stride;
+        int bq = wv::BF_BQ;
+        if (split) {
+            const char* e = std::getenv("WV_BF_BQ");
+            bq = e && std::atoi(e) == wv::BF_BQ ? wv::BF_BQ : 2 * wv::BF_BQ;
+        }
+        const int n_qblocks = (nq + bq - 1) / bq;
+        const wv::BfSchedule sch =
+            wv::bf_schedule(nq, n_scan, bq == wv::BF_BQ ? ix->bf_blocks : ix->bf_blocks / 2, bq);
         const size_t n_lists = (size_t)sch.n_slots * wv::BF_PROD;
         HIP_TRY(ix->cand_d.ensure((size_t)nq * n_lists * wv::BF_KP * 4));
         HIP_TRY(ix->cand_id.ensure((size_t)nq * n_lists * wv::BF_KP * 4));
         HIP_TRY(ix->q_nrm2.ensure((size_t)nq * 4));
         HIP_TRY(ix->fail.ensure((size_t)nq * 4));
         HIP_TRY(wv_launch_qnorm(d_q, nq, ix->dim, ix->dpad, ix->metric, ix->q_nrm2.as<float>(), s));
-        // B operand in whole BF_BQ-row query blocks, zero rows past nq: -2q
+        // B operand in whole bq-row query blocks, zero rows past nq: -2q
         // (L2) or -q, as fp32 rows or (split key pass: whole-corpus or shared
         // allow list scans) as the native bf16 hi/lo image
-        const bool split = ix->use_split && !d_rowidx && !allow_stride;
-        const size_t nq_pad = (size_t)n_qblocks * wv::BF_BQ;
+        const size_t nq_pad = (size_t)n_qblocks * bq;
         const int ldb = split ? ix->ldx : ix->dpad;
         const float bscale = ix->metric == WV_L2_SQUARED ? -2.f : -1.f;
         HIP_TRY(ix->q_scaled.ensure(nq_pad * ldb * 4));
@@ -478,6 +487,7 @@ int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
         }
         wv::BfParams bp{};
         bp.split = split ? 1 : 0;
+        bp.bq = bq;
         {
             const char* e = std::getenv("WV_BF_LOCALITY");   // ablation: 0..3, default 3
             bp.locality = e ? std::atoi(e) : 3;
@@ -537,6 +547,7 @@ int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
         HIP_TRY(ix->fail_thr.ensure((size_t)nq * 4));
         fp.fail_thr = ix->fail_thr.as<float>();
         fp.split = bp.split;
+        fp.bq = bq;
         if (ix->timing) HIP_TRY(hipEventRecord(ix->ev[2], s));
         HIP_TRY(wv_launch_bf_finalize(&fp, s));
         if (ix->timing) HIP_TRY(hipEventRecord(ix->ev[3], s));

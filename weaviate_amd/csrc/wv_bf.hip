@@ -395,16 +395,22 @@ __global__ __launch_bounds__(256, WV_BF_WAVES_PER_SIMD) void wv_bf_mfma_kernel(B
 //    wave's epilogue (VALU) overlaps another wave's MFMAs.
 // Shared allow list / tombstones only, no compacted rows, ldx <= 128 (the host
 // picks the LDS-staged fp32 kernel otherwise).  Wave (wm, wn) owns base rows
-// 64 wm .. +63 and queries 64 wn .. +63 of the 128 x 128 tile, as in
+// 64 wm .. +63 and queries 64 wn .. +63 of the 128 x (64 WN) tile, as in
 // wv_bf_mfma_kernel, so the lists and the finalize are shared.
-template <int NK, bool L2>
-__global__ __launch_bounds__(256, 2) void wv_bf_split_kernel(BfParams p) {
-    extern __shared__ uint4 qimg[];            // [4 query groups][NK][2 s][2 part][64 lanes]
+//
+// WN = 4 (the default): one 512-thread workgroup per CU holds a 256-query
+// block (128 KiB of LDS at D = 128) and its 8 waves sweep the same corpus
+// tiles, so every corpus byte fetched from L2/HBM feeds 256 queries instead of
+// 128: the 1M x 128 corpus image is streamed 40 times per 10k batch, not 79
+// (measured at WN = 2: 50 GB fetched per launch, 5.5 TB/s -- the bound).
+template <int NK, bool L2, int WN>
+__global__ __launch_bounds__(128 * WN, 4 / WN) void wv_bf_split_kernel(BfParams p) {
+    extern __shared__ uint4 qimg[];            // [2 WN query groups][NK][2 s][2 part][64 lanes]
     constexpr int GRP = NK * 4 * 64;           // uint4 per 32-row group of an image
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave >> 1, wn = wave & 1;
+    const int wm = wave / WN, wn = wave % WN;
     const int khalf = lane >> 5;
     const int l31 = lane & 31;
     const uint64_t tomb_words = (p.tomb_nbits + 63) / 64;
@@ -432,14 +438,14 @@ __global__ __launch_bounds__(256, 2) void wv_bf_split_kernel(BfParams p) {
                                   p.units_per_block) % p.ntiles;
             rt_begin = t_begin >= rot ? t_begin - rot : t_begin + p.ntiles - rot;
         }
-        const int jq0 = qb * BF_BQ + wn * 64 + l31;
+        const int jq0 = qb * 64 * WN + wn * 64 + l31;
         const int jq1 = jq0 + 32;
 
         __syncthreads();   // the previous segment's reads of qimg are done
         {
-            const uint4* __restrict__ src = Qg + (uint64_t)qb * 4 * GRP;
+            const uint4* __restrict__ src = Qg + (uint64_t)qb * 2 * WN * GRP;
 #pragma unroll
-            for (int i = 0; i < 4 * GRP / 256; ++i) qimg[tid + 256 * i] = src[tid + 256 * i];
+            for (int i = 0; i < GRP / 64; ++i) qimg[tid + 128 * WN * i] = src[tid + 128 * WN * i];
         }
         __syncthreads();
 
@@ -453,7 +459,10 @@ __global__ __launch_bounds__(256, 2) void wv_bf_split_kernel(BfParams p) {
         const uint4* __restrict__ qw = qimg + 2 * wn * GRP + lane;   // query groups 2 wn, 2 wn + 1
         // corpus operand block of (tile, 32-row half h, chunk c, step s, part)
         auto xsrc = [&](uint64_t tile, int c) { return X + (tile * 4 + 2 * wm) * GRP + c * 256 + lane; };
-        uint4 cur[8], nxt[8];   // [h][s][part]
+        // operand ping-pong: chunk c reads xb[c & 1] while chunk c + 1 loads
+        // into xb[(c + 1) & 1] (distinct registers, so the loads issue at the
+        // chunk start, a whole chunk ahead of their first use)
+        uint4 xb[2][8];   // [h][s][part]
         auto load_x = [&](uint4 (&dst)[8], const uint4* src) {
 #pragma unroll
             for (int h = 0; h < 2; ++h)
@@ -462,43 +471,51 @@ __global__ __launch_bounds__(256, 2) void wv_bf_split_kernel(BfParams p) {
         };
         // C-in of a tile's accumulators (L2): |x|^2 of this lane's 32 rows, as
         // the accumulator layout holds them (rows (r & 3) + 8 (r >> 2) + 4 khalf
-        // of each 32-row half); loaded one tile ahead, during the epilogue
-        float4 xn[8];
-        auto load_xn = [&](uint64_t tile) {
-            const float* xr = p.xnorm + tile * BF_BN + wm * 64 + 4 * khalf;
-#pragma unroll
-            for (int g4 = 0; g4 < 4; ++g4) {
-                xn[g4] = ld4(xr + 8 * g4);
-                xn[4 + g4] = ld4(xr + 32 + 8 * g4);
-            }
-        };
+        // of each 32-row half).  It depends on the row only, so xc0 / xc1 enter
+        // as the C operand of the tile's first MFMA on both query halves (no
+        // accumulator init moves); dot / cosine start from the constant 0.  The
+        // wave stages its 64 norms in a private LDS slot: one dword per lane is
+        // loaded a tile ahead (1 VGPR in flight instead of 32) and written at
+        // the end of the tile; the layout read is 8 ds_read_b128 at the tile start.
+        float* __restrict__ xnl = reinterpret_cast<float*>(qimg + 2 * WN * GRP) + wave * 64;
+        float xv = 0.f;
         const int ntile = (int)(t_end - t_begin);
         if (ntile > 0) {
-            load_x(cur, xsrc(rt_begin, 0));
-            if (L2) load_xn(rt_begin);
+            load_x(xb[0], xsrc(rt_begin, 0));
+            if (L2) xnl[lane] = p.xnorm[rt_begin * BF_BN + wm * 64 + lane];
         }
+        // eligibility words of a tile's 64 rows (this wave's half): tombstones
+        // and the shared allow list, fetched raw one tile ahead with |x|^2 and
+        // combined only in that tile's epilogue (a load whose value is used at
+        // once is waited for on the spot, and vmcnt drains in issue order)
+        uint64_t tw_next = 0, aw_next = ~0ull;
+        auto load_words = [&](uint64_t tile) {
+            const uint64_t w = (tile * BF_BN + wm * 64) >> 6;
+            tw_next = tomb && w < tomb_words ? tomb[w] : 0ull;
+            if (allow) aw_next = w < allow_words ? allow[w] : 0ull;
+        };
+        if (ntile > 0) load_words(rt_begin);
         for (int t = 0; t < ntile; ++t) {
             uint64_t tile = rt_begin + (uint64_t)t;
             if (tile >= p.ntiles) tile -= p.ntiles;
             uint64_t ntl = tile + 1;
             if (ntl >= p.ntiles) ntl -= p.ntiles;
             const uint64_t row0 = tile * BF_BN + wm * 64;
-            const uint64_t word = row0 >> 6;
-            uint64_t okw = ~0ull;
-            if (row0 + 64 > p.N) okw = p.N > row0 ? ((1ull << (p.N - row0)) - 1) : 0ull;
-            if (tomb && word < tomb_words) okw &= ~tomb[word];
-            if (allow) okw &= word < allow_words ? allow[word] : 0ull;
+            const uint64_t tw = tw_next, aw = aw_next;
 
             floatx16 acc00, acc01, acc10, acc11;
+            floatx16 xc0, xc1;
+            if (L2) {
 #pragma unroll
-            for (int g4 = 0; g4 < 4; ++g4) {
-                const float a0s[4] = {xn[g4].x, xn[g4].y, xn[g4].z, xn[g4].w};
-                const float a1s[4] = {xn[4 + g4].x, xn[4 + g4].y, xn[4 + g4].z, xn[4 + g4].w};
-#pragma unroll
-                for (int r3 = 0; r3 < 4; ++r3) {
-                    acc00[4 * g4 + r3] = L2 ? a0s[r3] : 0.f; acc01[4 * g4 + r3] = L2 ? a0s[r3] : 0.f;
-                    acc10[4 * g4 + r3] = L2 ? a1s[r3] : 0.f; acc11[4 * g4 + r3] = L2 ? a1s[r3] : 0.f;
+                for (int g4 = 0; g4 < 4; ++g4) {
+                    const float4 a = *reinterpret_cast<const float4*>(xnl + 4 * khalf + 8 * g4);
+                    const float4 b = *reinterpret_cast<const float4*>(xnl + 32 + 4 * khalf + 8 * g4);
+                    xc0[4 * g4] = a.x; xc0[4 * g4 + 1] = a.y; xc0[4 * g4 + 2] = a.z; xc0[4 * g4 + 3] = a.w;
+                    xc1[4 * g4] = b.x; xc1[4 * g4 + 1] = b.y; xc1[4 * g4 + 2] = b.z; xc1[4 * g4 + 3] = b.w;
                 }
+            } else {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) { xc0[r] = 0.f; xc1[r] = 0.f; }
             }
 #pragma unroll
             for (int c = 0; c < NK; ++c) {
@@ -506,9 +523,15 @@ __global__ __launch_bounds__(256, 2) void wv_bf_split_kernel(BfParams p) {
                 if (t == 0 && c == 0)
 #endif
                 {
-                    if (c + 1 < NK) load_x(nxt, xsrc(tile, c + 1));
-                    else if (t + 1 < ntile) load_x(nxt, xsrc(ntl, 0));
+                    if (c + 1 < NK) load_x(xb[(c + 1) & 1], xsrc(tile, c + 1));
+                    else if (t + 1 < ntile) load_x(xb[NK & 1], xsrc(ntl, 0));
                 }
+                if (L2 && c == 0 && t + 1 < ntile) xv = p.xnorm[ntl * BF_BN + wm * 64 + lane];
+                // issue the prefetch before anything of the chunk (the machine
+                // scheduler otherwise sinks it behind the first MFMAs)
+#ifndef WV_BF_NO_SGB
+                __builtin_amdgcn_sched_group_barrier(0x020, 9, 0);
+#endif
 #pragma unroll
                 for (int s2 = 0; s2 < 2; ++s2) {
                     const int qo = c * 256 + s2 * 128;
@@ -516,6 +539,7 @@ __global__ __launch_bounds__(256, 2) void wv_bf_split_kernel(BfParams p) {
                     const bf16x8 bl0 = __builtin_bit_cast(bf16x8, qw[qo + 64]);
                     const bf16x8 bh1 = __builtin_bit_cast(bf16x8, qw[GRP + qo]);
                     const bf16x8 bl1 = __builtin_bit_cast(bf16x8, qw[GRP + qo + 64]);
+                    const uint4* cur = xb[c & 1];
                     const bf16x8 ah0 = __builtin_bit_cast(bf16x8, cur[2 * s2]);
                     const bf16x8 al0 = __builtin_bit_cast(bf16x8, cur[2 * s2 + 1]);
                     const bf16x8 ah1 = __builtin_bit_cast(bf16x8, cur[4 + 2 * s2]);
@@ -524,10 +548,11 @@ __global__ __launch_bounds__(256, 2) void wv_bf_split_kernel(BfParams p) {
                     asm volatile("" ::"v"(ah0), "v"(al0), "v"(ah1), "v"(al1), "v"(bh0), "v"(bl0), "v"(bh1), "v"(bl1));
                     continue;
 #endif
-                    acc00 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al0, bh0, acc00, 0, 0, 0);
-                    acc01 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al0, bh1, acc01, 0, 0, 0);
-                    acc10 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al1, bh0, acc10, 0, 0, 0);
-                    acc11 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al1, bh1, acc11, 0, 0, 0);
+                    const bool first = c == 0 && s2 == 0;
+                    acc00 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al0, bh0, first ? xc0 : acc00, 0, 0, 0);
+                    acc01 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al0, bh1, first ? xc0 : acc01, 0, 0, 0);
+                    acc10 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al1, bh0, first ? xc1 : acc10, 0, 0, 0);
+                    acc11 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al1, bh1, first ? xc1 : acc11, 0, 0, 0);
                     acc00 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah0, bl0, acc00, 0, 0, 0);
                     acc01 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah0, bl1, acc01, 0, 0, 0);
                     acc10 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah1, bl0, acc10, 0, 0, 0);
@@ -537,12 +562,17 @@ __global__ __launch_bounds__(256, 2) void wv_bf_split_kernel(BfParams p) {
                     acc10 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah1, bh0, acc10, 0, 0, 0);
                     acc11 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah1, bh1, acc11, 0, 0, 0);
                 }
-#pragma unroll
-                for (int j = 0; j < 8; ++j) cur[j] = nxt[j];
                 // keep each chunk's LDS reads next to its MFMAs (register pressure)
                 __builtin_amdgcn_sched_barrier(0);
             }
-            if (L2 && t + 1 < ntile) load_xn(ntl);
+            if constexpr (NK & 1) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) xb[0][j] = xb[1][j];
+            }
+            if (L2 && t + 1 < ntile) xnl[lane] = xv;   // this wave's reads of xnl were at the tile start
+            if (t + 1 < ntile) load_words(ntl);
+            uint64_t okw = ~tw & aw;
+            if (row0 + 64 > p.N) okw &= p.N > row0 ? ((1ull << (p.N - row0)) - 1) : 0ull;
 #ifdef WV_BF_ABLATE_NO_EPILOGUE
             asm volatile("" ::"v"(acc00[0]), "v"(acc01[0]), "v"(acc10[0]), "v"(acc11[0]));
             if (acc00[3] == 1234.5f) l0d[0] = acc01[5] + (float)okw;
@@ -616,7 +646,7 @@ __global__ __launch_bounds__(256, 2) void wv_bf_split_kernel(BfParams p) {
 template <int METRIC>
 __device__ void finalize_one(const BfFinParams& p, int q, float* sd, uint32_t* si, float* qv) {
     const int lane = threadIdx.x & 63;
-    const int n_lists = bf_slots_of((uint64_t)(q / BF_BQ), p.ntiles, p.units_per_block) * BF_PROD;
+    const int n_lists = bf_slots_of((uint64_t)(q / p.bq), p.ntiles, p.units_per_block) * BF_PROD;
     const int n_ent = n_lists * BF_KP;
     const float* cd = p.cand_d + (size_t)q * p.n_slots * BF_PROD * BF_KP;
     const uint32_t* ci = p.cand_id + (size_t)q * p.n_slots * BF_PROD * BF_KP;
@@ -986,14 +1016,25 @@ hipError_t wv_launch_bf_mfma(const wv::BfParams* p, hipStream_t s) {
         const int nk = p->ldx / wv::BF_BK;
         if (p->ldx % wv::BF_BK || p->ldq != p->ldx || nk < 1 || nk > 4 || p->rowidx || p->allow_stride)
             return hipErrorInvalidValue;
-        const size_t lds = (size_t)nk * 16384;
         const bool l2 = p->metric == WV_METRIC_L2;
-        switch (nk) {
-            case 1: if (l2) hipLaunchKernelGGL((wv::wv_bf_split_kernel<1, true>), dim3(nb), dim3(256), lds, s, *p); else hipLaunchKernelGGL((wv::wv_bf_split_kernel<1, false>), dim3(nb), dim3(256), lds, s, *p); break;
-            case 2: if (l2) hipLaunchKernelGGL((wv::wv_bf_split_kernel<2, true>), dim3(nb), dim3(256), lds, s, *p); else hipLaunchKernelGGL((wv::wv_bf_split_kernel<2, false>), dim3(nb), dim3(256), lds, s, *p); break;
-            case 3: if (l2) hipLaunchKernelGGL((wv::wv_bf_split_kernel<3, true>), dim3(nb), dim3(256), lds, s, *p); else hipLaunchKernelGGL((wv::wv_bf_split_kernel<3, false>), dim3(nb), dim3(256), lds, s, *p); break;
-            default: if (l2) hipLaunchKernelGGL((wv::wv_bf_split_kernel<4, true>), dim3(nb), dim3(256), lds, s, *p); else hipLaunchKernelGGL((wv::wv_bf_split_kernel<4, false>), dim3(nb), dim3(256), lds, s, *p); break;
+        const bool wide = p->bq == 2 * wv::BF_BQ;
+        if (!wide && p->bq != wv::BF_BQ) return hipErrorInvalidValue;
+        const size_t lds = (size_t)nk * (wide ? 32768 : 16384) + (wide ? 8 : 4) * 256;   // + per-wave norm slots
+#define WV_SPLIT_LAUNCH(NK)                                                                                   \
+        if (wide) {                                                                                           \
+            if (l2) hipLaunchKernelGGL((wv::wv_bf_split_kernel<NK, true, 4>), dim3(nb), dim3(512), lds, s, *p);  \
+            else hipLaunchKernelGGL((wv::wv_bf_split_kernel<NK, false, 4>), dim3(nb), dim3(512), lds, s, *p);    \
+        } else {                                                                                              \
+            if (l2) hipLaunchKernelGGL((wv::wv_bf_split_kernel<NK, true, 2>), dim3(nb), dim3(256), lds, s, *p);  \
+            else hipLaunchKernelGGL((wv::wv_bf_split_kernel<NK, false, 2>), dim3(nb), dim3(256), lds, s, *p);    \
         }
+        switch (nk) {
+            case 1: WV_SPLIT_LAUNCH(1) break;
+            case 2: WV_SPLIT_LAUNCH(2) break;
+            case 3: WV_SPLIT_LAUNCH(3) break;
+            default: WV_SPLIT_LAUNCH(4) break;
+        }
+#undef WV_SPLIT_LAUNCH
         return hipGetLastError();
     }
     const size_t lds = wv::BF_LDS_BYTES;

@@ -31,6 +31,7 @@ struct BfParams {
     float* out_d;           // [nq][n_slots][BF_PROD*BF_KP]
     uint32_t* out_id;
     int split;              // X and Q are split images (split_hi_index): wv_bf_split_kernel
+    int bq;                 // queries per block (BF_BQ; the split kernel also runs 2 * BF_BQ)
     int locality;           // bit 1: XCD-contiguous block ids; bit 2: aligned tile rotation
 };
 
@@ -53,12 +54,13 @@ inline uint64_t split_hi_index(uint64_t row, int k, int nk) {
 // A block's run of units crosses at most a few query blocks; the lists it
 // produces for query block qb go to slot (block - first block of qb).
 struct BfSchedule {
-    int n_blocks, n_slots;
+    int n_blocks, n_slots, bq;
     uint64_t ntiles, units_per_block;
 };
-inline BfSchedule bf_schedule(int nq, uint64_t N, int target_blocks) {
+inline BfSchedule bf_schedule(int nq, uint64_t N, int target_blocks, int bq = BF_BQ) {
     BfSchedule s{};
-    const uint64_t nqb = (uint64_t)(nq + BF_BQ - 1) / BF_BQ;
+    s.bq = bq;
+    const uint64_t nqb = (uint64_t)(nq + bq - 1) / bq;
     s.ntiles = (N + BF_BN - 1) / BF_BN;
     const uint64_t total = nqb * s.ntiles;
     uint64_t nb = target_blocks > 0 ? (uint64_t)target_blocks : 1;
@@ -97,6 +99,7 @@ struct BfFinParams {
     int32_t* fail;          // per query: 1 = uncertified
     float* fail_thr;        // per query: exact d_k of the re-ranked set (upper bound of the true d_k)
     int split;              // approximate keys came from the bf16x3 pass (wider eps)
+    int bq;                 // queries per block of the key pass (BfParams.bq)
 };
 
 // Certificate fallback: exact distances of every row for a batch of failed
