@@ -641,3 +641,45 @@ def test_split_key_pass_equals_fp32_key_pass(metric):
     oi, od, on = O.flat_scan(metric, b, q, 10)
     for i in range(len(qs)):
         _same_tie_aware(ai[i], ad[i], oi[i], od[i])
+
+
+@pytest.mark.parametrize("dim", [32, 96, 128])
+@pytest.mark.parametrize("metric", [O.L2, O.DOT, O.COSINE])
+def test_split_pass_query_blocks_multi_segment(dim, metric):
+    """The split key pass in 256-query blocks (one 512-thread workgroup per CU,
+    default) and in 128-query blocks (WV_BF_BQ=128) over several query blocks
+    (nq = 700: a partial last block), a ragged corpus (last tile partial),
+    tombstones and a shared allow list that keeps over half the rows (masked
+    in the epilogue, not compacted); D = 32 / 96 / 128 = 1 / 3 / 4 k-chunks
+    (odd chunk counts take the ping-pong copy).  Both return the same ids and
+    distances, equal to the restatement's (cosine rows tie at the k boundary
+    on this data: the reference orders ties by heap layout)."""
+    import os
+    n = 20011
+    base, qs = _data(n, dim, 700, seed=41 + dim, metric=metric)
+    rng = np.random.default_rng(42)
+    tomb_ids = np.nonzero(rng.random(n) < 0.03)[0]
+    allow_ids = np.nonzero(rng.random(n) < 0.7)[0]
+    al = W.AllowList.from_ids(allow_ids, n)
+    tb = O.bits_from_ids(tomb_ids, n)
+    b = O.normalize_rows(base) if metric == O.COSINE else base
+    q = O.normalize_rows(qs) if metric == O.COSINE else qs
+    oi, od, on = O.flat_scan(metric, b, q, 10, allow_bits=al.words, tomb_bits=tb)
+    ui, ud, un = O.flat_scan(metric, b, q, 10, tomb_bits=tb)
+    runs = []
+    for bq in (None, "128"):
+        if bq:
+            os.environ["WV_BF_BQ"] = bq
+        try:
+            ix = W.GPUVectorIndex(dim, METRIC_NAMES[metric], capacity=n)
+            ix.upload_vectors(base)
+            ix.set_tombstones(tomb_ids)
+            runs.append((ix.search_batch(qs, 10, allow=al, mode="exact"), ix.search_batch(qs, 10, mode="exact")))
+            ix.close()
+        finally:
+            os.environ.pop("WV_BF_BQ", None)
+    for (ai, ad, an), (bi, bd, bn) in zip(runs[0], runs[1]):
+        _same(ai, ad, bi, bd)
+    for (gi, gd, gn), (ri, rd) in zip(runs[0], ((oi, od), (ui, ud))):
+        for i in range(len(qs)):
+            _same_tie_aware(gi[i], gd[i], ri[i], rd[i])
