@@ -571,7 +571,12 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void wv_bf_split_kernel(BfParams 
             }
             if (L2 && t + 1 < ntile) xnl[lane] = xv;   // this wave's reads of xnl were at the tile start
             if (t + 1 < ntile) load_words(ntl);
-            uint64_t okw = ~tw & aw;
+            // the words are the same on every lane: combine them on the scalar unit
+            auto uni64 = [](uint64_t v) {
+                return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
+                       ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32);
+            };
+            uint64_t okw = ~uni64(tw) & uni64(aw);
             if (row0 + 64 > p.N) okw &= p.N > row0 ? ((1ull << (p.N - row0)) - 1) : 0ull;
 #ifdef WV_BF_ABLATE_NO_EPILOGUE
             asm volatile("" ::"v"(acc00[0]), "v"(acc01[0]), "v"(acc10[0]), "v"(acc11[0]));
@@ -580,12 +585,14 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void wv_bf_split_kernel(BfParams 
 #endif
             // ---- epilogue of one 128x128 tile (as wv_bf_mfma_kernel) ----
             const uint32_t rb0 = (uint32_t)row0 + 4 * khalf;
+            const float INF = __builtin_inff();
+            // scalar fast path: every row eligible and every query column live
+            if (okw != ~0ull || (qb + 1) * 64 * WN > p.nq) {
             const uint64_t o0 = (jq0 < p.nq ? okw : 0ull) >> (4 * khalf);
             const uint64_t o1 = (jq1 < p.nq ? okw : 0ull) >> (4 * khalf);
             const uint32_t o0lo = (uint32_t)o0, o0hi = (uint32_t)(o0 >> 32);
             const uint32_t o1lo = (uint32_t)o1, o1hi = (uint32_t)(o1 >> 32);
             constexpr uint32_t LANE_ROWS = 0x0F0F0F0Fu;
-            const float INF = __builtin_inff();
             if (!__all((o0lo & o0hi & o1lo & o1hi & LANE_ROWS) == LANE_ROWS)) {
 #pragma unroll
                 for (int r = 0; r < 16; ++r) {
@@ -596,6 +603,7 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void wv_bf_split_kernel(BfParams 
                     acc11[r] = (o1hi >> bit) & 1u ? acc11[r] : INF;
                 }
             }
+            }
             float m0 = INF, m1 = INF;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
@@ -604,15 +612,17 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void wv_bf_split_kernel(BfParams 
             }
 #define WV_EXTRACT(M, A0, A1, LD, LI)                                                            \
             while (M <= LD[BF_KP - 1]) {                                                        \
+                uint32_t rb = rb0;  /* opaque: the row ids stay in this rare loop */             \
+                asm volatile("" : "+v"(rb));                                                    \
                 uint32_t idm = WV_NIL;                                                          \
                 _Pragma("unroll") for (int r = 0; r < 16; ++r) {                                \
                     const bool hit = idm == WV_NIL && A0[r] == M;                               \
-                    idm = hit ? rb0 + (r & 3) + 8 * (r >> 2) : idm;                             \
+                    idm = hit ? rb + (r & 3) + 8 * (r >> 2) : idm;                             \
                     A0[r] = hit ? INF : A0[r];                                                  \
                 }                                                                               \
                 _Pragma("unroll") for (int r = 0; r < 16; ++r) {                                \
                     const bool hit = idm == WV_NIL && A1[r] == M;                               \
-                    idm = hit ? rb0 + 32 + (r & 3) + 8 * (r >> 2) : idm;                        \
+                    idm = hit ? rb + 32 + (r & 3) + 8 * (r >> 2) : idm;                        \
                     A1[r] = hit ? INF : A1[r];                                                  \
                 }                                                                               \
                 if (!key_less(M, idm, LD[BF_KP - 1], LI[BF_KP - 1])) break;                     \
