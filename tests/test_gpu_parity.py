@@ -667,9 +667,10 @@ def test_split_pass_query_blocks_multi_segment(dim, metric):
     oi, od, on = O.flat_scan(metric, b, q, 10, allow_bits=al.words, tomb_bits=tb)
     ui, ud, un = O.flat_scan(metric, b, q, 10, tomb_bits=tb)
     runs = []
-    for bq in (None, "128"):
-        if bq:
-            os.environ["WV_BF_BQ"] = bq
+    # default (256-query blocks, two waves per SIMD), 128-query blocks, and the
+    # opt-in one-wave-per-SIMD kernel (4 k-chunks only)
+    for env in ({}, {"WV_BF_BQ": "128"}, {"WV_BF_SPLIT_1W": "1"}):
+        os.environ.update(env)
         try:
             ix = W.GPUVectorIndex(dim, METRIC_NAMES[metric], capacity=n)
             ix.upload_vectors(base)
@@ -677,9 +678,11 @@ def test_split_pass_query_blocks_multi_segment(dim, metric):
             runs.append((ix.search_batch(qs, 10, allow=al, mode="exact"), ix.search_batch(qs, 10, mode="exact")))
             ix.close()
         finally:
-            os.environ.pop("WV_BF_BQ", None)
-    for (ai, ad, an), (bi, bd, bn) in zip(runs[0], runs[1]):
-        _same(ai, ad, bi, bd)
+            for k in env:
+                os.environ.pop(k, None)
+    for other in runs[1:]:
+        for (ai, ad, an), (bi, bd, bn) in zip(runs[0], other):
+            _same(ai, ad, bi, bd)
     for (gi, gd, gn), (ri, rd) in zip(runs[0], ((oi, od), (ui, ud))):
         for i in range(len(qs)):
             _same_tie_aware(gi[i], gd[i], ri[i], rd[i])
