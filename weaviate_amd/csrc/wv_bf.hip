@@ -722,7 +722,7 @@ __global__ __launch_bounds__(256, 1) void wv_bf_split1_kernel(BfParams p) {
             for (int i = 0; i < BF_KP; ++i) { ld[j][i] = FLT_MAX; li[j][i] = WV_NIL; }
         const uint4* __restrict__ qw = qimg + 4 * wn * GRP + lane;   // query groups 4 wn .. 4 wn + 3
         auto xsrc = [&](uint64_t tile, int c) { return X + (tile * 4 + 2 * wm) * GRP + c * 256 + lane; };
-        uint4 xb[4][8];   // ring slot = chunk index
+        uint4 xb[2][8];   // operand ping-pong: slot = chunk & 1
         auto load_x = [&](uint4 (&dst)[8], const uint4* src) {
 #pragma unroll
             for (int h = 0; h < 2; ++h)
@@ -733,8 +733,6 @@ __global__ __launch_bounds__(256, 1) void wv_bf_split1_kernel(BfParams p) {
         const int ntile = (int)(t_end - t_begin);
         if (ntile > 0) {
             load_x(xb[0], xsrc(rt_begin, 0));
-            load_x(xb[1], xsrc(rt_begin, 1));
-            load_x(xb[2], xsrc(rt_begin, 2));
             if (L2) xnl[lane] = p.xnorm[rt_begin * BF_BN + wm * 64 + lane];
         }
         uint64_t tw_next = 0, aw_next = ~0ull;
@@ -744,6 +742,19 @@ __global__ __launch_bounds__(256, 1) void wv_bf_split1_kernel(BfParams p) {
             if (allow) aw_next = w < allow_words ? allow[w] : 0ull;
         };
         if (ntile > 0) load_words(rt_begin);
+        // B operands (queries, from LDS) double-buffered by k-step parity: the
+        // next step's 8 reads are issued before this step's 24 MFMAs; the
+        // step after the tile's last is step 0 again (same query block)
+        bf16x8 bh[2][4], bl[2][4];
+        auto load_b = [&](int buf, int c, int s2) {
+            const int qo = c * 256 + s2 * 128;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                bh[buf][j] = __builtin_bit_cast(bf16x8, qw[j * GRP + qo]);
+                bl[buf][j] = __builtin_bit_cast(bf16x8, qw[j * GRP + qo + 64]);
+            }
+        };
+        load_b(0, 0, 0);
         for (int t = 0; t < ntile; ++t) {
             uint64_t tile = rt_begin + (uint64_t)t;
             if (tile >= p.ntiles) tile -= p.ntiles;
@@ -768,21 +779,17 @@ __global__ __launch_bounds__(256, 1) void wv_bf_split1_kernel(BfParams p) {
             }
 #pragma unroll
             for (int c = 0; c < NK; ++c) {
-                // ring: chunk 3 of this tile, or chunk c - 1 of the next, three chunks ahead
-                if (c == 0) load_x(xb[3], xsrc(tile, 3));
-                else if (t + 1 < ntile) load_x(xb[c - 1], xsrc(ntl, c - 1));
+                if (c + 1 < NK) load_x(xb[(c + 1) & 1], xsrc(tile, c + 1));
+                else if (t + 1 < ntile) load_x(xb[0], xsrc(ntl, 0));
                 if (L2 && c == 0 && t + 1 < ntile) xv = p.xnorm[ntl * BF_BN + wm * 64 + lane];
                 __builtin_amdgcn_sched_group_barrier(0x020, 9, 0);
-                const uint4* cur = xb[c];
+                const uint4* cur = xb[c & 1];
 #pragma unroll
                 for (int s2 = 0; s2 < 2; ++s2) {
-                    const int qo = c * 256 + s2 * 128;
-                    bf16x8 bh[4], bl[4];
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        bh[j] = __builtin_bit_cast(bf16x8, qw[j * GRP + qo]);
-                        bl[j] = __builtin_bit_cast(bf16x8, qw[j * GRP + qo + 64]);
-                    }
+                    if (s2 == 0) load_b(1, c, 1);
+                    else load_b(0, (c + 1) % NK, 0);
+                    const bf16x8* bhc = bh[s2];
+                    const bf16x8* blc = bl[s2];
                     const bf16x8 ah0 = __builtin_bit_cast(bf16x8, cur[2 * s2]);
                     const bf16x8 al0 = __builtin_bit_cast(bf16x8, cur[2 * s2 + 1]);
                     const bf16x8 ah1 = __builtin_bit_cast(bf16x8, cur[4 + 2 * s2]);
@@ -790,18 +797,18 @@ __global__ __launch_bounds__(256, 1) void wv_bf_split1_kernel(BfParams p) {
                     const bool first = c == 0 && s2 == 0;
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
-                        acc[0][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al0, bh[j], first ? xc0 : acc[0][j], 0, 0, 0);
-                        acc[1][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al1, bh[j], first ? xc1 : acc[1][j], 0, 0, 0);
+                        acc[0][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al0, bhc[j], first ? xc0 : acc[0][j], 0, 0, 0);
+                        acc[1][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al1, bhc[j], first ? xc1 : acc[1][j], 0, 0, 0);
                     }
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
-                        acc[0][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah0, bl[j], acc[0][j], 0, 0, 0);
-                        acc[1][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah1, bl[j], acc[1][j], 0, 0, 0);
+                        acc[0][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah0, blc[j], acc[0][j], 0, 0, 0);
+                        acc[1][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah1, blc[j], acc[1][j], 0, 0, 0);
                     }
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
-                        acc[0][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah0, bh[j], acc[0][j], 0, 0, 0);
-                        acc[1][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah1, bh[j], acc[1][j], 0, 0, 0);
+                        acc[0][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah0, bhc[j], acc[0][j], 0, 0, 0);
+                        acc[1][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah1, bhc[j], acc[1][j], 0, 0, 0);
                     }
                 }
                 __builtin_amdgcn_sched_barrier(0);
