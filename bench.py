@@ -305,7 +305,8 @@ def main():
         "config": {
             "workload": ("exact brute-force %d-NN, %s x %d-d %s, %d-query batch%s"
                          % (K, f"{N:,}", D, args.metric, NQ,
-                            " (BASELINE configs[1])" if args.allow_frac <= 0 else
+                            (" (BASELINE configs[1])" if (N, D, args.metric) == (1_000_000, 128, "l2-squared")
+                             else "") if args.allow_frac <= 0 else
                             f", shared allow list p={args.allow_frac} ({n_allowed:,} rows on rank 0)"))
                         if mode == "exact" else
                         ("hnsw layer-0 beam search ef=%d, %s x %d-d %s, %d-query batch" % (args.ef, f"{N:,}", D,
