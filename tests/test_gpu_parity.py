@@ -647,7 +647,7 @@ def test_split_key_pass_equals_fp32_key_pass(metric):
 @pytest.mark.parametrize("metric", [O.L2, O.DOT, O.COSINE])
 def test_split_pass_query_blocks_multi_segment(dim, metric):
     """The split key pass in 256-query blocks (one 512-thread workgroup per CU,
-    default) and in 128-query blocks (WV_BF_BQ=128) over several query blocks
+    default), 128- and 192-query blocks (WV_BF_BQ) over several query blocks
     (nq = 700: a partial last block), a ragged corpus (last tile partial),
     tombstones and a shared allow list that keeps over half the rows (masked
     in the epilogue, not compacted); D = 32 / 96 / 128 = 1 / 3 / 4 k-chunks
@@ -667,9 +667,10 @@ def test_split_pass_query_blocks_multi_segment(dim, metric):
     oi, od, on = O.flat_scan(metric, b, q, 10, allow_bits=al.words, tomb_bits=tb)
     ui, ud, un = O.flat_scan(metric, b, q, 10, tomb_bits=tb)
     runs = []
-    # default (256-query blocks, two waves per SIMD), 128-query blocks, and the
-    # opt-in one-wave-per-SIMD kernel (4 k-chunks only)
-    for env in ({}, {"WV_BF_BQ": "128"}, {"WV_BF_SPLIT_1W": "1"}):
+    # default (256-query blocks, two waves per SIMD), 128-query blocks, the
+    # three-waves-per-SIMD kernel (192-query blocks) and the one-wave-per-SIMD
+    # kernel (4 k-chunks only)
+    for env in ({}, {"WV_BF_BQ": "128"}, {"WV_BF_BQ": "192"}, {"WV_BF_SPLIT_1W": "1"}):
         os.environ.update(env)
         try:
             ix = W.GPUVectorIndex(dim, METRIC_NAMES[metric], capacity=n)

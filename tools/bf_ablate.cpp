@@ -16,7 +16,8 @@ int main(int argc, char** argv) {
     for (uint64_t i = 0; i < N; ++i) { float s = 0; for (int k = 0; k < D; ++k) s += hx[i * D + k] * hx[i * D + k]; hn[i] = s; }
     float *X, *Q, *xn, *od; uint32_t* oi;
     const bool split = getenv("SPLIT") && atoi(getenv("SPLIT"));
-    const int bq = split ? (getenv("BQ") ? atoi(getenv("BQ")) : 256) : 128;
+    const int bq = split ? (getenv("BQ") ? atoi(getenv("BQ")) : 192) : 128;
+    const int prod = bq == 192 ? 8 : 4;
     const uint64_t Np = (N + 127) / 128 * 128; const size_t nqp = (nq + bq - 1) / bq * bq;
     hipMalloc(&X, Np * D * 4); hipMalloc(&Q, nqp * D * 4); hipMalloc(&xn, Np * 4);
     hipMemset(X, 0, Np * D * 4); hipMemset(Q, 0, nqp * D * 4); hipMemset(xn, 0, Np * 4);
@@ -43,13 +44,13 @@ int main(int argc, char** argv) {
     hipMemcpy(xn, hn.data(), N * 4, hipMemcpyHostToDevice);
     wv::BfParams p{};
     const int nqb = (nq + bq - 1) / bq;
-    const int target = getenv("BLOCKS") ? atoi(getenv("BLOCKS")) : 512 * 128 / bq;
+    const int target = getenv("BLOCKS") ? atoi(getenv("BLOCKS")) : (bq == 128 ? 512 : 256);
     const wv::BfSchedule sch = wv::bf_schedule(nq, N, target, bq);
     const int ns = sch.n_slots;
-    hipMalloc(&od, (size_t)nq * ns * 4 * wv::BF_KP * 4); hipMalloc(&oi, (size_t)nq * ns * 4 * wv::BF_KP * 4);
+    hipMalloc(&od, (size_t)nq * ns * prod * wv::BF_KP * 4); hipMalloc(&oi, (size_t)nq * ns * prod * wv::BF_KP * 4);
     p.X = X; p.Q = Q; p.xnorm = xn; p.N = N; p.nq = nq; p.D = D; p.ldx = D; p.ldq = D; p.metric = 0;
     p.n_qblocks = nqb; p.n_slots = ns; p.ntiles = sch.ntiles; p.units_per_block = sch.units_per_block; p.out_d = od; p.out_id = oi;
-    p.split = split; p.bq = bq; p.locality = getenv("LOC") ? atoi(getenv("LOC")) : 3;
+    p.split = split; p.bq = bq; p.prod = prod; p.locality = getenv("LOC") ? atoi(getenv("LOC")) : 3;
     hipEvent_t a, b; hipEventCreate(&a); hipEventCreate(&b);
     wv_launch_bf_mfma(&p, 0); hipDeviceSynchronize();
     float best = 1e9;

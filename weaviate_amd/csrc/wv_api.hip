@@ -454,18 +454,22 @@ int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
             }
         }
         // bf16x3 key pass on native images (whole-corpus or shared allow list
-        // scans); it runs 256-query blocks, one 512-thread workgroup per CU,
-        // unless WV_BF_BQ=128 (the two-workgroup 128-query variant)
+        // scans): 256-query blocks, one 512-thread workgroup per CU, two waves
+        // per SIMD (wv_bf_split_kernel, the fastest measured); WV_BF_BQ=128
+        // runs 128-query blocks (two 256-thread workgroups per CU) and
+        // WV_BF_BQ=192 the three-waves-per-SIMD kernel (wv_bf_split3_kernel)
         const bool split = ix->use_split && !d_rowidx && !allow_stride;
         int bq = wv::BF_BQ;
         if (split) {
             const char* e = std::getenv("WV_BF_BQ");
-            bq = e && std::atoi(e) == wv::BF_BQ ? wv::BF_BQ : 2 * wv::BF_BQ;
+            const int v = e ? std::atoi(e) : 0;
+            bq = v == wv::BF_BQ ? wv::BF_BQ : v == wv::BF_BQ3 ? wv::BF_BQ3 : 2 * wv::BF_BQ;
         }
+        const int prod = bq == wv::BF_BQ3 ? wv::BF_PROD3 : wv::BF_PROD;
         const int n_qblocks = (nq + bq - 1) / bq;
         const wv::BfSchedule sch =
             wv::bf_schedule(nq, n_scan, bq == wv::BF_BQ ? ix->bf_blocks : ix->bf_blocks / 2, bq);
-        const size_t n_lists = (size_t)sch.n_slots * wv::BF_PROD;
+        const size_t n_lists = (size_t)sch.n_slots * prod;
         HIP_TRY(ix->cand_d.ensure((size_t)nq * n_lists * wv::BF_KP * 4));
         HIP_TRY(ix->cand_id.ensure((size_t)nq * n_lists * wv::BF_KP * 4));
         HIP_TRY(ix->q_nrm2.ensure((size_t)nq * 4));
@@ -488,6 +492,7 @@ int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
         wv::BfParams bp{};
         bp.split = split ? 1 : 0;
         bp.bq = bq;
+        bp.prod = prod;
         {
             const char* e = std::getenv("WV_BF_LOCALITY");   // ablation: 0..3, default 3
             bp.locality = e ? std::atoi(e) : 3;
@@ -548,6 +553,7 @@ int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
         fp.fail_thr = ix->fail_thr.as<float>();
         fp.split = bp.split;
         fp.bq = bq;
+        fp.prod = prod;
         if (ix->timing) HIP_TRY(hipEventRecord(ix->ev[2], s));
         HIP_TRY(wv_launch_bf_finalize(&fp, s));
         if (ix->timing) HIP_TRY(hipEventRecord(ix->ev[3], s));

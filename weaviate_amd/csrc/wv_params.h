@@ -10,6 +10,8 @@ constexpr int BF_BK = 32;    // k-chunk staged through LDS
 constexpr int BF_LDT = 36;   // LDS row: 32 k + 4 pad floats (odd 16-byte stride: conflict-free b128)
 constexpr int BF_KP = 8;     // candidates kept per producer lane (register list)
 constexpr int BF_PROD = 4;   // producers per query: 2 base-row waves x 2 lane halves
+constexpr int BF_PROD3 = 8;  // wv_bf_split3_kernel: 4 base-row waves x 2 lane halves
+constexpr int BF_BQ3 = 192;  // wv_bf_split3_kernel: queries per block (3 query waves x 64)
 constexpr int FIN_KF = 32;   // candidates re-ranked exactly per query
 constexpr int BF_FAST_KMAX = 32;   // k served by the MFMA + finalize pipeline
 constexpr int HNSW_EF_MAX = 512;   // largest ef the LDS beam holds
@@ -31,7 +33,8 @@ struct BfParams {
     float* out_d;           // [nq][n_slots][BF_PROD*BF_KP]
     uint32_t* out_id;
     int split;              // X and Q are split images (split_hi_index): wv_bf_split_kernel
-    int bq;                 // queries per block (BF_BQ; the split kernel also runs 2 * BF_BQ)
+    int bq;                 // queries per block (BF_BQ; the split kernels also run 2 * BF_BQ and BF_BQ3)
+    int prod;               // producers (lists) per query per slot: BF_PROD, or BF_PROD3 at bq = BF_BQ3
     int locality;           // bit 1: XCD-contiguous block ids; bit 2: aligned tile rotation
 };
 
@@ -100,6 +103,7 @@ struct BfFinParams {
     float* fail_thr;        // per query: exact d_k of the re-ranked set (upper bound of the true d_k)
     int split;              // approximate keys came from the bf16x3 pass (wider eps)
     int bq;                 // queries per block of the key pass (BfParams.bq)
+    int prod;               // producers per query per slot (BfParams.prod)
 };
 
 // Certificate fallback: exact distances of every row for a batch of failed
