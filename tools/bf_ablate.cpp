@@ -5,6 +5,9 @@
 #include <vector>
 #include <cstring>
 #include "../weaviate_amd/csrc/wv_params.h"
+#ifdef WV_BF_DBG_ITERS
+extern "C" void wv_dbg_read(unsigned long long*);
+#endif
 extern "C" hipError_t wv_launch_bf_mfma(const wv::BfParams* p, hipStream_t s);
 int main(int argc, char** argv) {
     const uint64_t N = argc > 1 ? atoll(argv[1]) : 1000000;
@@ -60,5 +63,9 @@ int main(int argc, char** argv) {
     }
     printf("%s blocks=%d N=%llu nq=%d: %.3f ms  %.1f TF/s  (%.1f%% of 157.3) split=%d\n", argc > 3 ? argv[3] : "variant", sch.n_blocks,
            (unsigned long long)N, nq, best, 2.0 * D * N * nq / best / 1e9, 100 * 2.0 * D * N * nq / best / 1e9 / 157.3, (int)split);
+#ifdef WV_BF_DBG_ITERS
+    unsigned long long c[2]; wv_dbg_read(c);
+    printf("  wave-tiles %llu, extract iterations %llu (%.3f per wave-tile)\n", c[0], c[1], (double)c[1] / c[0]);
+#endif
     return 0;
 }

@@ -33,6 +33,15 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 // ---------------------------------------------------------------------------
 // v_min3_f32 without the IEEE canonicalisation hipcc wraps around fminf of
 // MFMA results (a NaN key never wins a comparison either way)
+#ifdef WV_BF_DBG_ITERS
+// ablation builds only: wave-level counts of tiles (0) and extract-loop iterations (1)
+__device__ unsigned long long wv_dbg_counts[2];
+#define WV_DBG_COUNT(i) if (__lane_id() == 0) atomicAdd(&wv_dbg_counts[i], 1ull);
+extern "C" void wv_dbg_read(unsigned long long* out) { hipMemcpyFromSymbol(out, HIP_SYMBOL(wv_dbg_counts), 16); }
+#else
+#define WV_DBG_COUNT(i)
+#endif
+
 __device__ __forceinline__ float min3_raw(float a, float b, float c) {
     float r;
     asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
@@ -374,6 +383,52 @@ __global__ __launch_bounds__(256, WV_BF_WAVES_PER_SIMD) void wv_bf_mfma_kernel(B
     }   // segments
 }
 
+// Split pass candidate extraction (rare: a lane runs it only when its tile
+// minimum M beats its list tail; the wave runs it while any lane does, so it
+// is kept branch-free).  A0 / A1 hold this lane's 32 keys of one query column
+// (row offsets (r & 3) + 8 (r >> 2) and 32 + the same); each round takes the
+// minimum, masks it to +inf and inserts it.  Insertion compares keys only:
+// a key equal to the tail is dropped, which the finalize's certificate (all
+// dropped keys >= the smallest tail) still covers, and the reported ids and
+// distances come from the exact re-rank.  PT is the lane-pair partner's tail
+// (a valid rejection threshold, see the caller).
+__device__ __forceinline__ void split_extract(float& M, floatx16& A0, floatx16& A1, float (&ld)[BF_KP],
+                                              uint32_t (&li)[BF_KP], float pt, uint32_t rb0) {
+    const float INF = __builtin_inff();
+    while (M <= fminf(ld[BF_KP - 1], pt)) {
+        WV_DBG_COUNT(1)
+        // position of M: a descending scan, so among equal keys the lowest row wins
+        uint32_t sel = 0;
+#pragma unroll
+        for (int r = 15; r >= 0; --r) sel = A1[r] == M ? 16u + r : sel;
+#pragma unroll
+        for (int r = 15; r >= 0; --r) sel = A0[r] == M ? (uint32_t)r : sel;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            A0[r] = sel == (uint32_t)r ? INF : A0[r];
+            A1[r] = sel == 16u + r ? INF : A1[r];
+        }
+        uint32_t rb = rb0;   // opaque: the row ids stay in this rare loop
+        asm volatile("" : "+v"(rb));
+        if (!(M < ld[BF_KP - 1])) break;
+        uint32_t id = rb + (sel & 3u) + 8u * ((sel >> 2) & 3u) + 32u * (sel >> 4);
+        float d = M;
+#pragma unroll
+        for (int i = 0; i < BF_KP; ++i) {
+            const bool lt = d < ld[i];
+            const float td = ld[i];
+            const uint32_t ti = li[i];
+            ld[i] = lt ? d : td;
+            li[i] = lt ? id : ti;
+            d = lt ? td : d;
+            id = lt ? ti : id;
+        }
+        M = INF;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) M = min3_raw(M, A0[r], A1[r]);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Split key pass: bf16x3 on MFMA-native operand images (wv_split_rows_kernel).
 //
@@ -502,6 +557,16 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void wv_bf_split_kernel(BfParams 
             if (ntl >= p.ntiles) ntl -= p.ntiles;
             const uint64_t row0 = tile * BF_BN + wm * 64;
             const uint64_t tw = tw_next, aw = aw_next;
+#ifndef WV_BF_NO_SHARED_TAIL
+            // lanes l and l ^ 32 keep lists for the same query column: either
+            // tail is a valid rejection threshold for both (tails only
+            // decrease, so the partner's value from the tile start is still
+            // >= its final tail, which the finalize's bound is taken over)
+            const float pt0 = __shfl_xor(l0d[BF_KP - 1], 32, 64);
+            const float pt1 = __shfl_xor(l1d[BF_KP - 1], 32, 64);
+#else
+            const float pt0 = FLT_MAX, pt1 = FLT_MAX;
+#endif
 
             floatx16 acc00, acc01, acc10, acc11;
             floatx16 xc0, xc1;
@@ -585,6 +650,7 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void wv_bf_split_kernel(BfParams 
 #endif
             // ---- epilogue of one 128x128 tile (as wv_bf_mfma_kernel) ----
             const uint32_t rb0 = (uint32_t)row0 + 4 * khalf;
+            WV_DBG_COUNT(0)
             const float INF = __builtin_inff();
             // scalar fast path: every row eligible and every query column live
             if (okw != ~0ull || (qb + 1) * 64 * WN > p.nq) {
@@ -610,29 +676,12 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void wv_bf_split_kernel(BfParams 
                 m0 = min3_raw(m0, acc00[r], acc10[r]);
                 m1 = min3_raw(m1, acc01[r], acc11[r]);
             }
-#define WV_EXTRACT(M, A0, A1, LD, LI)                                                            \
-            while (M <= LD[BF_KP - 1]) {                                                        \
-                uint32_t rb = rb0;  /* opaque: the row ids stay in this rare loop */             \
-                asm volatile("" : "+v"(rb));                                                    \
-                uint32_t idm = WV_NIL;                                                          \
-                _Pragma("unroll") for (int r = 0; r < 16; ++r) {                                \
-                    const bool hit = idm == WV_NIL && A0[r] == M;                               \
-                    idm = hit ? rb + (r & 3) + 8 * (r >> 2) : idm;                             \
-                    A0[r] = hit ? INF : A0[r];                                                  \
-                }                                                                               \
-                _Pragma("unroll") for (int r = 0; r < 16; ++r) {                                \
-                    const bool hit = idm == WV_NIL && A1[r] == M;                               \
-                    idm = hit ? rb + 32 + (r & 3) + 8 * (r >> 2) : idm;                        \
-                    A1[r] = hit ? INF : A1[r];                                                  \
-                }                                                                               \
-                if (!key_less(M, idm, LD[BF_KP - 1], LI[BF_KP - 1])) break;                     \
-                list_insert(LD, LI, M, idm);                                                    \
-                M = INF;                                                                        \
-                _Pragma("unroll") for (int r = 0; r < 16; ++r) M = min3_raw(M, A0[r], A1[r]);   \
-            }
-            WV_EXTRACT(m0, acc00, acc10, l0d, l0i)
-            WV_EXTRACT(m1, acc01, acc11, l1d, l1i)
-#undef WV_EXTRACT
+#ifdef WV_BF_ABLATE_NO_EXTRACT
+            if (m0 == 1234.5f) l0d[0] = m1;
+            continue;
+#endif
+            split_extract(m0, acc00, acc10, l0d, l0i, pt0, rb0);
+            split_extract(m1, acc01, acc11, l1d, l1i, pt1, rb0);
         }
 
         const int prod = wm * 2 + khalf;
