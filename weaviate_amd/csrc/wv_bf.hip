@@ -30,6 +30,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 
 
+
 // ---------------------------------------------------------------------------
 // v_min3_f32 without the IEEE canonicalisation hipcc wraps around fminf of
 // MFMA results (a NaN key never wins a comparison either way)
@@ -46,6 +47,54 @@ __device__ __forceinline__ float min3_raw(float a, float b, float c) {
     float r;
     asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
     return r;
+}
+
+// Split pass candidate extraction (rare: a lane runs it only when its tile
+// minimum M beats its list tail; the wave runs it while any lane does, so it
+// is kept branch-free).  A0 / A1 hold this lane's 32 keys of one query column
+// (row offsets (r & 3) + 8 (r >> 2) and 32 + the same); each round takes the
+// minimum, masks it to +inf and inserts it.  Insertion compares keys only:
+// a key equal to the tail is dropped, which the finalize's certificate (all
+// dropped keys >= the smallest tail) still covers, and the reported ids and
+// distances come from the exact re-rank.  PT is the lane-pair partner's tail
+// (a valid rejection threshold, see the caller).
+__device__ __forceinline__ void split_extract(float& M, floatx16& A0, floatx16& A1, float (&ld)[BF_KP],
+                                              uint32_t (&li)[BF_KP], float pt, uint32_t rb0,
+                                              const uint32_t* __restrict__ rowidx = nullptr) {
+    const float INF = __builtin_inff();
+    while (M <= fminf(ld[BF_KP - 1], pt)) {
+        WV_DBG_COUNT(1)
+        // position of M: a descending scan, so among equal keys the lowest row wins
+        uint32_t sel = 0;
+#pragma unroll
+        for (int r = 15; r >= 0; --r) sel = A1[r] == M ? 16u + r : sel;
+#pragma unroll
+        for (int r = 15; r >= 0; --r) sel = A0[r] == M ? (uint32_t)r : sel;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            A0[r] = sel == (uint32_t)r ? INF : A0[r];
+            A1[r] = sel == 16u + r ? INF : A1[r];
+        }
+        uint32_t rb = rb0;   // opaque: the row ids stay in this rare loop
+        asm volatile("" : "+v"(rb));
+        if (!(M < ld[BF_KP - 1])) break;
+        uint32_t id = rb + (sel & 3u) + 8u * ((sel >> 2) & 3u) + 32u * (sel >> 4);
+        if (rowidx) id = rowidx[id];   // corpus id; the map is increasing
+        float d = M;
+#pragma unroll
+        for (int i = 0; i < BF_KP; ++i) {
+            const bool lt = d < ld[i];
+            const float td = ld[i];
+            const uint32_t ti = li[i];
+            ld[i] = lt ? d : td;
+            li[i] = lt ? id : ti;
+            d = lt ? td : d;
+            id = lt ? ti : id;
+        }
+        M = INF;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) M = min3_raw(M, A0[r], A1[r]);
+    }
 }
 
 __device__ __forceinline__ void list_insert(float (&ld)[BF_KP], uint32_t (&li)[BF_KP], float d, uint32_t id) {
@@ -228,6 +277,9 @@ __global__ __launch_bounds__(256, WV_BF_WAVES_PER_SIMD) void wv_bf_mfma_kernel(B
             }
             // C-in of the tile = |x|^2 of the row (L2) or 0: with B = -2q (L2) or
             // -q (dot, cosine) the accumulator ends as the approximate key
+            // lane-pair shared tail (as wv_bf_split_kernel): read at the tile start
+            const float pt0 = __shfl_xor(l0d[BF_KP - 1], 32, 64);
+            const float pt1 = __shfl_xor(l1d[BF_KP - 1], 32, 64);
             floatx16 acc00, acc01, acc10, acc11;
             {
                 const float* xn = xnb + (t & 1) * BF_BN + wm * 64;
@@ -343,28 +395,8 @@ __global__ __launch_bounds__(256, WV_BF_WAVES_PER_SIMD) void wv_bf_mfma_kernel(B
             // pass 2 (rare after the first tiles): extract the minimum while it
             // beats the list tail; rows are scanned in ascending id, so among
             // equal keys the smallest id is taken first
-#define WV_EXTRACT(M, A0, A1, LD, LI)                                                            \
-            while (M <= LD[BF_KP - 1]) {                                                        \
-                uint32_t idm = WV_NIL;                                                          \
-                _Pragma("unroll") for (int r = 0; r < 16; ++r) {                                \
-                    const bool hit = idm == WV_NIL && A0[r] == M;                               \
-                    idm = hit ? rb0 + (r & 3) + 8 * (r >> 2) : idm;                             \
-                    A0[r] = hit ? INF : A0[r];                                                  \
-                }                                                                               \
-                _Pragma("unroll") for (int r = 0; r < 16; ++r) {                                \
-                    const bool hit = idm == WV_NIL && A1[r] == M;                               \
-                    idm = hit ? rb0 + 32 + (r & 3) + 8 * (r >> 2) : idm;                        \
-                    A1[r] = hit ? INF : A1[r];                                                  \
-                }                                                                               \
-                if (rowidx) idm = rowidx[idm];   /* corpus id; the map is increasing */      \
-                if (!key_less(M, idm, LD[BF_KP - 1], LI[BF_KP - 1])) break;                     \
-                list_insert(LD, LI, M, idm);                                                    \
-                M = INF;                                                                        \
-                _Pragma("unroll") for (int r = 0; r < 16; ++r) M = min3_raw(M, A0[r], A1[r]);   \
-            }
-            WV_EXTRACT(m0, acc00, acc10, l0d, l0i)
-            WV_EXTRACT(m1, acc01, acc11, l1d, l1i)
-#undef WV_EXTRACT
+            split_extract(m0, acc00, acc10, l0d, l0i, pt0, rb0, rowidx);
+            split_extract(m1, acc01, acc11, l1d, l1i, pt1, rb0, rowidx);
         }
 
         // write this lane's two lists: out[q][slot][producer][KP]
@@ -381,52 +413,6 @@ __global__ __launch_bounds__(256, WV_BF_WAVES_PER_SIMD) void wv_bf_mfma_kernel(B
             for (int i = 0; i < BF_KP; ++i) { p.out_d[base + i] = l1d[i]; p.out_id[base + i] = l1i[i]; }
         }
     }   // segments
-}
-
-// Split pass candidate extraction (rare: a lane runs it only when its tile
-// minimum M beats its list tail; the wave runs it while any lane does, so it
-// is kept branch-free).  A0 / A1 hold this lane's 32 keys of one query column
-// (row offsets (r & 3) + 8 (r >> 2) and 32 + the same); each round takes the
-// minimum, masks it to +inf and inserts it.  Insertion compares keys only:
-// a key equal to the tail is dropped, which the finalize's certificate (all
-// dropped keys >= the smallest tail) still covers, and the reported ids and
-// distances come from the exact re-rank.  PT is the lane-pair partner's tail
-// (a valid rejection threshold, see the caller).
-__device__ __forceinline__ void split_extract(float& M, floatx16& A0, floatx16& A1, float (&ld)[BF_KP],
-                                              uint32_t (&li)[BF_KP], float pt, uint32_t rb0) {
-    const float INF = __builtin_inff();
-    while (M <= fminf(ld[BF_KP - 1], pt)) {
-        WV_DBG_COUNT(1)
-        // position of M: a descending scan, so among equal keys the lowest row wins
-        uint32_t sel = 0;
-#pragma unroll
-        for (int r = 15; r >= 0; --r) sel = A1[r] == M ? 16u + r : sel;
-#pragma unroll
-        for (int r = 15; r >= 0; --r) sel = A0[r] == M ? (uint32_t)r : sel;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            A0[r] = sel == (uint32_t)r ? INF : A0[r];
-            A1[r] = sel == 16u + r ? INF : A1[r];
-        }
-        uint32_t rb = rb0;   // opaque: the row ids stay in this rare loop
-        asm volatile("" : "+v"(rb));
-        if (!(M < ld[BF_KP - 1])) break;
-        uint32_t id = rb + (sel & 3u) + 8u * ((sel >> 2) & 3u) + 32u * (sel >> 4);
-        float d = M;
-#pragma unroll
-        for (int i = 0; i < BF_KP; ++i) {
-            const bool lt = d < ld[i];
-            const float td = ld[i];
-            const uint32_t ti = li[i];
-            ld[i] = lt ? d : td;
-            li[i] = lt ? id : ti;
-            d = lt ? td : d;
-            id = lt ? ti : id;
-        }
-        M = INF;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) M = min3_raw(M, A0[r], A1[r]);
-    }
 }
 
 // ---------------------------------------------------------------------------
