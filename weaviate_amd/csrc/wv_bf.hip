@@ -542,7 +542,6 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void wv_bf_split_kernel(BfParams 
             uint64_t ntl = tile + 1;
             if (ntl >= p.ntiles) ntl -= p.ntiles;
             const uint64_t row0 = tile * BF_BN + wm * 64;
-            const uint64_t tw = tw_next, aw = aw_next;
 #ifndef WV_BF_NO_SHARED_TAIL
             // lanes l and l ^ 32 keep lists for the same query column: either
             // tail is a valid rejection threshold for both (tails only
@@ -574,10 +573,15 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void wv_bf_split_kernel(BfParams 
                 if (t == 0 && c == 0)
 #endif
                 {
+                    // unconditional (the last tile prefetches the wrapped next
+                    // tile, in bounds and unused): a load issued on one path
+                    // only makes the waitcnt pass merge counter states
+                    // pessimistically, and the last chunk's MFMAs then wait
+                    // for the next tile's operands (vmcnt(0) mid-chunk)
                     if (c + 1 < NK) load_x(xb[(c + 1) & 1], xsrc(tile, c + 1));
-                    else if (t + 1 < ntile) load_x(xb[NK & 1], xsrc(ntl, 0));
+                    else load_x(xb[NK & 1], xsrc(ntl, 0));
                 }
-                if (L2 && c == 0 && t + 1 < ntile) xv = p.xnorm[ntl * BF_BN + wm * 64 + lane];
+                if (L2 && c == 0) xv = p.xnorm[ntl * BF_BN + wm * 64 + lane];
                 // issue the prefetch before anything of the chunk (the machine
                 // scheduler otherwise sinks it behind the first MFMAs)
 #ifndef WV_BF_NO_SGB
@@ -620,14 +624,17 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void wv_bf_split_kernel(BfParams 
 #pragma unroll
                 for (int j = 0; j < 8; ++j) xb[0][j] = xb[1][j];
             }
-            if (L2 && t + 1 < ntile) xnl[lane] = xv;   // this wave's reads of xnl were at the tile start
-            if (t + 1 < ntile) load_words(ntl);
+            if (L2) xnl[lane] = xv;   // this wave's reads of xnl were at the tile start
             // the words are the same on every lane: combine them on the scalar unit
             auto uni64 = [](uint64_t v) {
                 return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
                        ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32);
             };
-            uint64_t okw = ~uni64(tw) & uni64(aw);
+            // consume this tile's words before the next tile's load reuses their
+            // registers: no loop-carried copy, so the back edge carries no
+            // vmcnt(0) (which would wait for the corpus prefetch of the next tile)
+            uint64_t okw = ~uni64(tw_next) & uni64(aw_next);
+            load_words(ntl);
             if (row0 + 64 > p.N) okw &= p.N > row0 ? ((1ull << (p.N - row0)) - 1) : 0ull;
 #ifdef WV_BF_ABLATE_NO_EPILOGUE
             asm volatile("" ::"v"(acc00[0]), "v"(acc01[0]), "v"(acc10[0]), "v"(acc11[0]));
