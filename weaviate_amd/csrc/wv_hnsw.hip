@@ -386,6 +386,10 @@ __device__ __forceinline__ void knn_one(const HnswParams& p, WaveState& w, int q
     }
 }
 
+// One instantiation per (metric, raw / PQ): each gets its own register
+// allocation (one kernel holding all six inlined searches spilled 431 SGPRs
+// into VGPR lanes); the host launches the matching one.
+template <int METRIC, bool PQ>
 __global__ __launch_bounds__(256) void wv_hnsw_kernel(HnswParams p) {
     extern __shared__ float lds[];
     const int wave = threadIdx.x >> 6;
@@ -404,17 +408,7 @@ __global__ __launch_bounds__(256) void wv_hnsw_kernel(HnswParams p) {
     w.vc = reinterpret_cast<uint32_t*>(cur); cur += (1 << p.vc_log2);
     w.xs = reinterpret_cast<uint32_t*>(cur); cur += (1 << p.xs_log2);
     w.ltomb = reinterpret_cast<uint32_t*>(cur); cur += MAX_LOCAL_TOMB;
-    // a compressed index (PQ codes) is its own instantiation: the raw-vector
-    // kernel keeps its registers and schedule
-    if (p.pq.codes) {
-        if (p.metric == WV_METRIC_L2) knn_one<WV_METRIC_L2, true>(p, w, q);
-        else if (p.metric == WV_METRIC_DOT) knn_one<WV_METRIC_DOT, true>(p, w, q);
-        else knn_one<WV_METRIC_COSINE, true>(p, w, q);
-    } else {
-        if (p.metric == WV_METRIC_L2) knn_one<WV_METRIC_L2, false>(p, w, q);
-        else if (p.metric == WV_METRIC_DOT) knn_one<WV_METRIC_DOT, false>(p, w, q);
-        else knn_one<WV_METRIC_COSINE, false>(p, w, q);
-    }
+    knn_one<METRIC, PQ>(p, w, q);
 }
 
 // ===========================================================================
@@ -688,7 +682,20 @@ hipError_t wv_launch_hnsw(const wv::HnswParams* p, int waves_per_block, hipStrea
     const size_t lds = (size_t)waves_per_block * p->per_wave_words * sizeof(float);
     const unsigned blocks = (unsigned)((p->nq + waves_per_block - 1) / waves_per_block);
     if (blocks == 0) return hipSuccess;
-    hipLaunchKernelGGL(wv::wv_hnsw_kernel, dim3(blocks), dim3(64 * waves_per_block), lds, s, *p);
+#define WV_HNSW_LAUNCH(M, PQ) \
+    hipLaunchKernelGGL((wv::wv_hnsw_kernel<M, PQ>), dim3(blocks), dim3(64 * waves_per_block), lds, s, *p)
+    // a compressed index (PQ codes) is its own instantiation: the raw-vector
+    // kernel keeps its registers and schedule
+    if (p->pq.codes) {
+        if (p->metric == WV_METRIC_L2) WV_HNSW_LAUNCH(WV_METRIC_L2, true);
+        else if (p->metric == WV_METRIC_DOT) WV_HNSW_LAUNCH(WV_METRIC_DOT, true);
+        else WV_HNSW_LAUNCH(WV_METRIC_COSINE, true);
+    } else {
+        if (p->metric == WV_METRIC_L2) WV_HNSW_LAUNCH(WV_METRIC_L2, false);
+        else if (p->metric == WV_METRIC_DOT) WV_HNSW_LAUNCH(WV_METRIC_DOT, false);
+        else WV_HNSW_LAUNCH(WV_METRIC_COSINE, false);
+    }
+#undef WV_HNSW_LAUNCH
     return hipGetLastError();
 }
 
