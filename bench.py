@@ -35,9 +35,29 @@ FP32_MFMA_PEAK_TF = 157.3    # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense
 BF16_MFMA_PEAK_TF = 2500.0   # MI355X_MICROARCH.md: bf16 dense MFMA peak (no sparsity)
 
 
+def _par_rows(fn, seed: int, row0: int, nrows: int, dim: int, chunk: int = 1 << 16) -> np.ndarray:
+    """fn(seed, row0, nrows, dim) over row chunks on a thread pool (numpy
+    releases the GIL in its ufuncs); rows are independent, so the result is
+    the same array as one call."""
+    if nrows <= chunk:
+        return fn(seed, row0, nrows, dim)
+    from concurrent.futures import ThreadPoolExecutor
+    out = np.empty((nrows, dim), np.float32)
+
+    def one(r0):
+        r1 = min(nrows, r0 + chunk)
+        out[r0:r1] = fn(seed, row0 + r0, r1 - r0, dim)
+
+    with ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 4)) as ex:
+        list(ex.map(one, range(0, nrows, chunk)))
+    return out
+
+
 def counter_uniform(seed: int, row0: int, nrows: int, dim: int) -> np.ndarray:
     """Counter-based U[0,1) float32: value(row, col) depends only on (seed, row,
     col), so every rank can generate exactly its own rows of the corpus."""
+    if nrows > (1 << 16):
+        return _par_rows(counter_uniform, seed, row0, nrows, dim)
     out = np.empty((nrows, dim), np.float32)
     chunk = max(1, (1 << 22) // dim)
     cols = np.arange(dim, dtype=np.uint64)
@@ -58,6 +78,8 @@ def counter_uniform(seed: int, row0: int, nrows: int, dim: int) -> np.ndarray:
 def counter_gauss(seed: int, row0: int, nrows: int, dim: int) -> np.ndarray:
     """N(0,1)/sqrt(dim) float32 by Box-Muller over two counter-based streams
     (GloVe / Deep / C4-shaped data)."""
+    if nrows > (1 << 16):
+        return _par_rows(counter_gauss, seed, row0, nrows, dim)
     u1 = counter_uniform(seed, row0, nrows, dim).astype(np.float64)
     u2 = counter_uniform(seed + 1000, row0, nrows, dim).astype(np.float64)
     z = np.sqrt(-2.0 * np.log(u1 + 2.0 ** -25)) * np.cos(2.0 * np.pi * u2)
@@ -73,6 +95,8 @@ def counter_sift(seed: int, row0: int, nrows: int, dim: int) -> np.ndarray:
     per row like counter_uniform.  Uniform 128-d data has intrinsic dimension
     128 and no HNSW operating point near recall 0.95 at ef=64; this does
     (about 0.99 at 100k rows)."""
+    if nrows > (1 << 16):
+        return _par_rows(counter_sift, seed, row0, nrows, dim)
     C, L = 1024, 24
     centres = counter_uniform(77, 0, C, dim) * np.float32(60.0)
     basis = counter_gauss(78, 0, dim, L) * np.float32(np.sqrt(L))
@@ -108,15 +132,418 @@ def dist_env():
     return ws, rank, local
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """`--gpus N` without a launcher: start N ranks (one process per GPU) as
+    a child torch.distributed.run and return its exit code.  Runs before this
+    process touches the GPU (nothing is exec'd)."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+class Ctx:
+    """One rank: its device, stream and the process group (if any)."""
+
+    def __init__(self, args):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist = torch, dist
+        self.ws, self.rank, self.local = dist_env()
+        self.gpu = self.local % max(torch.cuda.device_count(), 1)
+        self.gloo = self.ws > 1 and args.dist_backend == "gloo"
+        if self.ws > 1:
+            if self.gloo:
+                dist.init_process_group(backend="gloo")
+            else:
+                dist.init_process_group(backend="nccl", device_id=torch.device("cuda", self.gpu))
+        torch.cuda.set_device(self.gpu)
+        self.dev = torch.device("cuda", self.gpu)
+        self.stream = torch.cuda.current_stream(self.dev).cuda_stream
+        self.n_devices = self.ws
+        if self.ws > 1:   # distinct devices behind the ranks (a gloo rehearsal may share one)
+            t = torch.tensor([self.gpu], dtype=torch.int64)
+            parts = [torch.zeros(1, dtype=torch.int64) for _ in range(self.ws)]
+            if self.gloo:
+                dist.all_gather(parts, t)
+            else:
+                tt = t.to(self.dev)
+                pp = [p.to(self.dev) for p in parts]
+                dist.all_gather(pp, tt)
+                parts = [p.cpu() for p in pp]
+            self.n_devices = len({int(p.item()) for p in parts})
+
+    def barrier(self):
+        if self.ws > 1:
+            self.dist.barrier()
+
+    def max_over_ranks(self, x: float) -> float:
+        if self.ws == 1:
+            return x
+        t = self.torch.tensor([x], dtype=self.torch.float64, device="cpu" if self.gloo else self.dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def time_steps(self, step, steps, warmup):
+        """W untimed steps, then exactly K steps bracketed by barrier +
+        synchronize on both sides; the max over ranks (bench contract)."""
+        torch = self.torch
+        for _ in range(warmup):
+            step(False)
+        torch.cuda.synchronize(self.dev)
+        self.barrier()
+        torch.cuda.synchronize(self.dev)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step(True)
+        torch.cuda.synchronize(self.dev)
+        self.barrier()
+        torch.cuda.synchronize(self.dev)
+        return self.max_over_ranks(time.perf_counter() - t0)
+
+    def allgather(self, out, t):
+        """[ws, ...] all-gather of a device tensor: RCCL over xGMI (product),
+        or through host memory for a gloo rehearsal."""
+        if self.gloo:
+            parts = [self.torch.empty_like(t, device="cpu") for _ in range(self.ws)]
+            self.dist.all_gather(parts, t.cpu())
+            out.copy_(self.torch.stack(parts).to(self.dev))
+        else:
+            self.dist.all_gather_into_tensor(out, t)
+
+
+def _query_tensor(ctx, queries, dpad):
+    torch = ctx.torch
+    qt = torch.zeros((queries.shape[0], dpad), dtype=torch.float32, device=ctx.dev)
+    qt[:, : queries.shape[1]] = torch.from_numpy(queries).to(ctx.dev)
+    return qt
+
+
+def _out_tensors(ctx, nq, k):
+    torch = ctx.torch
+    return (torch.empty((nq, k), dtype=torch.int64, device=ctx.dev), torch.empty((nq, k), dtype=torch.float32,
+            device=ctx.dev), torch.empty((nq,), dtype=torch.int32, device=ctx.dev))
+
+
+def _allow_words(args, lo, n_local):
+    keep = counter_uniform(3, lo, n_local, 1)[:, 0] < args.allow_frac
+    words = np.zeros((n_local + 63) // 64, np.uint64)
+    idx = np.nonzero(keep)[0].astype(np.uint64)
+    np.bitwise_or.at(words, (idx >> np.uint64(6)).astype(np.int64), np.uint64(1) << (idx & np.uint64(63)))
+    return words, int(keep.sum())
+
+
+def _oracle():
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as O  # the checker / CPU baseline (test infrastructure), never the measured path
+    return O
+
+
+def exact_roofline(args, ix, kern_ms, stats, D, n_allowed, n_local, NQ):
+    mfma_ms = float(np.mean([k["bf_mfma_ms"] for k in kern_ms]))
+    flops = 2.0 * D * n_allowed * NQ    # algorithmic: 2*D*N_eff per query (SURVEY 8d)
+    achieved = flops / (mfma_ms * 1e-3) / 1e12
+    # The key pass runs either as bf16x3 (default: hi*hi + hi*lo + lo*hi on
+    # v_mfma_f32_32x32x16_bf16, 3 bf16 products per fp32 product, so its
+    # fp32-equivalent ceiling is the bf16 dense peak / 3) or as fp32 MFMA
+    # (WV_BF_FP32=1).  achieved stays the algorithmic 2*D*N_eff per query.
+    split = not os.environ.get("WV_BF_FP32") and D <= 128 and 2 * n_allowed >= n_local
+    peak = BF16_MFMA_PEAK_TF / 3 if split else FP32_MFMA_PEAK_TF
+    kname = "wv_bf_split_kernel" if split else "wv_bf_mfma_kernel"
+    return {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 2), "peak": round(peak, 1),
+            "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
+            "key_pass": "bf16x3 (peak = bf16 dense / 3)" if split else "fp32 MFMA",
+            "frac_of_fp32_mfma_peak": round(achieved / FP32_MFMA_PEAK_TF, 4), "kernel_ms": round(mfma_ms, 3),
+            "finalize_ms": round(float(np.mean([k["bf_finalize_ms"] for k in kern_ms])), 3),
+            "fallback_queries": stats["fallbacks"]}
+
+
+def attach_traffic(roof, n_local, NQ, D, data):
+    pmc = os.path.join(ROOT, "profiles", "pmc_%s.json" % roof["kernel"])
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            p = json.load(f)
+        if (p.get("N"), p.get("nq"), p.get("dim"), p.get("data", "uniform")) == (n_local, NQ, D, data):
+            roof["traffic"] = p.get("hbm_bytes_per_launch")
+            roof["traffic_source"] = p.get("source", os.path.relpath(pmc, ROOT))
+
+
+def run_exact(args, ctx, W):
+    """configs[1]: exact 10-NN (flatSearch semantics) over the whole corpus.
+    query split (default at N > 1): every rank holds the corpus and answers its
+    own nq-query batch -- queries are independent units, no collective (weak
+    scaling).  corpus split: rank r owns ids [r N/W, (r+1) N/W), all ranks take
+    the same batch, the per-shard top-k are all-gathered over RCCL and merged
+    on the device (index.go:967-1044; strong scaling)."""
+    torch = ctx.torch
+    N, D, NQ, K = args.rows, args.dim, args.nq, args.k
+    ws, rank = ctx.ws, ctx.rank
+    split = args.split
+    gen = {"uniform": counter_uniform, "gauss": counter_gauss, "sift": counter_sift}[args.data]
+    lo, hi = (N * rank // ws, N * (rank + 1) // ws) if split == "corpus" else (0, N)
+    n_local = hi - lo
+    base = gen(1, lo, n_local, D)
+    q_row0 = rank * NQ if split == "query" else 0
+    queries = gen(2, q_row0, NQ, D)
+    ix = W.GPUVectorIndex(D, args.metric, capacity=max(n_local, 1), device=ctx.gpu, id_base=lo)
+    ix.upload_vectors(base)
+    dpad = ix.query_ld()
+    qt = _query_tensor(ctx, queries, dpad)
+    out_ids, out_d, out_n = _out_tensors(ctx, NQ, K)
+    if split == "corpus" and ws > 1:
+        g_ids = torch.empty((ws, NQ, K), dtype=torch.int64, device=ctx.dev)
+        g_d = torch.empty((ws, NQ, K), dtype=torch.float32, device=ctx.dev)
+        g_n = torch.empty((ws, NQ), dtype=torch.int32, device=ctx.dev)
+        m_ids, m_d, m_n = _out_tensors(ctx, NQ, K)
+    allow_ptr, allow_bits, n_allowed, words = 0, 0, n_local, None
+    if args.allow_frac > 0:
+        words, n_allowed = _allow_words(args, lo, n_local)
+        allow_t = torch.from_numpy(words.view(np.int64)).to(ctx.dev)
+        allow_ptr, allow_bits = allow_t.data_ptr(), n_local
+    kern_ms = []
+
+    def step(timed):
+        ix.search_batch_device(qt.data_ptr(), NQ, K, out_ids.data_ptr(), out_d.data_ptr(), out_n.data_ptr(), ef=0,
+                               mode="exact", stream=ctx.stream, allow_ptr=allow_ptr, allow_nbits=allow_bits)
+        if timed:
+            kern_ms.append(ix.last_kernel_times())
+        if split == "corpus" and ws > 1:
+            ctx.allgather(g_ids, out_ids)
+            ctx.allgather(g_d, out_d)
+            ctx.allgather(g_n, out_n)
+            W.merge_shards_device(g_d.data_ptr(), g_ids.data_ptr(), g_n.data_ptr(), ws, NQ, K, m_d.data_ptr(),
+                                  m_ids.data_ptr(), m_n.data_ptr(), stream=ctx.stream)
+
+    ix.set_timing(True)
+    elapsed = ctx.time_steps(step, args.steps, args.warmup)
+    stats = ix.last_batch_stats()
+    fin_ids, fin_d = (m_ids, m_d) if (split == "corpus" and ws > 1) else (out_ids, out_d)
+    final_ids = fin_ids.cpu().numpy().view(np.uint64)
+    final_d = fin_d.cpu().numpy()
+    units = NQ * (ws if split == "query" else 1)
+    res = {
+        "value": round(units * args.steps / elapsed, 1),
+        "ms_per_step": round(1000 * elapsed / args.steps, 3),
+        "scaling": "weak" if split == "query" else "strong",
+        "workload": ("exact brute-force %d-NN, %s x %d-d %s, %d-query batch%s"
+                     % (K, f"{N:,}", D, args.metric, NQ,
+                        (" (BASELINE configs[1])" if (N, D, args.metric) == (1_000_000, 128, "l2-squared") else "")
+                        if args.allow_frac <= 0 else
+                        f", shared allow list p={args.allow_frac} ({n_allowed:,} rows on rank 0)")),
+        "parallelism": {"query": f"{ws} GPU(s), each holding the whole corpus and answering its own {NQ}-query "
+                                 f"batch (no collective)",
+                        "corpus": f"corpus sharded over {ws} GPU(s) by id range" + (
+                            ", RCCL all-gather of per-shard top-k + device merge" if ws > 1 else "")}[split],
+    }
+    roof = exact_roofline(args, ix, kern_ms, stats, D, n_allowed, n_local, NQ)
+    attach_traffic(roof, n_local, NQ, D, args.data)
+    res["roofline"] = roof
+    state = dict(ix=ix, base=base, queries=queries, final_ids=final_ids, final_d=final_d, words=words,
+                 n_allowed=n_allowed, lo=lo, n_local=n_local)
+    return res, state
+
+
+def exact_cpu_baseline(args, st, O):
+    """flatSearch restated in C (AVX2 asm-order distancer), on a bounded
+    sample of the same queries; T = --cpu-threads (GOMAXPROCS-equivalent) and
+    T = 1.  The same pass is the parity sample."""
+    K = args.k
+    base, queries = st["base"], st["queries"]
+    metric_id = O.METRICS[args.metric]
+    if args.metric == "cosine-dot":   # stored vectors normalized on insert (insert.go:56-60), queries per search
+        base = O.normalize_rows(base)
+        queries = O.normalize_rows(queries)
+    cpu_allow = st["words"]
+    out = {}
+    for threads, secs in ((args.cpu_threads, args.cpu_seconds), (1, args.cpu_seconds_t1)):
+        probe = max(2, min(32, 2 * threads))
+        t0 = time.perf_counter()
+        O.flat_scan(metric_id, base, queries[:probe], K, allow_bits=cpu_allow, threads=threads)
+        per_q = (time.perf_counter() - t0) / probe
+        ns = int(min(args.nq, max(probe, secs / max(per_q, 1e-9))))
+        t0 = time.perf_counter()
+        oi, od, on = O.flat_scan(metric_id, base, queries[:ns], K, allow_bits=cpu_allow, threads=threads)
+        out[threads] = (ns, time.perf_counter() - t0, oi, od)
+    ns, cpu_t, oi, od = out[args.cpu_threads]
+    id_eq, d_eq, tie_ok = parity_stats(st["final_ids"][:ns], st["final_d"][:ns], oi, od)
+    parity = {"queries": ns, "ids_and_dists_bit_identical": id_eq == 1.0 and d_eq == 1.0,
+              "dists_bitwise_equal_frac": d_eq, "tie_aware_identical_frac": tie_ok, "id_match_frac": id_eq}
+    n1, t1 = out[1][0], out[1][1]
+    base_line = {"value": round(ns / cpu_t, 1), "unit": "queries/s", "cores": args.cpu_threads, "kind": "port",
+                 "value_t1": round(n1 / t1, 2), "cores_t1": 1,
+                 "sample": f"{ns} (T={args.cpu_threads}) / {n1} (T=1) of the {args.nq} queries over the full "
+                           f"{args.rows:,}-row corpus ({cpu_t:.2f} s / {t1:.2f} s); flatSearch restated in C "
+                           f"(AVX2 asm-order distancer, oracle/), query-parallel like ssdhelpers.Concurrently, "
+                           f"GOMAXPROCS-equivalent T={args.cpu_threads} and T=1"}
+    return base_line, parity
+
+
+def build_hnsw_graph(args, ctx, ix, base, n_local, O):
+    """The configs[0] graph (M, efConstruction): on the GPU
+    (wv_index_build_graph, insert.go in batches) or by the CPU restatement's
+    sequential build (oracle/, test infrastructure)."""
+    torch = ctx.torch
+    cache = args.graph_cache % {"rank": ctx.rank} if args.graph_cache else ""
+    t0 = time.time()
+    if args.graph_build == "gpu":
+        torch.cuda.synchronize(ctx.dev)
+        ix.build_graph(ef_construction=args.efc, seed=1, batch_div=args.batch_div)
+        torch.cuda.synchronize(ctx.dev)
+        g = None
+        src = f"built on the GPU (wv_index_build_graph, batch = inserted/{args.batch_div})"
+    elif cache and os.path.exists(cache):
+        z = np.load(cache)
+        g = {k: (z[k] if z[k].ndim else int(z[k])) for k in z.files}
+        ix.upload_graph(g)
+        src = "loaded (cache) -- built earlier by the CPU restatement (oracle/)"
+    else:
+        import threading
+        done = threading.Event()
+
+        def progress():   # long CPU builds: keep the log moving
+            while not done.wait(30):
+                print(f"[bench] building hnsw graph over {n_local:,} rows: {time.time() - t0:.0f} s",
+                      file=sys.stderr, flush=True)
+        threading.Thread(target=progress, daemon=True).start()
+        ref = O.Index(args.dim, args.metric, args.M, args.efc, capacity=n_local, seed=1)
+        ref.add_batch(base, threads=args.hnsw_build_threads)
+        done.set()
+        g = ref.export_graph()
+        if cache:
+            np.savez(cache, **{k: np.asarray(v) for k, v in g.items()})
+        ix.upload_graph(g)
+        src = "built by the CPU restatement (oracle/)"
+    return {"build_s": round(time.time() - t0, 2), "M": args.M, "efConstruction": args.efc, "source": src}
+
+
+def run_hnsw(args, ctx, W, with_cpu):
+    """configs[0]: hnsw beam search (knnSearchByVector) at ef on SIFT-shaped
+    data; query split over the ranks (each rank holds the graph and answers
+    its own batch).  Recall@10 against exact truths from the exact path
+    (bit-identical to the restatement's flatSearch); on rank 0 at N = 1 also
+    the restatement's recall on the same graph and its CPU throughput."""
+    torch = ctx.torch
+    N, D, NQ, K = args.rows, args.dim, args.nq, args.k
+    data = args.hnsw_data
+    gen = {"uniform": counter_uniform, "gauss": counter_gauss, "sift": counter_sift}[data]
+    base = gen(1, 0, N, D)
+    queries = gen(2, ctx.rank * NQ, NQ, D)
+    ix = W.GPUVectorIndex(D, args.metric, capacity=N, device=ctx.gpu, max_connections=args.M)
+    ix.upload_vectors(base)
+    O = _oracle() if (with_cpu or args.graph_build != "gpu") else None
+    graph = build_hnsw_graph(args, ctx, ix, base, N, O)
+    graph["max_level"] = int(ix.graph_info()["max_level"])
+    dpad = ix.query_ld()
+    qt = _query_tensor(ctx, queries, dpad)
+    out_ids, out_d, out_n = _out_tensors(ctx, NQ, K)
+    kern_ms, stats = [], []
+
+    def step(timed):
+        ix.search_batch_device(qt.data_ptr(), NQ, K, out_ids.data_ptr(), out_d.data_ptr(), out_n.data_ptr(),
+                               ef=args.ef, mode="hnsw", stream=ctx.stream)
+        if timed:
+            kern_ms.append(ix.last_kernel_times())
+            stats.append(ix.last_batch_stats())
+
+    ix.set_timing(True)
+    elapsed = ctx.time_steps(step, args.steps, args.warmup)
+    hi_ids = out_ids.cpu().numpy().view(np.uint64)
+    hi_d = out_d.cpu().numpy()
+    # exact truths on the same queries (the exact path: ids bit-identical to
+    # flatSearch), timed once: SIFT-shaped data is integer-valued, so equal
+    # distances at the k boundary send queries to the certificate's fallback
+    ix.set_timing(False)
+    torch.cuda.synchronize(ctx.dev)
+    t0 = time.perf_counter()
+    ix.search_batch_device(qt.data_ptr(), NQ, K, out_ids.data_ptr(), out_d.data_ptr(), out_n.data_ptr(), ef=0,
+                           mode="exact", stream=ctx.stream)
+    torch.cuda.synchronize(ctx.dev)
+    exact_ms = 1000 * (time.perf_counter() - t0)
+    exact_fb = ix.last_batch_stats()["fallbacks"]
+    truth = out_ids.cpu().numpy().view(np.uint64)
+    rec = float(np.mean([len(set(a) & set(b)) / K for a, b in zip(hi_ids.tolist(), truth.tolist())]))
+    hnsw_ms = float(np.mean([k["hnsw_ms"] for k in kern_ms]))
+    e, x = stats[-1]["dist_evals"], stats[-1]["expansions"]
+    by = 4.0 * D * e + 4.0 * 2 * args.M * x   # 4*D*E + 4*deg_slots*X (deg0 = 2M)
+    achieved = by / (hnsw_ms * 1e-3) / 1e9
+    res = {
+        "metric": METRIC, "value": round(NQ * ctx.ws * args.steps / elapsed, 1), "unit": "queries/s",
+        "ms_per_step": round(1000 * elapsed / args.steps, 3), "recall@10": round(rec, 4),
+        "recall_truth": "exact path on the same queries (all of them)",
+        "scaling": "weak",
+        "workload": "hnsw knnSearchByVector ef=%d, %s x %d-d %s, %d-query batch per GPU (BASELINE configs[0] "
+                    "parameters M=%d, efConstruction=%d)" % (args.ef, f"{N:,}", D, args.metric, NQ, args.M, args.efc),
+        "data": {"sift": "SIFT-shaped (1024 centres + 24-d latent + noise, non-negative integers)",
+                 "uniform": "U[0,1)", "gauss": "N(0,1)/sqrt(D)"}[data],
+        "graph": graph,
+        "exact_same_data": {"ms_one_batch": round(exact_ms, 2), "fallback_queries": exact_fb,
+                            "note": "the exact path on these (tie-heavy, integer-valued) queries, one untimed-loop "
+                                    "call after the hnsw steps"},
+        "roofline": {"bound": "hbm", "kernel": "wv_hnsw_kernel", "achieved": round(achieved, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": None, "kernel_ms": round(hnsw_ms, 3), "counts_from": "GPU counters",
+                     "dist_evals_per_query": round(e / NQ, 1), "expansions_per_query": round(x / NQ, 1),
+                     "fallback_queries": stats[-1]["fallbacks"]},
+    }
+    attach_traffic(res["roofline"], N, NQ, D, data)
+    if with_cpu:
+        ref = O.Index(D, args.metric, args.M, args.efc, capacity=N, seed=1)
+        ref.import_graph(base, ix.download_graph())   # the restatement searches the very same graph
+        probe = min(NQ, 500)
+        t0 = time.perf_counter()
+        ref.search_batch(queries[:probe], K, args.ef, threads=args.cpu_threads)
+        per_q = (time.perf_counter() - t0) / probe
+        reps = max(1, int(args.cpu_seconds / max(per_q * NQ, 1e-9)))
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            oi, od, on, ost = ref.search_batch(queries, K, args.ef, threads=args.cpu_threads)
+        cpu_t = (time.perf_counter() - t0) / reps
+        n1 = int(min(NQ, max(100, args.cpu_seconds_t1 / max(per_q * args.cpu_threads, 1e-9))))
+        t0 = time.perf_counter()
+        ref.search_batch(queries[:n1], K, args.ef, threads=1)
+        t1 = time.perf_counter() - t0
+        # algorithmic bytes from the restatement's own count of distance
+        # evaluations E and expansions X on the same graph / queries / ef
+        # (SURVEY 8d), not from the GPU's counters
+        e, x = ost["dist_evals"], ost["expansions"]
+        by = 4.0 * D * e + 4.0 * 2 * args.M * x
+        achieved = by / (hnsw_ms * 1e-3) / 1e9
+        res["roofline"].update({"achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4),
+                                "counts_from": "CPU restatement (oracle/) on the same graph",
+                                "dist_evals_per_query": round(e / NQ, 1), "expansions_per_query": round(x / NQ, 1),
+                                "gpu_dist_evals_per_query": round(stats[-1]["dist_evals"] / NQ, 1)})
+        id_eq, d_eq, tie_ok = parity_stats(hi_ids, hi_d, oi, od)
+        rec_cpu = float(np.mean([len(set(a) & set(b)) / K for a, b in zip(oi.tolist(), truth.tolist())]))
+        res["parity_sample"] = {"queries": NQ, "id_match_frac": id_eq, "dists_bitwise_equal_frac": d_eq,
+                                "tie_aware_identical_frac": tie_ok, "recall@10_gpu": round(rec, 4),
+                                "recall@10_cpu_restatement": round(rec_cpu, 4)}
+        res["cpu_baseline"] = {"value": round(NQ / cpu_t, 1), "unit": "queries/s", "cores": args.cpu_threads,
+                               "kind": "port", "value_t1": round(n1 / t1, 1), "cores_t1": 1,
+                               "sample": f"all {NQ} queries x {reps} passes (T={args.cpu_threads}), {n1} queries "
+                                         f"(T=1); knnSearchByVector restated in C on the same graph (oracle/)"}
+    ix.close()
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", choices=["exact", "hnsw"], default="exact")
+    ap.add_argument("--split", choices=["query", "corpus"], default="",
+                    help="N>1: query = every GPU holds the corpus and answers its own batch (default, weak scaling); "
+                         "corpus = id-range shards + RCCL all-gather + device merge (strong scaling)")
     ap.add_argument("--rows", type=int, default=1_000_000, help="corpus rows N (all shards)")
     ap.add_argument("--dim", type=int, default=128)
-    ap.add_argument("--nq", type=int, default=10_000)
+    ap.add_argument("--nq", type=int, default=10_000, help="queries per batch (per GPU with --split query)")
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--ef", type=int, default=64)
     ap.add_argument("--metric", default="l2-squared")
@@ -126,304 +553,103 @@ def main():
                          "auto: uniform for exact, sift for hnsw")
     ap.add_argument("--allow-frac", type=float, default=0.0,
                     help="exact mode: shared allow list, Bernoulli(p) over ids (seed 3, BASELINE configs[3])")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample time")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time (T=all)")
+    ap.add_argument("--cpu-seconds-t1", type=float, default=5.0, help="target CPU-baseline sample time (T=1)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-hnsw-line", action="store_true",
+                    help="skip the configs[0] hnsw line that the exact workload reports beside its value")
+    ap.add_argument("--no-corpus-leg", action="store_true",
+                    help="N>1 exact: skip the corpus-sharded (RCCL merge) leg reported beside the query split")
     ap.add_argument("--hnsw-build-threads", type=int, default=16)
     ap.add_argument("--M", type=int, default=64, help="hnsw maxConnections (layer-0 degree 2M)")
     ap.add_argument("--efc", type=int, default=128, help="hnsw efConstruction")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (RCCL over xGMI, the product path); gloo only to rehearse N ranks on one GPU")
     ap.add_argument("--dump-ids", default="", help="rank 0 saves the final ids/dists (npz) for cross-N checks")
-    ap.add_argument("--graph-build", choices=["cpu", "gpu"], default="cpu",
-                    help="hnsw graph: the CPU restatement's sequential build (reference-equivalent) or "
-                         "wv_index_build_graph on the GPU")
+    ap.add_argument("--graph-build", choices=["cpu", "gpu"], default="gpu",
+                    help="hnsw graph: wv_index_build_graph on the GPU (default) or the CPU restatement's "
+                         "sequential build (reference-equivalent, slow at 1M)")
     ap.add_argument("--batch-div", type=int, default=64, help="GPU build: batch = inserted / batch_div")
     ap.add_argument("--graph-cache", default="", help="npz path: load the hnsw graph if present, else build and save")
     args = ap.parse_args()
 
-    ws, rank, local = dist_env()
-    import torch
-    import torch.distributed as dist
-
-    import weaviate_amd as W
-
-    gpu = local % max(torch.cuda.device_count(), 1)
-    if ws > 1:
-        if args.dist_backend == "nccl":
-            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", gpu))
-        else:
-            dist.init_process_group(backend="gloo")
-    torch.cuda.set_device(gpu)
-    dev = torch.device("cuda", gpu)
-    gloo = ws > 1 and args.dist_backend == "gloo"
-
-    # ---- corpus shard of this rank (contiguous id range) ----
-    N, D, NQ, K = args.rows, args.dim, args.nq, args.k
-    lo = N * rank // ws
-    hi = N * (rank + 1) // ws
-    n_local = hi - lo
+    if os.environ.get("WORLD_SIZE") is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    ws, rank, _ = dist_env()
+    if ws != args.gpus:
+        print(json.dumps({"error": f"--gpus {args.gpus} but WORLD_SIZE={ws}: launch with --nproc-per-node "
+                                   f"{args.gpus} or without a launcher"}), flush=True)
+        sys.exit(2)
+    if not args.split:
+        args.split = "query" if ws > 1 else "corpus"
     if args.data == "auto":
         args.data = "sift" if args.workload == "hnsw" else "uniform"
-    gen = {"uniform": counter_uniform, "gauss": counter_gauss, "sift": counter_sift}[args.data]
-    base = gen(1, lo, n_local, D)
-    queries = gen(2, 0, NQ, D)
+    args.hnsw_data = args.data if args.workload == "hnsw" else "sift"
 
-    ix = W.GPUVectorIndex(D, args.metric, capacity=max(n_local, 1), device=gpu, id_base=lo,
-                          max_connections=args.M)
-    ix.upload_vectors(base)
-    mode = "exact"
-    graph_info = None
-    ref = None
+    import weaviate_amd as W
+    ctx = Ctx(args)
+    with_cpu = rank == 0 and ws == 1 and not args.no_cpu_baseline
+
     if args.workload == "hnsw":
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import pyoracle as O  # graph construction = test infrastructure (CPU restatement)
-        t0 = time.time()
-        ref = O.Index(D, args.metric, args.M, args.efc, capacity=n_local, seed=1)
-        cache = args.graph_cache % {"rank": rank} if args.graph_cache else ""
-        if args.graph_build == "gpu":
-            torch.cuda.synchronize(dev)
-            t0 = time.time()
-            ix.build_graph(ef_construction=args.efc, seed=1, batch_div=args.batch_div)
-            g = ix.download_graph()
-            built = f"built on the GPU (wv_index_build_graph, batch = inserted/{args.batch_div})"
-            if rank == 0 and ws == 1 and not args.no_cpu_baseline:
-                ref.import_graph(base, g)   # the restatement searches the same graph
-        elif cache and os.path.exists(cache):
-            z = np.load(cache)
-            g = {k: (z[k] if z[k].ndim else int(z[k])) for k in z.files}
-            ref.import_graph(base, g)   # the restatement searches the same graph
-            built = "loaded (cache) -- built earlier"
-        else:
-            import threading
-            done = threading.Event()
-
-            def progress():   # long CPU builds: keep the log moving
-                while not done.wait(30):
-                    print(f"[bench] building hnsw graph over {n_local:,} rows: {time.time() - t0:.0f} s",
-                          file=sys.stderr, flush=True)
-            threading.Thread(target=progress, daemon=True).start()
-            ref.add_batch(base, threads=args.hnsw_build_threads)
-            done.set()
-            g = ref.export_graph()
-            if cache:
-                np.savez(cache, **{k: np.asarray(v) for k, v in g.items()})
-            built = "built"
-        if args.graph_build != "gpu":
-            ix.upload_graph(g)
-        graph_info = {"build_s": round(time.time() - t0, 2), "M": args.M, "efConstruction": args.efc,
-                      "max_level": int(g["max_level"]), "source": built if args.graph_build == "gpu"
-                      else built + " by the CPU restatement (oracle/)"}
-        mode = "hnsw"
-
-    dpad = (D + 3) & ~3
-    qt = torch.zeros((NQ, dpad), dtype=torch.float32, device=dev)
-    qt[:, :D] = torch.from_numpy(queries).to(dev)
-    out_ids = torch.empty((NQ, K), dtype=torch.int64, device=dev)
-    out_d = torch.empty((NQ, K), dtype=torch.float32, device=dev)
-    out_n = torch.empty((NQ,), dtype=torch.int32, device=dev)
-    if ws > 1:
-        g_ids = torch.empty((ws, NQ, K), dtype=torch.int64, device=dev)
-        g_d = torch.empty((ws, NQ, K), dtype=torch.float32, device=dev)
-        g_n = torch.empty((ws, NQ), dtype=torch.int32, device=dev)
-        m_ids = torch.empty((NQ, K), dtype=torch.int64, device=dev)
-        m_d = torch.empty((NQ, K), dtype=torch.float32, device=dev)
-        m_n = torch.empty((NQ,), dtype=torch.int32, device=dev)
-    stream = torch.cuda.current_stream(dev).cuda_stream
-    allow_ptr, allow_bits, n_allowed = 0, 0, n_local
-    if args.allow_frac > 0:
-        keep = counter_uniform(3, lo, n_local, 1)[:, 0] < args.allow_frac
-        words = np.zeros((n_local + 63) // 64, np.uint64)
-        idx = np.nonzero(keep)[0].astype(np.uint64)
-        np.bitwise_or.at(words, (idx >> np.uint64(6)).astype(np.int64), np.uint64(1) << (idx & np.uint64(63)))
-        allow_t = torch.from_numpy(words.view(np.int64)).to(dev)
-        allow_ptr, allow_bits, n_allowed = allow_t.data_ptr(), n_local, int(keep.sum())
-
-    kern_ms = []
-
-    def step(timed=False):
-        ix.search_batch_device(qt.data_ptr(), NQ, K, out_ids.data_ptr(), out_d.data_ptr(), out_n.data_ptr(),
-                               ef=args.ef if mode == "hnsw" else 0, mode=mode, stream=stream,
-                               allow_ptr=allow_ptr, allow_nbits=allow_bits)
-        if timed:
-            kern_ms.append(ix.last_kernel_times())
-        if ws > 1:
-            if gloo:   # rehearsal only: the gather goes through host memory
-                for g, o in ((g_ids, out_ids), (g_d, out_d), (g_n, out_n)):
-                    parts = [torch.empty_like(o, device="cpu") for _ in range(ws)]
-                    dist.all_gather(parts, o.cpu())
-                    g.copy_(torch.stack(parts).to(dev))
-            else:
-                dist.all_gather_into_tensor(g_ids, out_ids)
-                dist.all_gather_into_tensor(g_d, out_d)
-                dist.all_gather_into_tensor(g_n, out_n)
-            W.merge_shards_device(g_d.data_ptr(), g_ids.data_ptr(), g_n.data_ptr(), ws, NQ, K, m_d.data_ptr(),
-                                  m_ids.data_ptr(), m_n.data_ptr(), stream=stream)
-
-    ix.set_timing(True)
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    if ws > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(timed=True)
-    torch.cuda.synchronize(dev)
-    if ws > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    if ws > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if gloo else dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    stats = ix.last_batch_stats()
-
-    final_ids = (m_ids if ws > 1 else out_ids).cpu().numpy().view(np.uint64)
-    final_d = (m_d if ws > 1 else out_d).cpu().numpy()
-
-    if args.dump_ids and rank == 0:
-        np.savez(args.dump_ids, ids=final_ids, dists=final_d)
-    qps = NQ * args.steps / elapsed
-    result = {
-        "metric": METRIC,
-        "value": round(qps, 1),
-        "unit": "queries/s",
-        "n_gpus": ws,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(1000 * elapsed / args.steps, 3),
-        "higher_is_better": True,
-        "scaling": "strong",
-        "vs_baseline": None,
-        "dtype": "f32" if mode != "exact" or os.environ.get("WV_BF_FP32") else "f32 (bf16x3 MFMA keys, f32 re-rank)",
-        "data": "synthetic: counter-based %s float32 corpus (seed 1) and queries (seed 2)" % {
-            "uniform": "U[0,1)", "gauss": "N(0,1)/sqrt(D)",
-            "sift": "SIFT-shaped (1024 centres + 24-d latent + noise, non-negative integers)"}[args.data],
-        "config": {
-            "workload": ("exact brute-force %d-NN, %s x %d-d %s, %d-query batch%s"
-                         % (K, f"{N:,}", D, args.metric, NQ,
-                            (" (BASELINE configs[1])" if (N, D, args.metric) == (1_000_000, 128, "l2-squared")
-                             else "") if args.allow_frac <= 0 else
-                            f", shared allow list p={args.allow_frac} ({n_allowed:,} rows on rank 0)"))
-                        if mode == "exact" else
-                        ("hnsw layer-0 beam search ef=%d, %s x %d-d %s, %d-query batch" % (args.ef, f"{N:,}", D,
-                                                                                         args.metric, NQ)),
-            "N": N, "dim": D, "nq": NQ, "k": K, "metric": args.metric, "mode": mode,
-            "parallelism": f"corpus sharded over {ws} GPU(s) by id range" + (
-                ", RCCL all-gather of per-shard top-k + device merge" if ws > 1 else ""),
-        },
-    }
-
-    # ---- roofline of the dominant kernel (HIP events on its launch stream) ----
-    if mode == "exact":
-        mfma_ms = float(np.mean([k["bf_mfma_ms"] for k in kern_ms]))
-        flops = 2.0 * D * n_allowed * NQ    # algorithmic: 2*D*N_eff per query
-        achieved = flops / (mfma_ms * 1e-3) / 1e12
-        # The key pass runs either as bf16x3 (default: hi*hi + hi*lo + lo*hi on
-        # v_mfma_f32_32x32x16_bf16, 3 bf16 products per fp32 product, so its
-        # fp32-equivalent ceiling is the bf16 dense peak / 3) or as fp32 MFMA
-        # (WV_BF_FP32=1).  achieved stays the algorithmic 2*D*N_eff per query.
-        # (the library takes the split pass for D <= 128 unless a shared allow
-        # list is compacted into a row list: |allow| < N/2)
-        split = not os.environ.get("WV_BF_FP32") and D <= 128 and 2 * n_allowed >= n_local
-        peak = BF16_MFMA_PEAK_TF / 3 if split else FP32_MFMA_PEAK_TF
-        kname = "wv_bf_split_kernel" if split else "wv_bf_mfma_kernel"
-        result["roofline"] = {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 2),
-                              "peak": round(peak, 1), "unit": "TFLOP/s",
-                              "frac": round(achieved / peak, 4), "traffic": None,
-                              "key_pass": "bf16x3 (peak = bf16 dense / 3)" if split else "fp32 MFMA",
-                              "frac_of_fp32_mfma_peak": round(achieved / FP32_MFMA_PEAK_TF, 4),
-                              "kernel_ms": round(mfma_ms, 3),
-                              "finalize_ms": round(float(np.mean([k["bf_finalize_ms"] for k in kern_ms])), 3),
-                              "fallback_queries": stats["fallbacks"]}
+        h = run_hnsw(args, ctx, W, with_cpu)
+        result = {"metric": METRIC, "value": h["value"], "unit": "queries/s", "n_gpus": ws,
+                  "devices": ctx.n_devices, "steps": args.steps, "warmup": args.warmup,
+                  "ms_per_step": h["ms_per_step"], "higher_is_better": True, "scaling": "weak",
+                  "vs_baseline": None, "dtype": "f32", "data": "synthetic: counter-based " + h["data"],
+                  "config": {"workload": h["workload"], "N": args.rows, "dim": args.dim, "nq": args.nq,
+                             "k": args.k, "metric": args.metric, "mode": "hnsw",
+                             "parallelism": f"{ws} GPU(s), each holding the graph and answering its own batch"},
+                  "recall@10": h["recall@10"], "graph": h["graph"], "roofline": h["roofline"]}
+        for key in ("parity_sample", "cpu_baseline"):
+            if key in h:
+                result[key] = h[key]
     else:
-        hnsw_ms = float(np.mean([k["hnsw_ms"] for k in kern_ms]))
-        e, x = stats["dist_evals"], stats["expansions"]
-        by = 4.0 * D * e + 4.0 * 2 * args.M * x   # 4*D*E + 4*deg_slots*X (deg0 = 2M)
-        achieved = by / (hnsw_ms * 1e-3) / 1e9
-        result["roofline"] = {"bound": "hbm", "kernel": "wv_hnsw_kernel", "achieved": round(achieved, 1),
-                              "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                              "traffic": None, "kernel_ms": round(hnsw_ms, 3), "counts_from": "GPU counters",
-                              "dist_evals_per_query": round(e / NQ, 1), "expansions_per_query": round(x / NQ, 1)}
-        result["graph"] = graph_info
-    pmc = os.path.join(ROOT, "profiles", "pmc_%s.json" % result["roofline"]["kernel"])
-    if os.path.exists(pmc):
-        with open(pmc) as f:
-            p = json.load(f)
-        if (p.get("N"), p.get("nq"), p.get("dim"), p.get("data", "uniform")) == (n_local, NQ, D, args.data):
-            result["roofline"]["traffic"] = p.get("hbm_bytes_per_launch")
-
-    # ---- CPU baseline + parity sample (rank 0, N=1 only) ----
-    if rank == 0 and ws == 1 and not args.no_cpu_baseline:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import pyoracle as O
-        threads = args.cpu_threads
-        metric_id = O.METRICS[args.metric]
-        if mode == "exact":
-            probe = 32
-            t0 = time.perf_counter()
-            cpu_allow = words if args.allow_frac > 0 else None
-            if args.metric == "cosine-dot":   # stored vectors normalized on insert (insert.go:56-60), queries per search
-                base = O.normalize_rows(base)
-                queries = O.normalize_rows(queries)
-            oi, od, on = O.flat_scan(metric_id, base, queries[:probe], K, allow_bits=cpu_allow, threads=threads)
-            per_q = (time.perf_counter() - t0) / probe
-            ns = int(min(NQ, max(probe, args.cpu_seconds / max(per_q, 1e-9))))
-            t0 = time.perf_counter()
-            oi, od, on = O.flat_scan(metric_id, base, queries[:ns], K, allow_bits=cpu_allow, threads=threads)
-            cpu_t = time.perf_counter() - t0
-            kind_desc = "flatSearch restated in C (AVX2 asm-order distancer, oracle/)"
-            id_eq, d_eq, tie_ok = parity_stats(final_ids[:ns], final_d[:ns], oi, od)
-            result["parity_sample"] = {"queries": ns, "ids_and_dists_bit_identical": id_eq == 1.0 and d_eq == 1.0,
-                                       "dists_bitwise_equal_frac": d_eq, "tie_aware_identical_frac": tie_ok,
-                                       "id_match_frac": id_eq}
+        e, st = run_exact(args, ctx, W)
+        result = {
+            "metric": METRIC, "value": e["value"], "unit": "queries/s", "n_gpus": ws, "devices": ctx.n_devices,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": e["ms_per_step"], "higher_is_better": True,
+            "scaling": e["scaling"], "vs_baseline": None,
+            "dtype": "f32" if os.environ.get("WV_BF_FP32") else "f32 (bf16x3 MFMA keys, f32 re-rank)",
+            "data": "synthetic: counter-based %s float32 corpus (seed 1) and queries (seed 2)" % {
+                "uniform": "U[0,1)", "gauss": "N(0,1)/sqrt(D)",
+                "sift": "SIFT-shaped (1024 centres + 24-d latent + noise, non-negative integers)"}[args.data],
+            "config": {"workload": e["workload"], "N": args.rows, "dim": args.dim, "nq": args.nq, "k": args.k,
+                       "metric": args.metric, "mode": "exact", "recall@10": 1.0, "split": args.split,
+                       "parallelism": e["parallelism"]},
+            "roofline": e["roofline"],
+        }
+        if with_cpu:
+            O = _oracle()
+            result["cpu_baseline"], result["parity_sample"] = exact_cpu_baseline(args, st, O)
+        if args.dump_ids and rank == 0:
+            np.savez(args.dump_ids, ids=st["final_ids"], dists=st["final_d"])
+        # N > 1: the north-star layout beside the query split -- id-range
+        # shards, RCCL all-gather, device merge -- on rank 0's batch, whose
+        # merged answer must equal rank 0's whole-corpus answer bit for bit
+        if ws > 1 and args.split == "query" and not args.no_corpus_leg:
+            rank0_ids, rank0_d = st["final_ids"], st["final_d"]
+            st["ix"].close()
+            a2 = argparse.Namespace(**vars(args))
+            a2.split = "corpus"
+            c, cst = run_exact(a2, ctx, W)
+            result["corpus_sharded"] = {
+                "value": c["value"], "unit": "queries/s", "ms_per_step": c["ms_per_step"], "scaling": "strong",
+                "parallelism": c["parallelism"], "kernel_ms": c["roofline"]["kernel_ms"],
+                "ids_equal_query_split": bool(rank == 0 and np.array_equal(cst["final_ids"], rank0_ids)
+                                              and np.array_equal(cst["final_d"].view(np.uint32),
+                                                                 rank0_d.view(np.uint32)))}
+            cst["ix"].close()
         else:
-            probe = min(NQ, 500)
-            t0 = time.perf_counter()
-            ref.search_batch(queries[:probe], K, args.ef, threads=threads)
-            per_q = (time.perf_counter() - t0) / probe
-            reps = max(1, int(args.cpu_seconds / max(per_q * NQ, 1e-9)))
-            ns = NQ
-            t0 = time.perf_counter()
-            for _ in range(reps):
-                oi, od, on, ost = ref.search_batch(queries, K, args.ef, threads=threads)
-            cpu_t = (time.perf_counter() - t0) / reps
-            # algorithmic bytes from the restatement's own count of distance
-            # evaluations E and expansions X on the same graph / queries / ef
-            # (SURVEY 8d), not from the GPU's counters
-            e, x = ost["dist_evals"], ost["expansions"]
-            by = 4.0 * D * e + 4.0 * 2 * args.M * x
-            hnsw_ms = result["roofline"]["kernel_ms"]
-            achieved = by / (hnsw_ms * 1e-3) / 1e9
-            result["roofline"].update({"achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4),
-                                       "counts_from": "CPU restatement (oracle/) on the same graph",
-                                       "dist_evals_per_query": round(e / NQ, 1),
-                                       "expansions_per_query": round(x / NQ, 1),
-                                       "gpu_dist_evals_per_query": result["roofline"]["dist_evals_per_query"]})
-            kind_desc = "knnSearchByVector restated in C on the same graph (oracle/)"
-            same = float((oi == final_ids[:ns]).mean())
-            _, dist_same, tie_ok = parity_stats(final_ids[:ns], final_d[:ns], oi, od)
-            nt = min(NQ, 1000)   # exact truths for recall on a sample
-            ti, td, tn = O.flat_scan(metric_id, base, queries[:nt], K, threads=threads)
-            rec_gpu = float(np.mean([len(set(a) & set(b)) / K for a, b in zip(final_ids[:nt].tolist(), ti.tolist())]))
-            rec_cpu = float(np.mean([len(set(a) & set(b)) / K for a, b in zip(oi[:nt].tolist(), ti.tolist())]))
-            result["parity_sample"] = {"queries": ns, "id_match_frac": same, "dists_bitwise_equal_frac": dist_same,
-                                       "tie_aware_identical_frac": tie_ok, "recall@10_gpu": rec_gpu,
-                                       "recall@10_cpu_restatement": rec_cpu, "recall_sample": nt}
-        result["cpu_baseline"] = {"value": round(ns / cpu_t, 1), "unit": "queries/s", "cores": threads,
-                                  "kind": "port",
-                                  "sample": f"{ns} of the {NQ} queries over the full {N:,}-row corpus "
-                                            f"({cpu_t:.2f} s per pass{'' if mode == 'exact' else f' x {reps} passes'}, "
-                                            f"{threads} threads, GOMAXPROCS-equivalent); "
-                                            + kind_desc}
+            st["ix"].close()
+        if not args.no_hnsw_line and args.metric == "l2-squared":
+            h = run_hnsw(args, ctx, W, with_cpu)
+            h.pop("metric", None)
+            result["hnsw_c1"] = h
     if rank == 0:
         print(json.dumps(result), flush=True)
-    ix.close()
     if ws > 1:
-        dist.destroy_process_group()
+        ctx.dist.destroy_process_group()
 
 
 if __name__ == "__main__":

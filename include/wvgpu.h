@@ -97,8 +97,12 @@ int wv_index_upload_vectors_device(wv_index *ix, const float *d_rows, uint64_t n
  *   levels[n]                 node level, -1 for nil nodes
  *   layer0[n*deg0]            layer-0 neighbours in stored order, pad 0xFFFFFFFF
  *   upper_row[n]              row of the node in `upper` (0xFFFFFFFF if level 0)
- *   upper[n_upper*max_level*degU]  neighbours at level l in row[l-1]
- * deg0 <= 256 and degU <= 256. */
+ *   upper[n_upper*max_level*degU]  neighbours at level l in row[l-1]; the
+ *                             level stride is exactly max_level (lists above
+ *                             max_level are never searched, search.go:479)
+ * deg0 <= 256 and degU <= 256.  A nil entrypoint returns WV_EDELETED
+ * (search.go:473-476); an entrypoint whose level is below max_level is legal
+ * and is skipped at the layers above its level (search.go:226-233). */
 int wv_index_upload_graph(wv_index *ix, uint64_t n, const int8_t *levels, const uint32_t *layer0, int deg0,
                           const uint32_t *upper_row, const uint32_t *upper, uint64_t n_upper, int degU,
                           int max_level, uint64_t entrypoint);
@@ -159,8 +163,10 @@ int wv_index_download_pq_codes(wv_index *ix, uint16_t *out, uint64_t first_id, u
 /* compressed on/off (h.compressed); on requires a code for every row holding a vector */
 int wv_index_set_compressed(wv_index *ix, int on);
 
-/* searchTimeEF (search.go:30-62) for the current config. */
+/* searchTimeEF (search.go:30-62) for the current config; the same rule for a
+ * config without an index (no device needed). */
 int wv_search_time_ef(const wv_index *ix, int k);
+int wv_config_search_time_ef(const wv_config *cfg, int k);
 
 /* SearchByVector (search.go:64-79). out_ids/out_dists have room for k;
  * *out_n receives the count (0 for an empty index). */
@@ -180,14 +186,17 @@ int wv_search_batch(wv_index *ix, const float *queries, int nq, int k, int ef, c
                     uint64_t allow_nbits, uint64_t allow_stride_words, int mode, uint64_t *out_ids,
                     float *out_dists, int32_t *out_n);
 
-/* Device-resident variant: every pointer is device memory; the call is
- * asynchronous on `stream` (a hipStream_t, NULL = the index's own stream) and
- * needs no host synchronisation except for queries that fall back to the
- * exact re-scan (reported through *d_status).  Used by the benchmark so that
- * the timed region sees only device work. */
+/* Device-resident variant: every pointer is device memory.  d_queries holds
+ * nq rows at a stride of wv_index_query_ld(ix) floats (dim rounded up to 4;
+ * the pad columns are ignored).  The work is queued on `stream` (a
+ * hipStream_t, NULL = the index's own stream) and ordered after every earlier
+ * call on the index; later calls on the index are ordered after it.  Used by
+ * the benchmark so that the timed region sees only device work. */
 int wv_search_batch_device(wv_index *ix, const float *d_queries, int nq, int k, int ef,
                            const uint64_t *d_allow_bits, uint64_t allow_nbits, uint64_t allow_stride_words,
                            int mode, uint64_t *d_out_ids, float *d_out_dists, int32_t *d_out_n, void *stream);
+/* Row stride (floats) of the device query rows wv_search_batch_device reads. */
+int wv_index_query_ld(const wv_index *ix);
 
 /* Merge per-shard results: for each query, the k best (dist, id) of the
  * n_shards lists d_in_*[shard][nq][k] (entries beyond d_in_n are ignored).

@@ -32,6 +32,25 @@ def test_config_defaults_match_reference():
             c.flat_search_cutoff, c.forbid_flat) == (64, -1, 100, 500, 8, 40000, 0)
 
 
+def test_search_time_ef_abi_matches_dynamic_ef_kats(kats):
+    """searchTimeEF / autoEfFromK (search.go:30-62) through the C ABI,
+    against dynamic_ef_test.go:27-102 (k=100 -> 500, 10 -> 100, 23 -> 184,
+    explicit ef 78) and the oracle on a grid around the clamps."""
+    import ctypes as C
+    from weaviate_amd._lib import WvConfig
+    for c in kats["dynamic_ef"]["cases"]:
+        cfg = WvConfig()
+        W.lib().wv_config_default(C.byref(cfg))
+        cfg.ef, cfg.dynamic_ef_min, cfg.dynamic_ef_max, cfg.dynamic_ef_factor = c["ef"], c["min"], c["max"], c["factor"]
+        assert W.lib().wv_config_search_time_ef(C.byref(cfg), c["k"]) == c["expect"], c
+    for ef in (-1, 0, 1, 7, 64, 600):
+        for k in (1, 5, 10, 13, 50, 62, 63, 100, 700):
+            cfg = WvConfig()
+            W.lib().wv_config_default(C.byref(cfg))
+            cfg.ef = ef
+            assert W.lib().wv_config_search_time_ef(C.byref(cfg), k) == O.search_time_ef(ef, 100, 500, 8, k)
+
+
 def test_bad_arguments_return_errors_not_crashes():
     import ctypes as C
     h = C.c_void_p()

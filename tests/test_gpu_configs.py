@@ -1,0 +1,250 @@
+"""Parity at the BASELINE configs' own parameters (-m gpu).
+
+Each test runs the HIP path through the C ABI at the graph / data shape a
+headline number is quoted on, scaled down so the CPU restatement (oracle/)
+finishes in seconds:
+
+  configs[0]  SIFT-shaped 128-d L2, hnsw M=64 (layer-0 degree 128 fills the
+              kernel's 128-slot neighbour batch), efConstruction=128, ef=64
+  configs[2]  GloVe-shaped 100-d cosine (ldx 128 vs dpad 100), ef 128 / 256
+              (the largest LDS beams, the visited cache squeezed)
+  configs[4]  Deep-shaped 96-d L2, two id-range shards with their own graphs,
+              merged on the device (index.go:967-1044)
+  configs[3]/(e)  two processes on the GPU, each searching its shard through
+              libwvgpu.so, all-gathered (gloo) and merged by the device kernel:
+              identical to one search of the whole corpus
+
+plus SearchByVector's dispatch (flat vs HNSW by flatSearchCutoff,
+search.go:64-79) and searchTimeEF's default ef through the ABI.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import pyoracle as O
+import weaviate_amd as W
+from bench import counter_gauss, counter_sift, counter_uniform
+from helpers import merge_lists, recall, same, same_tie_aware, tie_aware_equal
+
+pytestmark = pytest.mark.gpu
+
+THREADS = 16
+
+
+def _unexplained(ref, qs, k, ef, gi, gd, oi, od):
+    """Queries whose GPU answer differs from the restatement's beyond tie
+    order, although the restatement took no decision between equal distances
+    (the reference orders equal distances by heap layout)."""
+    bad = []
+    for i in range(len(qs)):
+        if not tie_aware_equal(gi[i], gd[i], oi[i], od[i]):
+            if ref.knn_search(qs[i], k, ef, with_stats=True)[2]["ties"] == 0:
+                bad.append(i)
+    return bad
+
+
+def test_configs0_sift_hnsw_m64_efc128_ef64():
+    """configs[0]: maxConnections=64 -> layer-0 lists of up to 128 ids, two per
+    lane of the neighbour batch; recall within 0.5 pt of the restatement."""
+    n, d, nq, k, ef = 24000, 128, 600, 10, 64
+    base = counter_sift(1, 0, n, d)
+    qs = counter_sift(2, 0, nq, d)
+    ref = O.Index(d, "l2-squared", 64, 128, capacity=n, seed=1)
+    ref.add_batch(base, threads=THREADS)
+    g = ref.export_graph()
+    assert g["deg0"] == 128 and int(g["counts0"].max()) > 64   # rows longer than one lane's slot
+    ix = W.GPUVectorIndex(d, "l2-squared", capacity=n, max_connections=64)
+    ix.upload_vectors(base)
+    ix.upload_graph(g)
+    gi, gd, gn = ix.search_batch(qs, k, ef=ef, mode="hnsw")
+    oi, od, on, _ = ref.search_batch(qs, k, ef, threads=THREADS)
+    assert gn.tolist() == on.tolist()
+    assert not _unexplained(ref, qs, k, ef, gi, gd, oi, od)
+    truth, _, _ = O.flat_scan(O.L2, base, qs, k, threads=THREADS)
+    r_gpu, r_cpu = recall(gi, truth), recall(oi, truth)
+    assert abs(r_gpu - r_cpu) <= 0.005, (r_gpu, r_cpu)
+    assert r_gpu >= 0.95, r_gpu
+    ix.close()
+
+
+@pytest.mark.parametrize("ef", [128, 256])
+def test_configs2_glove_cosine_d100_large_ef(ef):
+    """configs[2]: 100-d cosine (stored rows normalized on upload, queries
+    per search), ef at the top of the sweep."""
+    n, d, nq, k = 20000, 100, 300, 10
+    base = counter_gauss(1, 0, n, d)
+    qs = counter_gauss(2, 0, nq, d)
+    ref = O.Index(d, "cosine-dot", 32, 128, capacity=n, seed=2)
+    ref.add_batch(base, threads=THREADS)
+    ix = W.GPUVectorIndex(d, "cosine-dot", capacity=n, max_connections=32)
+    ix.upload_vectors(base)
+    ix.upload_graph(ref.export_graph())
+    gi, gd, gn = ix.search_batch(qs, k, ef=ef, mode="hnsw")
+    oi, od, on, _ = ref.search_batch(qs, k, ef, threads=THREADS)
+    assert gn.tolist() == on.tolist()
+    assert not _unexplained(ref, qs, k, ef, gi, gd, oi, od)
+    assert ix.last_batch_stats()["fallbacks"] == 0
+    truth, _, _ = O.flat_scan(O.COSINE, O.normalize_rows(base), O.normalize_rows(qs), k, threads=THREADS)
+    assert abs(recall(gi, truth) - recall(oi, truth)) <= 0.005
+    ix.close()
+
+
+def test_configs4_deep_d96_two_shards_device_merge():
+    """configs[4] scaled down: 96-d L2 over two id-range shards, each with its
+    own graph (M=64, efC=128) and index (id_base), searched with ef=64 and
+    merged on the device == the restatement's per-shard searches merged."""
+    import torch
+    n, d, nq, k, ef = 16000, 96, 400, 10, 64
+    base = O.normalize_rows(counter_gauss(1, 0, n, d))
+    qs = O.normalize_rows(counter_gauss(2, 0, nq, d))
+    gpu_parts, ref_parts, refs = [], [], []
+    for lo, hi in ((0, n // 2), (n // 2, n)):
+        ref = O.Index(d, "l2-squared", 64, 128, capacity=hi - lo, seed=3 + lo)
+        ref.add_batch(base[lo:hi], threads=THREADS)
+        sh = W.GPUVectorIndex(d, "l2-squared", capacity=hi - lo, max_connections=64, id_base=lo)
+        sh.upload_vectors(base[lo:hi])
+        sh.upload_graph(ref.export_graph())
+        gi, gd, gn = sh.search_batch(qs, k, ef=ef, mode="hnsw")
+        oi, od, on, _ = ref.search_batch(qs, k, ef, threads=THREADS)
+        assert not _unexplained(ref, qs, k, ef, gi - np.uint64(lo), gd, oi, od)
+        gpu_parts.append((gi, gd, gn))
+        ref_parts.append((oi + np.uint64(lo), od, on))
+        sh.close()
+    dev = torch.device("cuda:0")
+    g_i = torch.from_numpy(np.stack([p[0] for p in gpu_parts]).view(np.int64)).to(dev)
+    g_d = torch.from_numpy(np.stack([p[1] for p in gpu_parts])).to(dev)
+    g_n = torch.from_numpy(np.stack([p[2] for p in gpu_parts])).to(dev)
+    m_d = torch.empty((nq, k), dtype=torch.float32, device=dev)
+    m_i = torch.empty((nq, k), dtype=torch.int64, device=dev)
+    m_n = torch.empty(nq, dtype=torch.int32, device=dev)
+    W.merge_shards_device(g_d.data_ptr(), g_i.data_ptr(), g_n.data_ptr(), 2, nq, k, m_d.data_ptr(), m_i.data_ptr(),
+                          m_n.data_ptr())
+    torch.cuda.synchronize()
+    mi, md, mn = m_i.cpu().numpy().view(np.uint64), m_d.cpu().numpy(), m_n.cpu().numpy()
+    wi, wd, wn = merge_lists(gpu_parts, k)
+    same(mi, md, wi, wd)                       # the device merge == (dist, id) merge
+    ri, rd, rn = merge_lists(ref_parts, k)
+    assert mn.tolist() == rn.tolist()
+    n_tie = sum(not tie_aware_equal(mi[i], md[i], ri[i], rd[i]) for i in range(nq))
+    assert n_tie <= nq // 100, n_tie           # only tie-order decisions (checked per shard above)
+
+
+def _gloo_rank(rank, world, port, n, d, nq, k, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    from weaviate_amd.sharded import allgather_topk, merge_topk, shard_bounds
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        base = counter_uniform(1, 0, n, d)
+        qs = counter_uniform(2, 0, nq, d)
+        lo, hi = shard_bounds(n, rank, world)
+        ix = W.GPUVectorIndex(d, "l2-squared", capacity=hi - lo, id_base=lo, device=0)
+        ix.upload_vectors(base[lo:hi])
+        ids, ds, cnt = ix.search_batch(qs, k, mode="exact")        # HIP key pass + exact re-rank
+        g_ids, g_d, g_n = allgather_topk(torch.from_numpy(ids.view(np.int64)), torch.from_numpy(ds),
+                                         torch.from_numpy(cnt), world)
+        dev = torch.device("cuda", 0)
+        m_ids, m_d, m_n = merge_topk(g_ids.to(dev), g_d.to(dev), g_n.to(dev), k)   # device merge kernel
+        torch.cuda.synchronize()
+        q.put((rank, m_ids.cpu().numpy().view(np.uint64), m_d.cpu().numpy(), m_n.cpu().numpy()))
+        ix.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_processes_on_gpu_gloo_shards_equal_single_search():
+    """(e): two ranks (one process each, both on this GPU) search their id
+    range through libwvgpu.so; the gathered [world, nq, k] lists merged by the
+    device kernel equal a single-index search of the whole corpus, bit for bit."""
+    import multiprocessing as mp
+    n, d, nq, k, world = 40000, 128, 300, 10, 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_gloo_rank, args=(r, world, port, n, d, nq, k, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=100) for _ in range(world)]
+    for p in ps:
+        p.join(30)
+        assert p.exitcode == 0
+    base = counter_uniform(1, 0, n, d)
+    qs = counter_uniform(2, 0, nq, d)
+    ix = W.GPUVectorIndex(d, "l2-squared", capacity=n)
+    ix.upload_vectors(base)
+    si, sd, sn = ix.search_batch(qs, k, mode="exact")
+    ix.close()
+    oi, od, on = O.flat_scan(O.L2, base, qs, k, threads=THREADS)
+    same(si, sd, oi, od)
+    for rank, mi, md, mn in res:
+        assert mn.tolist() == sn.tolist()
+        same(mi, md, si, sd)
+
+
+def _graph(n, d, metric, M=16, efc=64, seed=11):
+    base = counter_uniform(seed, 0, n, d)
+    ref = O.Index(d, metric, M, efc, capacity=n, seed=seed)
+    ref.add_batch(base, threads=THREADS)
+    return base, ref
+
+
+@pytest.mark.parametrize("forbid_flat", [False, True])
+def test_auto_dispatch_flat_cutoff_matches_restatement(forbid_flat):
+    """SearchByVector (search.go:64-79): an allow list shorter than
+    flatSearchCutoff is answered by flatSearch, otherwise (or with forbidFlat)
+    knnSearchByVector with searchTimeEF(k) -- per query, through
+    wv_search_by_vector and through one AUTO batch of mixed lists."""
+    n, d, k, cut = 6000, 32, 10, 1500
+    base, ref = _graph(n, d, "l2-squared")
+    ref.set_search_config(flat_search_cutoff=cut, forbid_flat=forbid_flat)
+    ix = W.GPUVectorIndex(d, "l2-squared", capacity=n, max_connections=16, flat_search_cutoff=cut,
+                          forbid_flat=forbid_flat)
+    ix.upload_vectors(base)
+    ix.upload_graph(ref.export_graph())
+    rng = np.random.default_rng(5)
+    sizes = [200, cut - 1, cut, cut + 1, 3000, 5999]
+    qs = counter_uniform(12, 0, 4 * len(sizes), d)
+    allows = [W.AllowList.from_ids(rng.choice(n, sizes[i % len(sizes)], replace=False), n) for i in range(len(qs))]
+    assert sorted({len(a) for a in allows}) == sorted(sizes)
+    want = []
+    for q, al in zip(qs, allows):
+        ri, rd = ref.search_by_vector(q, k, allow=al.words)
+        gi, gd = ix.search_by_vector(q, k, allow=al)
+        same(gi, gd, ri, rd)
+        want.append((ri, rd))
+    bi, bd, bn = ix.search_batch(qs, k, allow=allows, mode="auto")
+    for i, (ri, rd) in enumerate(want):
+        same(bi[i, : bn[i]], bd[i, : bn[i]], ri, rd)
+    # unfiltered: always the graph (search.go:74-78)
+    ui, ud = ix.search_by_vector(qs[0], k)
+    ri, rd = ref.search_by_vector(qs[0], k)
+    same(ui, ud, ri, rd)
+    ix.close()
+
+
+def test_default_ef_through_the_abi_matches_restatement():
+    """ef = -1 (the default): the search runs with searchTimeEF(k) =
+    clamp(k * 8, 100, 500) (search.go:30-62) -- checked on the index's own
+    entry point and on the results of an ef=0 batch."""
+    n, d = 5000, 24
+    base, ref = _graph(n, d, "l2-squared", seed=13)
+    ix = W.GPUVectorIndex(d, "l2-squared", capacity=n, max_connections=16)
+    ix.upload_vectors(base)
+    ix.upload_graph(ref.export_graph())
+    assert [ix.search_time_ef(k) for k in (10, 23, 100)] == [100, 184, 500]
+    qs = counter_uniform(14, 0, 100, d)
+    for k in (10, 23):
+        gi, gd, gn = ix.search_batch(qs, k, ef=0, mode="hnsw")
+        oi, od, on, _ = ref.search_batch(qs, k, O.search_time_ef(-1, 100, 500, 8, k), threads=THREADS)
+        same(gi, gd, oi, od)
+        for i in range(0, len(qs), 10):
+            ri, rd = ref.search_by_vector(qs[i], k)
+            same(gi[i], gd[i], ri, rd)
+    ix.update_user_config(ef=78)
+    assert ix.search_time_ef(5) == 78
+    ix.close()

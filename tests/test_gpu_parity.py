@@ -443,6 +443,56 @@ def test_graph_replayed_from_commit_log_serves_identical_searches():
     ix.close()
 
 
+def test_commit_log_node_above_entrypoint_level_keeps_upper_layout():
+    """A log whose highest node level exceeds the entrypoint's max level (an
+    AddNode above the top with its SetEntryPointWithMaxLayer torn off,
+    insert.go:206): the exported CSR's level stride (max node level) differs
+    from max_level, and the upload must re-lay it so every upper list is read
+    at the right offset -- searches equal those over the in-memory graph."""
+    import struct
+    n, d = 3000, 16
+    rng = np.random.default_rng(43)
+    base = rng.random((n, d), dtype=np.float32)
+    qs = rng.random((100, d), dtype=np.float32)
+    ref = O.Index(d, "l2-squared", 8, 32, capacity=n, seed=3)
+    ref.enable_commit_log()
+    ref.add_batch(base, threads=1)
+    top = ref.export_graph()["max_level"]
+    assert top >= 1
+    torn = struct.pack("<BQH", 0, n, top + 2)          # AddNode(n, top + 2), no SetEntryPoint after it
+    g = W.CommitLogGraph(ref.commit_log() + torn)
+    assert g.info()["max_node_level"] == top + 2 and g.info()["max_level"] == top
+    ix = W.GPUVectorIndex(d, "l2-squared", capacity=n + 1, max_connections=8)
+    ix.upload_vectors(base)
+    ix.upload_graph_from_commitlog(g)
+    ids, ds, _ = ix.search_batch(qs, 10, ef=32, mode="hnsw")
+    oi, od, on, _ = ref.search_batch(qs, 10, 32)
+    _same(ids, ds, oi, od)
+    ix.close()
+
+
+def test_add_with_repeated_ids_keeps_the_last_row():
+    """hnsw.Add applies writes one after another (insert.go:43-65): a batch
+    that repeats an id stores its last row (and that row's |x|^2, which the
+    exact path's certificate relies on)."""
+    n, d = 2000, 32
+    rng = np.random.default_rng(44)
+    base = rng.random((n, d), dtype=np.float32)
+    ix = W.GPUVectorIndex(d, "l2-squared", capacity=n)
+    ix.upload_vectors(base[:1000])
+    ids = np.array([1000 + (i % 50) for i in range(200)], np.uint64)     # every id four times
+    rows = rng.random((200, d), dtype=np.float32)
+    ix.add(ids, rows)
+    final = base.copy()
+    for i, r in zip(ids.tolist(), rows):
+        final[i] = r
+    qs = rows[150:] + np.float32(1e-3)                                  # near the last writes
+    gi, gd, _ = ix.search_batch(qs, 10, mode="exact")
+    oi, od, _ = O.flat_scan(O.L2, final[:1050], qs, 10)
+    _same(gi, gd, oi, od)
+    ix.close()
+
+
 def test_allow_list_compaction_equals_masking():
     """A shared allow list under half the corpus is compacted into a row list
     (contraction over |allow| rows); the masked full scan must agree bit for
@@ -574,12 +624,12 @@ def test_gpu_graph_build_invariants_and_recall():
     batches) keeps the reference's invariants -- layer-0 degree <= 2M, upper
     <= M (index_too_many_links_bug_integration_test.go:127-143), valid ids, no
     self links, the entrypoint on the top level -- reaches the recall of the
-    restatement's sequential build within 2 points, and the restatement
+    restatement's sequential build within 0.5 points, and the restatement
     searching the GPU-built graph answers exactly like the GPU does."""
     n, d, M, efc, ef = 20000, 32, 16, 64, 64
     rng = np.random.default_rng(61)
     base = rng.random((n, d), dtype=np.float32)
-    qs = rng.random((300, d), dtype=np.float32)
+    qs = rng.random((1000, d), dtype=np.float32)
     ix = W.GPUVectorIndex(d, "l2-squared", capacity=n, max_connections=M)
     ix.upload_vectors(base)
     ix.build_graph(ef_construction=efc, seed=7, batch_div=32)
@@ -600,7 +650,8 @@ def test_gpu_graph_build_invariants_and_recall():
     assert np.array_equal(ref.export_graph()["levels"][1:], lv[1:])   # same level draw (insert.go:132)
     oi, od, on, _ = ref.search_batch(qs, 10, ef, threads=8)
     r_gpu, r_cpu = _recall(gi, truth), _recall(oi, truth)
-    assert r_gpu >= r_cpu - 0.02, (r_gpu, r_cpu)
+    # north_star: HNSW recall within 0.5 pt of the reference index on the same data and ef
+    assert r_gpu >= r_cpu - 0.005, (r_gpu, r_cpu)
     # the restatement on the GPU-built graph == the GPU on it
     ref2 = O.Index(d, "l2-squared", M, efc, capacity=n, seed=7)
     ref2.import_graph(base, g)

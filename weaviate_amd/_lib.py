@@ -77,6 +77,7 @@ SIGNATURES = {
                                         C.c_uint64]),
     "wv_index_set_tombstones": (C.c_int, [_vp, _vp, C.c_uint64]),
     "wv_search_time_ef": (C.c_int, [_vp, C.c_int]),
+    "wv_config_search_time_ef": (C.c_int, [C.POINTER(WvConfig), C.c_int]),
     "wv_index_add": (C.c_int, [_vp, _vp, _vp, C.c_uint64]),
     "wv_index_build_graph": (C.c_int, [_vp, C.c_int, C.c_uint64, C.c_int]),
     "wv_index_graph_info": (C.c_int, [_vp, _u64p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int), _u64p,
@@ -98,6 +99,7 @@ SIGNATURES = {
                                   _vp]),
     "wv_search_batch_device": (C.c_int, [_vp, _vp, C.c_int, C.c_int, C.c_int, _vp, C.c_uint64, C.c_uint64, C.c_int,
                                          _vp, _vp, _vp, _vp]),
+    "wv_index_query_ld": (C.c_int, [_vp]),
     "wv_merge_shards_device": (C.c_int, [_vp, _vp, _vp, C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp]),
     "wv_last_batch_stats": (C.c_int, [_vp, _u64p, _u64p, _u64p]),
     "wv_index_set_timing": (C.c_int, [_vp, C.c_int]),

@@ -239,6 +239,11 @@ struct wv_index {
     DevBuf pk_key, pk_dist, pk_val, pk_skey, pk_sval, pk_off;
     // stats of the last batch
     uint64_t last_dist = 0, last_exp = 0, last_fallbacks = 0;
+    // ordering of work on a caller's stream (wv_search_batch_device) against
+    // the index's own stream: the call waits for ix->stream, and ix->stream
+    // then waits for the call, so the scratch and state buffers the call reads
+    // are never rewritten by a later call while it is still queued
+    hipEvent_t ev_in = nullptr, ev_out = nullptr;
     // optional kernel timing (hipEvents on the launch stream)
     bool timing = false;
     hipEvent_t ev[6] = {};
@@ -1060,8 +1065,11 @@ int wv_index_destroy(wv_index* ix) {
                       &ix->ac_cnt, &ix->ac_off, &ix->rowidx, &ix->pq_cent, &ix->pq_codes, &ix->pk_key,
                       &ix->pk_dist, &ix->pk_val, &ix->pk_skey, &ix->pk_sval, &ix->pk_off})
         b->release();
+    if (ix->stream) (void)hipStreamSynchronize(ix->stream);
     for (auto& e : ix->ev)
         if (e) (void)hipEventDestroy(e);
+    if (ix->ev_in) (void)hipEventDestroy(ix->ev_in);
+    if (ix->ev_out) (void)hipEventDestroy(ix->ev_out);
     if (ix->stream) (void)hipStreamDestroy(ix->stream);
     delete ix;
     return WV_OK;
@@ -1150,6 +1158,13 @@ int wv_index_upload_graph(wv_index* ix, uint64_t n, const int8_t* levels, const 
     if (n == 0 || n > ix->capacity || !levels || !layer0 || deg0 <= 0 || deg0 > 256 || max_level < 0 ||
         entrypoint >= n || (max_level > 0 && (!upper_row || !upper || degU <= 0 || degU > 256)))
         return fail(WV_EINVAL, "wv_index_upload_graph: bad argument");
+    // A nil entrypoint is the reference's "entrypoint was deleted"
+    // (search.go:473-476).  An entrypoint below max_level is legal: the
+    // descent skips a node whose level is below the layer (search.go:226-233),
+    // as after deleteEntrypoint wrote the lower level first (delete.go:405-414).
+    // Checked before any loop reads `upper`, whose size is n_upper * max_level
+    // * degU: the caller's array must have exactly that level stride.
+    if (levels[entrypoint] < 0) return fail(WV_EDELETED, "wv_index_upload_graph: entrypoint is a nil node");
     std::lock_guard<std::mutex> g(ix->mu);
     HIP_TRY(hipSetDevice(ix->cfg.device));
     // validate neighbour ids on the host once (a bad id would fault the kernel)
@@ -1163,7 +1178,6 @@ int wv_index_upload_graph(wv_index* ix, uint64_t n, const int8_t* levels, const 
         for (uint64_t i = 0; i < n_upper * (uint64_t)max_level * degU; ++i)
             if (upper[i] != WV_NIL && upper[i] >= n) return fail(WV_EINVAL, "upper neighbour out of range");
     }
-    if (levels[entrypoint] < max_level) return fail(WV_EINVAL, "entrypoint below max level");
     HIP_TRY(ix->levels.ensure(n));
     HIP_TRY(ix->layer0.ensure(n * (size_t)deg0 * 4));
     HIP_TRY(ix->upper_row.ensure(n * 4));
@@ -1215,12 +1229,41 @@ __global__ void scatter_rows_kernel(const float* src, int ld_src, const uint64_t
     if (threadIdx.x == 0) xnorm[id] = norms[r];
 }
 
-int wv_index_add(wv_index* ix, const uint64_t* ids, const float* rows, uint64_t n) {
-    if (check(ix) || (n && (!ids || !rows))) return fail(WV_EINVAL, "wv_index_add: bad argument");
-    if (n == 0) return WV_OK;
+int wv_index_add(wv_index* ix, const uint64_t* ids_in, const float* rows_in, uint64_t n_in) {
+    if (check(ix) || (n_in && (!ids_in || !rows_in))) return fail(WV_EINVAL, "wv_index_add: bad argument");
+    if (n_in == 0) return WV_OK;
+    for (uint64_t i = 0; i < n_in; ++i)
+        if (ids_in[i] >= ix->capacity) return fail(WV_EINVAL, "wv_index_add: id beyond capacity");
+    // The reference applies Adds one after another, so the last write of a
+    // repeated id wins (insert.go:43-65).  One scatter block per distinct id:
+    // two blocks writing one row would leave a mix of both rows, and its |x|^2
+    // (which the finalize certificate relies on) from either.
+    std::vector<uint64_t> ids_v;
+    std::vector<float> rows_v;
+    const uint64_t* ids = ids_in;
+    const float* rows = rows_in;
+    uint64_t n = n_in;
+    {
+        std::vector<uint64_t> sorted(ids_in, ids_in + n_in);
+        std::sort(sorted.begin(), sorted.end());
+        if (std::adjacent_find(sorted.begin(), sorted.end()) != sorted.end()) {
+            std::vector<uint64_t> last_pos;   // positions of the last occurrence, in input order
+            std::vector<uint8_t> seen(ix->bm_words * 64, 0);
+            for (uint64_t i = n_in; i-- > 0;)
+                if (!seen[ids_in[i]]) { seen[ids_in[i]] = 1; last_pos.push_back(i); }
+            std::reverse(last_pos.begin(), last_pos.end());
+            ids_v.resize(last_pos.size());
+            rows_v.resize(last_pos.size() * (size_t)ix->dim);
+            for (size_t j = 0; j < last_pos.size(); ++j) {
+                ids_v[j] = ids_in[last_pos[j]];
+                std::memcpy(rows_v.data() + j * ix->dim, rows_in + last_pos[j] * ix->dim, ix->dim * sizeof(float));
+            }
+            ids = ids_v.data();
+            rows = rows_v.data();
+            n = ids_v.size();
+        }
+    }
     std::lock_guard<std::mutex> g(ix->mu);
-    for (uint64_t i = 0; i < n; ++i)
-        if (ids[i] >= ix->capacity) return fail(WV_EINVAL, "wv_index_add: id beyond capacity");
     HIP_TRY(hipSetDevice(ix->cfg.device));
     hipStream_t s = ix->stream;
     // rows -> [n][ldx] padded (normalized for cosine, insert.go:56-60), their
@@ -1624,6 +1667,7 @@ int wv_index_set_compressed(wv_index* ix, int on) {
 }
 
 int wv_search_time_ef(const wv_index* ix, int k) { return ix ? search_time_ef(ix->cfg, k) : -1; }
+int wv_config_search_time_ef(const wv_config* cfg, int k) { return cfg ? search_time_ef(*cfg, k) : -1; }
 
 int wv_search_batch(wv_index* ix, const float* queries, int nq, int k, int ef, const uint64_t* allow_bits,
                     uint64_t allow_nbits, uint64_t allow_stride_words, int mode, uint64_t* out_ids, float* out_dists,
@@ -1677,7 +1721,17 @@ int wv_search_batch_device(wv_index* ix, const float* d_queries, int nq, int k, 
     std::lock_guard<std::mutex> g(ix->mu);
     HIP_TRY(hipSetDevice(ix->cfg.device));
     hipStream_t s = stream ? (hipStream_t)stream : ix->stream;
+    const bool foreign = s != ix->stream;
+    if (foreign) {
+        if (!ix->ev_in) {
+            HIP_TRY(hipEventCreateWithFlags(&ix->ev_in, hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&ix->ev_out, hipEventDisableTiming));
+        }
+        HIP_TRY(hipEventRecord(ix->ev_in, ix->stream));
+        HIP_TRY(hipStreamWaitEvent(s, ix->ev_in, 0));
+    }
     const float* dq = d_queries;
+    int rc = WV_OK;
     if (ix->metric == WV_COSINE_DOT) {
         // the caller's rows are [nq][dpad]; normalize a padded copy
         HIP_TRY(ix->q_norm.ensure((size_t)nq * ix->dpad * 4));
@@ -1685,9 +1739,16 @@ int wv_search_batch_device(wv_index* ix, const float* d_queries, int nq, int k, 
         HIP_TRY(wv_launch_normalize(ix->q_norm.as<float>(), ix->q_norm.as<float>(), nq, ix->dim, ix->dpad, s));
         dq = ix->q_norm.as<float>();
     }
-    return search_core(ix, dq, nq, k, ef, d_allow_bits, allow_nbits, allow_stride_words, mode, d_out_ids, d_out_dists,
-                       d_out_n, s);
+    rc = search_core(ix, dq, nq, k, ef, d_allow_bits, allow_nbits, allow_stride_words, mode, d_out_ids, d_out_dists,
+                     d_out_n, s);
+    if (foreign) {
+        HIP_TRY(hipEventRecord(ix->ev_out, s));
+        HIP_TRY(hipStreamWaitEvent(ix->stream, ix->ev_out, 0));
+    }
+    return rc;
 }
+
+int wv_index_query_ld(const wv_index* ix) { return ix ? ix->dpad : -1; }
 
 int wv_search_by_vector(wv_index* ix, const float* vector, int k, const uint64_t* allow_bits, uint64_t allow_nbits,
                         uint64_t* out_ids, float* out_dists, int32_t* out_n) {

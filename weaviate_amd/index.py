@@ -123,6 +123,18 @@ class GPUVectorIndex:
         layer0 = np.ascontiguousarray(g["layer0"], dtype=np.uint32)
         upper_row = np.ascontiguousarray(g["upper_row"], dtype=np.uint32)
         upper = np.ascontiguousarray(g["upper"], dtype=np.uint32)
+        if upper.ndim != 3:
+            raise WvError(1, "upper must be [n_upper][levels][degU]")
+        # The ABI's level stride of `upper` is max_level (the entrypoint's
+        # layer).  Levels above it are never searched -- the descent starts at
+        # max_level (search.go:479) -- so a wider array is cut and a narrower
+        # one padded with empty lists.
+        ml = int(g["max_level"])
+        if ml > 0 and upper.shape[1] != ml:
+            fixed = np.full((upper.shape[0], ml, upper.shape[2]), 0xFFFFFFFF, np.uint32)
+            keep = min(ml, upper.shape[1])
+            fixed[:, :keep, :] = upper[:, :keep, :]
+            upper = fixed
         check(lib().wv_index_upload_graph(self._h, g["n"], _ptr(levels), _ptr(layer0), layer0.shape[1],
                                           _ptr(upper_row), _ptr(upper), upper.shape[0], upper.shape[2],
                                           g["max_level"], g["entrypoint"]))
@@ -137,12 +149,28 @@ class GPUVectorIndex:
             raise WvError(4, "commit log holds a PQ-compressed index; the GPU path serves uncompressed vectors")
         m = self.cfg.max_connections
         g = graph.export_csr(max(2 * m, info["max_deg0"]), max(m, info["max_degU"], 1))
+        # export_csr lays `upper` out with a level stride of max(1,
+        # max_node_level), which differs from the entrypoint's max_level after
+        # a torn AddNode above the top (insert.go:206) or inside
+        # deleteEntrypoint's window (delete.go:405-414); upload_graph re-lays it
         self.upload_graph(g)
         check(lib().wv_index_set_tombstones(self._h, _ptr(g["tomb_bits"]), g["n"]))
 
     def build_graph(self, ef_construction: int = 128, seed: int = 1, batch_div: int = 32):
         """Build the HNSW graph of the uploaded rows on the GPU (wv_index_build_graph)."""
         check(lib().wv_index_build_graph(self._h, ef_construction, seed, batch_div))
+
+    def query_ld(self) -> int:
+        """Row stride (floats) of the device query rows search_batch_device reads."""
+        return lib().wv_index_query_ld(self._h)
+
+    def graph_info(self) -> dict:
+        n, ep, nu = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        d0, du, ml = C.c_int(), C.c_int(), C.c_int()
+        check(lib().wv_index_graph_info(self._h, C.byref(n), C.byref(d0), C.byref(du), C.byref(ml), C.byref(nu),
+                                        C.byref(ep)))
+        return dict(n=n.value, entrypoint=ep.value, max_level=ml.value, n_upper=nu.value, deg0=d0.value,
+                    degU=du.value)
 
     def download_graph(self) -> dict:
         """The index's graph in the upload_graph / export_graph layout."""
@@ -251,6 +279,8 @@ class GPUVectorIndex:
                                   allow: Optional[AllowList] = None, cap: int = 1 << 20):
         """SearchByVectorDistance (search.go:90-158)."""
         q = np.ascontiguousarray(vector, dtype=np.float32)
+        if q.size != self.dim:
+            raise WvError(1, f"vector lengths don't match: {q.size} vs {self.dim}")
         bits, nb, _ = self._allow_args(allow)
         ids = np.zeros(cap, np.uint64)
         ds = np.zeros(cap, np.float32)
