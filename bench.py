@@ -33,6 +33,7 @@ METRIC = "batched 10-NN QPS at recall@10≥0.95, 1M×128-d L2, on 1/2/4/8 MI355X
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 FP32_MFMA_PEAK_TF = 157.3    # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
 BF16_MFMA_PEAK_TF = 2500.0   # MI355X_MICROARCH.md: bf16 dense MFMA peak (no sparsity)
+F16_MFMA_PEAK_TF = 2500.0    # MI355X_MICROARCH.md: f16 MFMA runs at the bf16 rate (same cycles per instruction)
 
 
 def _par_rows(fn, seed: int, row0: int, nrows: int, dim: int, chunk: int = 1 << 16) -> np.ndarray:
@@ -248,21 +249,33 @@ def _oracle():
 
 def exact_roofline(args, ix, kern_ms, stats, D, n_allowed, n_local, NQ):
     mfma_ms = float(np.mean([k["bf_mfma_ms"] for k in kern_ms]))
+    seed_ms = float(np.mean([k.get("seed_ms", 0.0) for k in kern_ms]))
     flops = 2.0 * D * n_allowed * NQ    # algorithmic: 2*D*N_eff per query
     achieved = flops / (mfma_ms * 1e-3) / 1e12
-    # The key pass runs either as bf16x3 (default: hi*hi + hi*lo + lo*hi on
-    # v_mfma_f32_32x32x16_bf16, 3 bf16 products per fp32 product, so its
-    # fp32-equivalent ceiling is the bf16 dense peak / 3) or as fp32 MFMA
-    # (WV_BF_FP32=1).  achieved stays the algorithmic 2*D*N_eff per query.
-    split = not os.environ.get("WV_BF_FP32") and D <= 128 and 2 * n_allowed >= n_local
-    peak = BF16_MFMA_PEAK_TF / 3 if split else FP32_MFMA_PEAK_TF
-    kname = "wv_bf_split_kernel" if split else "wv_bf_mfma_kernel"
-    return {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 2), "peak": round(peak, 1),
-            "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
-            "key_pass": "bf16x3 (peak = bf16 dense / 3)" if split else "fp32 MFMA",
+    # Which key pass ran (wv_api.hip run_exact): the f16 pass (default, D <= 128,
+    # one v_mfma_f32_32x32x16_f16 product per fp32 product: peak = the dense
+    # f16 MFMA rate), the bf16x3 split pass (WV_BF_SPLIT=1: 3 bf16 products per
+    # fp32 product, peak = bf16 dense / 3) or the fp32 MFMA pass (WV_BF_FP32=1,
+    # D > 128, or a shared allow list compacted into a row list).
+    fp32 = bool(os.environ.get("WV_BF_FP32")) or D > 128
+    if os.environ.get("WV_BF_SPLIT") and not fp32:
+        kind = "split" if 2 * n_allowed >= n_local else "fp32"
+    elif not fp32:
+        kind = "h16" if 8 * n_allowed >= n_local else "fp32"
+    else:
+        kind = "fp32"
+    peak, kname, kp = {"h16": (F16_MFMA_PEAK_TF, "wv_bf_h16_kernel", "f16 MFMA keys (peak = f16 dense)"),
+                       "split": (BF16_MFMA_PEAK_TF / 3, "wv_bf_split_kernel", "bf16x3 (peak = bf16 dense / 3)"),
+                       "fp32": (FP32_MFMA_PEAK_TF, "wv_bf_mfma_kernel", "fp32 MFMA")}[kind]
+    roof = {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 2), "peak": round(peak, 1),
+            "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None, "key_pass": kp,
             "frac_of_fp32_mfma_peak": round(achieved / FP32_MFMA_PEAK_TF, 4), "kernel_ms": round(mfma_ms, 3),
             "finalize_ms": round(float(np.mean([k["bf_finalize_ms"] for k in kern_ms])), 3),
             "fallback_queries": stats["fallbacks"]}
+    if kind == "h16":
+        roof["seed_pass_ms"] = round(seed_ms, 3)
+        roof["achieved_incl_seed_pass"] = round(flops / ((mfma_ms + seed_ms) * 1e-3) / 1e12, 2)
+    return roof, kind
 
 
 def attach_traffic(roof, n_local, NQ, D, data):
@@ -342,9 +355,11 @@ def run_exact(args, ctx, W):
                         "corpus": f"corpus sharded over {ws} GPU(s) by id range" + (
                             ", RCCL all-gather of per-shard top-k + device merge" if ws > 1 else "")}[split],
     }
-    roof = exact_roofline(args, ix, kern_ms, stats, D, n_allowed, n_local, NQ)
+    roof, kind = exact_roofline(args, ix, kern_ms, stats, D, n_allowed, n_local, NQ)
     attach_traffic(roof, n_local, NQ, D, args.data)
     res["roofline"] = roof
+    res["dtype"] = {"h16": "f32 (f16 MFMA keys certified by an error bound, f32 reference-order re-rank)",
+                    "split": "f32 (bf16x3 MFMA keys, f32 re-rank)", "fp32": "f32"}[kind]
     state = dict(ix=ix, base=base, queries=queries, final_ids=final_ids, final_d=final_d, words=words,
                  n_allowed=n_allowed, lo=lo, n_local=n_local)
     return res, state
@@ -610,7 +625,7 @@ def main():
             "metric": METRIC, "value": e["value"], "unit": "queries/s", "n_gpus": ws, "devices": ctx.n_devices,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": e["ms_per_step"], "higher_is_better": True,
             "scaling": e["scaling"], "vs_baseline": None,
-            "dtype": "f32" if os.environ.get("WV_BF_FP32") else "f32 (bf16x3 MFMA keys, f32 re-rank)",
+            "dtype": e["dtype"],
             "data": "synthetic: counter-based %s float32 corpus (seed 1) and queries (seed 2)" % {
                 "uniform": "U[0,1)", "gauss": "N(0,1)/sqrt(D)",
                 "sift": "SIFT-shaped (1024 centres + 24-d latent + noise, non-negative integers)"}[args.data],

@@ -214,6 +214,9 @@ int wv_last_batch_stats(wv_index *ix, uint64_t *dist_evals, uint64_t *expansions
  * beam-search kernel (milliseconds, summed over the launches of the batch). */
 int wv_index_set_timing(wv_index *ix, int enable);
 int wv_last_kernel_times(wv_index *ix, float *bf_mfma_ms, float *bf_finalize_ms, float *hnsw_ms);
+/* The f16 key pass's seed pre-pass of the last batch (key pass over every
+ * 16th tile + its finalize), milliseconds; 0 when it did not run. */
+int wv_last_seed_time(wv_index *ix, float *seed_ms);
 
 /* HNSW commit log -> CSR.  Replays the write-ahead log a
  * Weaviate shard persists (adapters/repos/db/vector/hnsw/commitlog/logger.go

@@ -663,10 +663,11 @@ def test_gpu_graph_build_invariants_and_recall():
 
 @pytest.mark.parametrize("metric", [O.L2, O.DOT, O.COSINE])
 def test_split_key_pass_equals_fp32_key_pass(metric):
-    """The bf16x3 key pass (default) and the fp32 MFMA key pass (WV_BF_FP32=1)
-    only rank candidates; both re-rank in the reference's order, so ids and
-    distances agree bit for bit -- also on wide-range data (|x| up to 1e4),
-    where the split error bound of the certificate is largest."""
+    """The f16 key pass (default), the bf16x3 pass (WV_BF_SPLIT=1) and the fp32
+    MFMA key pass (WV_BF_FP32=1) only rank candidates; all re-rank in the
+    reference's order, so ids and distances agree bit for bit -- also on
+    wide-range data (|x| from 0.02 to 8e3), where the f16 scaling and the
+    error bound of the certificate are stretched most."""
     import os
     rng = np.random.default_rng(31 + metric)
     n, d = 15000, 128
@@ -674,19 +675,20 @@ def test_split_key_pass_equals_fp32_key_pass(metric):
     base = (rng.standard_normal((n, d)) * scale).astype(np.float32)
     qs = (rng.standard_normal((120, d)) * 30).astype(np.float32)
     out = []
-    for env in (None, "1"):
-        if env:
-            os.environ["WV_BF_FP32"] = env
+    for env in ({}, {"WV_BF_SPLIT": "1"}, {"WV_BF_FP32": "1"}):
+        os.environ.update(env)
         try:
             ix = W.GPUVectorIndex(d, METRIC_NAMES[metric], capacity=n)
         finally:
-            os.environ.pop("WV_BF_FP32", None)
+            for key in env:
+                os.environ.pop(key, None)
         ix.upload_vectors(base)
         out.append(ix.search_batch(qs, 10, mode="exact"))
         ix.close()
-    (ai, ad, an), (bi, bd, bn) = out
-    assert an.tolist() == bn.tolist()
-    _same(ai, ad, bi, bd)
+    (ai, ad, an) = out[0]
+    for (bi, bd, bn) in out[1:]:
+        assert an.tolist() == bn.tolist()
+        _same(ai, ad, bi, bd)
     b = O.normalize_rows(base) if metric == O.COSINE else base
     q = O.normalize_rows(qs) if metric == O.COSINE else qs
     oi, od, on = O.flat_scan(metric, b, q, 10)
@@ -718,10 +720,11 @@ def test_split_pass_query_blocks_multi_segment(dim, metric):
     oi, od, on = O.flat_scan(metric, b, q, 10, allow_bits=al.words, tomb_bits=tb)
     ui, ud, un = O.flat_scan(metric, b, q, 10, tomb_bits=tb)
     runs = []
-    # default (256-query blocks, two waves per SIMD), 128-query blocks, the
-    # three-waves-per-SIMD kernel (192-query blocks) and the one-wave-per-SIMD
-    # kernel (4 k-chunks only)
-    for env in ({}, {"WV_BF_BQ": "128"}, {"WV_BF_BQ": "192"}, {"WV_BF_SPLIT_1W": "1"}):
+    # default (the f16 key pass), and the bf16x3 split pass: 256-query blocks
+    # (two waves per SIMD), 128-query blocks, the three-waves-per-SIMD kernel
+    # (192-query blocks) and the one-wave-per-SIMD kernel (4 k-chunks only)
+    for env in ({}, {"WV_BF_SPLIT": "1"}, {"WV_BF_SPLIT": "1", "WV_BF_BQ": "128"},
+                {"WV_BF_SPLIT": "1", "WV_BF_BQ": "192"}, {"WV_BF_SPLIT": "1", "WV_BF_SPLIT_1W": "1"}):
         os.environ.update(env)
         try:
             ix = W.GPUVectorIndex(dim, METRIC_NAMES[metric], capacity=n)
@@ -738,3 +741,65 @@ def test_split_pass_query_blocks_multi_segment(dim, metric):
     for (gi, gd, gn), (ri, rd) in zip(runs[0], ((oi, od), (ui, ud))):
         for i in range(len(qs)):
             _same_tie_aware(gi[i], gd[i], ri[i], rd[i])
+
+
+@pytest.mark.parametrize("dim", [100, 128])
+@pytest.mark.parametrize("metric", [O.L2, O.DOT, O.COSINE])
+def test_h16_key_pass_seeded_equals_unseeded_and_fp32(dim, metric):
+    """The f16 key pass at a corpus size that runs the seed pre-pass (>= 64k
+    rows): seeded (default), unseeded (WV_H16_NO_SEED), without the XCD remap
+    (WV_BF_LOCALITY=0) and the fp32 pass return the same ids and distances,
+    with tombstones, a shared allow list kept in the epilogue and a partial
+    last query block -- and equal the restatement up to tie order.  D=100 is
+    GloVe-shaped (7 k-steps of 16: 112, not 128)."""
+    import os
+    n, nq = 70001, 600
+    base, qs = _data(n, dim, nq, seed=71 + dim, metric=metric)
+    rng = np.random.default_rng(72)
+    tomb_ids = np.nonzero(rng.random(n) < 0.02)[0]
+    allow_ids = np.nonzero(rng.random(n) < 0.6)[0]
+    al = W.AllowList.from_ids(allow_ids, n)
+    runs = []
+    for env in ({}, {"WV_H16_NO_SEED": "1"}, {"WV_BF_LOCALITY": "0"}, {"WV_BF_FP32": "1"}):
+        os.environ.update(env)
+        try:
+            ix = W.GPUVectorIndex(dim, METRIC_NAMES[metric], capacity=n)
+            ix.upload_vectors(base)
+            ix.set_tombstones(tomb_ids)
+            runs.append((ix.search_batch(qs, 10, mode="exact"), ix.search_batch(qs, 10, allow=al, mode="exact"),
+                         ix.last_batch_stats()["fallbacks"]))
+            ix.close()
+        finally:
+            for key in env:
+                os.environ.pop(key, None)
+    for other in runs[1:]:
+        for (ai, ad, an), (bi, bd, bn) in zip(runs[0][:2], other[:2]):
+            assert an.tolist() == bn.tolist()
+            _same(ai, ad, bi, bd)
+    assert runs[0][2] <= nq // 50, runs[0][2]      # the certificate holds for almost every query
+    b = O.normalize_rows(base) if metric == O.COSINE else base
+    q = O.normalize_rows(qs) if metric == O.COSINE else qs
+    tb = O.bits_from_ids(tomb_ids, n)
+    oi, od, on = O.flat_scan(metric, b, q, 10, allow_bits=al.words, tomb_bits=tb, threads=16)
+    gi, gd, gn = runs[0][1]
+    for i in range(nq):
+        _same_tie_aware(gi[i], gd[i], oi[i], od[i])
+
+
+def test_h16_integer_data_keys_exact():
+    """SIFT-shaped integer data: f16(s_x x) is exact (integers below 2048 x
+    2^k), so the residual terms of the certificate vanish and the f16 keys are
+    exact -- ids equal the restatement's up to tie order, few fallbacks."""
+    from bench import counter_sift
+    n, d, nq = 70000, 128, 400
+    base = counter_sift(1, 0, n, d)
+    qs = counter_sift(2, 0, nq, d)
+    ix = W.GPUVectorIndex(d, "l2-squared", capacity=n)
+    ix.upload_vectors(base)
+    gi, gd, gn = ix.search_batch(qs, 10, mode="exact")
+    fb = ix.last_batch_stats()["fallbacks"]
+    oi, od, on = O.flat_scan(O.L2, base, qs, 10, threads=16)
+    for i in range(nq):
+        _same_tie_aware(gi[i], gd[i], oi[i], od[i])
+    assert fb <= nq // 10, fb
+    ix.close()

@@ -104,6 +104,7 @@ SIGNATURES = {
     "wv_last_batch_stats": (C.c_int, [_vp, _u64p, _u64p, _u64p]),
     "wv_index_set_timing": (C.c_int, [_vp, C.c_int]),
     "wv_last_kernel_times": (C.c_int, [_vp, _f32p, _f32p, _f32p]),
+    "wv_last_seed_time": (C.c_int, [_vp, _f32p]),
     "wv_graph_load_commitlog_buffer": (C.c_int, [_vp, C.c_uint64, C.POINTER(C.c_void_p)]),
     "wv_graph_load_commitlogs": (C.c_int, [C.POINTER(C.c_char_p), C.c_int, C.POINTER(C.c_void_p)]),
     "wv_graph_load_commitlog_dir": (C.c_int, [C.c_char_p, C.POINTER(C.c_void_p)]),

@@ -42,6 +42,14 @@ hipError_t wv_launch_pq_encode(const float* X, int ldx, const uint64_t* ids, uin
 hipError_t wv_launch_pq_scan(const wv::PqScanParams* p, hipStream_t s);
 hipError_t wv_launch_split_rows(const float* in, int ld_in, const uint64_t* ids, uint64_t n, uint64_t n_valid, int D,
                                 float scale, void* out, int ld_out, uint64_t out_row0, hipStream_t s);
+hipError_t wv_launch_h16_rows(const float* in, int ld_in, const uint64_t* ids, uint64_t n, int D, int ns, float sign,
+                              float scale, const unsigned int* scale_from_max, void* out, uint64_t out_row0,
+                              unsigned int* res_max_bits, float* res_out, hipStream_t s);
+hipError_t wv_launch_absmax(const float* in, int ld, uint64_t n, int D, unsigned int* max_bits, hipStream_t s);
+hipError_t wv_launch_h16_qscale(const unsigned int* max_bits, float bsign, float* qscale, hipStream_t s);
+hipError_t wv_launch_h16_xns(const float* xnorm, uint64_t n, float sx, const float* qscale, float* xns, hipStream_t s);
+hipError_t wv_launch_bf_h16(const wv::H16Params* p, int ns, hipStream_t s);
+float wv_h16_pow2_scale(float maxabs);
 hipError_t wv_launch_pq_topk(const float* skey, const uint32_t* sval, const float* dist, const uint32_t* rows,
                              uint64_t nr, int q0, int nqc, int k, uint64_t id_base, uint64_t* out_ids, float* out_d,
                              int32_t* out_n, hipStream_t s);
@@ -194,6 +202,14 @@ struct wv_index {
     // the MFMA-native layout of split_hi_index), kept in step with every row write
     DevBuf xsplit;
     bool use_split = false;
+    // f16 image of vecs for the f16 key pass (wv_h16.hip, the default for
+    // D <= 128): f16(s_x x) in the layout of h16_index; h16_ex = max residual
+    // norm |x - f16(s_x x) / s_x| over the rows (rounded up), both host-cached
+    bool use_h16 = false;
+    int h16_ns = 0;
+    float h16_sx = 0.f, h16_ex = 0.f;
+    DevBuf ximg16, xns, qimg16, qres, qmax, qscale, tau, allow_pad, ex_bits;
+    float maxnorm_host = 0.f;   // max |x| (rounded up), cached after every row write
     DevBuf xnorm;           // [capacity]
     DevBuf maxnorm;         // unsigned bits of max |x|
     std::vector<uint64_t> has_vec;   // host copy of uploaded rows
@@ -246,8 +262,9 @@ struct wv_index {
     hipEvent_t ev_in = nullptr, ev_out = nullptr;
     // optional kernel timing (hipEvents on the launch stream)
     bool timing = false;
-    hipEvent_t ev[6] = {};
-    float t_mfma = 0.f, t_fin = 0.f, t_hnsw = 0.f;
+    hipEvent_t ev[8] = {};
+    float t_mfma = 0.f, t_fin = 0.f, t_hnsw = 0.f, t_pre = 0.f;
+    int n_cus = 256;
     // brute-force workgroups per launch: a whole number of resident waves of
     // workgroups (CUs x 2 per CU x WV_BF_ROUNDS)
     int bf_blocks = 512;
@@ -424,6 +441,147 @@ int run_pq_flat(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d
                 uint64_t allow_stride, uint64_t* d_out_ids, float* d_out_d, int32_t* d_out_n, hipStream_t s,
                 const uint64_t* d_rowmask, uint64_t rowmask_nbits);
 
+// f16 key pass (wv_h16.hip) over the whole corpus, optionally masked by a
+// shared allow list: query image + scale, an optional seed pre-pass over every
+// H_SAMPLE-th tile (its finalize yields per-query thresholds), the main pass
+// seeded with them, and the certifying finalize.  Appends uncertified queries
+// to `fails` (read back from the device).
+int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_allow, uint64_t allow_nbits, uint64_t N,
+            uint64_t* d_out_ids, float* d_out_d, int32_t* d_out_n, hipStream_t s, std::vector<int32_t>& fails) {
+    const int ns = ix->h16_ns;
+    const uint64_t ntl = (N + wv::H_BN - 1) / wv::H_BN;
+    const uint64_t* allow = d_allow;
+    if (d_allow && (allow_nbits + 63) / 64 < ntl) {   // the kernel reads one allow word per tile
+        HIP_TRY(ix->allow_pad.ensure(ntl * 8));
+        HIP_TRY(hipMemsetAsync(ix->allow_pad.p, 0, ntl * 8, s));
+        if (allow_nbits)
+            HIP_TRY(hipMemcpyAsync(ix->allow_pad.p, d_allow, (allow_nbits + 63) / 64 * 8, hipMemcpyDeviceToDevice, s));
+        allow = ix->allow_pad.as<uint64_t>();
+    }
+    const int nqb = (nq + wv::H_BQ - 1) / wv::H_BQ;
+    const size_t qbytes = (size_t)nqb * wv::H_BQ * ns * 16 * 2;
+    HIP_TRY(ix->qimg16.ensure(qbytes));
+    HIP_TRY(ix->qres.ensure((size_t)nq * 4));
+    HIP_TRY(ix->tau.ensure((size_t)nq * 4));
+    HIP_TRY(ix->q_nrm2.ensure((size_t)nq * 4));
+    HIP_TRY(ix->fail.ensure((size_t)nq * 4));
+    HIP_TRY(ix->fail_thr.ensure((size_t)nq * 4));
+    HIP_TRY(wv_launch_qnorm(d_q, nq, ix->dim, ix->dpad, ix->metric, ix->q_nrm2.as<float>(), s));
+    // B = f16(s_q b), b = -2q (L2) or -q; s_q from the batch's max |b|
+    const float bsign = ix->metric == WV_L2_SQUARED ? -2.f : -1.f;
+    HIP_TRY(hipMemsetAsync(ix->qmax.p, 0, 4, s));
+    HIP_TRY(hipMemsetAsync(ix->qimg16.p, 0, qbytes, s));
+    HIP_TRY(wv_launch_absmax(d_q, ix->dpad, nq, ix->dim, ix->qmax.as<unsigned int>(), s));
+    HIP_TRY(wv_launch_h16_qscale(ix->qmax.as<unsigned int>(), bsign, ix->qscale.as<float>(), s));
+    HIP_TRY(wv_launch_h16_rows(d_q, ix->dpad, nullptr, nq, ix->dim, ns, bsign, 1.f, ix->qmax.as<unsigned int>(),
+                               ix->qimg16.p, 0, nullptr, ix->qres.as<float>(), s));
+    if (ix->metric == WV_L2_SQUARED)
+        HIP_TRY(wv_launch_h16_xns(ix->xnorm.as<float>(), ntl * wv::H_BN, ix->h16_sx, ix->qscale.as<float>(),
+                                  ix->xns.as<float>(), s));
+    wv::H16Params hp{};
+    hp.X = ix->ximg16.p;
+    hp.Q = ix->qimg16.p;
+    hp.xns = ix->xns.as<float>();
+    hp.excl = ix->excl.as<uint64_t>();
+    hp.allow = allow;
+    hp.qscale = ix->qscale.as<float>();
+    hp.sx = ix->h16_sx;
+    hp.N = N;
+    hp.nq = nq;
+    hp.metric = ix->metric;
+    hp.n_qblocks = nqb;
+    hp.locality = 1;
+    if (const char* e = std::getenv("WV_BF_LOCALITY")) hp.locality = std::atoi(e);
+    wv::BfFinParams fp{};
+    fp.X = ix->vecs.as<float>();
+    fp.Q = d_q;
+    fp.qnorm = ix->q_nrm2.as<float>();
+    fp.xnorm_max = ix->maxnorm_host;
+    fp.nq = nq;
+    fp.D = ix->dim;
+    fp.ldx = ix->ldx;
+    fp.ldq = ix->dpad;
+    fp.metric = ix->metric;
+    fp.k = k;
+    fp.id_base = ix->cfg.id_base;
+    fp.out_ids = d_out_ids;
+    fp.out_d = d_out_d;
+    fp.out_n = d_out_n;
+    fp.fail = ix->fail.as<int32_t>();
+    fp.fail_thr = ix->fail_thr.as<float>();
+    fp.bq = wv::H_BQ;
+    fp.prod = wv::H_PROD;
+    fp.h16 = 1;
+    fp.qscale = ix->qscale.as<float>();
+    fp.sx = ix->h16_sx;
+    fp.ex_max = ix->h16_ex;
+    fp.qres = ix->qres.as<float>();
+    // seed pre-pass: the k-th exact distance over every H_SAMPLE-th tile bounds
+    // each query's true k-th distance, hence the keys worth keeping
+    const bool seed = ntl >= 64 * (uint64_t)wv::H_SAMPLE && !std::getenv("WV_H16_NO_SEED");
+    if (seed) {
+        const uint64_t nts = (ntl + wv::H_SAMPLE - 1) / wv::H_SAMPLE;
+        const wv::BfSchedule ss = wv::bf_schedule(nq, nts * wv::H_BN, ix->n_cus, wv::H_BQ, wv::H_BN);
+        HIP_TRY(ix->cand_d.ensure((size_t)nq * ss.n_slots * wv::H_PROD * wv::BF_KP * 4));
+        HIP_TRY(ix->cand_id.ensure((size_t)nq * ss.n_slots * wv::H_PROD * wv::BF_KP * 4));
+        hp.ntiles = ss.ntiles;
+        hp.units_per_block = ss.units_per_block;
+        hp.n_slots = ss.n_slots;
+        hp.tile_stride = wv::H_SAMPLE;
+        hp.tau = nullptr;
+        hp.out_d = ix->cand_d.as<float>();
+        hp.out_id = ix->cand_id.as<uint32_t>();
+        if (ix->timing) HIP_TRY(hipEventRecord(ix->ev[6], s));
+        HIP_TRY(wv_launch_bf_h16(&hp, ns, s));
+        fp.cand_d = ix->cand_d.as<float>();
+        fp.cand_id = ix->cand_id.as<uint32_t>();
+        fp.n_slots = ss.n_slots;
+        fp.ntiles = ss.ntiles;
+        fp.units_per_block = ss.units_per_block;
+        fp.tau_out = ix->tau.as<float>();
+        HIP_TRY(wv_launch_bf_finalize(&fp, s));
+        if (ix->timing) HIP_TRY(hipEventRecord(ix->ev[7], s));
+        fp.tau_out = nullptr;
+    }
+    const wv::BfSchedule sch = wv::bf_schedule(nq, N, ix->n_cus, wv::H_BQ, wv::H_BN);
+    HIP_TRY(ix->cand_d.ensure((size_t)nq * sch.n_slots * wv::H_PROD * wv::BF_KP * 4));
+    HIP_TRY(ix->cand_id.ensure((size_t)nq * sch.n_slots * wv::H_PROD * wv::BF_KP * 4));
+    hp.ntiles = sch.ntiles;
+    hp.units_per_block = sch.units_per_block;
+    hp.n_slots = sch.n_slots;
+    hp.tile_stride = 1;
+    hp.tau = seed ? ix->tau.as<float>() : nullptr;
+    hp.out_d = ix->cand_d.as<float>();
+    hp.out_id = ix->cand_id.as<uint32_t>();
+    if (ix->timing) HIP_TRY(hipEventRecord(ix->ev[0], s));
+    HIP_TRY(wv_launch_bf_h16(&hp, ns, s));
+    if (ix->timing) HIP_TRY(hipEventRecord(ix->ev[1], s));
+    fp.cand_d = ix->cand_d.as<float>();
+    fp.cand_id = ix->cand_id.as<uint32_t>();
+    fp.n_slots = sch.n_slots;
+    fp.ntiles = sch.ntiles;
+    fp.units_per_block = sch.units_per_block;
+    fp.tau_in = hp.tau;
+    if (ix->timing) HIP_TRY(hipEventRecord(ix->ev[2], s));
+    HIP_TRY(wv_launch_bf_finalize(&fp, s));
+    if (ix->timing) HIP_TRY(hipEventRecord(ix->ev[3], s));
+    std::vector<int32_t> f(nq);
+    HIP_TRY(hipMemcpyAsync(f.data(), ix->fail.p, 4 * (size_t)nq, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (ix->timing) {
+        float a = 0.f, b = 0.f, c = 0.f;
+        HIP_TRY(hipEventElapsedTime(&a, ix->ev[0], ix->ev[1]));
+        HIP_TRY(hipEventElapsedTime(&b, ix->ev[2], ix->ev[3]));
+        if (seed) HIP_TRY(hipEventElapsedTime(&c, ix->ev[6], ix->ev[7]));
+        ix->t_mfma += a;
+        ix->t_fin += b;
+        ix->t_pre += c;
+    }
+    for (int i = 0; i < nq; ++i)
+        if (f[i]) fails.push_back(i);
+    return WV_OK;
+}
+
 int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_allow, uint64_t allow_nbits,
               uint64_t allow_stride, uint64_t* d_out_ids, float* d_out_d, int32_t* d_out_n, hipStream_t s,
               const uint64_t* d_rowmask = nullptr, uint64_t rowmask_nbits = 0) {
@@ -453,10 +611,19 @@ int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
                 HIP_TRY(hipMemsetAsync(d_out_n, 0, sizeof(int32_t) * nq, s));
                 return WV_OK;
             }
-            if ((2 * n_ok < N && !std::getenv("WV_BF_NO_COMPACT")) || d_rowmask) {
+            // the f16 pass scans the whole corpus ~6x faster than the fp32
+            // pass over a row list: compact only very selective lists then
+            const uint64_t frac = ix->use_h16 && !allow_stride ? 8 : 2;
+            if ((frac * n_ok < N && !std::getenv("WV_BF_NO_COMPACT")) || d_rowmask) {
                 n_scan = n_ok;
                 d_rowidx = ix->rowidx.as<uint32_t>();
             }
+        }
+        if (ix->use_h16 && !d_rowidx && !allow_stride) {
+            const uint64_t* sh = d_allow && !allow_stride ? d_allow : nullptr;
+            int rc = run_h16(ix, d_q, nq, k, sh, allow_nbits, N, d_out_ids, d_out_d, d_out_n, s, fails);
+            if (rc) return rc;
+            goto fallbacks;
         }
         // bf16x3 key pass on native images (whole-corpus or shared allow list
         // scans): 256-query blocks, one 512-thread workgroup per CU, two waves
@@ -577,6 +744,7 @@ int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
     } else {
         for (int i = 0; i < nq; ++i) fails.push_back(i);
     }
+fallbacks:
     ix->last_fallbacks += fails.size();
     if (!fails.empty() && k <= wv::BF_FAST_KMAX) {
         // batched threshold filter over the corpus for every failed query
@@ -886,7 +1054,7 @@ int search_core(wv_index* ix, const float* d_q, int nq, int k, int ef, const uin
     int rc = refresh_bitmaps(ix);
     if (rc) return rc;
     ix->last_dist = ix->last_exp = ix->last_fallbacks = 0;
-    ix->t_mfma = ix->t_fin = ix->t_hnsw = 0.f;
+    ix->t_mfma = ix->t_fin = ix->t_hnsw = ix->t_pre = 0.f;
     if (ef <= 0) ef = search_time_ef(ix->cfg, k);
     if (mode == WV_MODE_EXACT)
         return run_exact(ix, d_q, nq, k, d_allow, allow_nbits, allow_stride, d_out_ids, d_out_d, d_out_n, s);
@@ -1023,6 +1191,7 @@ int wv_index_create(int dim, int metric, const wv_config* cfg, uint64_t capacity
         int rounds = 1;
         if (const char* r = std::getenv("WV_BF_ROUNDS")) rounds = std::max(1, std::atoi(r));
         ix->bf_blocks = cus * 2 * rounds;
+        ix->n_cus = cus;
     }
     ix->bm_words = (capacity + 63) / 64;
     // whole brute-force tiles (wv_bf.hip layout contract): zero rows past capacity
@@ -1037,7 +1206,23 @@ int wv_index_create(int dim, int metric, const wv_config* cfg, uint64_t capacity
     // bf16x3 key pass (wv_bf_split_kernel): whole 32-float chunks, stride <= 128
     // (the query block image stays resident in LDS); WV_BF_FP32=1 keeps the
     // fp32 MFMA pass for every scan
-    ix->use_split = ix->ldx % wv::BF_BK == 0 && ix->ldx <= 128 && !std::getenv("WV_BF_FP32");
+    // f16 key pass (wv_bf_h16_kernel) for D <= 128 unless an ablation switch
+    // asks for the bf16x3 (WV_BF_SPLIT=1) or the fp32 (WV_BF_FP32=1) pass
+    ix->use_h16 = dim <= 16 * wv::H_NS_MAX && !std::getenv("WV_BF_FP32") && !std::getenv("WV_BF_SPLIT");
+    if (ix->use_h16) {
+        ix->h16_ns = (dim + 15) / 16;
+        const size_t ibytes = cap_rows * (size_t)ix->h16_ns * 16 * 2;
+        if (ix->ximg16.ensure(ibytes) != hipSuccess || ix->xns.ensure(cap_rows * 4) != hipSuccess ||
+            ix->ex_bits.ensure(4) != hipSuccess || ix->qmax.ensure(4) != hipSuccess ||
+            ix->qscale.ensure(4) != hipSuccess) {
+            wv_index_destroy(ix);
+            return fail(WV_EOOM, "wv_index_create: device allocation failed");
+        }
+        (void)hipMemsetAsync(ix->ximg16.p, 0, ibytes, ix->stream);
+        (void)hipMemsetAsync(ix->xns.p, 0, cap_rows * 4, ix->stream);
+        (void)hipMemsetAsync(ix->ex_bits.p, 0, 4, ix->stream);
+    }
+    ix->use_split = !ix->use_h16 && ix->ldx % wv::BF_BK == 0 && ix->ldx <= 128 && !std::getenv("WV_BF_FP32");
     if (ix->use_split && ix->xsplit.ensure(vbytes) != hipSuccess) {
         wv_index_destroy(ix);
         return fail(WV_EOOM, "wv_index_create: device allocation failed");
@@ -1063,7 +1248,11 @@ int wv_index_destroy(wv_index* ix) {
                       &ix->sort_tmp, &ix->g_idx, &ix->g_q, &ix->g_allow, &ix->g_ids, &ix->g_d, &ix->g_n, &ix->g_cnt,
                       &ix->out_ids, &ix->out_d, &ix->out_n, &ix->stage, &ix->fail_thr, &ix->fb_idx, &ix->fb_d, &ix->fb_i, &ix->fb_n, &ix->fb_of,
                       &ix->ac_cnt, &ix->ac_off, &ix->rowidx, &ix->pq_cent, &ix->pq_codes, &ix->pk_key,
-                      &ix->pk_dist, &ix->pk_val, &ix->pk_skey, &ix->pk_sval, &ix->pk_off})
+                      &ix->pk_dist, &ix->pk_val, &ix->pk_skey, &ix->pk_sval, &ix->pk_off, &ix->ximg16, &ix->xns,
+                      &ix->qimg16, &ix->qres, &ix->qmax, &ix->qscale, &ix->tau, &ix->allow_pad, &ix->ex_bits,
+                      &ix->delta, &ix->dmask, &ix->dl_ids, &ix->dl_d, &ix->dl_n, &ix->dq_tmp, &ix->b_tgt, &ix->b_ci,
+                      &ix->b_cd, &ix->b_cn, &ix->b_cnt0, &ix->b_cntu, &ix->b_rk, &ix->b_rn, &ix->b_rk2, &ix->b_rn2,
+                      &ix->b_uk, &ix->b_ul, &ix->b_uo, &ix->b_nr, &ix->b_tmp})
         b->release();
     if (ix->stream) (void)hipStreamSynchronize(ix->stream);
     for (auto& e : ix->ev)
@@ -1083,6 +1272,40 @@ int wv_index_update_config(wv_index* ix, const wv_config* cfg) {
     ix->cfg = *cfg;
     ix->cfg.device = dev;   // the device and id base are fixed at creation
     ix->cfg.id_base = base;
+    return WV_OK;
+}
+
+// After rows were written to vecs (rownorm updated maxnorm; the stream is
+// synchronised): cache max |x| on the host (the finalize's eps needs it, and
+// reading it per batch would cost a host round trip), and keep the f16 image
+// in step.  s_x is fixed by the first write and only ever lowered (then the
+// whole image is rebuilt) so that no element overflows f16.
+static int rows_written(wv_index* ix, const uint64_t* d_ids, uint64_t n, uint64_t first_id) {
+    unsigned int mb = 0;
+    HIP_TRY(hipMemcpyAsync(&mb, ix->maxnorm.p, 4, hipMemcpyDeviceToHost, ix->stream));
+    HIP_TRY(hipStreamSynchronize(ix->stream));
+    std::memcpy(&ix->maxnorm_host, &mb, 4);
+    if (!ix->use_h16 || n == 0) return WV_OK;
+    const float sx = wv_h16_pow2_scale(ix->maxnorm_host);
+    const bool rebuild = ix->h16_sx != 0.f && sx < ix->h16_sx;
+    if (ix->h16_sx == 0.f || rebuild) ix->h16_sx = sx;
+    unsigned int* exb = ix->ex_bits.as<unsigned int>();
+    if (rebuild) {
+        HIP_TRY(hipMemsetAsync(exb, 0, 4, ix->stream));
+        HIP_TRY(wv_launch_h16_rows(ix->vecs.as<float>(), ix->ldx, nullptr, ix->n_rows, ix->dim, ix->h16_ns, 1.f,
+                                   ix->h16_sx, nullptr, ix->ximg16.p, 0, exb, nullptr, ix->stream));
+    } else if (d_ids) {
+        HIP_TRY(wv_launch_h16_rows(ix->vecs.as<float>(), ix->ldx, d_ids, n, ix->dim, ix->h16_ns, 1.f, ix->h16_sx,
+                                   nullptr, ix->ximg16.p, 0, exb, nullptr, ix->stream));
+    } else {
+        HIP_TRY(wv_launch_h16_rows(ix->vecs.as<float>() + first_id * ix->ldx, ix->ldx, nullptr, n, ix->dim,
+                                   ix->h16_ns, 1.f, ix->h16_sx, nullptr, ix->ximg16.p, first_id, exb, nullptr,
+                                   ix->stream));
+    }
+    unsigned int eb = 0;
+    HIP_TRY(hipMemcpyAsync(&eb, exb, 4, hipMemcpyDeviceToHost, ix->stream));
+    HIP_TRY(hipStreamSynchronize(ix->stream));
+    std::memcpy(&ix->h16_ex, &eb, 4);
     return WV_OK;
 }
 
@@ -1136,6 +1359,8 @@ static int upload_rows(wv_index* ix, const float* src, bool device_src, int ld, 
     for (uint64_t i = first_id; i < first_id + n; ++i) ix->has_vec[i >> 6] |= 1ull << (i & 63);
     ix->n_rows = std::max(ix->n_rows, first_id + n);
     ix->bitmaps_dirty = true;
+    int rc = rows_written(ix, nullptr, n, first_id);
+    if (rc) return rc;
     return pq_rows_written(ix, nullptr, nullptr, n, first_id);
 }
 
@@ -1292,6 +1517,8 @@ int wv_index_add(wv_index* ix, const uint64_t* ids_in, const float* rows_in, uin
         ix->n_rows = std::max(ix->n_rows, id + 1);
     }
     ix->bitmaps_dirty = true;
+    int rc = rows_written(ix, d_ids, n, 0);
+    if (rc) return rc;
     return pq_rows_written(ix, d_ids, ids, n, 0);
 }
 
@@ -1820,6 +2047,12 @@ int wv_last_kernel_times(wv_index* ix, float* bf_mfma_ms, float* bf_finalize_ms,
     if (bf_mfma_ms) *bf_mfma_ms = ix->t_mfma;
     if (bf_finalize_ms) *bf_finalize_ms = ix->t_fin;
     if (hnsw_ms) *hnsw_ms = ix->t_hnsw;
+    return WV_OK;
+}
+
+int wv_last_seed_time(wv_index* ix, float* seed_ms) {
+    if (check(ix) || !seed_ms) return fail(WV_EINVAL, "bad argument");
+    *seed_ms = ix->t_pre;
     return WV_OK;
 }
 

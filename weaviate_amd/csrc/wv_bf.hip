@@ -19,83 +19,17 @@
 //      every id, used for flagged queries and for large k.
 #include "wv_device.h"
 #include "wv_params.h"
+#include "wv_topk.h"
 
 #include <float.h>
 
 namespace wv {
 
 
-typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 
 
-
-// ---------------------------------------------------------------------------
-// v_min3_f32 without the IEEE canonicalisation hipcc wraps around fminf of
-// MFMA results (a NaN key never wins a comparison either way)
-#ifdef WV_BF_DBG_ITERS
-// ablation builds only: wave-level counts of tiles (0) and extract-loop iterations (1)
-__device__ unsigned long long wv_dbg_counts[2];
-#define WV_DBG_COUNT(i) if (__lane_id() == 0) atomicAdd(&wv_dbg_counts[i], 1ull);
-extern "C" void wv_dbg_read(unsigned long long* out) { hipMemcpyFromSymbol(out, HIP_SYMBOL(wv_dbg_counts), 16); }
-#else
-#define WV_DBG_COUNT(i)
-#endif
-
-__device__ __forceinline__ float min3_raw(float a, float b, float c) {
-    float r;
-    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
-}
-
-// Split pass candidate extraction (rare: a lane runs it only when its tile
-// minimum M beats its list tail; the wave runs it while any lane does, so it
-// is kept branch-free).  A0 / A1 hold this lane's 32 keys of one query column
-// (row offsets (r & 3) + 8 (r >> 2) and 32 + the same); each round takes the
-// minimum, masks it to +inf and inserts it.  Insertion compares keys only:
-// a key equal to the tail is dropped, which the finalize's certificate (all
-// dropped keys >= the smallest tail) still covers, and the reported ids and
-// distances come from the exact re-rank.  PT is the lane-pair partner's tail
-// (a valid rejection threshold, see the caller).
-__device__ __forceinline__ void split_extract(float& M, floatx16& A0, floatx16& A1, float (&ld)[BF_KP],
-                                              uint32_t (&li)[BF_KP], float pt, uint32_t rb0,
-                                              const uint32_t* __restrict__ rowidx = nullptr) {
-    const float INF = __builtin_inff();
-    while (M <= fminf(ld[BF_KP - 1], pt)) {
-        WV_DBG_COUNT(1)
-        // position of M: a descending scan, so among equal keys the lowest row wins
-        uint32_t sel = 0;
-#pragma unroll
-        for (int r = 15; r >= 0; --r) sel = A1[r] == M ? 16u + r : sel;
-#pragma unroll
-        for (int r = 15; r >= 0; --r) sel = A0[r] == M ? (uint32_t)r : sel;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            A0[r] = sel == (uint32_t)r ? INF : A0[r];
-            A1[r] = sel == 16u + r ? INF : A1[r];
-        }
-        uint32_t rb = rb0;   // opaque: the row ids stay in this rare loop
-        asm volatile("" : "+v"(rb));
-        if (!(M < ld[BF_KP - 1])) break;
-        uint32_t id = rb + (sel & 3u) + 8u * ((sel >> 2) & 3u) + 32u * (sel >> 4);
-        if (rowidx) id = rowidx[id];   // corpus id; the map is increasing
-        float d = M;
-#pragma unroll
-        for (int i = 0; i < BF_KP; ++i) {
-            const bool lt = d < ld[i];
-            const float td = ld[i];
-            const uint32_t ti = li[i];
-            ld[i] = lt ? d : td;
-            li[i] = lt ? id : ti;
-            d = lt ? td : d;
-            id = lt ? ti : id;
-        }
-        M = INF;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) M = min3_raw(M, A0[r], A1[r]);
-    }
-}
 
 __device__ __forceinline__ void list_insert(float (&ld)[BF_KP], uint32_t (&li)[BF_KP], float d, uint32_t id) {
     // bubble the new element through the sorted list; the largest falls off
@@ -1207,6 +1141,11 @@ __device__ void finalize_one(const BfFinParams& p, int q, float* sd, uint32_t* s
         const uint32_t ik = si[FIN_KF - 1];
         if (key_less(dk, ik, bound, bound_id)) { bound = dk; bound_id = ik; }
     }
+    // f16 keys carry the power-of-two scale s = s_x * s_q (exact to undo);
+    // a seeded pass dropped every key above its threshold, which therefore
+    // also bounds what was not seen
+    if (p.h16 && bound != FLT_MAX) bound *= 1.0f / (p.sx * p.qscale[0]);
+    if (p.tau_in) bound = fminf(bound, p.tau_in[q]);
 
     // query into LDS for the exact distance
     for (int i = lane; i < ((p.D + 3) & ~3); i += 64) qv[i] = i < p.D ? p.Q[(size_t)q * p.ldq + i] : 0.f;
@@ -1243,7 +1182,7 @@ __device__ void finalize_one(const BfFinParams& p, int q, float* sd, uint32_t* s
     const int k = p.k;
     int nvalid = 0;
     for (int j = 0; j < FIN_KF; ++j) nvalid += (si[j] != WV_NIL);
-    if (lane < FIN_KF && myi != WV_NIL && rank < k) {
+    if (lane < FIN_KF && myi != WV_NIL && rank < k && !p.tau_out) {
         p.out_ids[(size_t)q * k + rank] = p.id_base + myi;
         p.out_d[(size_t)q * k + rank] = myd;
     }
@@ -1259,19 +1198,37 @@ __device__ void finalize_one(const BfFinParams& p, int q, float* sd, uint32_t* s
     float eps, bfull;
     // bf16x3 keys: 3x the accumulated terms, plus the split error
     // 4 * 2^-16 * |x| |b| with b = -2q (L2) or -q
-    const float acc_f = p.split ? 12.f : 4.f;
+    const float acc_f = p.split ? 12.f : (p.h16 ? 6.f : 4.f);
     const float split_e = p.split ? 4.f * 1.52587890625e-05f : 0.f;   // 2^-16
+    // f16 keys: |sum f16(s_x x) f16(s_q b) / (s_x s_q) - x.b| <= |x - x~| |b~| +
+    // |x| |b - b~|, with the residual norms measured when the images were made
+    const float qres = p.h16 ? p.qres[q] : 0.f;
     if (METRIC == WV_METRIC_L2) {
         const float qn = sqrtf(p.qnorm[q]);
         const float s = qn + p.xnorm_max;
         eps = acc_f * D4 * u * s * s + 2.f * split_e * qn * p.xnorm_max;
+        if (p.h16) eps += p.ex_max * (2.f * qn + qres) + p.xnorm_max * qres;
         bfull = bound + p.qnorm[q];
     } else {
         const float qn = p.qnorm[q];
         eps = acc_f * D4 * u * qn * p.xnorm_max + 4.f * u + split_e * qn * p.xnorm_max;
+        if (p.h16) eps += p.ex_max * (qn + qres) + p.xnorm_max * qres;
         bfull = METRIC == WV_METRIC_DOT ? bound : 1.0f + bound;
     }
     eps *= 1.0001f;   // the float evaluation of the bound itself
+    if (p.tau_out) {
+        // seed pre-pass: every point of the true top k has key <= dk - (the
+        // key's offset from the distance) + eps, dk being the k-th exact
+        // distance of k real points (an upper bound of the true k-th)
+        float tau = __builtin_inff();
+        if (nvalid >= k && dk < FLT_MAX) {
+            const float off = METRIC == WV_METRIC_L2 ? p.qnorm[q] : (METRIC == WV_METRIC_DOT ? 0.f : 1.0f);
+            tau = dk - off + eps;
+            tau += 4.f * u * (fabsf(dk) + fabsf(off) + eps) + 1e-3f * eps;   // the rounding of this sum
+        }
+        if (lane == 0) p.tau_out[q] = tau;
+        return;
+    }
     bool certified;
     if (nvalid < k) certified = bound == FLT_MAX;     // everything eligible was seen
     else certified = (bound == FLT_MAX) || (bfull - eps > dk);

@@ -113,6 +113,11 @@ __device__ __forceinline__ void search_layer(const HnswParams& p, WaveState& w_i
     const uint32_t* nbr_base;
     int deg;
     for (;;) {
+        // A full side set or expanded-set table makes the state inexact (an
+        // expanded side candidate that X cannot record would be re-inserted
+        // and expanded again, forever): stop, the query is answered by the
+        // exact fallback (status != 0).
+        if (status) break;
         // ---- pop the best live candidate: first unexpanded R entry vs S head ----
         int ridx = Rl;
         for (int base = 0; base < Rl; base += 64) {

@@ -60,11 +60,11 @@ struct BfSchedule {
     int n_blocks, n_slots, bq;
     uint64_t ntiles, units_per_block;
 };
-inline BfSchedule bf_schedule(int nq, uint64_t N, int target_blocks, int bq = BF_BQ) {
+inline BfSchedule bf_schedule(int nq, uint64_t N, int target_blocks, int bq = BF_BQ, int tile_rows = BF_BN) {
     BfSchedule s{};
     s.bq = bq;
     const uint64_t nqb = (uint64_t)(nq + bq - 1) / bq;
-    s.ntiles = (N + BF_BN - 1) / BF_BN;
+    s.ntiles = (N + tile_rows - 1) / tile_rows;
     const uint64_t total = nqb * s.ntiles;
     uint64_t nb = target_blocks > 0 ? (uint64_t)target_blocks : 1;
     if (nb > total) nb = total;
@@ -85,6 +85,46 @@ inline int bf_slots_of(uint64_t qb, uint64_t ntiles, uint64_t upb) {
     return (int)(((qb + 1) * ntiles - 1) / upb) - bf_first_block(qb, ntiles, upb) + 1;
 }
 
+// ---- f16 key pass (wv_bf_h16_kernel, wv_h16.hip) ---------------------------
+// One f16 product per fp32 product: keys k~ = s * (|x|^2 + sum f16(s_x x) *
+// f16(s_q b)) / (s_x s_q) up to the certified error (BfFinParams.h16), b = -2q
+// (L2) or -q; s = s_x * s_q (powers of two).  Corpus image: f16 rows in the
+// MFMA-native A layout of h16_index, 64-row tiles of 2 * ns KiB contiguous.
+constexpr int H_BN = 64;      // corpus rows per tile
+constexpr int H_WAVES = 8;    // waves per workgroup (one 512-thread workgroup per CU)
+constexpr int H_BQ = 512;     // queries per block: 64 per wave, held in registers as B operands
+constexpr int H_PROD = 2;     // lists per query per slot (the two lane halves)
+constexpr int H_NS_MAX = 8;   // 16-k steps: D <= 128
+constexpr int H_SAMPLE = 16;  // seed pre-pass: every H_SAMPLE-th tile
+
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+inline uint64_t h16_index(uint64_t row, int k, int ns) {
+    const uint64_t block = (row >> 5) * (uint64_t)ns + (uint64_t)(k >> 4);   // (32-row group, 16-k step)
+    const uint64_t lane = (uint64_t)(((k >> 3) & 1) * 32) + (row & 31);
+    return (block * 64 + lane) * 8 + (uint64_t)(k & 7);
+}
+
+struct H16Params {
+    const void* X;            // corpus image (h16_index), rows padded to whole tiles (zeros)
+    const void* Q;            // query image (h16_index over query rows), padded to whole H_BQ blocks
+    const float* xns;         // s * |x|^2 per row (L2 only), padded to whole tiles
+    const uint64_t* excl;     // excluded rows (tombstones, nil nodes, no vector): one word per tile
+    const uint64_t* allow;    // shared allow bits (nullable): at least one word per tile
+    const float* tau;         // [nq] seed threshold in true key units (nullable): keys above it are dropped
+    const float* qscale;      // device scalar s_q (read at launch)
+    float sx;                 // corpus scale s_x
+    uint64_t N;               // rows
+    int nq, metric;
+    int n_qblocks, n_slots;
+    uint64_t ntiles, units_per_block;   // ntiles: tiles scanned (the sample's when tile_stride > 1)
+    int tile_stride;          // corpus tile = scanned tile * tile_stride (seed pre-pass)
+    int locality;             // bit 1: XCD-contiguous workgroup ids
+    float* out_d;             // [nq][n_slots][H_PROD][BF_KP] scaled keys
+    uint32_t* out_id;
+};
+
 struct BfFinParams {
     const float* X;
     const float* Q;
@@ -104,6 +144,15 @@ struct BfFinParams {
     int split;              // approximate keys came from the bf16x3 pass (wider eps)
     int bq;                 // queries per block of the key pass (BfParams.bq)
     int prod;               // producers per query per slot (BfParams.prod)
+    // f16 key pass (h16 = 1): keys are scaled by s = sx * qscale[0]; eps adds
+    // ex_max * |B| + xnorm_max * qres[q] (the f16 rounding of corpus and query)
+    int h16;
+    const float* qscale;    // device scalar s_q
+    float sx;
+    float ex_max;           // max_x |x - f16(s_x x) / s_x| (rounded up)
+    const float* qres;      // [nq] |b - f16(s_q b) / s_q| (rounded up)
+    const float* tau_in;    // [nq] seed threshold the key pass dropped keys above (nullable)
+    float* tau_out;         // seed pre-pass: [nq] threshold in true key units, no results written
 };
 
 // Certificate fallback: exact distances of every row for a batch of failed

@@ -1,0 +1,79 @@
+// wv_topk.h -- per-lane candidate lists of the brute-force key passes
+// (wv_bf.hip, wv_h16.hip): the tile minimum, and the rare extraction of keys
+// that beat a lane's list tail.
+#pragma once
+#include "wv_device.h"
+#include "wv_params.h"
+
+namespace wv {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+// ---------------------------------------------------------------------------
+// v_min3_f32 without the IEEE canonicalisation hipcc wraps around fminf of
+// MFMA results (a NaN key never wins a comparison either way)
+#ifdef WV_BF_DBG_ITERS
+// ablation builds only: wave-level counts of tiles (0) and extract-loop iterations (1)
+__device__ unsigned long long wv_dbg_counts[2];
+#define WV_DBG_COUNT(i) if (__lane_id() == 0) atomicAdd(&wv_dbg_counts[i], 1ull);
+extern "C" void wv_dbg_read(unsigned long long* out) { hipMemcpyFromSymbol(out, HIP_SYMBOL(wv_dbg_counts), 16); }
+#else
+#define WV_DBG_COUNT(i)
+#endif
+
+__device__ __forceinline__ float min3_raw(float a, float b, float c) {
+    float r;
+    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+// Split pass candidate extraction (rare: a lane runs it only when its tile
+// minimum M beats its list tail; the wave runs it while any lane does, so it
+// is kept branch-free).  A0 / A1 hold this lane's 32 keys of one query column
+// (row offsets (r & 3) + 8 (r >> 2) and 32 + the same); each round takes the
+// minimum, masks it to +inf and inserts it.  Insertion compares keys only:
+// a key equal to the tail is dropped, which the finalize's certificate (all
+// dropped keys >= the smallest tail) still covers, and the reported ids and
+// distances come from the exact re-rank.  PT is the lane-pair partner's tail
+// (a valid rejection threshold, see the caller).
+__device__ __forceinline__ void split_extract(float& M, floatx16& A0, floatx16& A1, float (&ld)[BF_KP],
+                                              uint32_t (&li)[BF_KP], float pt, uint32_t rb0,
+                                              const uint32_t* __restrict__ rowidx = nullptr) {
+    const float INF = __builtin_inff();
+    while (M <= fminf(ld[BF_KP - 1], pt)) {
+        WV_DBG_COUNT(1)
+        // position of M: a descending scan, so among equal keys the lowest row wins
+        uint32_t sel = 0;
+#pragma unroll
+        for (int r = 15; r >= 0; --r) sel = A1[r] == M ? 16u + r : sel;
+#pragma unroll
+        for (int r = 15; r >= 0; --r) sel = A0[r] == M ? (uint32_t)r : sel;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            A0[r] = sel == (uint32_t)r ? INF : A0[r];
+            A1[r] = sel == 16u + r ? INF : A1[r];
+        }
+        uint32_t rb = rb0;   // opaque: the row ids stay in this rare loop
+        asm volatile("" : "+v"(rb));
+        if (!(M < ld[BF_KP - 1])) break;
+        uint32_t id = rb + (sel & 3u) + 8u * ((sel >> 2) & 3u) + 32u * (sel >> 4);
+        if (rowidx) id = rowidx[id];   // corpus id; the map is increasing
+        float d = M;
+#pragma unroll
+        for (int i = 0; i < BF_KP; ++i) {
+            const bool lt = d < ld[i];
+            const float td = ld[i];
+            const uint32_t ti = li[i];
+            ld[i] = lt ? d : td;
+            li[i] = lt ? id : ti;
+            d = lt ? td : d;
+            id = lt ? ti : id;
+        }
+        M = INF;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) M = min3_raw(M, A0[r], A1[r]);
+    }
+}
+
+
+}  // namespace wv

@@ -317,7 +317,9 @@ class GPUVectorIndex:
     def last_kernel_times(self):
         a, b, c = C.c_float(), C.c_float(), C.c_float()
         check(lib().wv_last_kernel_times(self._h, C.byref(a), C.byref(b), C.byref(c)))
-        return {"bf_mfma_ms": a.value, "bf_finalize_ms": b.value, "hnsw_ms": c.value}
+        d = C.c_float()
+        check(lib().wv_last_seed_time(self._h, C.byref(d)))
+        return {"bf_mfma_ms": a.value, "bf_finalize_ms": b.value, "hnsw_ms": c.value, "seed_ms": d.value}
 
     def last_batch_stats(self):
         a, b, c = C.c_uint64(), C.c_uint64(), C.c_uint64()
