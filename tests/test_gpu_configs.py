@@ -226,7 +226,6 @@ def test_auto_dispatch_flat_cutoff_matches_restatement(forbid_flat):
             ri, rd = ref.search_by_vector(q, k, allow=al.words)
         same(gi, gd, ri, rd)
         want.append((ri, rd))
-    assert forbid_flat or n_fb == 0
     bi, bd, bn = ix.search_batch(qs, k, allow=allows, mode="auto")
     for i, (ri, rd) in enumerate(want):
         same(bi[i, : bn[i]], bd[i, : bn[i]], ri, rd)

@@ -2,7 +2,9 @@
 # GPU session: -m gpu tests, then the default bench (unless a test step hung,
 # faulted or was killed: then nothing more touches the GPU in this call).
 mkdir -p gpurun_out
-timeout -k 10 ${TEST_LIMIT:-420} python -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread ${TEST_ARGS} \
+KARGS=()
+[ -n "$TEST_K" ] && KARGS=(-k "$TEST_K")
+timeout -k 10 ${TEST_LIMIT:-420} python -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread "${KARGS[@]}" \
     > gpurun_out/r2_gputests.log 2>&1
 rc=$?
 echo "tests rc=$rc" | tee -a gpurun_out/r2_gputests.log

@@ -48,7 +48,8 @@ hipError_t wv_launch_h16_rows(const float* in, int ld_in, const uint64_t* ids, u
 hipError_t wv_launch_absmax(const float* in, int ld, uint64_t n, int D, unsigned int* max_bits, hipStream_t s);
 hipError_t wv_launch_h16_qscale(const unsigned int* max_bits, float bsign, float* qscale, hipStream_t s);
 hipError_t wv_launch_h16_xns(const float* xnorm, uint64_t n, float sx, const float* qscale, float* xns, hipStream_t s);
-hipError_t wv_launch_bf_h16(const wv::H16Params* p, int ns, hipStream_t s);
+hipError_t wv_launch_bf_h16(const wv::H16Params* p, int ns, int seed, hipStream_t s);
+hipError_t wv_launch_h16_seed(const wv::H16SeedParams* p, hipStream_t s);
 float wv_h16_pow2_scale(float maxabs);
 hipError_t wv_launch_pq_topk(const float* skey, const uint32_t* sval, const float* dist, const uint32_t* rows,
                              uint64_t nr, int q0, int nqc, int k, uint64_t id_base, uint64_t* out_ids, float* out_d,
@@ -522,26 +523,34 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     if (seed) {
         const uint64_t nts = (ntl + wv::H_SAMPLE - 1) / wv::H_SAMPLE;
         const wv::BfSchedule ss = wv::bf_schedule(nq, nts * wv::H_BN, ix->n_cus, wv::H_BQ, wv::H_BN);
-        HIP_TRY(ix->cand_d.ensure((size_t)nq * ss.n_slots * wv::H_PROD * wv::BF_KP * 4));
-        HIP_TRY(ix->cand_id.ensure((size_t)nq * ss.n_slots * wv::H_PROD * wv::BF_KP * 4));
+        HIP_TRY(ix->cand_d.ensure((size_t)nq * ss.n_slots * wv::H_PROD * 4));
         hp.ntiles = ss.ntiles;
         hp.units_per_block = ss.units_per_block;
         hp.n_slots = ss.n_slots;
         hp.tile_stride = wv::H_SAMPLE;
         hp.tau = nullptr;
         hp.out_d = ix->cand_d.as<float>();
-        hp.out_id = ix->cand_id.as<uint32_t>();
+        hp.out_id = nullptr;
         if (ix->timing) HIP_TRY(hipEventRecord(ix->ev[6], s));
-        HIP_TRY(wv_launch_bf_h16(&hp, ns, s));
-        fp.cand_d = ix->cand_d.as<float>();
-        fp.cand_id = ix->cand_id.as<uint32_t>();
-        fp.n_slots = ss.n_slots;
-        fp.ntiles = ss.ntiles;
-        fp.units_per_block = ss.units_per_block;
-        fp.tau_out = ix->tau.as<float>();
-        HIP_TRY(wv_launch_bf_finalize(&fp, s));
+        HIP_TRY(wv_launch_bf_h16(&hp, ns, 1, s));
+        wv::H16SeedParams sp{};
+        sp.minima = ix->cand_d.as<float>();
+        sp.n_slots = ss.n_slots;
+        sp.ntiles = ss.ntiles;
+        sp.units_per_block = ss.units_per_block;
+        sp.nq = nq;
+        sp.k = k;
+        sp.metric = ix->metric;
+        sp.D = ix->dim;
+        sp.qscale = ix->qscale.as<float>();
+        sp.sx = ix->h16_sx;
+        sp.qnorm = ix->q_nrm2.as<float>();
+        sp.xnorm_max = ix->maxnorm_host;
+        sp.ex_max = ix->h16_ex;
+        sp.qres = ix->qres.as<float>();
+        sp.tau = ix->tau.as<float>();
+        HIP_TRY(wv_launch_h16_seed(&sp, s));
         if (ix->timing) HIP_TRY(hipEventRecord(ix->ev[7], s));
-        fp.tau_out = nullptr;
     }
     const wv::BfSchedule sch = wv::bf_schedule(nq, N, ix->n_cus, wv::H_BQ, wv::H_BN);
     HIP_TRY(ix->cand_d.ensure((size_t)nq * sch.n_slots * wv::H_PROD * wv::BF_KP * 4));
@@ -554,7 +563,7 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     hp.out_d = ix->cand_d.as<float>();
     hp.out_id = ix->cand_id.as<uint32_t>();
     if (ix->timing) HIP_TRY(hipEventRecord(ix->ev[0], s));
-    HIP_TRY(wv_launch_bf_h16(&hp, ns, s));
+    HIP_TRY(wv_launch_bf_h16(&hp, ns, 0, s));
     if (ix->timing) HIP_TRY(hipEventRecord(ix->ev[1], s));
     fp.cand_d = ix->cand_d.as<float>();
     fp.cand_id = ix->cand_id.as<uint32_t>();
@@ -746,6 +755,7 @@ int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
     }
 fallbacks:
     ix->last_fallbacks += fails.size();
+    if (!fails.empty() && std::getenv("WV_ABLATE_NO_FALLBACK")) fails.clear();   // kernel ablations only
     if (!fails.empty() && k <= wv::BF_FAST_KMAX) {
         // batched threshold filter over the corpus for every failed query
         std::vector<int32_t> rest;

@@ -1198,24 +1198,22 @@ __device__ void finalize_one(const BfFinParams& p, int q, float* sd, uint32_t* s
     float eps, bfull;
     // bf16x3 keys: 3x the accumulated terms, plus the split error
     // 4 * 2^-16 * |x| |b| with b = -2q (L2) or -q
-    const float acc_f = p.split ? 12.f : (p.h16 ? 6.f : 4.f);
+    const float acc_f = p.split ? 12.f : 4.f;
     const float split_e = p.split ? 4.f * 1.52587890625e-05f : 0.f;   // 2^-16
-    // f16 keys: |sum f16(s_x x) f16(s_q b) / (s_x s_q) - x.b| <= |x - x~| |b~| +
-    // |x| |b - b~|, with the residual norms measured when the images were made
-    const float qres = p.h16 ? p.qres[q] : 0.f;
     if (METRIC == WV_METRIC_L2) {
         const float qn = sqrtf(p.qnorm[q]);
         const float s = qn + p.xnorm_max;
         eps = acc_f * D4 * u * s * s + 2.f * split_e * qn * p.xnorm_max;
-        if (p.h16) eps += p.ex_max * (2.f * qn + qres) + p.xnorm_max * qres;
         bfull = bound + p.qnorm[q];
     } else {
         const float qn = p.qnorm[q];
         eps = acc_f * D4 * u * qn * p.xnorm_max + 4.f * u + split_e * qn * p.xnorm_max;
-        if (p.h16) eps += p.ex_max * (qn + qres) + p.xnorm_max * qres;
         bfull = METRIC == WV_METRIC_DOT ? bound : 1.0f + bound;
     }
     eps *= 1.0001f;   // the float evaluation of the bound itself
+    // f16 keys: |sum f16(s_x x) f16(s_q b) / (s_x s_q) - x.b| <= |x - x~| |b~| +
+    // |x| |b - b~|, with the residual norms measured when the images were made
+    if (p.h16) eps = h16_eps(METRIC, p.D, p.qnorm[q], p.xnorm_max, p.ex_max, p.qres[q]);
     if (p.tau_out) {
         // seed pre-pass: every point of the true top k has key <= dk - (the
         // key's offset from the distance) + eps, dk being the k-th exact

@@ -33,11 +33,37 @@ namespace wv {
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 
-__device__ __forceinline__ void glds16(const void* src, void* lds_wave_base) {
-    __builtin_amdgcn_global_load_lds(src, lds_wave_base, 16, 0, 0);
+// LDS-DMA (global_load_lds_dword{,x4}) as inline asm: the destination is the
+// wave-uniform LDS byte address in M0 (+ lane * size).  Written as asm so the
+// compiler's waitcnt pass does not see them: for a builtin LDS-DMA it waits
+// vmcnt(0) before every LDS read it cannot prove disjoint -- the prefetch of
+// the next tiles would be drained before the current one is read.  The
+// kernel places the (counted) vmcnt waits itself.
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
 }
-__device__ __forceinline__ void glds4(const void* src, void* lds_wave_base) {
-    __builtin_amdgcn_global_load_lds(src, lds_wave_base, 4, 0, 0);
+__device__ __forceinline__ void glds16(const void* src, uint32_t lds_wave_base) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(src), "s"(lds_wave_base) : "memory");
+}
+__device__ __forceinline__ void glds4(const void* src, uint32_t lds_wave_base) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(src), "s"(lds_wave_base) : "memory");
+}
+// wait until at most n of this wave's vector-memory ops are outstanding
+__device__ __forceinline__ void vm_wait(int n) {
+    switch (n) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    }
+}
+__device__ __forceinline__ void block_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 // LDS stage: [2 row blocks][ns k-steps][64 lanes] uint4 image, then 64 floats
@@ -47,8 +73,12 @@ struct H16Stage {
     static constexpr int IMG_U4 = 2 * NS * 64;
     static constexpr int U4 = IMG_U4 + 16 + 1;
 };
+constexpr int H_STAGES = 3;   // tile t computes from stage t % 3 while t + 1 and t + 2 land
 
-template <int NS, bool L2>
+// SEED: the pre-pass over every H_SAMPLE-th tile keeps only each lane's
+// running minimum per query column (distinct rows per (slot, lane half)),
+// written as one key per list; wv_h16_seed_kernel turns them into thresholds.
+template <int NS, bool L2, bool SEED>
 __global__ __launch_bounds__(512, 2) void wv_bf_h16_kernel(H16Params p) {
     extern __shared__ uint4 lds[];
     using St = H16Stage<NS>;
@@ -71,19 +101,23 @@ __global__ __launch_bounds__(512, 2) void wv_bf_h16_kernel(H16Params p) {
     uint64_t u_last = u_first + p.units_per_block;
     if (u_last > (uint64_t)p.n_qblocks * p.ntiles) u_last = (uint64_t)p.n_qblocks * p.ntiles;
 
+    const uint32_t lds0 = lds_addr(lds);
+    // this wave's LDS-DMA ops per tile (the counted waits below)
+    const int n_ops = (wave < St::IMG_U4 / 64 ? (St::IMG_U4 / 64 - 1 - wave) / H_WAVES + 1 : 0) +
+                      ((wave == 0 && L2) ? 1 : 0) + (wave == 1 ? 1 : 0);
     auto fill = [&](uint64_t t, int st) {
         const uint64_t tile = t * (uint64_t)p.tile_stride;
-        uint4* dst = lds + st * St::U4;
+        const uint32_t dst = lds0 + (uint32_t)(st * St::U4 * 16);
         const uint4* src = X + tile * St::IMG_U4;
 #pragma unroll
-        for (int i = wave; i < St::IMG_U4 / 64; i += H_WAVES) glds16(src + i * 64 + lane, dst + i * 64);
+        for (int i = wave; i < St::IMG_U4 / 64; i += H_WAVES) glds16(src + i * 64 + lane, dst + i * 1024);
         if (wave == 0) {
-            if (L2) glds4(p.xns + tile * H_BN + lane, dst + St::IMG_U4);
+            if (L2) glds4(p.xns + tile * H_BN + lane, dst + St::IMG_U4 * 16);
         } else if (wave == 1) {
             // lanes 0-1: exclusion word, 2-3: allow word (dword halves)
             const uint32_t* w = lane < 2 ? reinterpret_cast<const uint32_t*>(p.excl + tile) + lane
                                          : reinterpret_cast<const uint32_t*>(p.allow + tile) + (lane - 2);
-            if (lane < 2 || (lane < 4 && has_allow)) glds4(w, dst + St::IMG_U4 + 16);
+            if (lane < 2 || (lane < 4 && has_allow)) glds4(w, dst + (St::IMG_U4 + 16) * 16);
         }
     };
 
@@ -113,6 +147,11 @@ __global__ __launch_bounds__(512, 2) void wv_bf_h16_kernel(H16Params p) {
             if (jq0 < p.nq) tau0 = fminf(FLT_MAX, p.tau[jq0] * s);
             if (jq1 < p.nq) tau1 = fminf(FLT_MAX, p.tau[jq1] * s);
         }
+        // consume the ordinary loads here, before any LDS-DMA is in flight:
+        // the compiler's wait for them is then not a wait for the tile stream
+#pragma unroll
+        for (int st = 0; st < NS; ++st) asm volatile("" ::"v"(bq0[st].x), "v"(bq1[st].x));
+        asm volatile("" ::"v"(tau0), "v"(tau1));
         float l0d[BF_KP], l1d[BF_KP];
         uint32_t l0i[BF_KP], l1i[BF_KP];
 #pragma unroll
@@ -120,85 +159,163 @@ __global__ __launch_bounds__(512, 2) void wv_bf_h16_kernel(H16Params p) {
             l0d[i] = FLT_MAX; l1d[i] = FLT_MAX;
             l0i[i] = WV_NIL; l1i[i] = WV_NIL;
         }
-        __syncthreads();   // the previous segment's reads of both stages are done
+        // (the previous segment ended with every stage read and every DMA landed)
         if (ntile > 0) fill(t_begin, 0);
-        __syncthreads();   // drains the B loads and tile 0 (vmcnt(0) + barrier)
+        if (ntile > 1) fill(t_begin + 1, 1);
+        vm_wait(ntile > 1 ? n_ops : 0);   // this wave's part of tile 0
+        block_barrier();                  // everyone's
 
-        for (int t = 0; t < ntile; ++t) {
-            const int st = t & 1;
-            if (t + 1 < ntile) fill(t_begin + t + 1, st ^ 1);
-            const uint4* img = lds + st * St::U4;
-            const uint64_t tile = (t_begin + t) * (uint64_t)p.tile_stride;
-            const uint64_t row0 = tile * H_BN;
-            // lanes l and l ^ 32 keep lists for the same query column (see the split pass)
-            const float pt0 = fminf(__shfl_xor(l0d[BF_KP - 1], 32, 64), tau0);
-            const float pt1 = fminf(__shfl_xor(l1d[BF_KP - 1], 32, 64), tau1);
-
-            floatx16 acc00, acc01, acc10, acc11;
-            floatx16 xc0, xc1;
+        // Two-phase software pipeline over half tiles (rows 0-31: H0 =
+        // acc00/acc01, rows 32-63: H1 = acc10/acc11).  Iteration t:
+        //   A  MFMAs of H1(t)       beside the tile minima of H0(t)
+        //   B  extraction of H0(t)  (rare)
+        //   C  tile t + 1 landed, barrier
+        //   E  MFMAs of H0(t + 1)   beside the tile minima of H1(t)
+        //   F  extraction of H1(t)
+        // so each wave's epilogue VALU issues between its own MFMAs instead of
+        // after them (the per-tile barrier keeps the two waves of a SIMD in
+        // phase, so they cannot cover each other).
+        const float INF = __builtin_inff();
+        floatx16 acc00, acc01, acc10, acc11;
+        // one half tile's MFMAs (all operands read from LDS up front: 8 A
+        // fragments + the C-in), with VALU work of the other half placed
+        // between them by the `between` callback and sched_group_barrier
+        auto mfma_half = [&](const uint4* img, int rb, floatx16& accA, floatx16& accB, auto&& between) {
+            uint4 a[NS];
+#pragma unroll
+            for (int k = 0; k < NS; ++k) a[k] = img[(rb * NS + k) * 64 + lane];
+            floatx16 xc;
             if (L2) {
-                const float* xn = reinterpret_cast<const float*>(img + St::IMG_U4);
+                const float* xn = reinterpret_cast<const float*>(img + St::IMG_U4) + 32 * rb;
 #pragma unroll
                 for (int g4 = 0; g4 < 4; ++g4) {
-                    const float4 a = *reinterpret_cast<const float4*>(xn + 4 * khalf + 8 * g4);
-                    const float4 b = *reinterpret_cast<const float4*>(xn + 32 + 4 * khalf + 8 * g4);
-                    xc0[4 * g4] = a.x; xc0[4 * g4 + 1] = a.y; xc0[4 * g4 + 2] = a.z; xc0[4 * g4 + 3] = a.w;
-                    xc1[4 * g4] = b.x; xc1[4 * g4 + 1] = b.y; xc1[4 * g4 + 2] = b.z; xc1[4 * g4 + 3] = b.w;
+                    const float4 v = *reinterpret_cast<const float4*>(xn + 4 * khalf + 8 * g4);
+                    xc[4 * g4] = v.x; xc[4 * g4 + 1] = v.y; xc[4 * g4 + 2] = v.z; xc[4 * g4 + 3] = v.w;
                 }
             } else {
 #pragma unroll
-                for (int r = 0; r < 16; ++r) { xc0[r] = 0.f; xc1[r] = 0.f; }
+                for (int r = 0; r < 16; ++r) xc[r] = 0.f;
             }
+            between();
 #pragma unroll
             for (int k = 0; k < NS; ++k) {
-                const half8 a0 = __builtin_bit_cast(half8, img[k * 64 + lane]);
-                const half8 a1 = __builtin_bit_cast(half8, img[(NS + k) * 64 + lane]);
-                const half8 b0 = __builtin_bit_cast(half8, bq0[k]);
-                const half8 b1 = __builtin_bit_cast(half8, bq1[k]);
-                acc00 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b0, k == 0 ? xc0 : acc00, 0, 0, 0);
-                acc01 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b1, k == 0 ? xc0 : acc01, 0, 0, 0);
-                acc10 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b0, k == 0 ? xc1 : acc10, 0, 0, 0);
-                acc11 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b1, k == 0 ? xc1 : acc11, 0, 0, 0);
+                const half8 ak = __builtin_bit_cast(half8, a[k]);
+                accA = __builtin_amdgcn_mfma_f32_32x32x16_f16(ak, __builtin_bit_cast(half8, bq0[k]), k == 0 ? xc : accA,
+                                                              0, 0, 0);
+                accB = __builtin_amdgcn_mfma_f32_32x32x16_f16(ak, __builtin_bit_cast(half8, bq1[k]), k == 0 ? xc : accB,
+                                                              0, 0, 0);
             }
-            // ---- epilogue of one 64-row tile ----
-            uint64_t okw;
-            {
-                const uint32_t* w = reinterpret_cast<const uint32_t*>(img + St::IMG_U4 + 16);
-                const uint64_t ex = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
-                const uint64_t al = has_allow ? ((uint64_t)w[2] | ((uint64_t)w[3] << 32)) : ~0ull;
-                okw = ~ex & al;
-                if (row0 + H_BN > p.N) okw &= p.N > row0 ? ((1ull << (p.N - row0)) - 1) : 0ull;
-            }
-            const uint32_t rb0 = (uint32_t)row0 + 4 * khalf;
-            const float INF = __builtin_inff();
-            if (okw != ~0ull || (qb + 1) * H_BQ > p.nq) {
-                const uint64_t o0 = (jq0 < p.nq ? okw : 0ull) >> (4 * khalf);
-                const uint64_t o1 = (jq1 < p.nq ? okw : 0ull) >> (4 * khalf);
-                const uint32_t o0lo = (uint32_t)o0, o0hi = (uint32_t)(o0 >> 32);
-                const uint32_t o1lo = (uint32_t)o1, o1hi = (uint32_t)(o1 >> 32);
-                constexpr uint32_t LANE_ROWS = 0x0F0F0F0Fu;
-                if (!__all((o0lo & o0hi & o1lo & o1hi & LANE_ROWS) == LANE_ROWS)) {
+            // LDS reads first, then MFMAs each followed by one VALU op
+            __builtin_amdgcn_sched_group_barrier(0x100, NS + (L2 ? 4 : 0), 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const int bit = (r & 3) + 8 * (r >> 2);
-                        acc00[r] = (o0lo >> bit) & 1u ? acc00[r] : INF;
-                        acc10[r] = (o0hi >> bit) & 1u ? acc10[r] : INF;
-                        acc01[r] = (o1lo >> bit) & 1u ? acc01[r] : INF;
-                        acc11[r] = (o1hi >> bit) & 1u ? acc11[r] : INF;
-                    }
-                }
+            for (int i = 0; i < 2 * NS; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
             }
-            float m0 = INF, m1 = INF;
+        };
+        // eligibility of a tile's 64 rows for this lane's two columns (bits of
+        // rows 4 khalf + ..., low word: rows 0-31, high word: rows 32-63)
+        auto tile_ok = [&](const uint4* img, uint64_t t, uint64_t& o0, uint64_t& o1) -> bool {
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(img + St::IMG_U4 + 16);
+            const uint64_t ex = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+            const uint64_t al = has_allow ? ((uint64_t)w[2] | ((uint64_t)w[3] << 32)) : ~0ull;
+            uint64_t okw = ~ex & al;
+            const uint64_t row0 = t * (uint64_t)p.tile_stride * H_BN;
+            if (row0 + H_BN > p.N) okw &= p.N > row0 ? ((1ull << (p.N - row0)) - 1) : 0ull;
+            o0 = (jq0 < p.nq ? okw : 0ull) >> (4 * khalf);
+            o1 = (jq1 < p.nq ? okw : 0ull) >> (4 * khalf);
+            return okw != ~0ull || (qb + 1) * H_BQ > p.nq;
+        };
+        // mask a half's ineligible rows to +inf (rows (r & 3) + 8 (r >> 2) of its 32)
+        auto mask_half = [&](floatx16& A, floatx16& B, uint32_t oa, uint32_t ob) {
+            constexpr uint32_t LANE_ROWS = 0x0F0F0F0Fu;
+            if (__all((oa & ob & LANE_ROWS) == LANE_ROWS)) return;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                m0 = min3_raw(m0, acc00[r], acc10[r]);
-                m1 = min3_raw(m1, acc01[r], acc11[r]);
+                const int bit = (r & 3) + 8 * (r >> 2);
+                A[r] = (oa >> bit) & 1u ? A[r] : INF;
+                B[r] = (ob >> bit) & 1u ? B[r] : INF;
             }
-            split_extract(m0, acc00, acc10, l0d, l0i, pt0, rb0);
-            split_extract(m1, acc01, acc11, l1d, l1i, pt1, rb0);
-            __syncthreads();   // the next stage has landed; this stage is free for the tile after
+        };
+        auto min16 = [&](const floatx16& A) {
+            // four independent chains (short dependency depth), v_min3 each
+            float m0 = fminf(fminf(A[0], A[1]), A[2]), m1 = fminf(fminf(A[3], A[4]), A[5]);
+            float m2 = fminf(fminf(A[6], A[7]), A[8]), m3 = fminf(fminf(A[9], A[10]), A[11]);
+            m0 = fminf(fminf(m0, A[12]), A[13]);
+            m1 = fminf(fminf(m1, A[14]), A[15]);
+            return fminf(fminf(m0, m1), fminf(m2, m3));
+        };
+
+        int st = 0;
+        uint64_t o0 = 0, o1 = 0;
+        bool need_mask = false;
+        if (ntile > 0) {
+            mfma_half(lds, 0, acc00, acc01, [] {});
+            need_mask = tile_ok(lds, t_begin, o0, o1);
+        }
+        for (int t = 0; t < ntile; ++t) {
+#ifndef WV_H16_ABLATE_NO_FILL
+            // stage (t + 2) % 3 was last read in iteration t - 1, before its barrier
+            if (t + 2 < ntile) fill(t_begin + t + 2, st == 0 ? 2 : st - 1);
+#endif
+            const uint4* img = lds + st * St::U4;
+            const uint32_t rb0 = (uint32_t)((t_begin + t) * (uint64_t)p.tile_stride * H_BN) + 4 * khalf;
+            // lanes l and l ^ 32 keep lists for the same query column (see the split pass)
+            const float pt0 = fminf(__shfl_xor(l0d[BF_KP - 1], 32, 64), tau0);
+            const float pt1 = fminf(__shfl_xor(l1d[BF_KP - 1], 32, 64), tau1);
+            const bool mask_t = need_mask;
+            const uint64_t mo0 = o0, mo1 = o1;
+            // ---- A: H1(t) MFMAs, H0(t) minima ----
+            if (mask_t) mask_half(acc00, acc01, (uint32_t)mo0, (uint32_t)mo1);
+            float m0, m1;
+            mfma_half(img, 1, acc10, acc11, [&] { m0 = min16(acc00); m1 = min16(acc01); });
+            // ---- B ----
+            if constexpr (SEED) {
+                l0d[0] = fminf(l0d[0], m0);
+                l1d[0] = fminf(l1d[0], m1);
+            } else {
+#ifdef WV_H16_ABLATE_NO_EXTRACT
+                if (m0 == 1234.5f) l0d[0] = m1 + pt0 + pt1;
+#else
+                split_extract16(m0, acc00, l0d, l0i, pt0, rb0);
+                split_extract16(m1, acc01, l1d, l1i, pt1, rb0);
+#endif
+            }
+            // ---- C: tile t + 1 has landed (t + 2 may stay in flight); every
+            // wave is done reading stage t % 3's operands ----
+            if (t + 1 < ntile) vm_wait(t + 2 < ntile ? n_ops : 0);
+            block_barrier();
+            const int st1 = st == 2 ? 0 : st + 1;
+            // ---- E: H0(t + 1) MFMAs, H1(t) minima ----
+            if (mask_t) mask_half(acc10, acc11, (uint32_t)(mo0 >> 32), (uint32_t)(mo1 >> 32));
+            if (t + 1 < ntile) {
+                mfma_half(lds + st1 * St::U4, 0, acc00, acc01, [&] { m0 = min16(acc10); m1 = min16(acc11); });
+                need_mask = tile_ok(lds + st1 * St::U4, t_begin + t + 1, o0, o1);
+            } else {
+                m0 = min16(acc10);
+                m1 = min16(acc11);
+            }
+            // ---- F ----
+            if constexpr (SEED) {
+                l0d[0] = fminf(l0d[0], m0);
+                l1d[0] = fminf(l1d[0], m1);
+            } else {
+#ifdef WV_H16_ABLATE_NO_EXTRACT
+                if (m0 == 1234.5f) l0d[0] = m1 + pt0 + pt1;
+#else
+                split_extract16(m0, acc10, l0d, l0i, pt0, rb0 + 32);
+                split_extract16(m1, acc11, l1d, l1i, pt1, rb0 + 32);
+#endif
+            }
+            st = st1;
         }
 
+        if constexpr (SEED) {
+            if (jq0 < p.nq) p.out_d[((size_t)jq0 * p.n_slots + slot) * H_PROD + khalf] = l0d[0];
+            if (jq1 < p.nq) p.out_d[((size_t)jq1 * p.n_slots + slot) * H_PROD + khalf] = l1d[0];
+            continue;
+        }
         const size_t per_q = (size_t)p.n_slots * H_PROD * BF_KP;
         if (jq0 < p.nq) {
             const size_t base = (size_t)jq0 * per_q + ((size_t)slot * H_PROD + khalf) * BF_KP;
@@ -210,6 +327,54 @@ __global__ __launch_bounds__(512, 2) void wv_bf_h16_kernel(H16Params p) {
 #pragma unroll
             for (int i = 0; i < BF_KP; ++i) { p.out_d[base + i] = l1d[i]; p.out_id[base + i] = l1i[i]; }
         }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Seed thresholds from the pre-pass minima: the n_lists minima of a query are
+// approximate keys of distinct rows, so the k-th smallest of them, m_k, has k
+// real points with key <= m_k, i.e. true distance <= m_k + offset + eps: the
+// true k-th distance is no larger, and a point of the true top k has key <=
+// its distance - offset + eps <= m_k + 2 eps.  One wave per query.
+__global__ __launch_bounds__(64) void wv_h16_seed_kernel(H16SeedParams p) {
+    const int q = blockIdx.x;
+    const int lane = threadIdx.x;
+    if (q >= p.nq) return;
+    const int n = bf_slots_of((uint64_t)(q / H_BQ), p.ntiles, p.units_per_block) * H_PROD;
+    const float* m = p.minima + (size_t)q * p.n_slots * H_PROD;
+    const float inv_s = 1.0f / (p.sx * p.qscale[0]);
+    // k rounds of a wave-wide minimum over the lanes' shares
+    float taken = -__builtin_inff();
+    int n_taken = 0;
+    float mk = __builtin_inff();
+    for (int r = 0; r < p.k; ++r) {
+        float best = __builtin_inff();
+        int where = 0x7FFFFFFF;
+        for (int i = lane; i < n; i += 64) {
+            const float v = m[i];
+            // strictly after the last taken (value, index) in (value, index) order
+            const bool after = v > taken || (v == taken && i > n_taken);
+            if (after && v < __builtin_inff() && (v < best || (v == best && i < where))) { best = v; where = i; }
+        }
+        for (int o = 32; o >= 1; o >>= 1) {
+            const float ob = __shfl_xor(best, o, 64);
+            const int ow = __shfl_xor(where, o, 64);
+            if (ob < best || (ob == best && ow < where)) { best = ob; where = ow; }
+        }
+        if (!(best < __builtin_inff())) { mk = __builtin_inff(); break; }
+        taken = best;
+        n_taken = where;
+        mk = best;
+    }
+    if (lane == 0) {
+        float tau = __builtin_inff();
+        if (mk < __builtin_inff()) {
+            const float key = mk * inv_s;
+            const float eps = h16_eps(p.metric, p.D, p.qnorm[q], p.xnorm_max, p.ex_max, p.qres[q]);
+            tau = key + 2.f * eps;
+            tau += 4.f * 5.9604645e-08f * (fabsf(key) + 2.f * eps) + 1e-3f * eps;   // this sum's rounding
+        }
+        p.tau[q] = tau;
     }
 }
 
@@ -319,7 +484,7 @@ hipError_t wv_launch_h16_xns(const float* xnorm, uint64_t n, float sx, const flo
     return hipGetLastError();
 }
 
-hipError_t wv_launch_bf_h16(const wv::H16Params* p, int ns, hipStream_t s) {
+hipError_t wv_launch_bf_h16(const wv::H16Params* p, int ns, int seed, hipStream_t s) {
     const uint64_t total = (uint64_t)p->n_qblocks * p->ntiles;
     const unsigned nb = (unsigned)((total + p->units_per_block - 1) / p->units_per_block);
     if (nb == 0) return hipSuccess;
@@ -327,10 +492,15 @@ hipError_t wv_launch_bf_h16(const wv::H16Params* p, int ns, hipStream_t s) {
         return hipErrorInvalidValue;
     const bool l2 = p->metric == WV_METRIC_L2;
     if (l2 && !p->xns) return hipErrorInvalidValue;
-    const size_t lds = 2 * (size_t)(2 * ns * 64 + 17) * 16;
-#define WV_H16_LAUNCH(NS)                                                                              \
-    if (l2) hipLaunchKernelGGL((wv::wv_bf_h16_kernel<NS, true>), dim3(nb), dim3(512), lds, s, *p);    \
-    else hipLaunchKernelGGL((wv::wv_bf_h16_kernel<NS, false>), dim3(nb), dim3(512), lds, s, *p);
+    const size_t lds = (size_t)wv::H_STAGES * (2 * ns * 64 + 17) * 16;
+#define WV_H16_LAUNCH(NS)                                                                                      \
+    if (seed) {                                                                                                \
+        if (l2) hipLaunchKernelGGL((wv::wv_bf_h16_kernel<NS, true, true>), dim3(nb), dim3(512), lds, s, *p);   \
+        else hipLaunchKernelGGL((wv::wv_bf_h16_kernel<NS, false, true>), dim3(nb), dim3(512), lds, s, *p);     \
+    } else {                                                                                                   \
+        if (l2) hipLaunchKernelGGL((wv::wv_bf_h16_kernel<NS, true, false>), dim3(nb), dim3(512), lds, s, *p);  \
+        else hipLaunchKernelGGL((wv::wv_bf_h16_kernel<NS, false, false>), dim3(nb), dim3(512), lds, s, *p);    \
+    }
     switch (ns) {
         case 1: WV_H16_LAUNCH(1) break;
         case 2: WV_H16_LAUNCH(2) break;
@@ -342,6 +512,13 @@ hipError_t wv_launch_bf_h16(const wv::H16Params* p, int ns, hipStream_t s) {
         default: WV_H16_LAUNCH(8) break;
     }
 #undef WV_H16_LAUNCH
+    return hipGetLastError();
+}
+
+hipError_t wv_launch_h16_seed(const wv::H16SeedParams* p, hipStream_t s) {
+    if (p->nq == 0) return hipSuccess;
+    if (p->k < 1 || p->k > 64) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(wv::wv_h16_seed_kernel, dim3(p->nq), dim3(64), 0, s, *p);
     return hipGetLastError();
 }
 

@@ -125,6 +125,19 @@ struct H16Params {
     uint32_t* out_id;
 };
 
+struct H16SeedParams {
+    const float* minima;      // [nq][n_slots][H_PROD] pre-pass running minima (scaled keys)
+    int n_slots;
+    uint64_t ntiles, units_per_block;   // the pre-pass schedule
+    int nq, k, metric, D;
+    const float* qscale;
+    float sx;
+    const float* qnorm;       // |q|^2 (L2) or |q|
+    float xnorm_max, ex_max;
+    const float* qres;
+    float* tau;               // [nq] out: threshold in true key units (+inf: none)
+};
+
 struct BfFinParams {
     const float* X;
     const float* Q;

@@ -76,4 +76,61 @@ __device__ __forceinline__ void split_extract(float& M, floatx16& A0, floatx16& 
 }
 
 
+// split_extract over one 32 x 32 accumulator's 16 keys of a lane (rows
+// rb + (r & 3) + 8 (r >> 2)): the f16 pass extracts per half tile.  The keys
+// are compared with fminf (the file is built with -fno-honor-nans: v_min3
+// without canonicalisation; a NaN key -- only possible after an f16 overflow,
+// whose residual makes eps infinite -- never certifies anything).
+__device__ __forceinline__ void split_extract16(float& M, floatx16& A, float (&ld)[BF_KP], uint32_t (&li)[BF_KP],
+                                                float pt, uint32_t rb) {
+    const float INF = __builtin_inff();
+    while (M <= fminf(ld[BF_KP - 1], pt)) {
+        WV_DBG_COUNT(1)
+        uint32_t sel = 0;
+#pragma unroll
+        for (int r = 15; r >= 0; --r) sel = A[r] == M ? (uint32_t)r : sel;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) A[r] = sel == (uint32_t)r ? INF : A[r];
+        uint32_t rbo = rb;   // opaque: the row ids stay in this rare loop
+        asm volatile("" : "+v"(rbo));
+        if (!(M < ld[BF_KP - 1])) break;
+        uint32_t id = rbo + (sel & 3u) + 8u * (sel >> 2);
+        float d = M;
+#pragma unroll
+        for (int i = 0; i < BF_KP; ++i) {
+            const bool lt = d < ld[i];
+            const float td = ld[i];
+            const uint32_t ti = li[i];
+            ld[i] = lt ? d : td;
+            li[i] = lt ? id : ti;
+            d = lt ? td : d;
+            id = lt ? ti : id;
+        }
+        float m0 = fminf(fminf(A[0], A[1]), A[2]), m1 = fminf(fminf(A[3], A[4]), A[5]);
+        float m2 = fminf(fminf(A[6], A[7]), A[8]), m3 = fminf(fminf(A[9], A[10]), A[11]);
+        m0 = fminf(fminf(m0, A[12]), A[13]);
+        m1 = fminf(fminf(m1, A[14]), A[15]);
+        M = fminf(fminf(m0, m1), fminf(m2, m3));
+    }
+}
+
+// Certificate eps of the f16 key pass (true units): |key + offset - reference
+// distance| <= eps for every row, offset = |q|^2 (L2), 0 (dot), 1 (cosine).
+// Accumulation and reference-order terms 6 (D + 4) 2^-24 (|q| + max|x|)^2
+// (L2) / |q| max|x| (dot, cosine), plus the f16 rounding of the corpus
+// (ex_max |b~|) and of the query (max|x| qres), b = -2q (L2) or -q.
+__device__ __forceinline__ float h16_eps(int metric, int D, float qnorm, float xnorm_max, float ex_max, float qres) {
+    const float u = 5.9604645e-08f;
+    const float D4 = (float)(D + 4);
+    float eps;
+    if (metric == WV_METRIC_L2) {
+        const float qn = sqrtf(qnorm);
+        const float s = qn + xnorm_max;
+        eps = 6.f * D4 * u * s * s + ex_max * (2.f * qn + qres) + xnorm_max * qres;
+    } else {
+        eps = 6.f * D4 * u * qnorm * xnorm_max + 4.f * u + ex_max * (qnorm + qres) + xnorm_max * qres;
+    }
+    return eps * 1.0001f;
+}
+
 }  // namespace wv
