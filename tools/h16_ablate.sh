@@ -6,7 +6,7 @@ set -e
 B=build/h16; mkdir -p $B
 C=weaviate_amd/csrc
 HF="-O3 -std=c++17 --offload-arch=gfx950 -fPIC -ffp-contract=off"
-VARIANTS=${VARIANTS:-"base= noext=-DWV_H16_ABLATE_NO_EXTRACT noepi=-DWV_H16_ABLATE_NO_EPILOGUE nofill=-DWV_H16_ABLATE_NO_FILL"}
+VARIANTS=${VARIANTS:-"base= nomin=-DWV_H16_ABLATE_NO_EXTRACT:-DWV_H16_ABLATE_NO_MIN pure=-DWV_H16_ABLATE_NO_EXTRACT:-DWV_H16_ABLATE_NO_MIN:-DWV_H16_ABLATE_NO_BARRIER:-DWV_H16_ABLATE_NO_FILL pure_nolds=-DWV_H16_ABLATE_NO_EXTRACT:-DWV_H16_ABLATE_NO_MIN:-DWV_H16_ABLATE_NO_BARRIER:-DWV_H16_ABLATE_NO_FILL:-DWV_H16_ABLATE_NO_LDS nomin_nolds=-DWV_H16_ABLATE_NO_EXTRACT:-DWV_H16_ABLATE_NO_MIN:-DWV_H16_ABLATE_NO_LDS"}
 if [ "$1" == "build" ]; then
   make -s -C $C ARCH=gfx950
   /opt/rocm/bin/hipcc $HF -x hip -c tools/h16_ablate.cpp -o $B/main.o

@@ -1,0 +1,34 @@
+#!/bin/bash
+# f16 key pass on the harness (build/h16/abl_base, tools/h16_ablate.sh):
+# rocprofv3 kernel trace + stats, then separate PMC passes (no tracing in
+# the counter runs).  Output under gpurun_out/pmc_h16/.
+set -e
+O=gpurun_out/pmc_h16; mkdir -p $O
+export TMPDIR=/tmp
+B=${B:-build/h16/abl_base}
+ARGS="${N:-1000000} ${NQ:-10000} ${D:-128} pmc"
+timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- $B $ARGS > $O/trace.log 2>&1
+i=0
+for set in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE" \
+           "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_MISC SQ_INSTS_MFMA" \
+           "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_SCA SQ_INSTS_SMEM SQ_INST_CYCLES_VMEM_RD SQ_WAVES" \
+           "FETCH_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
+  i=$((i+1))
+  timeout -s KILL 60 rocprofv3 --pmc $set --output-format csv -d $O/p$i -o run -- $B $ARGS > $O/p$i.log 2>&1 || echo "pass $i failed rc=$?"
+done
+python3 - <<'PY'
+import csv, glob, statistics, json
+out = {}
+for f in sorted(glob.glob("gpurun_out/pmc_h16/p*/run_counter_collection.csv")):
+    vals = {}
+    for r in csv.DictReader(open(f)):
+        if "h16_kernel<8, true, false>" in r["Kernel_Name"]:
+            vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+    for k, v in vals.items():
+        out[k] = statistics.mean(v)
+for f in glob.glob("gpurun_out/pmc_h16/trace/run_kernel_stats.csv"):
+    for r in csv.DictReader(open(f)):
+        print(r["Name"][:70], r["Calls"], r["AverageNs"])
+print(json.dumps(out, indent=1))
+json.dump(out, open("gpurun_out/pmc_h16/summary.json", "w"), indent=1)
+PY

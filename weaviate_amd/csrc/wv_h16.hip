@@ -63,7 +63,11 @@ __device__ __forceinline__ void vm_wait(int n) {
     }
 }
 __device__ __forceinline__ void block_barrier() {
+#ifdef WV_H16_ABLATE_NO_BARRIER
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#else
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#endif
 }
 
 // LDS stage: [2 row blocks][ns k-steps][64 lanes] uint4 image, then 64 floats
@@ -73,7 +77,8 @@ struct H16Stage {
     static constexpr int IMG_U4 = 2 * NS * 64;
     static constexpr int U4 = IMG_U4 + 16 + 1;
 };
-constexpr int H_STAGES = 3;   // tile t computes from stage t % 3 while t + 1 and t + 2 land
+constexpr int H_STAGES = 3;   // a stage holds H_TPS tiles; stage p % 3 computes while p + 1, p + 2 land
+constexpr int H_TPS = 2;      // tiles per stage: one barrier per H_TPS tiles
 
 // SEED: the pre-pass over every H_SAMPLE-th tile keeps only each lane's
 // running minimum per query column (distinct rows per (slot, lane half)),
@@ -102,6 +107,11 @@ __global__ __launch_bounds__(512, 2) void wv_bf_h16_kernel(H16Params p) {
     if (u_last > (uint64_t)p.n_qblocks * p.ntiles) u_last = (uint64_t)p.n_qblocks * p.ntiles;
 
     const uint32_t lds0 = lds_addr(lds);
+#ifdef WV_H16_PRIO
+    // the second-dispatched half of the workgroup loses every issue
+    // arbitration to its SIMD partner: static priority for it (guide T5)
+    if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
     // this wave's LDS-DMA ops per tile (the counted waits below)
     const int n_ops = (wave < St::IMG_U4 / 64 ? (St::IMG_U4 / 64 - 1 - wave) / H_WAVES + 1 : 0) +
                       ((wave == 0 && L2) ? 1 : 0) + (wave == 1 ? 1 : 0);
@@ -120,6 +130,19 @@ __global__ __launch_bounds__(512, 2) void wv_bf_h16_kernel(H16Params p) {
             if (lane < 2 || (lane < 4 && has_allow)) glds4(w, dst + (St::IMG_U4 + 16) * 16);
         }
     };
+
+    // the tiles of stage-group g (H_TPS consecutive tiles) into LDS stage g % 3
+    auto fill_group = [&](uint64_t t_begin, int g, int ntile) {
+        const int st = g % H_STAGES;
+        int n = 0;
+#pragma unroll
+        for (int j = 0; j < H_TPS; ++j) {
+            const int t = g * H_TPS + j;
+            if (t < ntile) { fill(t_begin + t, st * H_TPS + j); ++n; }
+        }
+        return n * n_ops;   // this wave's DMA ops for the group
+    };
+    auto tile_lds = [&](int t) { return lds + ((t / H_TPS) % H_STAGES * H_TPS + t % H_TPS) * St::U4; };
 
     for (uint64_t u = u_first; u < u_last;) {
         const int qb = (int)(u / p.ntiles);
@@ -159,12 +182,6 @@ __global__ __launch_bounds__(512, 2) void wv_bf_h16_kernel(H16Params p) {
             l0d[i] = FLT_MAX; l1d[i] = FLT_MAX;
             l0i[i] = WV_NIL; l1i[i] = WV_NIL;
         }
-        // (the previous segment ended with every stage read and every DMA landed)
-        if (ntile > 0) fill(t_begin, 0);
-        if (ntile > 1) fill(t_begin + 1, 1);
-        vm_wait(ntile > 1 ? n_ops : 0);   // this wave's part of tile 0
-        block_barrier();                  // everyone's
-
         // Two-phase software pipeline over half tiles (rows 0-31: H0 =
         // acc00/acc01, rows 32-63: H1 = acc10/acc11).  Iteration t:
         //   A  MFMAs of H1(t)       beside the tile minima of H0(t)
@@ -181,9 +198,9 @@ __global__ __launch_bounds__(512, 2) void wv_bf_h16_kernel(H16Params p) {
         // fragments + the C-in), with VALU work of the other half placed
         // between them by the `between` callback and sched_group_barrier
         auto mfma_half = [&](const uint4* img, int rb, floatx16& accA, floatx16& accB, auto&& between) {
-            uint4 a[NS];
-#pragma unroll
-            for (int k = 0; k < NS; ++k) a[k] = img[(rb * NS + k) * 64 + lane];
+            // the C-in first, then the A fragments in k order: the LDS returns
+            // in issue order, so each MFMA waits (counted lgkmcnt) only for
+            // its own fragment, not for the whole half's reads
             floatx16 xc;
             if (L2) {
                 const float* xn = reinterpret_cast<const float*>(img + St::IMG_U4) + 32 * rb;
@@ -196,6 +213,15 @@ __global__ __launch_bounds__(512, 2) void wv_bf_h16_kernel(H16Params p) {
 #pragma unroll
                 for (int r = 0; r < 16; ++r) xc[r] = 0.f;
             }
+            __builtin_amdgcn_sched_barrier(0);   // the C-in reads issue first
+            uint4 a[NS];
+#ifdef WV_H16_ABLATE_NO_LDS
+#pragma unroll
+            for (int k = 0; k < NS; ++k) { a[k] = bq1[k]; a[k].x ^= (uint32_t)rb; }
+#else
+#pragma unroll
+            for (int k = 0; k < NS; ++k) a[k] = img[(rb * NS + k) * 64 + lane];
+#endif
             between();
 #pragma unroll
             for (int k = 0; k < NS; ++k) {
@@ -205,9 +231,11 @@ __global__ __launch_bounds__(512, 2) void wv_bf_h16_kernel(H16Params p) {
                 accB = __builtin_amdgcn_mfma_f32_32x32x16_f16(ak, __builtin_bit_cast(half8, bq1[k]), k == 0 ? xc : accB,
                                                               0, 0, 0);
             }
-            // LDS reads first, then MFMAs each followed by one VALU op
-            __builtin_amdgcn_sched_group_barrier(0x100, NS + (L2 ? 4 : 0), 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+            // LDS reads first (in source order), a few VALU while they land,
+            // then the MFMAs (k-interleaved over the two accumulators) each
+            // followed by one VALU op
+            __builtin_amdgcn_sched_group_barrier(0x100, NS, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
 #pragma unroll
             for (int i = 0; i < 2 * NS; ++i) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
@@ -239,6 +267,9 @@ __global__ __launch_bounds__(512, 2) void wv_bf_h16_kernel(H16Params p) {
             }
         };
         auto min16 = [&](const floatx16& A) {
+#ifdef WV_H16_ABLATE_NO_MIN
+            return A[0];
+#endif
             // four independent chains (short dependency depth), v_min3 each
             float m0 = fminf(fminf(A[0], A[1]), A[2]), m1 = fminf(fminf(A[3], A[4]), A[5]);
             float m2 = fminf(fminf(A[6], A[7]), A[8]), m3 = fminf(fminf(A[9], A[10]), A[11]);
@@ -247,19 +278,27 @@ __global__ __launch_bounds__(512, 2) void wv_bf_h16_kernel(H16Params p) {
             return fminf(fminf(m0, m1), fminf(m2, m3));
         };
 
-        int st = 0;
         uint64_t o0 = 0, o1 = 0;
         bool need_mask = false;
+        const int ngroups = (ntile + H_TPS - 1) / H_TPS;
+        // (the previous segment ended with every stage read and every DMA landed)
+        int ops_in_flight = 0;   // this wave's DMA ops of the newest group issued
+        if (ngroups > 0) fill_group(t_begin, 0, ntile);
+        if (ngroups > 1) ops_in_flight = fill_group(t_begin, 1, ntile);
+        vm_wait(ops_in_flight);   // this wave's part of group 0
+        block_barrier();          // everyone's
         if (ntile > 0) {
-            mfma_half(lds, 0, acc00, acc01, [] {});
-            need_mask = tile_ok(lds, t_begin, o0, o1);
+            mfma_half(tile_lds(0), 0, acc00, acc01, [] {});
+            need_mask = tile_ok(tile_lds(0), t_begin, o0, o1);
         }
         for (int t = 0; t < ntile; ++t) {
+            const int g = t / H_TPS;
 #ifndef WV_H16_ABLATE_NO_FILL
-            // stage (t + 2) % 3 was last read in iteration t - 1, before its barrier
-            if (t + 2 < ntile) fill(t_begin + t + 2, st == 0 ? 2 : st - 1);
+            // group g + 2 goes to stage (g + 2) % 3 = (g - 1) % 3, last read in
+            // group g - 1, before its closing barrier
+            if (t % H_TPS == 0) ops_in_flight = g + 2 < ngroups ? fill_group(t_begin, g + 2, ntile) : 0;
 #endif
-            const uint4* img = lds + st * St::U4;
+            const uint4* img = tile_lds(t);
             const uint32_t rb0 = (uint32_t)((t_begin + t) * (uint64_t)p.tile_stride * H_BN) + 4 * khalf;
             // lanes l and l ^ 32 keep lists for the same query column (see the split pass)
             const float pt0 = fminf(__shfl_xor(l0d[BF_KP - 1], 32, 64), tau0);
@@ -282,16 +321,17 @@ __global__ __launch_bounds__(512, 2) void wv_bf_h16_kernel(H16Params p) {
                 split_extract16(m1, acc01, l1d, l1i, pt1, rb0);
 #endif
             }
-            // ---- C: tile t + 1 has landed (t + 2 may stay in flight); every
-            // wave is done reading stage t % 3's operands ----
-            if (t + 1 < ntile) vm_wait(t + 2 < ntile ? n_ops : 0);
-            block_barrier();
-            const int st1 = st == 2 ? 0 : st + 1;
+            // ---- C (last tile of a group): group g + 1 has landed (g + 2 may
+            // stay in flight); every wave is done reading group g's stage ----
+            if (t % H_TPS == H_TPS - 1 || t == ntile - 1) {
+                if (g + 1 < ngroups) vm_wait(ops_in_flight);
+                block_barrier();
+            }
             // ---- E: H0(t + 1) MFMAs, H1(t) minima ----
             if (mask_t) mask_half(acc10, acc11, (uint32_t)(mo0 >> 32), (uint32_t)(mo1 >> 32));
             if (t + 1 < ntile) {
-                mfma_half(lds + st1 * St::U4, 0, acc00, acc01, [&] { m0 = min16(acc10); m1 = min16(acc11); });
-                need_mask = tile_ok(lds + st1 * St::U4, t_begin + t + 1, o0, o1);
+                mfma_half(tile_lds(t + 1), 0, acc00, acc01, [&] { m0 = min16(acc10); m1 = min16(acc11); });
+                need_mask = tile_ok(tile_lds(t + 1), t_begin + t + 1, o0, o1);
             } else {
                 m0 = min16(acc10);
                 m1 = min16(acc11);
@@ -308,7 +348,6 @@ __global__ __launch_bounds__(512, 2) void wv_bf_h16_kernel(H16Params p) {
                 split_extract16(m1, acc11, l1d, l1i, pt1, rb0 + 32);
 #endif
             }
-            st = st1;
         }
 
         if constexpr (SEED) {
@@ -492,7 +531,7 @@ hipError_t wv_launch_bf_h16(const wv::H16Params* p, int ns, int seed, hipStream_
         return hipErrorInvalidValue;
     const bool l2 = p->metric == WV_METRIC_L2;
     if (l2 && !p->xns) return hipErrorInvalidValue;
-    const size_t lds = (size_t)wv::H_STAGES * (2 * ns * 64 + 17) * 16;
+    const size_t lds = (size_t)wv::H_STAGES * wv::H_TPS * (2 * ns * 64 + 17) * 16;
 #define WV_H16_LAUNCH(NS)                                                                                      \
     if (seed) {                                                                                                \
         if (l2) hipLaunchKernelGGL((wv::wv_bf_h16_kernel<NS, true, true>), dim3(nb), dim3(512), lds, s, *p);   \
