@@ -547,6 +547,67 @@ def run_hnsw(args, ctx, W, with_cpu):
     return res
 
 
+def group_leg(args):
+    """Child process (no torch.distributed): one process drives `--group-devices`
+    through libwvgpu.so's in-process group (wv_group_*, the layout a single Go
+    server uses): the corpus sharded by id range, per-shard top-k gathered to
+    the first device over RCCL (ncclCommInitAll) and merged there.  Timed
+    through the host entry point (query upload and result download included)."""
+    import weaviate_amd as W
+    devs = [int(x) for x in args.group_devices.split(",")]
+    N, D, NQ, K = args.rows, args.dim, args.nq, args.k
+    gen = {"uniform": counter_uniform, "gauss": counter_gauss, "sift": counter_sift}[args.data]
+    base = gen(1, 0, N, D)
+    queries = gen(2, 0, NQ, D)
+    g = W.GPUGroup(devs, D, args.metric, capacity=N, layout="shard")
+    g.upload_vectors(base)
+    del base
+    for _ in range(args.warmup):
+        g.search_batch(queries, K, mode="exact")
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ids, ds, n = g.search_batch(queries, K, mode="exact")
+    dt = time.perf_counter() - t0
+    res = {"value": round(NQ * args.steps / dt, 1), "unit": "queries/s", "ms_per_step": round(1e3 * dt / args.steps, 3),
+           "members": len(devs), "uses_rccl": g.info()["uses_rccl"],
+           "workload": f"exact {K}-NN, {N:,} x {D}-d {args.metric}, {NQ}-query batch, corpus sharded over "
+                       f"{len(devs)} devices in ONE process (wv_group_search_batch, host buffers in and out)"}
+    if args.dump_ids and os.path.exists(args.dump_ids):
+        ref = np.load(args.dump_ids)
+        res["ids_equal_single_gpu"] = bool(np.array_equal(ids, ref["ids"]) and
+                                           np.array_equal(ds.view(np.uint32), ref["dists"].view(np.uint32)))
+    g.close()
+    print(json.dumps(res), flush=True)
+
+
+def run_group_leg_child(args, ws, final_ids, final_d):
+    """Rank 0 after every rank left the process group: the in-process group
+    leg in a child process, bounded by a timeout (its failure is reported, not
+    fatal to the bench line)."""
+    import subprocess
+    import tempfile
+    with tempfile.TemporaryDirectory() as td:
+        ref = os.path.join(td, "rank0.npz")
+        np.savez(ref, ids=final_ids, dists=final_d)
+        env = {k: v for k, v in os.environ.items()
+               if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
+                            "ROLE_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID")}
+        cmd = [sys.executable, os.path.abspath(__file__), "--group-leg", "--group-devices",
+               ",".join(str(i) for i in range(ws)), "--rows", str(args.rows), "--dim", str(args.dim), "--nq",
+               str(args.nq), "--k", str(args.k), "--metric", args.metric, "--data", args.data, "--steps",
+               str(args.steps), "--warmup", str(args.warmup), "--dump-ids", ref]
+        try:
+            p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+        except subprocess.TimeoutExpired:
+            return {"error": "timed out after 240 s"}
+        if p.returncode != 0:
+            return {"error": f"exit {p.returncode}", "stderr_tail": p.stderr[-600:]}
+        try:
+            return json.loads(p.stdout.strip().splitlines()[-1])
+        except Exception:
+            return {"error": "no JSON line", "stdout_tail": p.stdout[-600:]}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -587,7 +648,15 @@ def main():
                          "sequential build (reference-equivalent, slow at 1M)")
     ap.add_argument("--batch-div", type=int, default=64, help="GPU build: batch = inserted / batch_div")
     ap.add_argument("--graph-cache", default="", help="npz path: load the hnsw graph if present, else build and save")
+    ap.add_argument("--no-group-leg", action="store_true",
+                    help="N>1 exact: skip the in-process multi-GPU group leg (wv_group, RCCL gather) run by rank 0")
+    ap.add_argument("--group-leg", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--group-devices", default="0", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.group_leg:
+        if args.data == "auto":
+            args.data = "uniform"
+        return group_leg(args)
 
     if os.environ.get("WORLD_SIZE") is None and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus))
@@ -639,6 +708,7 @@ def main():
             result["cpu_baseline"], result["parity_sample"] = exact_cpu_baseline(args, st, O)
         if args.dump_ids and rank == 0:
             np.savez(args.dump_ids, ids=st["final_ids"], dists=st["final_d"])
+        rank0_final = (st["final_ids"], st["final_d"])
         # N > 1: the north-star layout beside the query split -- id-range
         # shards, RCCL all-gather, device merge -- on rank 0's batch, whose
         # merged answer must equal rank 0's whole-corpus answer bit for bit
@@ -661,10 +731,15 @@ def main():
             h = run_hnsw(args, ctx, W, with_cpu)
             h.pop("metric", None)
             result["hnsw_c1"] = h
+    if ws > 1:
+        ctx.barrier()
+        ctx.dist.destroy_process_group()
+        # the other ranks exit here and leave their GPUs idle for the group leg
+        if (rank == 0 and args.workload == "exact" and not args.no_group_leg and args.split == "query"
+                and ctx.n_devices == ws and args.allow_frac == 0):
+            result["group_in_process"] = run_group_leg_child(args, ws, *rank0_final)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if ws > 1:
-        ctx.dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -273,6 +273,40 @@ int wv_batcher_search(wv_batcher *b, const float *vector, int k, const uint64_t 
 int wv_batcher_stats(wv_batcher *b, uint64_t *requests, uint64_t *batches);
 int wv_batcher_destroy(wv_batcher *b);
 
+/* In-process multi-GPU group (adapters/repos/db/index.go:967-1044):
+ * one wv_index per device, driven from one process (the Go server).
+ *   WV_GROUP_SHARD    corpus split by id range (member i holds global ids
+ *                     [base_i, base_i + cap_i), base_i a multiple of 64);
+ *                     every member searches the batch over its shard, the
+ *                     per-shard top-k lists are gathered on the first device
+ *                     over RCCL (ncclCommInitAll, grouped ncclGather; device
+ *                     copies when members share a device) and merged there.
+ *   WV_GROUP_REPLICA  every member holds the whole corpus; a batch is split
+ *                     into contiguous query ranges, one per member, no
+ *                     collective.
+ * The search has wv_search_batch's signature and result (global ids). */
+typedef struct wv_group wv_group;
+enum { WV_GROUP_SHARD = 0, WV_GROUP_REPLICA = 1 };
+int wv_group_create(const int *devices, int n_devices, int dim, int metric, const wv_config *cfg, uint64_t capacity,
+                    int layout, wv_group **out);
+int wv_group_destroy(wv_group *g);
+int wv_group_info(const wv_group *g, int *n_members, int *uses_rccl);
+/* member i's index (for per-member uploads such as a graph), its id base and capacity */
+int wv_group_member(wv_group *g, int i, wv_index **ix, uint64_t *id_base, uint64_t *capacity);
+/* rows of global ids first_id.. routed to their shard (every replica) */
+int wv_group_upload_vectors(wv_group *g, const float *rows, uint64_t n, uint64_t first_id);
+/* every member builds the graph of its own rows (wv_index_build_graph), in parallel */
+int wv_group_build_graph(wv_group *g, int ef_construction, uint64_t seed, int batch_div);
+int wv_group_add(wv_group *g, const uint64_t *ids, const float *rows, uint64_t n);
+int wv_group_add_tombstones(wv_group *g, const uint64_t *ids, uint64_t n);
+int wv_group_remove_tombstones(wv_group *g, const uint64_t *ids, uint64_t n);
+int wv_group_update_config(wv_group *g, const wv_config *cfg);
+int wv_group_search_batch(wv_group *g, const float *queries, int nq, int k, int ef, const uint64_t *allow_bits,
+                          uint64_t allow_nbits, uint64_t allow_stride_words, int mode, uint64_t *out_ids,
+                          float *out_dists, int32_t *out_n);
+/* the micro-batcher over a group (wv_batcher_search / _stats / _destroy as above) */
+int wv_batcher_create_group(wv_group *g, int dim, int max_batch, int max_wait_us, wv_batcher **out);
+
 const char *wv_last_error(void);
 const char *wv_version(void);
 

@@ -116,6 +116,20 @@ SIGNATURES = {
     "wv_batcher_search": (C.c_int, [_vp, _vp, C.c_int, _vp, C.c_uint64, _vp, _vp, _vp]),
     "wv_batcher_stats": (C.c_int, [_vp, _u64p, _u64p]),
     "wv_batcher_destroy": (C.c_int, [_vp]),
+    "wv_group_create": (C.c_int, [_vp, C.c_int, C.c_int, C.c_int, C.POINTER(WvConfig), C.c_uint64, C.c_int,
+                                  C.POINTER(C.c_void_p)]),
+    "wv_group_destroy": (C.c_int, [_vp]),
+    "wv_group_info": (C.c_int, [_vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "wv_group_member": (C.c_int, [_vp, C.c_int, C.POINTER(C.c_void_p), _u64p, _u64p]),
+    "wv_group_upload_vectors": (C.c_int, [_vp, _vp, C.c_uint64, C.c_uint64]),
+    "wv_group_build_graph": (C.c_int, [_vp, C.c_int, C.c_uint64, C.c_int]),
+    "wv_group_add": (C.c_int, [_vp, _vp, _vp, C.c_uint64]),
+    "wv_group_add_tombstones": (C.c_int, [_vp, _vp, C.c_uint64]),
+    "wv_group_remove_tombstones": (C.c_int, [_vp, _vp, C.c_uint64]),
+    "wv_group_update_config": (C.c_int, [_vp, C.POINTER(WvConfig)]),
+    "wv_group_search_batch": (C.c_int, [_vp, _vp, C.c_int, C.c_int, C.c_int, _vp, C.c_uint64, C.c_uint64, C.c_int,
+                                        _vp, _vp, _vp]),
+    "wv_batcher_create_group": (C.c_int, [_vp, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p)]),
     "wv_last_error": (C.c_char_p, []),
     "wv_version": (C.c_char_p, []),
 }

@@ -47,6 +47,7 @@ struct Request {
 
 struct wv_batcher {
     wv_index* ix = nullptr;
+    wv_group* grp = nullptr;   // a multi-GPU group instead of one index
     int dim = 0;
     int max_batch = 256;
     int max_wait_us = 200;
@@ -79,8 +80,10 @@ struct wv_batcher {
         std::vector<uint64_t> ids((size_t)n * k);
         std::vector<float> ds((size_t)n * k);
         std::vector<int32_t> cnt(n);
-        const int rc = wv_search_batch(ix, q.data(), n, k, 0, filtered ? bits.data() : nullptr, nbits, stride,
-                                       WV_MODE_AUTO, ids.data(), ds.data(), cnt.data());
+        const int rc = grp ? wv_group_search_batch(grp, q.data(), n, k, 0, filtered ? bits.data() : nullptr, nbits,
+                                                   stride, WV_MODE_AUTO, ids.data(), ds.data(), cnt.data())
+                           : wv_search_batch(ix, q.data(), n, k, 0, filtered ? bits.data() : nullptr, nbits, stride,
+                                             WV_MODE_AUTO, ids.data(), ds.data(), cnt.data());
         const std::string msg = rc ? wv_last_error() : "";
         std::lock_guard<std::mutex> l(mu);
         for (int i = 0; i < n; ++i) {
@@ -136,19 +139,28 @@ struct wv_batcher {
 
 extern "C" {
 
-int wv_batcher_create(wv_index* ix, int dim, int max_batch, int max_wait_us, wv_batcher** out) {
-    if (!ix || !out || dim <= 0 || max_batch <= 0 || max_wait_us < 0) {
+static int create_batcher(wv_index* ix, wv_group* grp, int dim, int max_batch, int max_wait_us, wv_batcher** out) {
+    if ((!ix && !grp) || !out || dim <= 0 || max_batch <= 0 || max_wait_us < 0) {
         wv_internal_set_error("wv_batcher_create: bad argument");
         return WV_EINVAL;
     }
     auto* b = new wv_batcher();
     b->ix = ix;
+    b->grp = grp;
     b->dim = dim;
     b->max_batch = max_batch;
     b->max_wait_us = max_wait_us;
     b->th = std::thread([b] { b->loop(); });
     *out = b;
     return WV_OK;
+}
+
+int wv_batcher_create(wv_index* ix, int dim, int max_batch, int max_wait_us, wv_batcher** out) {
+    return create_batcher(ix, nullptr, dim, max_batch, max_wait_us, out);
+}
+
+int wv_batcher_create_group(wv_group* g, int dim, int max_batch, int max_wait_us, wv_batcher** out) {
+    return create_batcher(nullptr, g, dim, max_batch, max_wait_us, out);
 }
 
 int wv_batcher_search(wv_batcher* b, const float* vector, int k, const uint64_t* allow_bits, uint64_t allow_nbits,

@@ -88,11 +88,21 @@ class GPUVectorIndex:
         h = C.c_void_p()
         check(lib().wv_index_create(dim, METRICS[distance], C.byref(self.cfg), capacity, C.byref(h)))
         self._h = h
+        self._owned = True
+
+    @classmethod
+    def _borrow(cls, handle, dim: int, distance: str, capacity: int, cfg: WvConfig, owner):
+        """A view of an index another object owns (a wv_group member)."""
+        ix = cls.__new__(cls)
+        ix.dim, ix.distance, ix.capacity, ix.cfg = dim, distance, capacity, cfg
+        ix._h, ix._owned, ix._owner = handle, False, owner
+        return ix
 
     # -- lifecycle -----------------------------------------------------------
     def close(self):
         if getattr(self, "_h", None):
-            lib().wv_index_destroy(self._h)
+            if getattr(self, "_owned", True):
+                lib().wv_index_destroy(self._h)
             self._h = None
 
     def __del__(self):
@@ -384,15 +394,91 @@ class CommitLogGraph:
             pass
 
 
-class Batcher:
-    """Native micro-batcher over one index (wv_batcher_*): `search` has the
-    signature and result of GPUVectorIndex.search_by_vector and is meant to be
-    called from many threads at once (ctypes releases the GIL for the call)."""
+class GPUGroup:
+    """Several devices driven from one process (wv_group_*): the corpus split
+    by id range over the members with an RCCL gather + device merge
+    (layout="shard", index.go:967-1044), or replicated with the batch split by
+    queries (layout="replica").  `search_batch` has GPUVectorIndex's result."""
 
-    def __init__(self, index: GPUVectorIndex, max_batch: int = 256, max_wait_us: int = 200):
+    def __init__(self, devices, dim: int, distance: str = "l2-squared", capacity: int = 1 << 20, *,
+                 layout: str = "shard", max_connections: int = 64, ef: int = -1, flat_search_cutoff: int = 40000,
+                 forbid_flat: bool = False):
+        if distance not in METRICS:
+            raise WvError(1, f"unsupported distance {distance!r}")
+        self.dim, self.distance, self.capacity, self.layout = dim, distance, capacity, layout
+        self.cfg = WvConfig()
+        lib().wv_config_default(C.byref(self.cfg))
+        self.cfg.max_connections, self.cfg.ef = max_connections, ef
+        self.cfg.flat_search_cutoff, self.cfg.forbid_flat = flat_search_cutoff, int(forbid_flat)
+        devs = (C.c_int * len(devices))(*devices)
+        h = C.c_void_p()
+        check(lib().wv_group_create(devs, len(devices), dim, METRICS[distance], C.byref(self.cfg), capacity,
+                                    {"shard": 0, "replica": 1}[layout], C.byref(h)))
+        self._h = h
+
+    def info(self):
+        n, r = C.c_int(), C.c_int()
+        check(lib().wv_group_info(self._h, C.byref(n), C.byref(r)))
+        return {"members": n.value, "uses_rccl": bool(r.value)}
+
+    def member(self, i: int):
+        """(GPUVectorIndex view of member i, its id base, its capacity)."""
+        h, base, cap = C.c_void_p(), C.c_uint64(), C.c_uint64()
+        check(lib().wv_group_member(self._h, i, C.byref(h), C.byref(base), C.byref(cap)))
+        return GPUVectorIndex._borrow(h, self.dim, self.distance, cap.value, self.cfg, self), base.value, cap.value
+
+    def upload_vectors(self, rows: np.ndarray, first_id: int = 0):
+        rows = np.ascontiguousarray(rows, dtype=np.float32)
+        if rows.ndim != 2 or rows.shape[1] != self.dim:
+            raise WvError(1, f"vector lengths don't match: {rows.shape[-1]} vs {self.dim}")
+        check(lib().wv_group_upload_vectors(self._h, _ptr(rows), rows.shape[0], first_id))
+
+    def build_graph(self, ef_construction: int = 128, seed: int = 1, batch_div: int = 32):
+        check(lib().wv_group_build_graph(self._h, ef_construction, seed, batch_div))
+
+    def add(self, ids, rows):
+        ids = np.ascontiguousarray(ids, dtype=np.uint64)
+        rows = np.ascontiguousarray(rows, dtype=np.float32).reshape(-1, self.dim)
+        check(lib().wv_group_add(self._h, _ptr(ids), _ptr(rows), ids.size))
+
+    def add_tombstones(self, ids):
+        ids = np.ascontiguousarray(ids, dtype=np.uint64)
+        check(lib().wv_group_add_tombstones(self._h, _ptr(ids), ids.size))
+
+    def search_batch(self, queries, k: int, ef: int = 0, allow=None, mode: str = "auto"):
+        qs = np.ascontiguousarray(queries, dtype=np.float32).reshape(-1, self.dim)
+        nq = qs.shape[0]
+        bits, nb, stride = GPUVectorIndex._allow_args(allow)
+        ids = np.zeros((nq, k), np.uint64)
+        ds = np.zeros((nq, k), np.float32)
+        n = np.zeros(nq, np.int32)
+        check(lib().wv_group_search_batch(self._h, _ptr(qs), nq, k, ef, _ptr(bits), nb, stride, _MODES[mode],
+                                          _ptr(ids), _ptr(ds), _ptr(n)))
+        return ids, ds, n
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().wv_group_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Batcher:
+    """Native micro-batcher over one index or one GPUGroup (wv_batcher_*):
+    `search` has the signature and result of GPUVectorIndex.search_by_vector
+    and is meant to be called from many threads at once (ctypes releases the
+    GIL for the call)."""
+
+    def __init__(self, index, max_batch: int = 256, max_wait_us: int = 200):
         self.index = index
         h = C.c_void_p()
-        check(lib().wv_batcher_create(index._h, index.dim, max_batch, max_wait_us, C.byref(h)))
+        create = lib().wv_batcher_create_group if isinstance(index, GPUGroup) else lib().wv_batcher_create
+        check(create(index._h, index.dim, max_batch, max_wait_us, C.byref(h)))
         self._h = h
 
     def search(self, vector, k: int, allow: Optional[AllowList] = None):
