@@ -365,6 +365,55 @@ def run_exact(args, ctx, W):
     return res, state
 
 
+def wide_k_line(args, ctx, st, W):
+    """Secondary exact lines on the same index (N=1): k=100 through the batched
+    wide path (search.go:90-158 asks limit 100 first), and SearchByVectorDistance
+    (deepening from limit 100) on single queries over a flat allow list."""
+    torch = ctx.torch
+    ix, NQ = st["ix"], args.nq
+    qt = _query_tensor(ctx, st["queries"], ix.query_ld())
+    out = {}
+    for k in (100,):
+        oi, od, on = _out_tensors(ctx, NQ, k)
+        ix.search_batch_device(qt.data_ptr(), NQ, k, oi.data_ptr(), od.data_ptr(), on.data_ptr(), mode="exact",
+                               stream=ctx.stream)
+        torch.cuda.synchronize(ctx.dev)
+        t0 = time.perf_counter()
+        reps = 3
+        fb = 0
+        for _ in range(reps):
+            ix.search_batch_device(qt.data_ptr(), NQ, k, oi.data_ptr(), od.data_ptr(), on.data_ptr(), mode="exact",
+                                   stream=ctx.stream)
+            fb += ix.last_batch_stats()["fallbacks"]
+        torch.cuda.synchronize(ctx.dev)
+        dt = (time.perf_counter() - t0) / reps
+        out[f"exact_k{k}"] = {"value": round(NQ / dt, 1), "unit": "queries/s", "ms_per_batch": round(1e3 * dt, 3),
+                              "fallback_queries_per_batch": fb / reps, "nq": NQ}
+        if k == 100:
+            d100 = od.cpu().numpy()
+    # SearchByVectorDistance: target = each query's 150th-nearest distance, so
+    # the deepening runs two rounds (limit 100, then 200)
+    n_local = st["n_local"]
+    allow = W.AllowList.from_ids(np.arange(n_local, dtype=np.uint64), n_local)
+    ix.update_user_config(flat_search_cutoff=n_local + 1)
+    o256 = _out_tensors(ctx, 4, 256)
+    qs4 = _query_tensor(ctx, st["queries"][:4], ix.query_ld())
+    ix.search_batch_device(qs4.data_ptr(), 4, 256, o256[0].data_ptr(), o256[1].data_ptr(), o256[2].data_ptr(),
+                           mode="exact", stream=ctx.stream)
+    targets = o256[1].cpu().numpy()[:, 149]
+    times, counts = [], []
+    for i in range(4):
+        t0 = time.perf_counter()
+        ids, ds = ix.search_by_vector_distance(st["queries"][i], float(targets[i]), -1, allow=allow)
+        times.append(time.perf_counter() - t0)
+        counts.append(int(len(ids)))
+    ix.update_user_config(flat_search_cutoff=40000)
+    out["search_by_vector_distance"] = {"ms_per_query": round(1e3 * float(np.median(times[1:])), 3),
+                                        "results_per_query": counts, "note": "one query per call, host "
+                                        "entry point, flat allow list of every id, 150 results (two rounds)"}
+    return out
+
+
 def exact_cpu_baseline(args, st, O):
     """flatSearch restated in C (AVX2 asm-order distancer), on a bounded
     sample of the same queries; T = --cpu-threads (GOMAXPROCS-equivalent) and
@@ -648,6 +697,7 @@ def main():
                          "sequential build (reference-equivalent, slow at 1M)")
     ap.add_argument("--batch-div", type=int, default=64, help="GPU build: batch = inserted / batch_div")
     ap.add_argument("--graph-cache", default="", help="npz path: load the hnsw graph if present, else build and save")
+    ap.add_argument("--no-wide-line", action="store_true", help="skip the k=100 / SearchByVectorDistance lines")
     ap.add_argument("--no-group-leg", action="store_true",
                     help="N>1 exact: skip the in-process multi-GPU group leg (wv_group, RCCL gather) run by rank 0")
     ap.add_argument("--group-leg", action="store_true", help=argparse.SUPPRESS)
@@ -706,6 +756,8 @@ def main():
         if with_cpu:
             O = _oracle()
             result["cpu_baseline"], result["parity_sample"] = exact_cpu_baseline(args, st, O)
+        if ws == 1 and args.allow_frac == 0 and not args.no_wide_line:
+            result["wide_k"] = wide_k_line(args, ctx, st, W)
         if args.dump_ids and rank == 0:
             np.savez(args.dump_ids, ids=st["final_ids"], dists=st["final_d"])
         rank0_final = (st["final_ids"], st["final_d"])

@@ -25,6 +25,7 @@
 extern "C" {
 hipError_t wv_launch_bf_mfma(const wv::BfParams* p, hipStream_t s);
 hipError_t wv_launch_bf_finalize(const wv::BfFinParams* p, hipStream_t s);
+hipError_t wv_launch_bf_finalize_wide(const wv::BfFinParams* p, hipStream_t s);
 hipError_t wv_launch_exact_scan(const wv::ScanParams* p, hipStream_t s);
 hipError_t wv_launch_fb(const wv::FbParams* p, hipStream_t s);
 hipError_t wv_launch_rownorm(const float* X, uint64_t N, int D, int ldx, float* norm2, unsigned int* maxbits,
@@ -519,10 +520,20 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     fp.qres = ix->qres.as<float>();
     // seed pre-pass: the k-th exact distance over every H_SAMPLE-th tile bounds
     // each query's true k-th distance, hence the keys worth keeping
+    // k > FIN_KF (the wide finalize): at least k slots per query block, i.e.
+    // >= 2k lists of BF_KP per query, so that no list is likely to hold more
+    // than BF_KP of the top k (which would leave its tail below the k-th key
+    // and fail the certificate); the seed pass needs >= k minima likewise
+    const bool wide = k > wv::FIN_KF;
+    auto target = [&](uint64_t tiles) {
+        uint64_t t = (uint64_t)ix->n_cus;
+        if (wide) t = std::max<uint64_t>(t, (uint64_t)nqb * std::min<uint64_t>(tiles, (uint64_t)k + 2));
+        return (int)std::min<uint64_t>(t, 1u << 30);
+    };
     const bool seed = ntl >= 64 * (uint64_t)wv::H_SAMPLE && !std::getenv("WV_H16_NO_SEED");
     if (seed) {
         const uint64_t nts = (ntl + wv::H_SAMPLE - 1) / wv::H_SAMPLE;
-        const wv::BfSchedule ss = wv::bf_schedule(nq, nts * wv::H_BN, ix->n_cus, wv::H_BQ, wv::H_BN);
+        const wv::BfSchedule ss = wv::bf_schedule(nq, nts * wv::H_BN, target(nts), wv::H_BQ, wv::H_BN);
         HIP_TRY(ix->cand_d.ensure((size_t)nq * ss.n_slots * wv::H_PROD * 4));
         hp.ntiles = ss.ntiles;
         hp.units_per_block = ss.units_per_block;
@@ -552,7 +563,9 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
         HIP_TRY(wv_launch_h16_seed(&sp, s));
         if (ix->timing) HIP_TRY(hipEventRecord(ix->ev[7], s));
     }
-    const wv::BfSchedule sch = wv::bf_schedule(nq, N, ix->n_cus, wv::H_BQ, wv::H_BN);
+    const wv::BfSchedule sch = wv::bf_schedule(nq, N, target(ntl), wv::H_BQ, wv::H_BN);
+    if (wide && (uint64_t)sch.n_slots * wv::H_PROD * wv::BF_KP > (uint64_t)wv::FINW_NE)
+        return fail(WV_ESTATE, "run_h16: too many lists for the wide finalize");
     HIP_TRY(ix->cand_d.ensure((size_t)nq * sch.n_slots * wv::H_PROD * wv::BF_KP * 4));
     HIP_TRY(ix->cand_id.ensure((size_t)nq * sch.n_slots * wv::H_PROD * wv::BF_KP * 4));
     hp.ntiles = sch.ntiles;
@@ -572,7 +585,7 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     fp.units_per_block = sch.units_per_block;
     fp.tau_in = hp.tau;
     if (ix->timing) HIP_TRY(hipEventRecord(ix->ev[2], s));
-    HIP_TRY(wv_launch_bf_finalize(&fp, s));
+    HIP_TRY(wide ? wv_launch_bf_finalize_wide(&fp, s) : wv_launch_bf_finalize(&fp, s));
     if (ix->timing) HIP_TRY(hipEventRecord(ix->ev[3], s));
     std::vector<int32_t> f(nq);
     HIP_TRY(hipMemcpyAsync(f.data(), ix->fail.p, 4 * (size_t)nq, hipMemcpyDeviceToHost, s));
@@ -603,7 +616,12 @@ int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
         return WV_OK;
     }
     std::vector<int32_t> fails;
-    if (k <= wv::BF_FAST_KMAX) {
+    // the f16 pass (whole corpus or a shared allow list) serves k up to
+    // BF_WIDE_KMAX; the other key passes k up to BF_FAST_KMAX
+    const bool h16_ok = ix->use_h16 && !allow_stride && !d_rowmask;
+    // the key pass + finalize ran: fail_thr holds each failed query's bound
+    const bool keyed = k <= wv::BF_FAST_KMAX || (h16_ok && k <= wv::BF_WIDE_KMAX);
+    if (keyed) {
         // A shared allow list that keeps under half the corpus is compacted
         // into a row list first: the contraction then runs over |allow| rows
         // (the reference's flatSearch also walks only the allow list,
@@ -623,7 +641,7 @@ int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
             // the f16 pass scans the whole corpus ~6x faster than the fp32
             // pass over a row list: compact only very selective lists then
             const uint64_t frac = ix->use_h16 && !allow_stride ? 8 : 2;
-            if ((frac * n_ok < N && !std::getenv("WV_BF_NO_COMPACT")) || d_rowmask) {
+            if (((frac * n_ok < N && !std::getenv("WV_BF_NO_COMPACT")) || d_rowmask) && k <= wv::BF_FAST_KMAX) {
                 n_scan = n_ok;
                 d_rowidx = ix->rowidx.as<uint32_t>();
             }
@@ -756,7 +774,7 @@ int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
 fallbacks:
     ix->last_fallbacks += fails.size();
     if (!fails.empty() && std::getenv("WV_ABLATE_NO_FALLBACK")) fails.clear();   // kernel ablations only
-    if (!fails.empty() && k <= wv::BF_FAST_KMAX) {
+    if (!fails.empty() && keyed) {
         // batched threshold filter over the corpus for every failed query
         std::vector<int32_t> rest;
         for (size_t b0 = 0; b0 < fails.size(); b0 += 256) {

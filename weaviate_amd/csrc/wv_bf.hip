@@ -1253,6 +1253,167 @@ __global__ __launch_bounds__(64) void wv_bf_finalize_kernel(BfFinParams p) {
 }
 
 // ---------------------------------------------------------------------------
+// Wide finalize (k > FIN_KF, up to BF_WIDE_KMAX): one 256-thread workgroup per
+// query sorts all its list entries in LDS, re-ranks exactly (reference order)
+// every entry whose key could still be in the top k -- key <= the k-th key +
+// 3 eps -- and certifies the result exactly as finalize_one does: the bound on
+// what was not re-ranked is the smallest full-list tail, the first key not
+// re-ranked and the seed threshold.
+__device__ __forceinline__ void bitonic_sort_lds(float* sd, uint32_t* si, int len) {
+    for (int kk = 2; kk <= len; kk <<= 1) {
+        for (int j = kk >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < len; i += blockDim.x) {
+                const int o = i ^ j;
+                if (o > i) {
+                    const bool asc = (i & kk) == 0;
+                    if (key_less(sd[o], si[o], sd[i], si[i]) == asc) {
+                        const float td = sd[i]; sd[i] = sd[o]; sd[o] = td;
+                        const uint32_t ti = si[i]; si[i] = si[o]; si[o] = ti;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+template <int METRIC>
+__device__ void finalize_wide(const BfFinParams& p, int q, float* qv, float* sd, uint32_t* si, float* red_d,
+                              uint32_t* red_i, int* cnt) {
+    const int tid = threadIdx.x, nt = blockDim.x;
+    const int n_lists = bf_slots_of((uint64_t)(q / p.bq), p.ntiles, p.units_per_block) * p.prod;
+    const int n_ent = n_lists * BF_KP;
+    const float* cd = p.cand_d + (size_t)q * p.n_slots * p.prod * BF_KP;
+    const uint32_t* ci = p.cand_id + (size_t)q * p.n_slots * p.prod * BF_KP;
+    // smallest full-list tail: everything a list dropped is >= its tail
+    float bound = FLT_MAX;
+    uint32_t bound_id = WV_NIL;
+    for (int l = tid; l < n_lists; l += nt) {
+        const float d = cd[l * BF_KP + BF_KP - 1];
+        const uint32_t i = ci[l * BF_KP + BF_KP - 1];
+        if (key_less(d, i, bound, bound_id)) { bound = d; bound_id = i; }
+    }
+    for (int m = 32; m >= 1; m >>= 1) {
+        const float od = __shfl_xor(bound, m, 64);
+        const uint32_t oi = __shfl_xor(bound_id, m, 64);
+        if (key_less(od, oi, bound, bound_id)) { bound = od; bound_id = oi; }
+    }
+    if (tid == 0) *cnt = 0;
+    if ((tid & 63) == 0) { red_d[tid >> 6] = bound; red_i[tid >> 6] = bound_id; }
+    __syncthreads();
+    for (int w = 0; w < (nt >> 6); ++w)
+        if (key_less(red_d[w], red_i[w], bound, bound_id)) { bound = red_d[w]; bound_id = red_i[w]; }
+    // every valid entry into LDS (the host sizes the lists so they fit)
+    for (int e = tid; e < n_ent; e += nt) {
+        const uint32_t id = ci[e];
+        if (id == WV_NIL) continue;
+        const int pos = atomicAdd(cnt, 1);
+        if (pos < FINW_NE) { sd[pos] = cd[e]; si[pos] = id; }
+    }
+    __syncthreads();
+    const int n_all = *cnt;
+    const int n = n_all < FINW_NE ? n_all : FINW_NE;
+    int len = 1;
+    while (len < n) len <<= 1;
+    for (int i = n + tid; i < len; i += nt) { sd[i] = FLT_MAX; si[i] = WV_NIL; }
+    for (int i = tid; i < ((p.D + 3) & ~3); i += nt) qv[i] = i < p.D ? p.Q[(size_t)q * p.ldq + i] : 0.f;
+    __syncthreads();
+    bitonic_sort_lds(sd, si, len);
+
+    // certificate eps (true units) and the key scale
+    const float u = 5.9604645e-08f;
+    const float D4 = (float)(p.D + 4);
+    float eps;
+    const float acc_f = p.split ? 12.f : 4.f;
+    const float split_e = p.split ? 4.f * 1.52587890625e-05f : 0.f;
+    if (METRIC == WV_METRIC_L2) {
+        const float qn = sqrtf(p.qnorm[q]);
+        const float s = qn + p.xnorm_max;
+        eps = acc_f * D4 * u * s * s + 2.f * split_e * qn * p.xnorm_max;
+    } else {
+        const float qn = p.qnorm[q];
+        eps = acc_f * D4 * u * qn * p.xnorm_max + 4.f * u + split_e * qn * p.xnorm_max;
+    }
+    eps *= 1.0001f;
+    if (p.h16) eps = h16_eps(METRIC, p.D, p.qnorm[q], p.xnorm_max, p.ex_max, p.qres[q]);
+    const float ks = p.h16 ? p.sx * p.qscale[0] : 1.f;   // key = ks * true-unit key
+    const int k = p.k;
+    // re-rank every entry that may beat the k-th key by the keys' error
+    int kf = n < k ? n : k;
+    if (n > k) {
+        const float lim = sd[k - 1] + 3.f * eps * ks * 1.001f;
+        // sd is sorted: count entries <= lim among the first FINW_KF
+        int c = 0;
+        for (int i = tid; i < n && i < FINW_KF; i += nt) c += sd[i] <= lim;
+        for (int m = 32; m >= 1; m >>= 1) c += __shfl_xor(c, m, 64);
+        __syncthreads();
+        if ((tid & 63) == 0) red_i[tid >> 6] = (uint32_t)c;
+        __syncthreads();
+        c = 0;
+        for (int w = 0; w < (nt >> 6); ++w) c += (int)red_i[w];
+        kf = c > kf ? c : kf;
+        if (kf > FINW_KF) kf = FINW_KF;
+        if (kf < n && key_less(sd[kf], si[kf], bound, bound_id)) { bound = sd[kf]; bound_id = si[kf]; }
+    }
+    if (n_all > FINW_NE) bound = -FLT_MAX;   // entries were lost: never certify
+    if (p.h16 && bound != FLT_MAX && bound != -FLT_MAX) bound *= 1.0f / ks;
+    if (p.tau_in) bound = fminf(bound, p.tau_in[q]);
+    __syncthreads();
+    // exact distances of the kf candidates (8 lanes per row), in place
+    const int g = tid & 7, grp = tid >> 3, ngrp = nt >> 3;
+    for (int c0 = 0; c0 < kf; c0 += ngrp) {
+        const int c = c0 + grp;
+        float d = FLT_MAX;
+        uint32_t id = WV_NIL;
+        if (c < kf) {
+            id = si[c];
+            d = exact_dist_group8<METRIC>(qv, p.X + (size_t)id * p.ldx, p.D, g);
+        }
+        __syncthreads();
+        if (c < kf && g == 0) sd[c] = d;
+        __syncthreads();
+    }
+    int len2 = 1;
+    while (len2 < kf) len2 <<= 1;
+    for (int i = kf + tid; i < len2; i += nt) { sd[i] = FLT_MAX; si[i] = WV_NIL; }
+    __syncthreads();
+    bitonic_sort_lds(sd, si, len2);
+    const int nk = kf < k ? kf : k;
+    for (int i = tid; i < nk; i += nt) {
+        p.out_ids[(size_t)q * k + i] = p.id_base + si[i];
+        p.out_d[(size_t)q * k + i] = sd[i];
+    }
+    if (tid == 0) {
+        const float dk = nk > 0 ? sd[nk - 1] : -FLT_MAX;
+        float bfull;
+        if (METRIC == WV_METRIC_L2) bfull = bound + p.qnorm[q];
+        else bfull = METRIC == WV_METRIC_DOT ? bound : 1.0f + bound;
+        bool certified;
+        if (n < k) certified = bound == FLT_MAX;
+        else certified = (bound == FLT_MAX) || (bfull - eps > dk);
+        p.out_n[q] = nk;
+        p.fail[q] = certified ? 0 : 1;
+        p.fail_thr[q] = n < k ? __builtin_inff() : dk;
+    }
+}
+
+__global__ __launch_bounds__(256) void wv_bf_finalize_wide_kernel(BfFinParams p) {
+    extern __shared__ float lds_w[];
+    const int dpad = (p.D + 3) & ~3;
+    float* qv = lds_w;
+    float* sd = qv + dpad;
+    uint32_t* si = reinterpret_cast<uint32_t*>(sd + FINW_NE);
+    float* red_d = reinterpret_cast<float*>(si + FINW_NE);
+    uint32_t* red_i = reinterpret_cast<uint32_t*>(red_d + 4);
+    int* cnt = reinterpret_cast<int*>(red_i + 4);
+    const int q = blockIdx.x;
+    if (q >= p.nq) return;
+    if (p.metric == WV_METRIC_L2) finalize_wide<WV_METRIC_L2>(p, q, qv, sd, si, red_d, red_i, cnt);
+    else if (p.metric == WV_METRIC_DOT) finalize_wide<WV_METRIC_DOT>(p, q, qv, sd, si, red_d, red_i, cnt);
+    else finalize_wide<WV_METRIC_COSINE>(p, q, qv, sd, si, red_d, red_i, cnt);
+}
+
+// ---------------------------------------------------------------------------
 // Exact full scan for one query: dist[i] = reference-order distance, or +inf
 // when ineligible.  8 lanes per row, 32 rows per 256-thread block pass.
 
@@ -1527,6 +1688,15 @@ hipError_t wv_launch_split_rows(const float* in, int ld_in, const uint64_t* ids,
 hipError_t wv_launch_bf_finalize(const wv::BfFinParams* p, hipStream_t s) {
     const size_t lds = (((p->D + 3) & ~3) + 2 * wv::FIN_KF) * sizeof(float);
     hipLaunchKernelGGL(wv::wv_bf_finalize_kernel, dim3(p->nq), dim3(64), lds, s, *p);
+    return hipGetLastError();
+}
+
+hipError_t wv_launch_bf_finalize_wide(const wv::BfFinParams* p, hipStream_t s) {
+    if (p->nq == 0) return hipSuccess;
+    if (p->k < 1 || p->k > wv::BF_WIDE_KMAX || (uint64_t)p->n_slots * p->prod * wv::BF_KP > 4ull * wv::FINW_NE)
+        return hipErrorInvalidValue;
+    const size_t lds = (((p->D + 3) & ~3) + 2 * wv::FINW_NE + 9) * sizeof(float);
+    hipLaunchKernelGGL(wv::wv_bf_finalize_wide_kernel, dim3(p->nq), dim3(256), lds, s, *p);
     return hipGetLastError();
 }
 

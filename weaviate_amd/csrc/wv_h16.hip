@@ -556,7 +556,7 @@ hipError_t wv_launch_bf_h16(const wv::H16Params* p, int ns, int seed, hipStream_
 
 hipError_t wv_launch_h16_seed(const wv::H16SeedParams* p, hipStream_t s) {
     if (p->nq == 0) return hipSuccess;
-    if (p->k < 1 || p->k > 64) return hipErrorInvalidValue;
+    if (p->k < 1 || p->k > wv::BF_WIDE_KMAX) return hipErrorInvalidValue;
     hipLaunchKernelGGL(wv::wv_h16_seed_kernel, dim3(p->nq), dim3(64), 0, s, *p);
     return hipGetLastError();
 }

@@ -14,6 +14,11 @@ constexpr int BF_PROD3 = 8;  // wv_bf_split3_kernel: 4 base-row waves x 2 lane h
 constexpr int BF_BQ3 = 192;  // wv_bf_split3_kernel: queries per block (3 query waves x 64)
 constexpr int FIN_KF = 32;   // candidates re-ranked exactly per query
 constexpr int BF_FAST_KMAX = 32;   // k served by the MFMA + finalize pipeline
+// larger k (searches with limit > 32, SearchByVectorDistance's deepening): the
+// f16 key pass with at least 2k lists per query, merged by the wide finalize
+constexpr int BF_WIDE_KMAX = 256;
+constexpr int FINW_NE = 8192;      // list entries one wide-finalize workgroup sorts in LDS
+constexpr int FINW_KF = 1024;      // candidates it re-ranks exactly at most
 constexpr int HNSW_EF_MAX = 512;   // largest ef the LDS beam holds
 
 struct BfParams {
