@@ -167,7 +167,12 @@ class Ctx:
                 dist.init_process_group(backend="nccl", device_id=torch.device("cuda", self.gpu))
         torch.cuda.set_device(self.gpu)
         self.dev = torch.device("cuda", self.gpu)
-        self.stream = torch.cuda.current_stream(self.dev).cuda_stream
+        # one real stream for everything this rank queues (torch ops and the
+        # library's device batches): the default stream's handle is 0, which
+        # the C ABI reads as "the index's own stream"
+        self.stream_obj = torch.cuda.Stream(self.dev)
+        torch.cuda.set_stream(self.stream_obj)
+        self.stream = self.stream_obj.cuda_stream
         self.n_devices = self.ws
         if self.ws > 1:   # distinct devices behind the ranks (a gloo rehearsal may share one)
             t = torch.tensor([self.gpu], dtype=torch.int64)
@@ -192,13 +197,16 @@ class Ctx:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
-    def time_steps(self, step, steps, warmup):
+    def time_steps(self, step, steps, warmup, before_timed=None):
         """W untimed steps, then exactly K steps bracketed by barrier +
-        synchronize on both sides; the max over ranks (bench contract)."""
+        synchronize on both sides; the max over ranks (bench contract).
+        before_timed runs after the warmup, outside the timed region."""
         torch = self.torch
         for _ in range(warmup):
             step(False)
         torch.cuda.synchronize(self.dev)
+        if before_timed:
+            before_timed()
         self.barrier()
         torch.cuda.synchronize(self.dev)
         t0 = time.perf_counter()
@@ -322,11 +330,11 @@ def run_exact(args, ctx, W):
         allow_ptr, allow_bits = allow_t.data_ptr(), n_local
     kern_ms = []
 
+    # no host round trip inside the timed region: the kernel times (HIP
+    # events per batch) and the batch stats are read after it
     def step(timed):
         ix.search_batch_device(qt.data_ptr(), NQ, K, out_ids.data_ptr(), out_d.data_ptr(), out_n.data_ptr(), ef=0,
                                mode="exact", stream=ctx.stream, allow_ptr=allow_ptr, allow_nbits=allow_bits)
-        if timed:
-            kern_ms.append(ix.last_kernel_times())
         if split == "corpus" and ws > 1:
             ctx.allgather(g_ids, out_ids)
             ctx.allgather(g_d, out_d)
@@ -335,7 +343,8 @@ def run_exact(args, ctx, W):
                                   m_ids.data_ptr(), m_n.data_ptr(), stream=ctx.stream)
 
     ix.set_timing(True)
-    elapsed = ctx.time_steps(step, args.steps, args.warmup)
+    elapsed = ctx.time_steps(step, args.steps, args.warmup, before_timed=ix.last_kernel_times)
+    kern_ms.append(ix.last_kernel_times())   # per-batch averages over the timed steps
     stats = ix.last_batch_stats()
     fin_ids, fin_d = (m_ids, m_d) if (split == "corpus" and ws > 1) else (out_ids, out_d)
     final_ids = fin_ids.cpu().numpy().view(np.uint64)
@@ -380,13 +389,12 @@ def wide_k_line(args, ctx, st, W):
         torch.cuda.synchronize(ctx.dev)
         t0 = time.perf_counter()
         reps = 3
-        fb = 0
         for _ in range(reps):
             ix.search_batch_device(qt.data_ptr(), NQ, k, oi.data_ptr(), od.data_ptr(), on.data_ptr(), mode="exact",
                                    stream=ctx.stream)
-            fb += ix.last_batch_stats()["fallbacks"]
         torch.cuda.synchronize(ctx.dev)
         dt = (time.perf_counter() - t0) / reps
+        fb = ix.last_batch_stats()["fallbacks"] * reps   # the last batch's (all batches are the same)
         out[f"exact_k{k}"] = {"value": round(NQ / dt, 1), "unit": "queries/s", "ms_per_batch": round(1e3 * dt, 3),
                               "fallback_queries_per_batch": fb / reps, "nq": NQ}
         if k == 100:
@@ -512,12 +520,11 @@ def run_hnsw(args, ctx, W, with_cpu):
     def step(timed):
         ix.search_batch_device(qt.data_ptr(), NQ, K, out_ids.data_ptr(), out_d.data_ptr(), out_n.data_ptr(),
                                ef=args.ef, mode="hnsw", stream=ctx.stream)
-        if timed:
-            kern_ms.append(ix.last_kernel_times())
-            stats.append(ix.last_batch_stats())
 
     ix.set_timing(True)
-    elapsed = ctx.time_steps(step, args.steps, args.warmup)
+    elapsed = ctx.time_steps(step, args.steps, args.warmup, before_timed=ix.last_kernel_times)
+    kern_ms.append(ix.last_kernel_times())   # per-batch averages over the timed steps
+    stats.append(ix.last_batch_stats())
     hi_ids = out_ids.cpu().numpy().view(np.uint64)
     hi_d = out_d.cpu().numpy()
     # exact truths on the same queries (the exact path: ids bit-identical to

@@ -190,13 +190,21 @@ int wv_search_batch(wv_index *ix, const float *queries, int nq, int k, int ef, c
  * nq rows at a stride of wv_index_query_ld(ix) floats (dim rounded up to 4;
  * the pad columns are ignored).  The work is queued on `stream` (a
  * hipStream_t, NULL = the index's own stream) and ordered after every earlier
- * call on the index; later calls on the index are ordered after it.  Used by
- * the benchmark so that the timed region sees only device work. */
+ * call on the index; later calls on the index are ordered after it.  The
+ * results are complete when the stream reaches the end of the queued work.
+ * Exact searches (k <= 256 on the f16 key pass, k <= 32 otherwise) and HNSW
+ * searches without an allow list queue everything, certificate fallbacks
+ * included (resolved on the device), and return without waiting for the GPU;
+ * allow lists (AUTO's per-query flat/HNSW decision, row compaction), the
+ * exact scan for larger k and PQ-compressed fallbacks still read counts back.
+ * Batch stats and kernel times are read (one sync) only when asked for. */
 int wv_search_batch_device(wv_index *ix, const float *d_queries, int nq, int k, int ef,
                            const uint64_t *d_allow_bits, uint64_t allow_nbits, uint64_t allow_stride_words,
                            int mode, uint64_t *d_out_ids, float *d_out_dists, int32_t *d_out_n, void *stream);
 /* Row stride (floats) of the device query rows wv_search_batch_device reads. */
 int wv_index_query_ld(const wv_index *ix);
+/* Wait for every call queued on the index's own stream (a NULL `stream`). */
+int wv_index_synchronize(wv_index *ix);
 
 /* Merge per-shard results: for each query, the k best (dist, id) of the
  * n_shards lists d_in_*[shard][nq][k] (entries beyond d_in_n are ignored).
@@ -204,14 +212,17 @@ int wv_index_query_ld(const wv_index *ix);
 int wv_merge_shards_device(const float *d_in_dists, const uint64_t *d_in_ids, const int32_t *d_in_n, int n_shards,
                            int nq, int k, float *d_out_dists, uint64_t *d_out_ids, int32_t *d_out_n, void *stream);
 
-/* Per-query statistics of the last HNSW batch on this thread (nullable
- * outputs): distance evaluations and expansions summed over the batch. */
+/* Statistics of the last batch on the index (nullable outputs): HNSW distance
+ * evaluations and expansions summed over the batch, and the queries answered
+ * by the certificate fallback.  Waits for the batch to finish. */
 int wv_last_batch_stats(wv_index *ix, uint64_t *dist_evals, uint64_t *expansions, uint64_t *fallbacks);
 
 /* Kernel timing with HIP events on the launch stream (off by default).  When
- * enabled, the last batch records the device time of its dominant kernels:
- * the MFMA brute-force kernel, the exact re-rank/finalize kernel and the HNSW
- * beam-search kernel (milliseconds, summed over the launches of the batch). */
+ * enabled, every batch records the device time of its dominant kernels: the
+ * MFMA brute-force kernel, the exact re-rank/finalize kernel and the HNSW
+ * beam-search kernel.  wv_last_kernel_times / wv_last_seed_time wait for the
+ * recorded batches and return the per-batch average (milliseconds) over the
+ * batches since the previous read (or since timing was enabled). */
 int wv_index_set_timing(wv_index *ix, int enable);
 int wv_last_kernel_times(wv_index *ix, float *bf_mfma_ms, float *bf_finalize_ms, float *hnsw_ms);
 /* The f16 key pass's seed pre-pass of the last batch (key pass over every

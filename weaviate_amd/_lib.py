@@ -100,6 +100,7 @@ SIGNATURES = {
     "wv_search_batch_device": (C.c_int, [_vp, _vp, C.c_int, C.c_int, C.c_int, _vp, C.c_uint64, C.c_uint64, C.c_int,
                                          _vp, _vp, _vp, _vp]),
     "wv_index_query_ld": (C.c_int, [_vp]),
+    "wv_index_synchronize": (C.c_int, [_vp]),
     "wv_merge_shards_device": (C.c_int, [_vp, _vp, _vp, C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp]),
     "wv_last_batch_stats": (C.c_int, [_vp, _u64p, _u64p, _u64p]),
     "wv_index_set_timing": (C.c_int, [_vp, C.c_int]),

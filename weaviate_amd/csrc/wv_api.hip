@@ -8,6 +8,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <cmath>
 #include <cstdio>
@@ -28,6 +29,9 @@ hipError_t wv_launch_bf_finalize(const wv::BfFinParams* p, hipStream_t s);
 hipError_t wv_launch_bf_finalize_wide(const wv::BfFinParams* p, hipStream_t s);
 hipError_t wv_launch_exact_scan(const wv::ScanParams* p, hipStream_t s);
 hipError_t wv_launch_fb(const wv::FbParams* p, hipStream_t s);
+hipError_t wv_launch_fbd(const int32_t* flags, int nq, const wv::FbParams* fb, hipStream_t s);
+hipError_t wv_launch_fbd_mark(const int32_t* status, int nq, int32_t* flags, float* thr, hipStream_t s);
+hipError_t wv_launch_hnsw_stats(const uint32_t* counters, int nq, unsigned long long* acc, hipStream_t s);
 hipError_t wv_launch_rownorm(const float* X, uint64_t N, int D, int ldx, float* norm2, unsigned int* maxbits,
                              hipStream_t s);
 hipError_t wv_launch_normalize(const float* in, float* out, uint64_t n, int D, int ld, hipStream_t s);
@@ -72,6 +76,14 @@ int fail(int code, const std::string& msg) {
         if (_e != hipSuccess)                                                                  \
             return fail(_e == hipErrorOutOfMemory ? WV_EOOM : WV_EDEVICE,                      \
                         std::string(#expr) + ": " + hipGetErrorString(_e));                   \
+    } while (0)
+// record timing event i of the current batch's set (wv_index::ev)
+#define TREC(i)                                                                     \
+    do {                                                                            \
+        if (ix->timing && ix->ev) {                                                 \
+            HIP_TRY(hipEventRecord(ix->ev[i], s));                                  \
+            ix->ev_mask[ix->ev_used - 1] |= (uint8_t)(1u << (i));                   \
+        }                                                                           \
     } while (0)
 
 // growable device scratch buffer
@@ -255,16 +267,29 @@ struct wv_index {
     std::vector<uint64_t> has_code;
     DevBuf pq_cent, pq_codes;
     DevBuf pk_key, pk_dist, pk_val, pk_skey, pk_sval, pk_off;
-    // stats of the last batch
+    // stats of the last batch: host-side counts plus device accumulators
+    // (stat_acc: distance evaluations, expansions, device-resolved
+    // fallbacks), read -- after a sync -- only when the stats are asked for
     uint64_t last_dist = 0, last_exp = 0, last_fallbacks = 0;
+    DevBuf stat_acc;
+    hipStream_t stat_stream = nullptr;
+    // device-resolved certificate fallback (wv_launch_fbd): failed-query list
+    // and count, survivors, overflow flags, full-scan slots
+    DevBuf fbd_list, fbd_nf, fbd_over, fbd_cd, fbd_ci, fbd_cn, fbd_scr;
     // ordering of work on a caller's stream (wv_search_batch_device) against
     // the index's own stream: the call waits for ix->stream, and ix->stream
     // then waits for the call, so the scratch and state buffers the call reads
     // are never rewritten by a later call while it is still queued
     hipEvent_t ev_in = nullptr, ev_out = nullptr;
-    // optional kernel timing (hipEvents on the launch stream)
+    // optional kernel timing (hipEvents on the launch stream): each batch
+    // records into its own event set (pairs 0-1 key pass, 2-3 finalize, 4-5
+    // HNSW, 6-7 seed pass); the sets are read -- after a sync -- only when the
+    // times are asked for, so timing adds no host round trip per batch
     bool timing = false;
-    hipEvent_t ev[8] = {};
+    hipEvent_t* ev = nullptr;                    // the current batch's set
+    std::vector<std::array<hipEvent_t, 8>> ev_pool;
+    std::vector<uint8_t> ev_mask;                // pairs recorded per set
+    size_t ev_used = 0;                          // sets recorded since the last read
     float t_mfma = 0.f, t_fin = 0.f, t_hnsw = 0.f, t_pre = 0.f;
     int n_cus = 256;
     // brute-force workgroups per launch: a whole number of resident waves of
@@ -542,7 +567,7 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
         hp.tau = nullptr;
         hp.out_d = ix->cand_d.as<float>();
         hp.out_id = nullptr;
-        if (ix->timing) HIP_TRY(hipEventRecord(ix->ev[6], s));
+        TREC(6);
         HIP_TRY(wv_launch_bf_h16(&hp, ns, 1, s));
         wv::H16SeedParams sp{};
         sp.minima = ix->cand_d.as<float>();
@@ -561,7 +586,7 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
         sp.qres = ix->qres.as<float>();
         sp.tau = ix->tau.as<float>();
         HIP_TRY(wv_launch_h16_seed(&sp, s));
-        if (ix->timing) HIP_TRY(hipEventRecord(ix->ev[7], s));
+        TREC(7);
     }
     const wv::BfSchedule sch = wv::bf_schedule(nq, N, target(ntl), wv::H_BQ, wv::H_BN);
     if (wide && (uint64_t)sch.n_slots * wv::H_PROD * wv::BF_KP > (uint64_t)wv::FINW_NE)
@@ -575,32 +600,65 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     hp.tau = seed ? ix->tau.as<float>() : nullptr;
     hp.out_d = ix->cand_d.as<float>();
     hp.out_id = ix->cand_id.as<uint32_t>();
-    if (ix->timing) HIP_TRY(hipEventRecord(ix->ev[0], s));
+    TREC(0);
     HIP_TRY(wv_launch_bf_h16(&hp, ns, 0, s));
-    if (ix->timing) HIP_TRY(hipEventRecord(ix->ev[1], s));
+    TREC(1);
     fp.cand_d = ix->cand_d.as<float>();
     fp.cand_id = ix->cand_id.as<uint32_t>();
     fp.n_slots = sch.n_slots;
     fp.ntiles = sch.ntiles;
     fp.units_per_block = sch.units_per_block;
     fp.tau_in = hp.tau;
-    if (ix->timing) HIP_TRY(hipEventRecord(ix->ev[2], s));
+    TREC(2);
     HIP_TRY(wide ? wv_launch_bf_finalize_wide(&fp, s) : wv_launch_bf_finalize(&fp, s));
-    if (ix->timing) HIP_TRY(hipEventRecord(ix->ev[3], s));
-    std::vector<int32_t> f(nq);
-    HIP_TRY(hipMemcpyAsync(f.data(), ix->fail.p, 4 * (size_t)nq, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    if (ix->timing) {
-        float a = 0.f, b = 0.f, c = 0.f;
-        HIP_TRY(hipEventElapsedTime(&a, ix->ev[0], ix->ev[1]));
-        HIP_TRY(hipEventElapsedTime(&b, ix->ev[2], ix->ev[3]));
-        if (seed) HIP_TRY(hipEventElapsedTime(&c, ix->ev[6], ix->ev[7]));
-        ix->t_mfma += a;
-        ix->t_fin += b;
-        ix->t_pre += c;
-    }
-    for (int i = 0; i < nq; ++i)
-        if (f[i]) fails.push_back(i);
+    TREC(3);
+    (void)fails;   // uncertified queries are resolved on the device (queue_fbd)
+    return WV_OK;
+}
+
+// Queue the device-resolved fallback for the queries whose flag in ix->fail
+// is set (threshold ix->fail_thr): no host round trip (wv_bf.hip, fbd kernels).
+int queue_fbd(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_allow, uint64_t allow_nbits,
+              uint64_t allow_stride, uint64_t* d_out_ids, float* d_out_d, int32_t* d_out_n, hipStream_t s) {
+    const uint64_t N = ix->n_rows;
+    HIP_TRY(ix->fbd_list.ensure((size_t)nq * 4));
+    HIP_TRY(ix->fbd_nf.ensure(16));
+    HIP_TRY(ix->fbd_over.ensure((size_t)nq * 4));
+    HIP_TRY(ix->fbd_cd.ensure((size_t)nq * wv::FB_CAP * 4));
+    HIP_TRY(ix->fbd_ci.ensure((size_t)nq * wv::FB_CAP * 4));
+    HIP_TRY(ix->fbd_cn.ensure((size_t)nq * 4));
+    HIP_TRY(ix->fbd_scr.ensure((size_t)wv::FBD_SCR * std::max<uint64_t>(N, 1) * 4));
+    HIP_TRY(ix->stat_acc.ensure(32));
+    wv::FbParams bp{};
+    bp.X = ix->vecs.as<float>();
+    bp.Q = d_q;
+    bp.qidx = ix->fbd_list.as<int32_t>();
+    bp.thr = ix->fail_thr.as<float>();
+    bp.tomb = ix->excl.as<uint64_t>();
+    bp.tomb_nbits = ix->capacity;
+    bp.allow = d_allow;
+    bp.allow_nbits = allow_nbits;
+    bp.allow_stride = allow_stride;
+    bp.N = N;
+    bp.nf = nq;
+    bp.D = ix->dim;
+    bp.ldx = ix->ldx;
+    bp.ldq = ix->dpad;
+    bp.metric = ix->metric;
+    bp.k = k;
+    bp.id_base = ix->cfg.id_base;
+    bp.cand_d = ix->fbd_cd.as<float>();
+    bp.cand_id = ix->fbd_ci.as<uint32_t>();
+    bp.cand_n = ix->fbd_cn.as<uint32_t>();
+    bp.out_ids = d_out_ids;
+    bp.out_d = d_out_d;
+    bp.out_n = d_out_n;
+    bp.overflow = ix->fbd_over.as<int32_t>();
+    bp.d_nf = ix->fbd_nf.as<int32_t>();
+    bp.scratch = ix->fbd_scr.as<float>();
+    bp.n_scr = wv::FBD_SCR;
+    bp.fb_total = ix->stat_acc.as<unsigned long long>() + 2;
+    HIP_TRY(wv_launch_fbd(ix->fail.as<int32_t>(), nq, &bp, s));
     return WV_OK;
 }
 
@@ -650,7 +708,7 @@ int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
             const uint64_t* sh = d_allow && !allow_stride ? d_allow : nullptr;
             int rc = run_h16(ix, d_q, nq, k, sh, allow_nbits, N, d_out_ids, d_out_d, d_out_n, s, fails);
             if (rc) return rc;
-            goto fallbacks;
+            return queue_fbd(ix, d_q, nq, k, d_allow, allow_nbits, allow_stride, d_out_ids, d_out_d, d_out_n, s);
         }
         // bf16x3 key pass on native images (whole-corpus or shared allow list
         // scans): 256-query blocks, one 512-thread workgroup per CU, two waves
@@ -719,14 +777,10 @@ int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
         bp.units_per_block = sch.units_per_block;
         bp.out_d = ix->cand_d.as<float>();
         bp.out_id = ix->cand_id.as<uint32_t>();
-        if (ix->timing) HIP_TRY(hipEventRecord(ix->ev[0], s));
+        TREC(0);
         HIP_TRY(wv_launch_bf_mfma(&bp, s));
-        if (ix->timing) HIP_TRY(hipEventRecord(ix->ev[1], s));
-        unsigned int mb = 0;
-        HIP_TRY(hipMemcpyAsync(&mb, ix->maxnorm.p, 4, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipStreamSynchronize(s));
-        float maxn;
-        std::memcpy(&maxn, &mb, 4);
+        TREC(1);
+        const float maxn = ix->maxnorm_host;   // cached at every row write
         wv::BfFinParams fp{};
         fp.X = ix->vecs.as<float>();
         fp.Q = d_q;
@@ -753,25 +807,13 @@ int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
         fp.split = bp.split;
         fp.bq = bq;
         fp.prod = prod;
-        if (ix->timing) HIP_TRY(hipEventRecord(ix->ev[2], s));
+        TREC(2);
         HIP_TRY(wv_launch_bf_finalize(&fp, s));
-        if (ix->timing) HIP_TRY(hipEventRecord(ix->ev[3], s));
-        std::vector<int32_t> f(nq);
-        HIP_TRY(hipMemcpyAsync(f.data(), ix->fail.p, 4 * (size_t)nq, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipStreamSynchronize(s));
-        if (ix->timing) {
-            float a = 0.f, b = 0.f;
-            HIP_TRY(hipEventElapsedTime(&a, ix->ev[0], ix->ev[1]));
-            HIP_TRY(hipEventElapsedTime(&b, ix->ev[2], ix->ev[3]));
-            ix->t_mfma += a;
-            ix->t_fin += b;
-        }
-        for (int i = 0; i < nq; ++i)
-            if (f[i]) fails.push_back(i);
+        TREC(3);
+        return queue_fbd(ix, d_q, nq, k, d_allow, allow_nbits, allow_stride, d_out_ids, d_out_d, d_out_n, s);
     } else {
         for (int i = 0; i < nq; ++i) fails.push_back(i);
     }
-fallbacks:
     ix->last_fallbacks += fails.size();
     if (!fails.empty() && std::getenv("WV_ABLATE_NO_FALLBACK")) fails.clear();   // kernel ablations only
     if (!fails.empty() && keyed) {
@@ -991,23 +1033,21 @@ int run_hnsw(wv_index* ix, const float* d_q, int nq, int k, int ef, const uint64
     hp.status = ix->status.as<int32_t>();
     hp.counters = ix->counters.as<uint32_t>();
     if (ix->pq_on) hp.pq = pq_params(ix);   // compressed: PQ distances (search.go:171-199)
-    if (ix->timing) HIP_TRY(hipEventRecord(ix->ev[4], s));
+    TREC(4);
     HIP_TRY(wv_launch_hnsw(&hp, wpb, s));
-    if (ix->timing) HIP_TRY(hipEventRecord(ix->ev[5], s));
+    TREC(5);
+    HIP_TRY(ix->stat_acc.ensure(32));
+    HIP_TRY(wv_launch_hnsw_stats(ix->counters.as<uint32_t>(), nq, ix->stat_acc.as<unsigned long long>(), s));
+    if (!ix->pq_on) {
+        // queries whose side state outgrew LDS: exact answer on the device
+        HIP_TRY(ix->fail.ensure((size_t)nq * 4));
+        HIP_TRY(ix->fail_thr.ensure((size_t)nq * 4));
+        HIP_TRY(wv_launch_fbd_mark(ix->status.as<int32_t>(), nq, ix->fail.as<int32_t>(), ix->fail_thr.as<float>(), s));
+        return queue_fbd(ix, d_q, nq, k, d_allow, allow_nbits, allow_stride, d_out_ids, d_out_d, d_out_n, s);
+    }
     std::vector<int32_t> st(nq);
-    std::vector<uint32_t> ct(2 * (size_t)nq);
     HIP_TRY(hipMemcpyAsync(st.data(), ix->status.p, 4 * (size_t)nq, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(ct.data(), ix->counters.p, 8 * (size_t)nq, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    if (ix->timing) {
-        float a = 0.f;
-        HIP_TRY(hipEventElapsedTime(&a, ix->ev[4], ix->ev[5]));
-        ix->t_hnsw += a;
-    }
-    for (int i = 0; i < nq; ++i) {
-        ix->last_dist += ct[2 * i];
-        ix->last_exp += ct[2 * i + 1];
-    }
     // Queries whose side-candidate set outgrew LDS are answered exactly
     // (flatSearch over the same allow list: a superset in quality).
     for (int q = 0; q < nq; ++q) {
@@ -1060,12 +1100,10 @@ int run_hnsw_delta(wv_index* ix, const float* d_q, int nq, int k, int ef, const 
                        ix->dmask.as<uint64_t>());
     HIP_TRY(hipGetLastError());
     const uint64_t st = d_allow && allow_stride ? words : 0;
-    const float t_h = ix->t_hnsw;
     const uint64_t e = ix->last_dist, x = ix->last_exp, f = ix->last_fallbacks;
     rc = run_exact(ix, d_q, nq, k, ix->dmask.as<uint64_t>(), ix->capacity, st, ids + nk, ds + nk, ns + nq, s,
                    st ? ix->delta.as<uint64_t>() : nullptr, ix->capacity);
     if (rc) return rc;
-    ix->t_hnsw = t_h;
     ix->last_dist = e;
     ix->last_exp = x;
     ix->last_fallbacks += f;
@@ -1082,7 +1120,20 @@ int search_core(wv_index* ix, const float* d_q, int nq, int k, int ef, const uin
     int rc = refresh_bitmaps(ix);
     if (rc) return rc;
     ix->last_dist = ix->last_exp = ix->last_fallbacks = 0;
-    ix->t_mfma = ix->t_fin = ix->t_hnsw = ix->t_pre = 0.f;
+    HIP_TRY(ix->stat_acc.ensure(32));
+    HIP_TRY(hipMemsetAsync(ix->stat_acc.p, 0, 32, s));
+    ix->stat_stream = s;
+    if (ix->timing) {
+        if (ix->ev_used == ix->ev_pool.size()) {
+            std::array<hipEvent_t, 8> e{};
+            for (auto& x : e) HIP_TRY(hipEventCreate(&x));
+            ix->ev_pool.push_back(e);
+            ix->ev_mask.push_back(0);
+        }
+        ix->ev = ix->ev_pool[ix->ev_used].data();
+        ix->ev_mask[ix->ev_used] = 0;
+        ix->ev_used++;
+    }
     if (ef <= 0) ef = search_time_ef(ix->cfg, k);
     if (mode == WV_MODE_EXACT)
         return run_exact(ix, d_q, nq, k, d_allow, allow_nbits, allow_stride, d_out_ids, d_out_d, d_out_n, s);
@@ -1280,11 +1331,13 @@ int wv_index_destroy(wv_index* ix) {
                       &ix->qimg16, &ix->qres, &ix->qmax, &ix->qscale, &ix->tau, &ix->allow_pad, &ix->ex_bits,
                       &ix->delta, &ix->dmask, &ix->dl_ids, &ix->dl_d, &ix->dl_n, &ix->dq_tmp, &ix->b_tgt, &ix->b_ci,
                       &ix->b_cd, &ix->b_cn, &ix->b_cnt0, &ix->b_cntu, &ix->b_rk, &ix->b_rn, &ix->b_rk2, &ix->b_rn2,
-                      &ix->b_uk, &ix->b_ul, &ix->b_uo, &ix->b_nr, &ix->b_tmp})
+                      &ix->b_uk, &ix->b_ul, &ix->b_uo, &ix->b_nr, &ix->b_tmp, &ix->stat_acc, &ix->fbd_list,
+                      &ix->fbd_nf, &ix->fbd_over, &ix->fbd_cd, &ix->fbd_ci, &ix->fbd_cn, &ix->fbd_scr})
         b->release();
     if (ix->stream) (void)hipStreamSynchronize(ix->stream);
-    for (auto& e : ix->ev)
-        if (e) (void)hipEventDestroy(e);
+    for (auto& set : ix->ev_pool)
+        for (auto e : set)
+            if (e) (void)hipEventDestroy(e);
     if (ix->ev_in) (void)hipEventDestroy(ix->ev_in);
     if (ix->ev_out) (void)hipEventDestroy(ix->ev_out);
     if (ix->stream) (void)hipStreamDestroy(ix->stream);
@@ -2005,6 +2058,14 @@ int wv_search_batch_device(wv_index* ix, const float* d_queries, int nq, int k, 
 
 int wv_index_query_ld(const wv_index* ix) { return ix ? ix->dpad : -1; }
 
+int wv_index_synchronize(wv_index* ix) {
+    if (check(ix)) return fail(WV_EINVAL, "wv_index_synchronize: bad argument");
+    std::lock_guard<std::mutex> g(ix->mu);
+    HIP_TRY(hipSetDevice(ix->cfg.device));
+    HIP_TRY(hipStreamSynchronize(ix->stream));
+    return WV_OK;
+}
+
 int wv_search_by_vector(wv_index* ix, const float* vector, int k, const uint64_t* allow_bits, uint64_t allow_nbits,
                         uint64_t* out_ids, float* out_dists, int32_t* out_n) {
     return wv_search_batch(ix, vector, 1, k, 0, allow_bits, allow_nbits, 0, WV_MODE_AUTO, out_ids, out_dists, out_n);
@@ -2064,14 +2125,41 @@ int wv_index_set_timing(wv_index* ix, int enable) {
     if (check(ix)) return WV_EINVAL;
     std::lock_guard<std::mutex> g(ix->mu);
     HIP_TRY(hipSetDevice(ix->cfg.device));
-    if (enable && !ix->ev[0])
-        for (auto& e : ix->ev) HIP_TRY(hipEventCreate(&e));
     ix->timing = enable != 0;
+    ix->ev_used = 0;
+    return WV_OK;
+}
+
+// the recorded event sets -> per-batch averages (one sync, on request)
+static int read_timing(wv_index* ix) {
+    if (ix->ev_used == 0) return WV_OK;
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
+    for (size_t b = 0; b < ix->ev_used; ++b) {
+        const auto& e = ix->ev_pool[b];
+        const uint8_t m = ix->ev_mask[b];
+        for (int pr = 0; pr < 4; ++pr) {
+            if ((m & (3u << (2 * pr))) != (3u << (2 * pr))) continue;
+            HIP_TRY(hipEventSynchronize(e[2 * pr + 1]));
+            float t = 0.f;
+            HIP_TRY(hipEventElapsedTime(&t, e[2 * pr], e[2 * pr + 1]));
+            a[pr] += t;
+        }
+    }
+    const float inv = 1.0f / (float)ix->ev_used;
+    ix->t_mfma = a[0] * inv;
+    ix->t_fin = a[1] * inv;
+    ix->t_hnsw = a[2] * inv;
+    ix->t_pre = a[3] * inv;
+    ix->ev_used = 0;
     return WV_OK;
 }
 
 int wv_last_kernel_times(wv_index* ix, float* bf_mfma_ms, float* bf_finalize_ms, float* hnsw_ms) {
     if (check(ix)) return WV_EINVAL;
+    std::lock_guard<std::mutex> g(ix->mu);
+    HIP_TRY(hipSetDevice(ix->cfg.device));
+    int rc = read_timing(ix);
+    if (rc) return rc;
     if (bf_mfma_ms) *bf_mfma_ms = ix->t_mfma;
     if (bf_finalize_ms) *bf_finalize_ms = ix->t_fin;
     if (hnsw_ms) *hnsw_ms = ix->t_hnsw;
@@ -2080,15 +2168,26 @@ int wv_last_kernel_times(wv_index* ix, float* bf_mfma_ms, float* bf_finalize_ms,
 
 int wv_last_seed_time(wv_index* ix, float* seed_ms) {
     if (check(ix) || !seed_ms) return fail(WV_EINVAL, "bad argument");
+    std::lock_guard<std::mutex> g(ix->mu);
+    HIP_TRY(hipSetDevice(ix->cfg.device));
+    int rc = read_timing(ix);
+    if (rc) return rc;
     *seed_ms = ix->t_pre;
     return WV_OK;
 }
 
 int wv_last_batch_stats(wv_index* ix, uint64_t* dist_evals, uint64_t* expansions, uint64_t* fallbacks) {
     if (check(ix)) return WV_EINVAL;
-    if (dist_evals) *dist_evals = ix->last_dist;
-    if (expansions) *expansions = ix->last_exp;
-    if (fallbacks) *fallbacks = ix->last_fallbacks;
+    std::lock_guard<std::mutex> g(ix->mu);
+    HIP_TRY(hipSetDevice(ix->cfg.device));
+    unsigned long long acc[3] = {0, 0, 0};
+    if (ix->stat_acc.p) {
+        HIP_TRY(hipMemcpyAsync(acc, ix->stat_acc.p, 24, hipMemcpyDeviceToHost, ix->stat_stream));
+        HIP_TRY(hipStreamSynchronize(ix->stat_stream));
+    }
+    if (dist_evals) *dist_evals = ix->last_dist + acc[0];
+    if (expansions) *expansions = ix->last_exp + acc[1];
+    if (fallbacks) *fallbacks = ix->last_fallbacks + acc[2];
     return WV_OK;
 }
 

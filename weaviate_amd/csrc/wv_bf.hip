@@ -1526,6 +1526,266 @@ __global__ __launch_bounds__(1024) void wv_fb_select_kernel(FbParams p) {
 }
 
 // ---------------------------------------------------------------------------
+// Device-resolved certificate fallback (wv_api.hip queues it after every keyed
+// pass and after the HNSW kernel, so a batch needs no host round trip):
+//  1. compact: the failed queries (flag != 0) listed in query order, count;
+//  2. filter: for each listed query, rows with exact distance <= thr[q] (an
+//     upper bound of its true k-th distance) kept, up to FB_CAP;
+//  3. select: the survivors sorted by (dist, id), first k written;
+//  4. full: a query whose survivors overflowed FB_CAP (ties, thr = +inf for an
+//     HNSW query whose side state overflowed) gets every row's distance in a
+//     scratch slot, a radix select of the k-th (dist, id) and an ordered
+//     collection -- the result of a full sort, as exact_full computes it.
+__global__ __launch_bounds__(1024) void wv_fbd_compact_kernel(const int32_t* __restrict__ flags, int nq,
+                                                              int32_t* __restrict__ list, int32_t* __restrict__ count,
+                                                              unsigned long long* total) {
+    __shared__ int wsum[16];
+    __shared__ int base;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (tid == 0) base = 0;
+    __syncthreads();
+    for (int c0 = 0; c0 < nq; c0 += 1024) {
+        const int q = c0 + tid;
+        const bool f = q < nq && flags[q] != 0;
+        const uint64_t b = __ballot(f);
+        const int r = __popcll(b & ((1ull << lane) - 1ull));
+        if (lane == 0) wsum[w] = __popcll(b);
+        __syncthreads();
+        int off = base;
+        for (int i = 0; i < w; ++i) off += wsum[i];
+        if (f) list[off + r] = q;
+        __syncthreads();
+        if (tid == 0)
+            for (int i = 0; i < 16; ++i) base += wsum[i];
+        __syncthreads();
+    }
+    if (tid == 0) {
+        *count = base;
+        if (total) atomicAdd(total, (unsigned long long)base);
+    }
+}
+
+// HNSW per-query counters [nq][2] (distance evaluations, expansions) summed
+// into acc[0], acc[1] on the device (read only when stats are asked for)
+__global__ void wv_hnsw_stats_kernel(const uint32_t* __restrict__ ct, int nq, unsigned long long* acc) {
+    unsigned long long a = 0, b = 0;
+    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += gridDim.x * blockDim.x) {
+        a += ct[2 * q];
+        b += ct[2 * q + 1];
+    }
+    for (int m = 32; m >= 1; m >>= 1) {
+        a += __shfl_xor(a, m, 64);
+        b += __shfl_xor(b, m, 64);
+    }
+    if ((threadIdx.x & 63) == 0 && (a || b)) {
+        atomicAdd(&acc[0], a);
+        atomicAdd(&acc[1], b);
+    }
+}
+
+__global__ void wv_fbd_mark_kernel(const int32_t* __restrict__ status, int nq, int32_t* __restrict__ flags,
+                                   float* __restrict__ thr) {
+    // HNSW queries whose side state overflowed: exact answer, no threshold
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nq) return;
+    flags[q] = status[q] != 0;
+    thr[q] = __builtin_inff();
+}
+
+template <int METRIC>
+__device__ void fbd_filter_one(const FbParams& p, const float* qv, int f, int q) {
+    const int g = threadIdx.x & 7;
+    const uint64_t grp = (uint64_t)blockIdx.x * (blockDim.x >> 3) + (threadIdx.x >> 3);
+    const uint64_t stride = (uint64_t)gridDim.x * (blockDim.x >> 3);
+    const float thr = p.thr[q];
+    const uint64_t* al = p.allow ? p.allow + (p.allow_stride ? (uint64_t)q * p.allow_stride : 0) : nullptr;
+    for (uint64_t r = grp; r < p.N; r += stride) {
+        const float d = exact_dist_group8<METRIC>(qv, p.X + r * p.ldx, p.D, g);
+        if (g == 0 && d <= thr) {
+            bool ok = true;
+            if (p.tomb) ok = !bit_test(p.tomb, p.tomb_nbits, r);
+            if (al && ok) ok = bit_test(al, p.allow_nbits, r);
+            if (ok) {
+                const uint32_t pos = atomicAdd(&p.cand_n[f], 1u);
+                if (pos < FB_CAP) {
+                    p.cand_d[(size_t)f * FB_CAP + pos] = d;
+                    p.cand_id[(size_t)f * FB_CAP + pos] = (uint32_t)r;
+                }
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void wv_fbd_filter_kernel(FbParams p) {
+    extern __shared__ float qv[];
+    const int nf = *p.d_nf;
+    const int dpad = (p.D + 3) & ~3;
+    for (int f = 0; f < nf; ++f) {
+        const int q = p.qidx[f];
+        for (int i = threadIdx.x; i < dpad; i += blockDim.x) qv[i] = i < p.D ? p.Q[(size_t)q * p.ldq + i] : 0.f;
+        __syncthreads();
+        if (p.metric == WV_METRIC_L2) fbd_filter_one<WV_METRIC_L2>(p, qv, f, q);
+        else if (p.metric == WV_METRIC_DOT) fbd_filter_one<WV_METRIC_DOT>(p, qv, f, q);
+        else fbd_filter_one<WV_METRIC_COSINE>(p, qv, f, q);
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(1024) void wv_fbd_select_kernel(FbParams p) {
+    __shared__ float sd[FB_CAP];
+    __shared__ uint32_t si[FB_CAP];
+    const int nf = *p.d_nf;
+    for (int f = blockIdx.x; f < nf; f += gridDim.x) {
+        const uint32_t n_all = p.cand_n[f];
+        const int n = (int)(n_all < (uint32_t)FB_CAP ? n_all : (uint32_t)FB_CAP);
+        int len = 1;
+        while (len < n) len <<= 1;
+        for (int i = threadIdx.x; i < len; i += blockDim.x) {
+            sd[i] = i < n ? p.cand_d[(size_t)f * FB_CAP + i] : __builtin_inff();
+            si[i] = i < n ? p.cand_id[(size_t)f * FB_CAP + i] : WV_NIL;
+        }
+        __syncthreads();
+        bitonic_sort_lds(sd, si, len);
+        const int q = p.qidx[f];
+        const bool over = n_all > (uint32_t)FB_CAP;
+        if (!over) {
+            const int m = n < p.k ? n : p.k;
+            for (int i = threadIdx.x; i < m; i += blockDim.x) {
+                p.out_ids[(size_t)q * p.k + i] = p.id_base + si[i];
+                p.out_d[(size_t)q * p.k + i] = sd[i];
+            }
+            if (threadIdx.x == 0) p.out_n[q] = m;
+        }
+        if (threadIdx.x == 0) p.overflow[f] = over ? 1 : 0;
+        __syncthreads();
+    }
+}
+
+__device__ __forceinline__ uint32_t fkey(float d) {   // order-preserving (d1 < d2 <=> key1 < key2)
+    const uint32_t b = __float_as_uint(d);
+    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float fkey_inv(uint32_t k) {
+    return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
+}
+
+template <int METRIC>
+__device__ void fbd_scan_slot(const FbParams& p, const float* qv, int q, uint32_t* sk) {
+    const int g = threadIdx.x & 7;
+    const uint64_t* al = p.allow ? p.allow + (p.allow_stride ? (uint64_t)q * p.allow_stride : 0) : nullptr;
+    for (uint64_t r = threadIdx.x >> 3; r < p.N; r += blockDim.x >> 3) {
+        const float d = exact_dist_group8<METRIC>(qv, p.X + r * p.ldx, p.D, g);
+        if (g == 0) {
+            bool ok = true;
+            if (p.tomb) ok = !bit_test(p.tomb, p.tomb_nbits, r);
+            if (al && ok) ok = bit_test(al, p.allow_nbits, r);
+            sk[r] = ok ? fkey(d) : 0xFFFFFFFFu;
+        }
+    }
+}
+
+constexpr int FBD_K = 256;   // largest k the full-scan slot collects (BF_WIDE_KMAX)
+
+__global__ __launch_bounds__(256) void wv_fbd_full_kernel(FbParams p) {
+    extern __shared__ float qv[];
+    __shared__ uint32_t hist[256];
+    __shared__ float od[FBD_K];
+    __shared__ uint32_t oi[FBD_K];
+    __shared__ uint32_t s_T, s_need, s_n, s_eq_base;
+    __shared__ int wsum[4];
+    const int nf = *p.d_nf;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int dpad = (p.D + 3) & ~3;
+    uint32_t* sk = reinterpret_cast<uint32_t*>(p.scratch) + (size_t)blockIdx.x * p.N;
+    const uint32_t INFK = fkey(__builtin_inff());
+    const int k = p.k < FBD_K ? p.k : FBD_K;
+    for (int f = blockIdx.x; f < nf; f += gridDim.x) {
+        if (!p.overflow[f]) continue;
+        const int q = p.qidx[f];
+        for (int i = tid; i < dpad; i += blockDim.x) qv[i] = i < p.D ? p.Q[(size_t)q * p.ldq + i] : 0.f;
+        __syncthreads();
+        if (p.metric == WV_METRIC_L2) fbd_scan_slot<WV_METRIC_L2>(p, qv, q, sk);
+        else if (p.metric == WV_METRIC_DOT) fbd_scan_slot<WV_METRIC_DOT>(p, qv, q, sk);
+        else fbd_scan_slot<WV_METRIC_COSINE>(p, qv, q, sk);
+        __syncthreads();
+        // eligible rows (finite distance, as exact_full keeps)
+        uint32_t c = 0;
+        for (uint64_t r = tid; r < p.N; r += blockDim.x) c += sk[r] < INFK;
+        for (int m = 32; m >= 1; m >>= 1) c += __shfl_xor(c, m, 64);
+        if (lane == 0) wsum[w] = (int)c;
+        __syncthreads();
+        const uint32_t n_el = (uint32_t)(wsum[0] + wsum[1] + wsum[2] + wsum[3]);
+        __syncthreads();
+        // T = the k-th smallest key (radix select, 8 bits per pass); need =
+        // how many rows equal to T belong to the top k (the smallest ids)
+        if (tid == 0) { s_T = INFK; s_need = 0; s_n = 0; s_eq_base = 0; }
+        if (n_el > (uint32_t)k) {
+            uint32_t prefix = 0, pmask = 0, kk = (uint32_t)k;
+            for (int shift = 24; shift >= 0; shift -= 8) {
+                hist[tid] = 0;
+                __syncthreads();
+                for (uint64_t r = tid; r < p.N; r += blockDim.x) {
+                    const uint32_t v = sk[r];
+                    if ((v & pmask) == prefix) atomicAdd(&hist[(v >> shift) & 255u], 1u);
+                }
+                __syncthreads();
+                if (tid == 0) {
+                    uint32_t cum = 0, b = 0;
+                    for (; b < 256; ++b) {
+                        if (cum + hist[b] >= kk) break;
+                        cum += hist[b];
+                    }
+                    s_need = kk - cum;
+                    s_T = prefix | (b << shift);
+                }
+                __syncthreads();
+                kk = s_need;
+                prefix = s_T;
+                pmask |= 255u << shift;
+                __syncthreads();
+            }
+        }
+        __syncthreads();
+        const uint32_t T = s_T, need = s_need;
+        // ordered collection: every key < T, and the first `need` keys == T
+        for (uint64_t c0 = 0; c0 < p.N; c0 += blockDim.x) {
+            const uint64_t r = c0 + tid;
+            const uint32_t v = r < p.N ? sk[r] : 0xFFFFFFFFu;
+            const bool lt = v < T && v < INFK;
+            const bool eq = v == T && T < INFK;
+            if (lt) {
+                const uint32_t pos = atomicAdd(&s_n, 1u);
+                if (pos < (uint32_t)FBD_K) { od[pos] = fkey_inv(v); oi[pos] = (uint32_t)r; }
+            }
+            const uint64_t b = __ballot(eq);
+            if (lane == 0) wsum[w] = __popcll(b);
+            __syncthreads();
+            uint32_t rank = s_eq_base + __popcll(b & ((1ull << lane) - 1ull));
+            for (int i = 0; i < w; ++i) rank += (uint32_t)wsum[i];
+            if (eq && rank < need) {
+                const uint32_t pos = atomicAdd(&s_n, 1u);
+                if (pos < (uint32_t)FBD_K) { od[pos] = fkey_inv(v); oi[pos] = (uint32_t)r; }
+            }
+            __syncthreads();
+            if (tid == 0) s_eq_base += (uint32_t)(wsum[0] + wsum[1] + wsum[2] + wsum[3]);
+            __syncthreads();
+        }
+        const int n = (int)(s_n < (uint32_t)k ? s_n : (uint32_t)k);
+        int len = 1;
+        while (len < n) len <<= 1;
+        for (int i = n + tid; i < len; i += blockDim.x) { od[i] = __builtin_inff(); oi[i] = WV_NIL; }
+        __syncthreads();
+        bitonic_sort_lds(od, oi, len);
+        for (int i = tid; i < n; i += blockDim.x) {
+            p.out_ids[(size_t)q * p.k + i] = p.id_base + oi[i];
+            p.out_d[(size_t)q * p.k + i] = od[i];
+        }
+        if (tid == 0) p.out_n[q] = n;
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
 // |x|^2 (fp32, any order: only feeds the approximate distance) and max |x|.
 __global__ void wv_rownorm_kernel(const float* X, uint64_t N, int D, int ldx, float* norm2,
                                   unsigned int* max_norm_bits) {
@@ -1711,6 +1971,39 @@ hipError_t wv_launch_fb(const wv::FbParams* p, hipStream_t s) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(wv::wv_fb_select_kernel, dim3(p->nf), dim3(1024), 0, s, *p);
+    return hipGetLastError();
+}
+
+// the device fallback over `flags` [nq]: fb->qidx / d_nf / overflow / cand_* /
+// scratch are [nq]-sized device buffers; flags and fb->thr are read on the device
+hipError_t wv_launch_fbd(const int32_t* flags, int nq, const wv::FbParams* fb, hipStream_t s) {
+    if (nq == 0) return hipSuccess;
+    if (fb->k < 1 || fb->k > wv::FBD_K || !fb->d_nf || !fb->scratch || fb->n_scr < 1) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(wv::wv_fbd_compact_kernel, dim3(1), dim3(1024), 0, s, flags, nq, const_cast<int32_t*>(fb->qidx),
+                       const_cast<int32_t*>(fb->d_nf), fb->fb_total);
+    hipError_t e = hipMemsetAsync(fb->cand_n, 0, (size_t)nq * 4, s);
+    if (e != hipSuccess) return e;
+    uint64_t blocks = (fb->N + 255) / 256;
+    if (blocks > 512) blocks = 512;
+    if (blocks == 0) blocks = 1;
+    const size_t lds = ((fb->D + 3) & ~3) * sizeof(float);
+    hipLaunchKernelGGL(wv::wv_fbd_filter_kernel, dim3((unsigned)blocks), dim3(256), lds, s, *fb);
+    hipLaunchKernelGGL(wv::wv_fbd_select_kernel, dim3(64), dim3(1024), 0, s, *fb);
+    hipLaunchKernelGGL(wv::wv_fbd_full_kernel, dim3(fb->n_scr), dim3(256), lds, s, *fb);
+    return hipGetLastError();
+}
+
+hipError_t wv_launch_hnsw_stats(const uint32_t* counters, int nq, unsigned long long* acc, hipStream_t s) {
+    if (nq == 0) return hipSuccess;
+    unsigned blocks = (unsigned)((nq + 255) / 256);
+    if (blocks > 64) blocks = 64;
+    hipLaunchKernelGGL(wv::wv_hnsw_stats_kernel, dim3(blocks), dim3(256), 0, s, counters, nq, acc);
+    return hipGetLastError();
+}
+
+hipError_t wv_launch_fbd_mark(const int32_t* status, int nq, int32_t* flags, float* thr, hipStream_t s) {
+    if (nq == 0) return hipSuccess;
+    hipLaunchKernelGGL(wv::wv_fbd_mark_kernel, dim3((nq + 255) / 256), dim3(256), 0, s, status, nq, flags, thr);
     return hipGetLastError();
 }
 

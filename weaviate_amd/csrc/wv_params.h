@@ -195,7 +195,16 @@ struct FbParams {
     float* out_d;
     int32_t* out_n;
     int32_t* overflow;       // [nf] 1 = more than FB_CAP survivors
+    // device-resolved fallback (no host round trip): the failed queries are
+    // listed on the device (qidx, *d_nf <= nf); the filter / select kernels
+    // loop over them, and an overflowed query is answered by a full scan into
+    // scratch[slot][N] plus a radix select (fbd kernels, wv_bf.hip)
+    const int32_t* d_nf;
+    float* scratch;
+    int n_scr;
+    unsigned long long* fb_total;   // += number of listed queries (batch stats; nullable)
 };
+constexpr int FBD_SCR = 8;   // full-scan slots of the device fallback
 
 struct ScanParams {
     const float* X;

@@ -315,11 +315,16 @@ class GPUVectorIndex:
     def search_batch_device(self, q_ptr: int, nq: int, k: int, out_ids_ptr: int, out_d_ptr: int, out_n_ptr: int,
                             ef: int = 0, allow_ptr: int = 0, allow_nbits: int = 0, allow_stride: int = 0,
                             mode: str = "exact", stream: int = 0):
-        """Device-resident batch (pointers from torch tensors on this device)."""
+        """Device-resident batch (pointers from torch tensors on this device),
+        queued on `stream` without a host round trip.  stream 0 (torch's
+        default stream) queues on the index's own stream and then waits for
+        it, so that default-stream callers read complete results."""
         check(lib().wv_search_batch_device(self._h, C.c_void_p(q_ptr), nq, k, ef,
                                            C.c_void_p(allow_ptr) if allow_ptr else None, allow_nbits, allow_stride,
                                            _MODES[mode], C.c_void_p(out_ids_ptr), C.c_void_p(out_d_ptr),
                                            C.c_void_p(out_n_ptr), C.c_void_p(stream) if stream else None))
+        if not stream:
+            check(lib().wv_index_synchronize(self._h))
 
     def set_timing(self, enable: bool = True):
         check(lib().wv_index_set_timing(self._h, int(enable)))
