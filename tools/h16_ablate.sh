@@ -6,7 +6,7 @@ set -e
 B=build/h16; mkdir -p $B
 C=weaviate_amd/csrc
 HF="-O3 -std=c++17 --offload-arch=gfx950 -fPIC -ffp-contract=off"
-VARIANTS=${VARIANTS:-"base= nomin=-DWV_H16_ABLATE_NO_EXTRACT:-DWV_H16_ABLATE_NO_MIN pure=-DWV_H16_ABLATE_NO_EXTRACT:-DWV_H16_ABLATE_NO_MIN:-DWV_H16_ABLATE_NO_BARRIER:-DWV_H16_ABLATE_NO_FILL pure_nolds=-DWV_H16_ABLATE_NO_EXTRACT:-DWV_H16_ABLATE_NO_MIN:-DWV_H16_ABLATE_NO_BARRIER:-DWV_H16_ABLATE_NO_FILL:-DWV_H16_ABLATE_NO_LDS nomin_nolds=-DWV_H16_ABLATE_NO_EXTRACT:-DWV_H16_ABLATE_NO_MIN:-DWV_H16_ABLATE_NO_LDS"}
+VARIANTS=${VARIANTS:-"base= noext=-DWV_H16_ABLATE_NO_EXTRACT pure=-DWV_H16_ABLATE_NO_EXTRACT:-DWV_H16_ABLATE_NO_MIN:-DWV_H16_ABLATE_NO_BARRIER:-DWV_H16_ABLATE_NO_FILL"}
 if [ "$1" == "build" ]; then
   make -s -C $C ARCH=gfx950
   /opt/rocm/bin/hipcc $HF -x hip -c tools/h16_ablate.cpp -o $B/main.o
@@ -15,7 +15,7 @@ if [ "$1" == "build" ]; then
     name=${v%%=*}; defs=${v#*=}; defs=${defs//:/ }
     /opt/rocm/bin/hipcc $HF -fno-honor-nans $defs -c $C/wv_h16.hip -o $B/h16_$name.o
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -pthread $B/main.o $B/h16_$name.o $C/wv_bf.o $C/wv_hnsw.o $C/wv_pq.o \
-        $C/wv_api.o $C/wv_batcher.o $C/wv_commitlog.o -o $B/abl_$name
+        $C/wv_api.o $C/wv_batcher.o $C/wv_commitlog.o $C/wv_group.o -L/opt/rocm/lib -lrccl -o $B/abl_$name
   done
   exit 0
 fi
@@ -24,3 +24,4 @@ for f in $B/abl_*; do
   timeout -k 5 120 $f ${N:-1000000} ${NQ:-10000} ${D:-128} ${f##*/abl_}
 done
 WV_H16_NO_SEED=1 timeout -k 5 120 $B/abl_base ${N:-1000000} ${NQ:-10000} ${D:-128} base_noseed
+WV_H16_NO_RUNNING=1 timeout -k 5 120 $B/abl_base ${N:-1000000} ${NQ:-10000} ${D:-128} base_norunning

@@ -55,6 +55,10 @@ hipError_t wv_launch_h16_qscale(const unsigned int* max_bits, float bsign, float
 hipError_t wv_launch_h16_xns(const float* xnorm, uint64_t n, float sx, const float* qscale, float* xns, hipStream_t s);
 hipError_t wv_launch_bf_h16(const wv::H16Params* p, int ns, int seed, hipStream_t s);
 hipError_t wv_launch_h16_seed(const wv::H16SeedParams* p, hipStream_t s);
+hipError_t wv_launch_h16_margin(int metric, int D, const float* qnorm, const float* qres, float xnorm_max,
+                                float ex_max, float sx, const float* qscale, int nq, float* marg, hipStream_t s);
+hipError_t wv_launch_h16_gtau(const unsigned int* gtau, int nq, float sx, const float* qscale, float* tau,
+                              hipStream_t s);
 float wv_h16_pow2_scale(float maxabs);
 hipError_t wv_launch_pq_topk(const float* skey, const uint32_t* sval, const float* dist, const uint32_t* rows,
                              uint64_t nr, int q0, int nqc, int k, uint64_t id_base, uint64_t* out_ids, float* out_d,
@@ -222,7 +226,7 @@ struct wv_index {
     bool use_h16 = false;
     int h16_ns = 0;
     float h16_sx = 0.f, h16_ex = 0.f;
-    DevBuf ximg16, xns, qimg16, qres, qmax, qscale, tau, allow_pad, ex_bits;
+    DevBuf ximg16, xns, qimg16, qres, qmax, qscale, tau, gtau, marg, allow_pad, ex_bits;
     float maxnorm_host = 0.f;   // max |x| (rounded up), cached after every row write
     DevBuf xnorm;           // [capacity]
     DevBuf maxnorm;         // unsigned bits of max |x|
@@ -490,6 +494,7 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     HIP_TRY(ix->qimg16.ensure(qbytes));
     HIP_TRY(ix->qres.ensure((size_t)nq * 4));
     HIP_TRY(ix->tau.ensure((size_t)nq * 4));
+    HIP_TRY(ix->gtau.ensure((size_t)nq * 4));
     HIP_TRY(ix->q_nrm2.ensure((size_t)nq * 4));
     HIP_TRY(ix->fail.ensure((size_t)nq * 4));
     HIP_TRY(ix->fail_thr.ensure((size_t)nq * 4));
@@ -585,6 +590,7 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
         sp.ex_max = ix->h16_ex;
         sp.qres = ix->qres.as<float>();
         sp.tau = ix->tau.as<float>();
+        sp.gtau = ix->gtau.as<unsigned int>();
         HIP_TRY(wv_launch_h16_seed(&sp, s));
         TREC(7);
     }
@@ -597,7 +603,21 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     hp.units_per_block = sch.units_per_block;
     hp.n_slots = sch.n_slots;
     hp.tile_stride = 1;
-    hp.tau = seed ? ix->tau.as<float>() : nullptr;
+    hp.tau = nullptr;
+    // the running threshold (k <= 2 BF_KP), started at the seed's
+    if (!seed) HIP_TRY(hipMemsetAsync(ix->gtau.p, 0xFF, (size_t)nq * 4, s));
+    hp.gtau = ix->gtau.as<unsigned int>();
+    // (with the seed's threshold the running one only adds work: measured
+    // 3.048 vs 3.092 ms per 1M x 10k key pass; without a seed -- corpora below
+    // 64 * H_SAMPLE tiles -- it cuts the pass 4.13 -> 3.43 ms at 1M)
+    hp.kth = k <= 2 * wv::BF_KP && !seed && !std::getenv("WV_H16_NO_RUNNING") ? k : 0;
+    if (hp.kth) {
+        HIP_TRY(ix->marg.ensure((size_t)nq * 4));
+        HIP_TRY(wv_launch_h16_margin(ix->metric, ix->dim, ix->q_nrm2.as<float>(), ix->qres.as<float>(),
+                                     ix->maxnorm_host, ix->h16_ex, ix->h16_sx, ix->qscale.as<float>(), nq,
+                                     ix->marg.as<float>(), s));
+        hp.marg = ix->marg.as<float>();
+    }
     hp.out_d = ix->cand_d.as<float>();
     hp.out_id = ix->cand_id.as<uint32_t>();
     TREC(0);
@@ -608,7 +628,9 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     fp.n_slots = sch.n_slots;
     fp.ntiles = sch.ntiles;
     fp.units_per_block = sch.units_per_block;
-    fp.tau_in = hp.tau;
+    HIP_TRY(wv_launch_h16_gtau(ix->gtau.as<unsigned int>(), nq, ix->h16_sx, ix->qscale.as<float>(), ix->tau.as<float>(),
+                               s));
+    fp.tau_in = ix->tau.as<float>();
     TREC(2);
     HIP_TRY(wide ? wv_launch_bf_finalize_wide(&fp, s) : wv_launch_bf_finalize(&fp, s));
     TREC(3);
@@ -658,6 +680,7 @@ int queue_fbd(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
     bp.scratch = ix->fbd_scr.as<float>();
     bp.n_scr = wv::FBD_SCR;
     bp.fb_total = ix->stat_acc.as<unsigned long long>() + 2;
+    if (std::getenv("WV_ABLATE_NO_FALLBACK")) return WV_OK;   // kernel ablations only
     HIP_TRY(wv_launch_fbd(ix->fail.as<int32_t>(), nq, &bp, s));
     return WV_OK;
 }
@@ -1328,7 +1351,7 @@ int wv_index_destroy(wv_index* ix) {
                       &ix->out_ids, &ix->out_d, &ix->out_n, &ix->stage, &ix->fail_thr, &ix->fb_idx, &ix->fb_d, &ix->fb_i, &ix->fb_n, &ix->fb_of,
                       &ix->ac_cnt, &ix->ac_off, &ix->rowidx, &ix->pq_cent, &ix->pq_codes, &ix->pk_key,
                       &ix->pk_dist, &ix->pk_val, &ix->pk_skey, &ix->pk_sval, &ix->pk_off, &ix->ximg16, &ix->xns,
-                      &ix->qimg16, &ix->qres, &ix->qmax, &ix->qscale, &ix->tau, &ix->allow_pad, &ix->ex_bits,
+                      &ix->qimg16, &ix->qres, &ix->qmax, &ix->qscale, &ix->tau, &ix->gtau, &ix->marg, &ix->allow_pad, &ix->ex_bits,
                       &ix->delta, &ix->dmask, &ix->dl_ids, &ix->dl_d, &ix->dl_n, &ix->dq_tmp, &ix->b_tgt, &ix->b_ci,
                       &ix->b_cd, &ix->b_cn, &ix->b_cnt0, &ix->b_cntu, &ix->b_rk, &ix->b_rn, &ix->b_rk2, &ix->b_rn2,
                       &ix->b_uk, &ix->b_ul, &ix->b_uo, &ix->b_nr, &ix->b_tmp, &ix->stat_acc, &ix->fbd_list,

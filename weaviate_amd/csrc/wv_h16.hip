@@ -166,15 +166,24 @@ __global__ __launch_bounds__(512, 2) void wv_bf_h16_kernel(H16Params p) {
             }
         }
         float tau0 = FLT_MAX, tau1 = FLT_MAX;
-        if (p.tau) {
+        if (!SEED && p.gtau) {
+            if (jq0 < p.nq) tau0 = fminf(FLT_MAX, h16_key_dec(p.gtau[jq0]));
+            if (jq1 < p.nq) tau1 = fminf(FLT_MAX, h16_key_dec(p.gtau[jq1]));
+        } else if (p.tau) {
             if (jq0 < p.nq) tau0 = fminf(FLT_MAX, p.tau[jq0] * s);
             if (jq1 < p.nq) tau1 = fminf(FLT_MAX, p.tau[jq1] * s);
+        }
+        // the running threshold's margin: 2 eps (scaled) + the rounding of the sum
+        float marg0 = 0.f, marg1 = 0.f;
+        if (!SEED && p.kth) {
+            if (jq0 < p.nq) marg0 = p.marg[jq0];
+            if (jq1 < p.nq) marg1 = p.marg[jq1];
         }
         // consume the ordinary loads here, before any LDS-DMA is in flight:
         // the compiler's wait for them is then not a wait for the tile stream
 #pragma unroll
         for (int st = 0; st < NS; ++st) asm volatile("" ::"v"(bq0[st].x), "v"(bq1[st].x));
-        asm volatile("" ::"v"(tau0), "v"(tau1));
+        asm volatile("" ::"v"(tau0), "v"(tau1), "v"(marg0), "v"(marg1));
         float l0d[BF_KP], l1d[BF_KP];
         uint32_t l0i[BF_KP], l1i[BF_KP];
 #pragma unroll
@@ -244,17 +253,17 @@ __global__ __launch_bounds__(512, 2) void wv_bf_h16_kernel(H16Params p) {
         };
         // eligibility of a tile's 64 rows for this lane's two columns (bits of
         // rows 4 khalf + ..., low word: rows 0-31, high word: rows 32-63)
-        auto tile_ok = [&](const uint4* img, uint64_t t, uint64_t& o0, uint64_t& o1) -> bool {
+        // (the lane-dependent shifts happen only when a tile needs the mask)
+        auto tile_ok = [&](const uint4* img, uint64_t t, uint64_t& okw) -> bool {
             const uint32_t* w = reinterpret_cast<const uint32_t*>(img + St::IMG_U4 + 16);
             const uint64_t ex = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
             const uint64_t al = has_allow ? ((uint64_t)w[2] | ((uint64_t)w[3] << 32)) : ~0ull;
-            uint64_t okw = ~ex & al;
+            okw = ~ex & al;
             const uint64_t row0 = t * (uint64_t)p.tile_stride * H_BN;
             if (row0 + H_BN > p.N) okw &= p.N > row0 ? ((1ull << (p.N - row0)) - 1) : 0ull;
-            o0 = (jq0 < p.nq ? okw : 0ull) >> (4 * khalf);
-            o1 = (jq1 < p.nq ? okw : 0ull) >> (4 * khalf);
             return okw != ~0ull || (qb + 1) * H_BQ > p.nq;
         };
+        auto lane_ok = [&](uint64_t okw, int jq) -> uint64_t { return (jq < p.nq ? okw : 0ull) >> (4 * khalf); };
         // mask a half's ineligible rows to +inf (rows (r & 3) + 8 (r >> 2) of its 32)
         auto mask_half = [&](floatx16& A, floatx16& B, uint32_t oa, uint32_t ob) {
             constexpr uint32_t LANE_ROWS = 0x0F0F0F0Fu;
@@ -278,8 +287,47 @@ __global__ __launch_bounds__(512, 2) void wv_bf_h16_kernel(H16Params p) {
             return fminf(fminf(m0, m1), fminf(m2, m3));
         };
 
-        uint64_t o0 = 0, o1 = 0;
+        uint64_t okw = 0;
         bool need_mask = false;
+        // extraction thresholds: min(partner's list tail, running threshold),
+        // refreshed only when a list or the threshold changed
+        float pt0 = 0.f, pt1 = 0.f;
+        auto refresh_pt = [&] {
+            pt0 = fminf(__shfl_xor(l0d[BF_KP - 1], 32, 64), tau0);
+            pt1 = fminf(__shfl_xor(l1d[BF_KP - 1], 32, 64), tau1);
+        };
+        refresh_pt();
+        // running threshold: k of the pair's list entries bound the k-th key
+        // (ia from this lane's list, ib from the partner's), + 2 eps
+        // (the lists pass through a per-lane LDS scratch after the stages:
+        // a uniform index into register arrays would hold one mask per entry
+        // in SGPRs for the whole loop)
+        const int ia = (p.kth + 1) >> 1, ib = p.kth >> 1;
+        float* scr_all = reinterpret_cast<float*>(lds + H_STAGES * H_TPS * St::U4);
+        float* scr = scr_all + (wave * 64 + lane) * (2 * BF_KP);
+        const float* pscr = scr_all + (wave * 64 + (lane ^ 32)) * (2 * BF_KP);
+        auto publish = [&] {
+#pragma unroll
+            for (int i = 0; i < BF_KP; ++i) { scr[i] = l0d[i]; scr[BF_KP + i] = l1d[i]; }
+            const float a0 = ia > 0 ? scr[ia - 1] : -FLT_MAX, a1 = ia > 0 ? scr[BF_KP + ia - 1] : -FLT_MAX;
+            const float b0 = ib > 0 ? pscr[ib - 1] : -FLT_MAX, b1 = ib > 0 ? pscr[BF_KP + ib - 1] : -FLT_MAX;
+            const float k0 = fmaxf(a0, b0), k1 = fmaxf(a1, b1);
+            if (khalf == 0) {
+                const float u4 = 4.f * 5.9604645e-08f;
+                if (jq0 < p.nq && k0 < FLT_MAX) {
+                    const float t = k0 + marg0;
+                    atomicMin(&p.gtau[jq0], h16_key_enc(t + u4 * (fabsf(k0) + marg0)));
+                }
+                if (jq1 < p.nq && k1 < FLT_MAX) {
+                    const float t = k1 + marg1;
+                    atomicMin(&p.gtau[jq1], h16_key_enc(t + u4 * (fabsf(k1) + marg1)));
+                }
+            }
+            if (jq0 < p.nq) tau0 = fminf(tau0, h16_key_dec(__atomic_load_n(&p.gtau[jq0], __ATOMIC_RELAXED)));
+            if (jq1 < p.nq) tau1 = fminf(tau1, h16_key_dec(__atomic_load_n(&p.gtau[jq1], __ATOMIC_RELAXED)));
+            refresh_pt();
+        };
+        const bool running = !SEED && p.kth > 0 && p.gtau != nullptr;
         const int ngroups = (ntile + H_TPS - 1) / H_TPS;
         // (the previous segment ended with every stage read and every DMA landed)
         int ops_in_flight = 0;   // this wave's DMA ops of the newest group issued
@@ -289,7 +337,7 @@ __global__ __launch_bounds__(512, 2) void wv_bf_h16_kernel(H16Params p) {
         block_barrier();          // everyone's
         if (ntile > 0) {
             mfma_half(tile_lds(0), 0, acc00, acc01, [] {});
-            need_mask = tile_ok(tile_lds(0), t_begin, o0, o1);
+            need_mask = tile_ok(tile_lds(0), t_begin, okw);
         }
         for (int t = 0; t < ntile; ++t) {
             const int g = t / H_TPS;
@@ -301,10 +349,9 @@ __global__ __launch_bounds__(512, 2) void wv_bf_h16_kernel(H16Params p) {
             const uint4* img = tile_lds(t);
             const uint32_t rb0 = (uint32_t)((t_begin + t) * (uint64_t)p.tile_stride * H_BN) + 4 * khalf;
             // lanes l and l ^ 32 keep lists for the same query column (see the split pass)
-            const float pt0 = fminf(__shfl_xor(l0d[BF_KP - 1], 32, 64), tau0);
-            const float pt1 = fminf(__shfl_xor(l1d[BF_KP - 1], 32, 64), tau1);
             const bool mask_t = need_mask;
-            const uint64_t mo0 = o0, mo1 = o1;
+            const uint64_t mo0 = mask_t ? lane_ok(okw, jq0) : 0ull, mo1 = mask_t ? lane_ok(okw, jq1) : 0ull;
+            bool grew = false;   // a list of this wave changed: thresholds to refresh
             // ---- A: H1(t) MFMAs, H0(t) minima ----
             if (mask_t) mask_half(acc00, acc01, (uint32_t)mo0, (uint32_t)mo1);
             float m0, m1;
@@ -317,8 +364,10 @@ __global__ __launch_bounds__(512, 2) void wv_bf_h16_kernel(H16Params p) {
 #ifdef WV_H16_ABLATE_NO_EXTRACT
                 if (m0 == 1234.5f) l0d[0] = m1 + pt0 + pt1;
 #else
-                split_extract16(m0, acc00, l0d, l0i, pt0, rb0);
-                split_extract16(m1, acc01, l1d, l1i, pt1, rb0);
+                const bool x0 = m0 <= fminf(l0d[BF_KP - 1], pt0), x1 = m1 <= fminf(l1d[BF_KP - 1], pt1);
+                if (x0) split_extract16(m0, acc00, l0d, l0i, pt0, rb0);
+                if (x1) split_extract16(m1, acc01, l1d, l1i, pt1, rb0);
+                grew = __any(x0 || x1);
 #endif
             }
             // ---- C (last tile of a group): group g + 1 has landed (g + 2 may
@@ -331,7 +380,7 @@ __global__ __launch_bounds__(512, 2) void wv_bf_h16_kernel(H16Params p) {
             if (mask_t) mask_half(acc10, acc11, (uint32_t)(mo0 >> 32), (uint32_t)(mo1 >> 32));
             if (t + 1 < ntile) {
                 mfma_half(tile_lds(t + 1), 0, acc00, acc01, [&] { m0 = min16(acc10); m1 = min16(acc11); });
-                need_mask = tile_ok(tile_lds(t + 1), t_begin + t + 1, o0, o1);
+                need_mask = tile_ok(tile_lds(t + 1), t_begin + t + 1, okw);
             } else {
                 m0 = min16(acc10);
                 m1 = min16(acc11);
@@ -344,9 +393,13 @@ __global__ __launch_bounds__(512, 2) void wv_bf_h16_kernel(H16Params p) {
 #ifdef WV_H16_ABLATE_NO_EXTRACT
                 if (m0 == 1234.5f) l0d[0] = m1 + pt0 + pt1;
 #else
-                split_extract16(m0, acc10, l0d, l0i, pt0, rb0 + 32);
-                split_extract16(m1, acc11, l1d, l1i, pt1, rb0 + 32);
+                const bool x0 = m0 <= fminf(l0d[BF_KP - 1], pt0), x1 = m1 <= fminf(l1d[BF_KP - 1], pt1);
+                if (x0) split_extract16(m0, acc10, l0d, l0i, pt0, rb0 + 32);
+                if (x1) split_extract16(m1, acc11, l1d, l1i, pt1, rb0 + 32);
+                grew = __any(x0 || x1) || grew;
 #endif
+                if (running && (t & 15) == 15) publish();
+                else if (grew) refresh_pt();
             }
         }
 
@@ -414,7 +467,22 @@ __global__ __launch_bounds__(64) void wv_h16_seed_kernel(H16SeedParams p) {
             tau += 4.f * 5.9604645e-08f * (fabsf(key) + 2.f * eps) + 1e-3f * eps;   // this sum's rounding
         }
         p.tau[q] = tau;
+        if (p.gtau) p.gtau[q] = h16_key_enc(tau * (p.sx * p.qscale[0]));
     }
+}
+
+// the running threshold's per-query margin: 2 eps in scaled key units
+__global__ void wv_h16_margin_kernel(int metric, int D, const float* qnorm, const float* qres, float xnorm_max,
+                                     float ex_max, float sx, const float* qscale, int nq, float* marg) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < nq) marg[q] = 2.f * (sx * qscale[0]) * h16_eps(metric, D, qnorm[q], xnorm_max, ex_max, qres[q]) * 1.001f;
+}
+
+// the running threshold after the key pass -> true units, for the finalize
+// (every key the pass dropped was above it)
+__global__ void wv_h16_gtau_kernel(const unsigned int* gtau, int nq, float sx, const float* qscale, float* tau) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < nq) tau[q] = h16_key_dec(gtau[q]) * (1.0f / (sx * qscale[0]));
 }
 
 // ---------------------------------------------------------------------------
@@ -531,7 +599,9 @@ hipError_t wv_launch_bf_h16(const wv::H16Params* p, int ns, int seed, hipStream_
         return hipErrorInvalidValue;
     const bool l2 = p->metric == WV_METRIC_L2;
     if (l2 && !p->xns) return hipErrorInvalidValue;
-    const size_t lds = (size_t)wv::H_STAGES * wv::H_TPS * (2 * ns * 64 + 17) * 16;
+    // the stages, then (key pass with a running threshold) the per-lane list scratch
+    const size_t lds = (size_t)wv::H_STAGES * wv::H_TPS * (2 * ns * 64 + 17) * 16 +
+                       (seed ? 0 : (size_t)wv::H_WAVES * 64 * 2 * wv::BF_KP * 4);
 #define WV_H16_LAUNCH(NS)                                                                                      \
     if (seed) {                                                                                                \
         if (l2) hipLaunchKernelGGL((wv::wv_bf_h16_kernel<NS, true, true>), dim3(nb), dim3(512), lds, s, *p);   \
@@ -551,6 +621,21 @@ hipError_t wv_launch_bf_h16(const wv::H16Params* p, int ns, int seed, hipStream_
         default: WV_H16_LAUNCH(8) break;
     }
 #undef WV_H16_LAUNCH
+    return hipGetLastError();
+}
+
+hipError_t wv_launch_h16_gtau(const unsigned int* gtau, int nq, float sx, const float* qscale, float* tau,
+                              hipStream_t s) {
+    if (nq == 0) return hipSuccess;
+    hipLaunchKernelGGL(wv::wv_h16_gtau_kernel, dim3((nq + 255) / 256), dim3(256), 0, s, gtau, nq, sx, qscale, tau);
+    return hipGetLastError();
+}
+
+hipError_t wv_launch_h16_margin(int metric, int D, const float* qnorm, const float* qres, float xnorm_max,
+                                float ex_max, float sx, const float* qscale, int nq, float* marg, hipStream_t s) {
+    if (nq == 0) return hipSuccess;
+    hipLaunchKernelGGL(wv::wv_h16_margin_kernel, dim3((nq + 255) / 256), dim3(256), 0, s, metric, D, qnorm, qres,
+                       xnorm_max, ex_max, sx, qscale, nq, marg);
     return hipGetLastError();
 }
 

@@ -128,7 +128,34 @@ struct H16Params {
     int locality;             // bit 1: XCD-contiguous workgroup ids
     float* out_d;             // [nq][n_slots][H_PROD][BF_KP] scaled keys
     uint32_t* out_id;
+    // running per-query threshold shared by every slot (k <= 2 BF_KP): each
+    // lane pair publishes an upper bound of the query's k-th key (k of its own
+    // list entries) + 2 eps, atomicMin'ed into gtau (order-preserving keys of
+    // scaled units, h16_key_enc); keys above it are dropped everywhere
+    unsigned int* gtau;       // [nq] (nullable)
+    int kth;                  // k (0: no running threshold)
+    const float* marg;        // [nq] 2 eps in scaled key units, rounded up (wv_h16_margin_kernel)
 };
+
+// order-preserving uint keys of floats (a < b <=> enc(a) < enc(b)); +inf and
+// above (0xFF800000..) decode to +inf
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+inline unsigned int h16_key_enc(float f) {
+    union { float f; unsigned int u; } v;
+    v.f = f;
+    return (v.u & 0x80000000u) ? ~v.u : (v.u | 0x80000000u);
+}
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+inline float h16_key_dec(unsigned int k) {
+    if (k >= 0xFF800000u) return __builtin_inff();
+    union { float f; unsigned int u; } v;
+    v.u = (k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k;
+    return v.f;
+}
 
 struct H16SeedParams {
     const float* minima;      // [nq][n_slots][H_PROD] pre-pass running minima (scaled keys)
@@ -141,6 +168,7 @@ struct H16SeedParams {
     float xnorm_max, ex_max;
     const float* qres;
     float* tau;               // [nq] out: threshold in true key units (+inf: none)
+    unsigned int* gtau;       // [nq] out (nullable): h16_key_enc(tau * s), the running threshold's start
 };
 
 struct BfFinParams {
