@@ -260,19 +260,21 @@ def exact_roofline(args, ix, kern_ms, stats, D, n_allowed, n_local, NQ):
     seed_ms = float(np.mean([k.get("seed_ms", 0.0) for k in kern_ms]))
     flops = 2.0 * D * n_allowed * NQ    # algorithmic: 2*D*N_eff per query
     achieved = flops / (mfma_ms * 1e-3) / 1e12
-    # Which key pass ran (wv_api.hip run_exact): the f16 pass (default, D <= 128,
+    # Which key pass ran (wv_api.hip run_exact): the f16 pass (default, D <= 1024;
+    # wv_bf_h16w_kernel above D = 128,
     # one v_mfma_f32_32x32x16_f16 product per fp32 product: peak = the dense
     # f16 MFMA rate), the bf16x3 split pass (WV_BF_SPLIT=1: 3 bf16 products per
     # fp32 product, peak = bf16 dense / 3) or the fp32 MFMA pass (WV_BF_FP32=1,
-    # D > 128, or a shared allow list compacted into a row list).
-    fp32 = bool(os.environ.get("WV_BF_FP32")) or D > 128
+    # D > 1024, or a shared allow list compacted into a row list).
+    fp32 = bool(os.environ.get("WV_BF_FP32")) or D > 1024
     if os.environ.get("WV_BF_SPLIT") and not fp32:
         kind = "split" if 2 * n_allowed >= n_local else "fp32"
     elif not fp32:
         kind = "h16" if 8 * n_allowed >= n_local else "fp32"
     else:
         kind = "fp32"
-    peak, kname, kp = {"h16": (F16_MFMA_PEAK_TF, "wv_bf_h16_kernel", "f16 MFMA keys (peak = f16 dense)"),
+    peak, kname, kp = {"h16": (F16_MFMA_PEAK_TF, "wv_bf_h16_kernel" if D <= 128 else "wv_bf_h16w_kernel",
+                               "f16 MFMA keys (peak = f16 dense)"),
                        "split": (BF16_MFMA_PEAK_TF / 3, "wv_bf_split_kernel", "bf16x3 (peak = bf16 dense / 3)"),
                        "fp32": (FP32_MFMA_PEAK_TF, "wv_bf_mfma_kernel", "fp32 MFMA")}[kind]
     roof = {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 2), "peak": round(peak, 1),

@@ -1,0 +1,74 @@
+"""The f16 key pass for D > 128 (wv_bf_h16w_kernel, -m gpu).
+
+Both operands stream through LDS in 64-k chunks; the epilogue and the
+certificate are those of the D <= 128 pass.  Exact results must equal the CPU
+restatement's flatSearch (oracle/) bit for bit (ties by id), at the C4 shape
+(768-d dot product, BASELINE configs[3]) and at ragged D, with shared allow
+lists, tombstones, k > 32 and corpora that end inside a 128-row tile.
+"""
+import numpy as np
+import pytest
+
+import pyoracle as O
+import weaviate_amd as W
+from helpers import same_tie_aware
+
+pytestmark = pytest.mark.gpu
+NAMES = {O.L2: "l2-squared", O.DOT: "dot", O.COSINE: "cosine-dot"}
+
+
+def _gauss(n, d, seed):
+    rng = np.random.default_rng(seed)
+    return (rng.standard_normal((n, d)) / np.sqrt(d)).astype(np.float32)
+
+
+def _check(ix, base, qs, k, metric, allow_bits=None, allow=None, tomb=None):
+    ids, ds, n = ix.search_batch(qs, k, mode="exact", allow=allow)
+    b = O.normalize_rows(base) if metric == O.COSINE else base
+    q = O.normalize_rows(qs) if metric == O.COSINE else qs
+    oi, od, on = O.flat_scan(metric, b, q, k, allow_bits=allow_bits, tomb_bits=tomb)
+    assert n.tolist() == on.tolist()
+    for i in range(len(qs)):
+        same_tie_aware(ids[i, : n[i]], ds[i, : n[i]], oi[i, : on[i]], od[i, : on[i]])
+    return ix.last_batch_stats()
+
+
+@pytest.mark.parametrize("metric", [O.DOT, O.L2, O.COSINE])
+def test_c4_shape_768_equals_restatement(metric):
+    n, d = 60_000, 768
+    base, qs = _gauss(n, d, 1), _gauss(700, d, 2)
+    ix = W.GPUVectorIndex(d, NAMES[metric], capacity=n)
+    ix.upload_vectors(base)
+    st = _check(ix, base, qs, 10, metric)
+    assert st["fallbacks"] <= 7, st   # the f16 keys certify (nearly) every query
+    ix.close()
+
+
+@pytest.mark.parametrize("d", [129, 200, 256, 300, 1000])
+def test_ragged_wide_dims(d):
+    n = 20_001   # ends inside a 128-row tile
+    rng = np.random.default_rng(d)
+    base = rng.random((n, d), dtype=np.float32)
+    qs = rng.random((300, d), dtype=np.float32)
+    ix = W.GPUVectorIndex(d, "l2-squared", capacity=n)
+    ix.upload_vectors(base)
+    _check(ix, base, qs, 10, O.L2)
+    ix.close()
+
+
+def test_wide_d_allow_list_tombstones_and_large_k():
+    n, d = 40_000, 768
+    base, qs = _gauss(n, d, 3), _gauss(300, d, 4)
+    ix = W.GPUVectorIndex(d, "dot", capacity=n)
+    ix.upload_vectors(base)
+    rng = np.random.default_rng(5)
+    dead = rng.choice(n, 2000, replace=False)
+    ix.add_tombstones(dead)
+    tomb = O.bits_from_ids(dead, n)
+    # 50 %: the whole-corpus pass with the allow mask in the epilogue
+    ids_a = np.nonzero(rng.random(n) < 0.5)[0]
+    al = W.AllowList.from_ids(ids_a, n)
+    _check(ix, base, qs, 10, O.DOT, allow_bits=al.words, allow=al, tomb=tomb)
+    for k in (64, 200):
+        _check(ix, base, qs, k, O.DOT, tomb=tomb)
+    ix.close()

@@ -54,6 +54,7 @@ hipError_t wv_launch_absmax(const float* in, int ld, uint64_t n, int D, unsigned
 hipError_t wv_launch_h16_qscale(const unsigned int* max_bits, float bsign, float* qscale, hipStream_t s);
 hipError_t wv_launch_h16_xns(const float* xnorm, uint64_t n, float sx, const float* qscale, float* xns, hipStream_t s);
 hipError_t wv_launch_bf_h16(const wv::H16Params* p, int ns, int seed, hipStream_t s);
+hipError_t wv_launch_bf_h16w(const wv::H16Params* p, hipStream_t s);
 hipError_t wv_launch_h16_seed(const wv::H16SeedParams* p, hipStream_t s);
 hipError_t wv_launch_h16_margin(int metric, int D, const float* qnorm, const float* qres, float xnorm_max,
                                 float ex_max, float sx, const float* qscale, int nq, float* marg, hipStream_t s);
@@ -224,6 +225,7 @@ struct wv_index {
     // D <= 128): f16(s_x x) in the layout of h16_index; h16_ex = max residual
     // norm |x - f16(s_x x) / s_x| over the rows (rounded up), both host-cached
     bool use_h16 = false;
+    bool h16_wide = false;  // D > 128: wv_bf_h16w_kernel (both operands through LDS, 128-row tiles)
     int h16_ns = 0;
     float h16_sx = 0.f, h16_ex = 0.f;
     DevBuf ximg16, xns, qimg16, qres, qmax, qscale, tau, gtau, marg, allow_pad, ex_bits;
@@ -480,17 +482,21 @@ int run_pq_flat(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d
 int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_allow, uint64_t allow_nbits, uint64_t N,
             uint64_t* d_out_ids, float* d_out_d, int32_t* d_out_n, hipStream_t s, std::vector<int32_t>& fails) {
     const int ns = ix->h16_ns;
-    const uint64_t ntl = (N + wv::H_BN - 1) / wv::H_BN;
+    const bool wd = ix->h16_wide;   // D > 128: the wide-D kernel
+    const int tile_rows = wd ? wv::HW_BN : wv::H_BN, bq = wd ? wv::HW_BQ : wv::H_BQ;
+    const int prod = wd ? wv::HW_PROD : wv::H_PROD;
+    const uint64_t ntl = (N + tile_rows - 1) / tile_rows;
+    const uint64_t words = ntl * (uint64_t)(tile_rows / 64);   // allow words the kernel reads
     const uint64_t* allow = d_allow;
-    if (d_allow && (allow_nbits + 63) / 64 < ntl) {   // the kernel reads one allow word per tile
-        HIP_TRY(ix->allow_pad.ensure(ntl * 8));
-        HIP_TRY(hipMemsetAsync(ix->allow_pad.p, 0, ntl * 8, s));
+    if (d_allow && (allow_nbits + 63) / 64 < words) {
+        HIP_TRY(ix->allow_pad.ensure(words * 8));
+        HIP_TRY(hipMemsetAsync(ix->allow_pad.p, 0, words * 8, s));
         if (allow_nbits)
             HIP_TRY(hipMemcpyAsync(ix->allow_pad.p, d_allow, (allow_nbits + 63) / 64 * 8, hipMemcpyDeviceToDevice, s));
         allow = ix->allow_pad.as<uint64_t>();
     }
-    const int nqb = (nq + wv::H_BQ - 1) / wv::H_BQ;
-    const size_t qbytes = (size_t)nqb * wv::H_BQ * ns * 16 * 2;
+    const int nqb = (nq + bq - 1) / bq;
+    const size_t qbytes = (size_t)nqb * bq * ns * 16 * 2;
     HIP_TRY(ix->qimg16.ensure(qbytes));
     HIP_TRY(ix->qres.ensure((size_t)nq * 4));
     HIP_TRY(ix->tau.ensure((size_t)nq * 4));
@@ -508,7 +514,7 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     HIP_TRY(wv_launch_h16_rows(d_q, ix->dpad, nullptr, nq, ix->dim, ns, bsign, 1.f, ix->qmax.as<unsigned int>(),
                                ix->qimg16.p, 0, nullptr, ix->qres.as<float>(), s));
     if (ix->metric == WV_L2_SQUARED)
-        HIP_TRY(wv_launch_h16_xns(ix->xnorm.as<float>(), ntl * wv::H_BN, ix->h16_sx, ix->qscale.as<float>(),
+        HIP_TRY(wv_launch_h16_xns(ix->xnorm.as<float>(), ntl * tile_rows, ix->h16_sx, ix->qscale.as<float>(),
                                   ix->xns.as<float>(), s));
     wv::H16Params hp{};
     hp.X = ix->ximg16.p;
@@ -541,9 +547,10 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     fp.out_n = d_out_n;
     fp.fail = ix->fail.as<int32_t>();
     fp.fail_thr = ix->fail_thr.as<float>();
-    fp.bq = wv::H_BQ;
-    fp.prod = wv::H_PROD;
+    fp.bq = bq;
+    fp.prod = prod;
     fp.h16 = 1;
+    hp.ns = ns;
     fp.qscale = ix->qscale.as<float>();
     fp.sx = ix->h16_sx;
     fp.ex_max = ix->h16_ex;
@@ -560,7 +567,7 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
         if (wide) t = std::max<uint64_t>(t, (uint64_t)nqb * std::min<uint64_t>(tiles, (uint64_t)k + 2));
         return (int)std::min<uint64_t>(t, 1u << 30);
     };
-    const bool seed = ntl >= 64 * (uint64_t)wv::H_SAMPLE && !std::getenv("WV_H16_NO_SEED");
+    const bool seed = !wd && ntl >= 64 * (uint64_t)wv::H_SAMPLE && !std::getenv("WV_H16_NO_SEED");
     if (seed) {
         const uint64_t nts = (ntl + wv::H_SAMPLE - 1) / wv::H_SAMPLE;
         const wv::BfSchedule ss = wv::bf_schedule(nq, nts * wv::H_BN, target(nts), wv::H_BQ, wv::H_BN);
@@ -594,11 +601,11 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
         HIP_TRY(wv_launch_h16_seed(&sp, s));
         TREC(7);
     }
-    const wv::BfSchedule sch = wv::bf_schedule(nq, N, target(ntl), wv::H_BQ, wv::H_BN);
-    if (wide && (uint64_t)sch.n_slots * wv::H_PROD * wv::BF_KP > (uint64_t)wv::FINW_NE)
+    const wv::BfSchedule sch = wv::bf_schedule(nq, N, target(ntl), bq, tile_rows);
+    if (wide && (uint64_t)sch.n_slots * prod * wv::BF_KP > (uint64_t)wv::FINW_NE)
         return fail(WV_ESTATE, "run_h16: too many lists for the wide finalize");
-    HIP_TRY(ix->cand_d.ensure((size_t)nq * sch.n_slots * wv::H_PROD * wv::BF_KP * 4));
-    HIP_TRY(ix->cand_id.ensure((size_t)nq * sch.n_slots * wv::H_PROD * wv::BF_KP * 4));
+    HIP_TRY(ix->cand_d.ensure((size_t)nq * sch.n_slots * prod * wv::BF_KP * 4));
+    HIP_TRY(ix->cand_id.ensure((size_t)nq * sch.n_slots * prod * wv::BF_KP * 4));
     hp.ntiles = sch.ntiles;
     hp.units_per_block = sch.units_per_block;
     hp.n_slots = sch.n_slots;
@@ -610,7 +617,7 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     // (with the seed's threshold the running one only adds work: measured
     // 3.048 vs 3.092 ms per 1M x 10k key pass; without a seed -- corpora below
     // 64 * H_SAMPLE tiles -- it cuts the pass 4.13 -> 3.43 ms at 1M)
-    hp.kth = k <= 2 * wv::BF_KP && !seed && !std::getenv("WV_H16_NO_RUNNING") ? k : 0;
+    hp.kth = k <= 2 * wv::BF_KP && !seed && !wd && !std::getenv("WV_H16_NO_RUNNING") ? k : 0;
     if (hp.kth) {
         HIP_TRY(ix->marg.ensure((size_t)nq * 4));
         HIP_TRY(wv_launch_h16_margin(ix->metric, ix->dim, ix->q_nrm2.as<float>(), ix->qres.as<float>(),
@@ -621,7 +628,7 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     hp.out_d = ix->cand_d.as<float>();
     hp.out_id = ix->cand_id.as<uint32_t>();
     TREC(0);
-    HIP_TRY(wv_launch_bf_h16(&hp, ns, 0, s));
+    HIP_TRY(wd ? wv_launch_bf_h16w(&hp, s) : wv_launch_bf_h16(&hp, ns, 0, s));
     TREC(1);
     fp.cand_d = ix->cand_d.as<float>();
     fp.cand_id = ix->cand_id.as<uint32_t>();
@@ -1301,7 +1308,7 @@ int wv_index_create(int dim, int metric, const wv_config* cfg, uint64_t capacity
     const size_t vbytes = cap_rows * (size_t)ix->ldx * 4;
     if (ix->vecs.ensure(vbytes) != hipSuccess || ix->xnorm.ensure(cap_rows * 4) != hipSuccess ||
         ix->maxnorm.ensure(4) != hipSuccess || ix->tomb.ensure(ix->bm_words * 8) != hipSuccess ||
-        ix->excl.ensure(ix->bm_words * 8) != hipSuccess) {
+        ix->excl.ensure((ix->bm_words + 2) * 8) != hipSuccess) {   // + the word pair of a last 128-row tile
         wv_index_destroy(ix);
         return fail(WV_EOOM, "wv_index_create: device allocation failed");
     }
@@ -1310,9 +1317,12 @@ int wv_index_create(int dim, int metric, const wv_config* cfg, uint64_t capacity
     // fp32 MFMA pass for every scan
     // f16 key pass (wv_bf_h16_kernel) for D <= 128 unless an ablation switch
     // asks for the bf16x3 (WV_BF_SPLIT=1) or the fp32 (WV_BF_FP32=1) pass
-    ix->use_h16 = dim <= 16 * wv::H_NS_MAX && !std::getenv("WV_BF_FP32") && !std::getenv("WV_BF_SPLIT");
+    ix->use_h16 = dim <= 16 * wv::HW_NS_MAX && !std::getenv("WV_BF_FP32") && !std::getenv("WV_BF_SPLIT") &&
+                  (dim <= 16 * wv::H_NS_MAX || !std::getenv("WV_BF_NO_H16W"));
     if (ix->use_h16) {
-        ix->h16_ns = (dim + 15) / 16;
+        // D > 128: the wide-D kernel, whose chunks are HW_KC 16-k steps
+        ix->h16_wide = dim > 16 * wv::H_NS_MAX;
+        ix->h16_ns = ix->h16_wide ? (dim + 16 * wv::HW_KC - 1) / (16 * wv::HW_KC) * wv::HW_KC : (dim + 15) / 16;
         const size_t ibytes = cap_rows * (size_t)ix->h16_ns * 16 * 2;
         if (ix->ximg16.ensure(ibytes) != hipSuccess || ix->xns.ensure(cap_rows * 4) != hipSuccess ||
             ix->ex_bits.ensure(4) != hipSuccess || ix->qmax.ensure(4) != hipSuccess ||

@@ -59,7 +59,11 @@ __device__ __forceinline__ void vm_wait(int n) {
         case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
         case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
         case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
-        default: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+        case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+        case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
     }
 }
 __device__ __forceinline__ void block_barrier() {
@@ -423,6 +427,201 @@ __global__ __launch_bounds__(512, 2) void wv_bf_h16_kernel(H16Params p) {
 }
 
 // ---------------------------------------------------------------------------
+// f16 key pass for D > 128 (C4's 768-d dot product): both operands through
+// LDS.  Workgroup = 512 threads, one per CU; tile = 128 corpus rows x 256
+// queries; wave w computes rows 64 (w & 1) .. +64 x queries 64 (w >> 1) .. +64
+// (2 x 2 accumulators of 32 x 32).  The corpus and query images are h16_index
+// images with ns 16-k steps (ns a multiple of HW_KC, zero padded), so a chunk
+// (HW_KC steps) of a 32-row group is HW_KC contiguous 1 KiB operand blocks:
+// LDS-DMA'd as is, read back as one ds_read_b128 per operand.  Chunks go
+// through a 3-stage ring (wait for chunk g, barrier, issue chunk g + 2,
+// compute g); per tile a 2-slot ring holds s|x|^2 (the L2 C-in) and the tile's
+// exclusion / allow words.  The epilogue -- mask, minima, candidate
+// extraction into the same per-lane lists as the D <= 128 pass -- runs once
+// per tile, i.e. once per ns / HW_KC chunks.
+struct HWStage {
+    static constexpr int A_U4 = 4 * HW_KC * 64;    // 4 row groups x HW_KC steps x 64 lanes
+    static constexpr int B_U4 = 8 * HW_KC * 64;    // 8 query groups
+    static constexpr int U4 = A_U4 + B_U4;
+    static constexpr int EX_U4 = HW_BN / 4 + 2;    // s|x|^2 of the tile, then excl[2] and allow[2] words
+};
+constexpr int HW_STAGES = 3;
+
+template <bool L2>
+__global__ __launch_bounds__(512, 1) void wv_bf_h16w_kernel(H16Params p) {
+    extern __shared__ uint4 lds[];
+    using St = HWStage;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int khalf = lane >> 5;
+    const int l31 = lane & 31;
+    const int rh = wave & 1, qq = wave >> 1;
+    const int ns = p.ns, nch = ns / HW_KC;
+    const uint4* __restrict__ X = reinterpret_cast<const uint4*>(p.X);
+    const uint4* __restrict__ Qg = reinterpret_cast<const uint4*>(p.Q);
+    const bool has_allow = p.allow != nullptr;
+    int lb = (int)blockIdx.x;
+    if ((p.locality & 1) && gridDim.x >= 8) {
+        const int nwg = (int)gridDim.x, q8 = nwg / 8, r8 = nwg % 8, xcd = (int)blockIdx.x % 8;
+        lb = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (int)blockIdx.x / 8;
+    }
+    const uint64_t u_first = (uint64_t)lb * p.units_per_block;
+    uint64_t u_last = u_first + p.units_per_block;
+    if (u_last > (uint64_t)p.n_qblocks * p.ntiles) u_last = (uint64_t)p.n_qblocks * p.ntiles;
+    const uint32_t lds0 = lds_addr(lds);
+    const uint32_t ex0 = lds0 + (uint32_t)(HW_STAGES * St::U4 * 16);
+    const uint4* ex_lds = lds + HW_STAGES * St::U4;
+
+    for (uint64_t u = u_first; u < u_last;) {
+        const int qb = (int)(u / p.ntiles);
+        const uint64_t t_begin = u % p.ntiles;
+        uint64_t t_end = t_begin + (u_last - u);
+        if (t_end > p.ntiles) t_end = p.ntiles;
+        u += t_end - t_begin;
+        const int slot = lb - bf_first_block(qb, p.ntiles, p.units_per_block);
+        const int jq0 = qb * HW_BQ + qq * 64 + l31;
+        const int jq1 = jq0 + 32;
+        const int ntile = (int)(t_end - t_begin);
+        const int nchunks = ntile * nch;
+
+        // chunk g = (tile t, chunk c) into stage g % 3; with c == 0 also the
+        // tile's extras into slot t & 1.  Returns this wave's DMA op count.
+        auto fill = [&](int g) -> int {
+            const int t = g / nch, c = g % nch;
+            const uint64_t tile = t_begin + t;
+            const uint32_t dst = lds0 + (uint32_t)((g % HW_STAGES) * St::U4 * 16);
+            int n = 0;
+            for (int b = wave; b < (St::A_U4 + St::B_U4) / 64; b += H_WAVES) {
+                const int isb = b >= St::A_U4 / 64;
+                const int bb = isb ? b - St::A_U4 / 64 : b;      // (group, step) block
+                const int grp = bb / HW_KC, st = bb % HW_KC;
+                const uint64_t G = isb ? (uint64_t)qb * (HW_BQ / 32) + grp : tile * (HW_BN / 32) + grp;
+                const uint4* src = (isb ? Qg : X) + ((G * ns + (uint64_t)c * HW_KC + st) * 64 + lane);
+                glds16(src, dst + (uint32_t)(b * 1024));
+                ++n;
+            }
+            if (c == 0) {
+                const uint32_t xd = ex0 + (uint32_t)((t & 1) * St::EX_U4 * 16);
+                if (wave == 0 && L2) {
+                    glds4(p.xns + tile * HW_BN + lane, xd);
+                    glds4(p.xns + tile * HW_BN + 64 + lane, xd + 256);
+                    n += 2;
+                } else if (wave == 1) {
+                    // lanes 0-3: the tile's two exclusion words, 4-7: its two allow words
+                    const uint32_t* w = lane < 4 ? reinterpret_cast<const uint32_t*>(p.excl + 2 * tile) + lane
+                                                 : reinterpret_cast<const uint32_t*>(p.allow + 2 * tile) + (lane - 4);
+                    if (lane < 4 || (lane < 8 && has_allow)) glds4(w, xd + (HW_BN / 4) * 16);
+                    n += 1;
+                }
+            }
+            return n;
+        };
+
+        float l0d[BF_KP], l1d[BF_KP];
+        uint32_t l0i[BF_KP], l1i[BF_KP];
+#pragma unroll
+        for (int i = 0; i < BF_KP; ++i) {
+            l0d[i] = FLT_MAX; l1d[i] = FLT_MAX;
+            l0i[i] = WV_NIL; l1i[i] = WV_NIL;
+        }
+        floatx16 acc00, acc01, acc10, acc11;
+        const float INF = __builtin_inff();
+        auto min16 = [&](const floatx16& A) {
+            float m0 = fminf(fminf(A[0], A[1]), A[2]), m1 = fminf(fminf(A[3], A[4]), A[5]);
+            float m2 = fminf(fminf(A[6], A[7]), A[8]), m3 = fminf(fminf(A[9], A[10]), A[11]);
+            m0 = fminf(fminf(m0, A[12]), A[13]);
+            m1 = fminf(fminf(m1, A[14]), A[15]);
+            return fminf(fminf(m0, m1), fminf(m2, m3));
+        };
+        int ops[HW_STAGES] = {0, 0, 0};
+        // (the previous segment ended with every stage read and every DMA landed)
+        if (nchunks > 0) ops[0] = fill(0);
+        if (nchunks > 1) ops[1] = fill(1);
+        for (int g = 0; g < nchunks; ++g) {
+            const int t = g / nch, c = g % nch;
+            // chunk g landed (g + 1 may stay in flight), for every wave
+            vm_wait(g + 1 < nchunks ? ops[(g + 1) % HW_STAGES] : 0);
+            block_barrier();
+            if (g + 2 < nchunks) ops[(g + 2) % HW_STAGES] = fill(g + 2);
+            const uint4* st = lds + (g % HW_STAGES) * St::U4;
+            if (c == 0) {
+                // C-in: s|x|^2 of the wave's rows (L2) or zero
+                if (L2) {
+                    const float* xn = reinterpret_cast<const float*>(ex_lds + (t & 1) * St::EX_U4) + 64 * rh;
+#pragma unroll
+                    for (int g4 = 0; g4 < 4; ++g4) {
+                        const float4 v0 = *reinterpret_cast<const float4*>(xn + 4 * khalf + 8 * g4);
+                        const float4 v1 = *reinterpret_cast<const float4*>(xn + 32 + 4 * khalf + 8 * g4);
+                        acc00[4 * g4] = v0.x; acc00[4 * g4 + 1] = v0.y; acc00[4 * g4 + 2] = v0.z; acc00[4 * g4 + 3] = v0.w;
+                        acc10[4 * g4] = v1.x; acc10[4 * g4 + 1] = v1.y; acc10[4 * g4 + 2] = v1.z; acc10[4 * g4 + 3] = v1.w;
+                    }
+                    acc01 = acc00;
+                    acc11 = acc10;
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) { acc00[r] = 0.f; acc01[r] = 0.f; acc10[r] = 0.f; acc11[r] = 0.f; }
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < HW_KC; ++k) {
+                const half8 a0 = __builtin_bit_cast(half8, st[((2 * rh) * HW_KC + k) * 64 + lane]);
+                const half8 a1 = __builtin_bit_cast(half8, st[((2 * rh + 1) * HW_KC + k) * 64 + lane]);
+                const half8 b0 = __builtin_bit_cast(half8, st[St::A_U4 + ((2 * qq) * HW_KC + k) * 64 + lane]);
+                const half8 b1 = __builtin_bit_cast(half8, st[St::A_U4 + ((2 * qq + 1) * HW_KC + k) * 64 + lane]);
+                acc00 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b0, acc00, 0, 0, 0);
+                acc01 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b1, acc01, 0, 0, 0);
+                acc10 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b0, acc10, 0, 0, 0);
+                acc11 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b1, acc11, 0, 0, 0);
+            }
+            if (c != nch - 1) continue;
+            // ---- tile epilogue ----
+            const uint64_t tile = t_begin + t;
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(ex_lds + (t & 1) * St::EX_U4 + HW_BN / 4);
+            // the wave's 64 rows are the tile's word rh
+            uint64_t okw = ~((uint64_t)w[2 * rh] | ((uint64_t)w[2 * rh + 1] << 32));
+            if (has_allow) okw &= (uint64_t)w[4 + 2 * rh] | ((uint64_t)w[4 + 2 * rh + 1] << 32);
+            const uint64_t row0 = tile * HW_BN + 64 * rh;
+            if (row0 + 64 > p.N) okw &= p.N > row0 ? ((1ull << (p.N - row0)) - 1) : 0ull;
+            if (okw != ~0ull || (qb + 1) * HW_BQ > p.nq) {
+                const uint64_t o0 = (jq0 < p.nq ? okw : 0ull) >> (4 * khalf);
+                const uint64_t o1 = (jq1 < p.nq ? okw : 0ull) >> (4 * khalf);
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int bit = (r & 3) + 8 * (r >> 2);
+                    acc00[r] = (o0 >> bit) & 1u ? acc00[r] : INF;
+                    acc01[r] = (o1 >> bit) & 1u ? acc01[r] : INF;
+                    acc10[r] = (o0 >> (32 + bit)) & 1u ? acc10[r] : INF;
+                    acc11[r] = (o1 >> (32 + bit)) & 1u ? acc11[r] : INF;
+                }
+            }
+            const uint32_t rb0 = (uint32_t)row0 + 4 * khalf;
+            const float pt0 = __shfl_xor(l0d[BF_KP - 1], 32, 64);
+            const float pt1 = __shfl_xor(l1d[BF_KP - 1], 32, 64);
+            float m;
+            m = min16(acc00); if (m <= fminf(l0d[BF_KP - 1], pt0)) split_extract16(m, acc00, l0d, l0i, pt0, rb0);
+            m = min16(acc10); if (m <= fminf(l0d[BF_KP - 1], pt0)) split_extract16(m, acc10, l0d, l0i, pt0, rb0 + 32);
+            m = min16(acc01); if (m <= fminf(l1d[BF_KP - 1], pt1)) split_extract16(m, acc01, l1d, l1i, pt1, rb0);
+            m = min16(acc11); if (m <= fminf(l1d[BF_KP - 1], pt1)) split_extract16(m, acc11, l1d, l1i, pt1, rb0 + 32);
+        }
+        vm_wait(0);
+        block_barrier();   // every stage read before the next segment's fills
+        const int prod = rh * 2 + khalf;
+        const size_t per_q = (size_t)p.n_slots * HW_PROD * BF_KP;
+        if (jq0 < p.nq) {
+            const size_t base = (size_t)jq0 * per_q + ((size_t)slot * HW_PROD + prod) * BF_KP;
+#pragma unroll
+            for (int i = 0; i < BF_KP; ++i) { p.out_d[base + i] = l0d[i]; p.out_id[base + i] = l0i[i]; }
+        }
+        if (jq1 < p.nq) {
+            const size_t base = (size_t)jq1 * per_q + ((size_t)slot * HW_PROD + prod) * BF_KP;
+#pragma unroll
+            for (int i = 0; i < BF_KP; ++i) { p.out_d[base + i] = l1d[i]; p.out_id[base + i] = l1i[i]; }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Seed thresholds from the pre-pass minima: the n_lists minima of a query are
 // approximate keys of distinct rows, so the k-th smallest of them, m_k, has k
 // real points with key <= m_k, i.e. true distance <= m_k + offset + eps: the
@@ -565,7 +764,7 @@ hipError_t wv_launch_h16_rows(const float* in, int ld_in, const uint64_t* ids, u
                               float scale, const unsigned int* scale_from_max, void* out, uint64_t out_row0,
                               unsigned int* res_max_bits, float* res_out, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    if (ns < 1 || ns > wv::H_NS_MAX || D > ns * 16) return hipErrorInvalidValue;
+    if (ns < 1 || ns > wv::HW_NS_MAX || D > ns * 16) return hipErrorInvalidValue;
     hipLaunchKernelGGL(wv::wv_h16_rows_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, in, ld_in, ids, n, D,
                        ns, sign, scale, scale_from_max, static_cast<uint16_t*>(out), out_row0, res_max_bits, res_out);
     return hipGetLastError();
@@ -636,6 +835,21 @@ hipError_t wv_launch_h16_margin(int metric, int D, const float* qnorm, const flo
     if (nq == 0) return hipSuccess;
     hipLaunchKernelGGL(wv::wv_h16_margin_kernel, dim3((nq + 255) / 256), dim3(256), 0, s, metric, D, qnorm, qres,
                        xnorm_max, ex_max, sx, qscale, nq, marg);
+    return hipGetLastError();
+}
+
+hipError_t wv_launch_bf_h16w(const wv::H16Params* p, hipStream_t s) {
+    const uint64_t total = (uint64_t)p->n_qblocks * p->ntiles;
+    const unsigned nb = (unsigned)((total + p->units_per_block - 1) / p->units_per_block);
+    if (nb == 0) return hipSuccess;
+    if (p->ns < 2 * wv::HW_KC || p->ns > wv::HW_NS_MAX || p->ns % wv::HW_KC || !p->X || !p->Q || !p->excl ||
+        p->tile_stride != 1)
+        return hipErrorInvalidValue;
+    const bool l2 = p->metric == WV_METRIC_L2;
+    if (l2 && !p->xns) return hipErrorInvalidValue;
+    const size_t lds = ((size_t)wv::HW_STAGES * wv::HWStage::U4 + 2 * wv::HWStage::EX_U4) * 16;
+    if (l2) hipLaunchKernelGGL((wv::wv_bf_h16w_kernel<true>), dim3(nb), dim3(512), lds, s, *p);
+    else hipLaunchKernelGGL((wv::wv_bf_h16w_kernel<false>), dim3(nb), dim3(512), lds, s, *p);
     return hipGetLastError();
 }
 

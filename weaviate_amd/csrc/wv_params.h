@@ -135,7 +135,18 @@ struct H16Params {
     unsigned int* gtau;       // [nq] (nullable)
     int kth;                  // k (0: no running threshold)
     const float* marg;        // [nq] 2 eps in scaled key units, rounded up (wv_h16_margin_kernel)
+    int ns;                   // 16-k steps of the images (the wide-D kernel: a multiple of HW_KC)
 };
+
+// ---- f16 key pass for D > 128 (wv_bf_h16w_kernel, wv_h16.hip) --------------
+// Both operands stream through LDS in 64-k chunks (3 stages): 128 corpus rows
+// x 256 queries per 512-thread workgroup, 64 x 64 per wave; the tile epilogue
+// (mask, minima, extraction) runs once per D / 64 chunks.
+constexpr int HW_BN = 128;    // corpus rows per tile
+constexpr int HW_BQ = 256;    // queries per block
+constexpr int HW_KC = 4;      // 16-k steps per chunk
+constexpr int HW_PROD = 4;    // lists per query per slot: 2 row halves x 2 lane halves
+constexpr int HW_NS_MAX = 64; // D <= 1024
 
 // order-preserving uint keys of floats (a < b <=> enc(a) < enc(b)); +inf and
 // above (0xFF800000..) decode to +inf
