@@ -53,7 +53,7 @@ hipError_t wv_launch_h16_rows(const float* in, int ld_in, const uint64_t* ids, u
 hipError_t wv_launch_absmax(const float* in, int ld, uint64_t n, int D, unsigned int* max_bits, hipStream_t s);
 hipError_t wv_launch_h16_qscale(const unsigned int* max_bits, float bsign, float* qscale, hipStream_t s);
 hipError_t wv_launch_h16_xns(const float* xnorm, uint64_t n, float sx, const float* qscale, float* xns, hipStream_t s);
-hipError_t wv_launch_bf_h16(const wv::H16Params* p, int ns, int seed, hipStream_t s);
+hipError_t wv_launch_bf_h16(const wv::H16Params* p, int ns, int seed, int waves, hipStream_t s);
 hipError_t wv_launch_bf_h16w(const wv::H16Params* p, hipStream_t s);
 hipError_t wv_launch_h16_seed(const wv::H16SeedParams* p, hipStream_t s);
 hipError_t wv_launch_h16_margin(int metric, int D, const float* qnorm, const float* qres, float xnorm_max,
@@ -483,7 +483,11 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
             uint64_t* d_out_ids, float* d_out_d, int32_t* d_out_n, hipStream_t s, std::vector<int32_t>& fails) {
     const int ns = ix->h16_ns;
     const bool wd = ix->h16_wide;   // D > 128: the wide-D kernel
-    const int tile_rows = wd ? wv::HW_BN : wv::H_BN, bq = wd ? wv::HW_BQ : wv::H_BQ;
+    // D <= 128: 8-wave (512-query) workgroups, one per CU; WV_H16_WAVES=4:
+    // 4-wave (256-query) workgroups, two independent ones per CU
+    const int waves = std::getenv("WV_H16_WAVES") && std::atoi(std::getenv("WV_H16_WAVES")) == 4 ? 4 : 8;
+    const int wg_per_cu = wd ? 1 : 8 / waves;
+    const int tile_rows = wd ? wv::HW_BN : wv::H_BN, bq = wd ? wv::HW_BQ : waves * 64;
     const int prod = wd ? wv::HW_PROD : wv::H_PROD;
     const uint64_t ntl = (N + tile_rows - 1) / tile_rows;
     const uint64_t words = ntl * (uint64_t)(tile_rows / 64);   // allow words the kernel reads
@@ -563,14 +567,14 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     // and fail the certificate); the seed pass needs >= k minima likewise
     const bool wide = k > wv::FIN_KF;
     auto target = [&](uint64_t tiles) {
-        uint64_t t = (uint64_t)ix->n_cus;
+        uint64_t t = (uint64_t)ix->n_cus * wg_per_cu;
         if (wide) t = std::max<uint64_t>(t, (uint64_t)nqb * std::min<uint64_t>(tiles, (uint64_t)k + 2));
         return (int)std::min<uint64_t>(t, 1u << 30);
     };
     const bool seed = !wd && ntl >= 64 * (uint64_t)wv::H_SAMPLE && !std::getenv("WV_H16_NO_SEED");
     if (seed) {
         const uint64_t nts = (ntl + wv::H_SAMPLE - 1) / wv::H_SAMPLE;
-        const wv::BfSchedule ss = wv::bf_schedule(nq, nts * wv::H_BN, target(nts), wv::H_BQ, wv::H_BN);
+        const wv::BfSchedule ss = wv::bf_schedule(nq, nts * wv::H_BN, target(nts), bq, wv::H_BN);
         HIP_TRY(ix->cand_d.ensure((size_t)nq * ss.n_slots * wv::H_PROD * 4));
         hp.ntiles = ss.ntiles;
         hp.units_per_block = ss.units_per_block;
@@ -580,7 +584,7 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
         hp.out_d = ix->cand_d.as<float>();
         hp.out_id = nullptr;
         TREC(6);
-        HIP_TRY(wv_launch_bf_h16(&hp, ns, 1, s));
+        HIP_TRY(wv_launch_bf_h16(&hp, ns, 1, waves, s));
         wv::H16SeedParams sp{};
         sp.minima = ix->cand_d.as<float>();
         sp.n_slots = ss.n_slots;
@@ -598,6 +602,7 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
         sp.qres = ix->qres.as<float>();
         sp.tau = ix->tau.as<float>();
         sp.gtau = ix->gtau.as<unsigned int>();
+        sp.bq = bq;
         HIP_TRY(wv_launch_h16_seed(&sp, s));
         TREC(7);
     }
@@ -628,7 +633,7 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     hp.out_d = ix->cand_d.as<float>();
     hp.out_id = ix->cand_id.as<uint32_t>();
     TREC(0);
-    HIP_TRY(wd ? wv_launch_bf_h16w(&hp, s) : wv_launch_bf_h16(&hp, ns, 0, s));
+    HIP_TRY(wd ? wv_launch_bf_h16w(&hp, s) : wv_launch_bf_h16(&hp, ns, 0, waves, s));
     TREC(1);
     fp.cand_d = ix->cand_d.as<float>();
     fp.cand_id = ix->cand_id.as<uint32_t>();

@@ -47,6 +47,13 @@ __device__ __forceinline__ void glds16(const void* src, uint32_t lds_wave_base) 
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep) : "v"(src), "s"(lds_wave_base) : "memory");
 }
+// the same from a wave-uniform base (SGPR pair) + a per-lane 32-bit byte
+// offset: a tile's address update is scalar work, no per-lane 64-bit adds
+__device__ __forceinline__ void glds16s(const void* sbase, uint32_t voff, uint32_t lds_wave_base) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds_wave_base) : "memory");
+}
 __device__ __forceinline__ void glds4(const void* src, uint32_t lds_wave_base) {
     uint32_t keep;
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
@@ -87,8 +94,12 @@ constexpr int H_TPS = 2;      // tiles per stage: one barrier per H_TPS tiles
 // SEED: the pre-pass over every H_SAMPLE-th tile keeps only each lane's
 // running minimum per query column (distinct rows per (slot, lane half)),
 // written as one key per list; wv_h16_seed_kernel turns them into thresholds.
-template <int NS, bool L2, bool SEED>
-__global__ __launch_bounds__(512, 2) void wv_bf_h16_kernel(H16Params p) {
+// WAVES = 8: one 512-query workgroup per CU (two waves per SIMD, kept in
+// phase by the stage barrier); WAVES = 4: two independent 256-query
+// workgroups per CU (one wave per SIMD each), TPS tiles per LDS stage.
+template <int NS, bool L2, bool SEED, int WAVES, int TPS>
+__global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Params p) {
+    constexpr int BQ = WAVES * 64;
     extern __shared__ uint4 lds[];
     using St = H16Stage<NS>;
     const int tid = threadIdx.x;
@@ -117,14 +128,15 @@ __global__ __launch_bounds__(512, 2) void wv_bf_h16_kernel(H16Params p) {
     if (wave >= 4) __builtin_amdgcn_s_setprio(1);
 #endif
     // this wave's LDS-DMA ops per tile (the counted waits below)
-    const int n_ops = (wave < St::IMG_U4 / 64 ? (St::IMG_U4 / 64 - 1 - wave) / H_WAVES + 1 : 0) +
+    const int n_ops = (wave < St::IMG_U4 / 64 ? (St::IMG_U4 / 64 - 1 - wave) / WAVES + 1 : 0) +
                       ((wave == 0 && L2) ? 1 : 0) + (wave == 1 ? 1 : 0);
     auto fill = [&](uint64_t t, int st) {
         const uint64_t tile = t * (uint64_t)p.tile_stride;
         const uint32_t dst = lds0 + (uint32_t)(st * St::U4 * 16);
         const uint4* src = X + tile * St::IMG_U4;
 #pragma unroll
-        for (int i = wave; i < St::IMG_U4 / 64; i += H_WAVES) glds16(src + i * 64 + lane, dst + i * 1024);
+        for (int i = wave; i < St::IMG_U4 / 64; i += WAVES)
+            glds16s(src, (uint32_t)(i * 1024 + lane * 16), dst + i * 1024);
         if (wave == 0) {
             if (L2) glds4(p.xns + tile * H_BN + lane, dst + St::IMG_U4 * 16);
         } else if (wave == 1) {
@@ -135,18 +147,18 @@ __global__ __launch_bounds__(512, 2) void wv_bf_h16_kernel(H16Params p) {
         }
     };
 
-    // the tiles of stage-group g (H_TPS consecutive tiles) into LDS stage g % 3
+    // the tiles of stage-group g (TPS consecutive tiles) into LDS stage g % 3
     auto fill_group = [&](uint64_t t_begin, int g, int ntile) {
         const int st = g % H_STAGES;
         int n = 0;
 #pragma unroll
-        for (int j = 0; j < H_TPS; ++j) {
-            const int t = g * H_TPS + j;
-            if (t < ntile) { fill(t_begin + t, st * H_TPS + j); ++n; }
+        for (int j = 0; j < TPS; ++j) {
+            const int t = g * TPS + j;
+            if (t < ntile) { fill(t_begin + t, st * TPS + j); ++n; }
         }
         return n * n_ops;   // this wave's DMA ops for the group
     };
-    auto tile_lds = [&](int t) { return lds + ((t / H_TPS) % H_STAGES * H_TPS + t % H_TPS) * St::U4; };
+    auto tile_lds = [&](int t) { return lds + ((t / TPS) % H_STAGES * TPS + t % TPS) * St::U4; };
 
     for (uint64_t u = u_first; u < u_last;) {
         const int qb = (int)(u / p.ntiles);
@@ -155,14 +167,14 @@ __global__ __launch_bounds__(512, 2) void wv_bf_h16_kernel(H16Params p) {
         if (t_end > p.ntiles) t_end = p.ntiles;
         u += t_end - t_begin;
         const int slot = lb - bf_first_block(qb, p.ntiles, p.units_per_block);
-        const int jq0 = qb * H_BQ + wave * 64 + l31;
+        const int jq0 = qb * BQ + wave * 64 + l31;
         const int jq1 = jq0 + 32;
         const int ntile = (int)(t_end - t_begin);
 
         // the wave's 64 queries as B operands, for the whole segment
         uint4 bq0[NS], bq1[NS];
         {
-            const uint64_t g0 = (uint64_t)qb * (H_BQ / 32) + 2 * wave;
+            const uint64_t g0 = (uint64_t)qb * (BQ / 32) + 2 * wave;
 #pragma unroll
             for (int st = 0; st < NS; ++st) {
                 bq0[st] = Qg[(g0 * NS + st) * 64 + lane];
@@ -265,7 +277,7 @@ __global__ __launch_bounds__(512, 2) void wv_bf_h16_kernel(H16Params p) {
             okw = ~ex & al;
             const uint64_t row0 = t * (uint64_t)p.tile_stride * H_BN;
             if (row0 + H_BN > p.N) okw &= p.N > row0 ? ((1ull << (p.N - row0)) - 1) : 0ull;
-            return okw != ~0ull || (qb + 1) * H_BQ > p.nq;
+            return okw != ~0ull || (qb + 1) * BQ > p.nq;
         };
         auto lane_ok = [&](uint64_t okw, int jq) -> uint64_t { return (jq < p.nq ? okw : 0ull) >> (4 * khalf); };
         // mask a half's ineligible rows to +inf (rows (r & 3) + 8 (r >> 2) of its 32)
@@ -307,7 +319,7 @@ __global__ __launch_bounds__(512, 2) void wv_bf_h16_kernel(H16Params p) {
         // a uniform index into register arrays would hold one mask per entry
         // in SGPRs for the whole loop)
         const int ia = (p.kth + 1) >> 1, ib = p.kth >> 1;
-        float* scr_all = reinterpret_cast<float*>(lds + H_STAGES * H_TPS * St::U4);
+        float* scr_all = reinterpret_cast<float*>(lds + H_STAGES * TPS * St::U4);
         float* scr = scr_all + (wave * 64 + lane) * (2 * BF_KP);
         const float* pscr = scr_all + (wave * 64 + (lane ^ 32)) * (2 * BF_KP);
         auto publish = [&] {
@@ -332,7 +344,7 @@ __global__ __launch_bounds__(512, 2) void wv_bf_h16_kernel(H16Params p) {
             refresh_pt();
         };
         const bool running = !SEED && p.kth > 0 && p.gtau != nullptr;
-        const int ngroups = (ntile + H_TPS - 1) / H_TPS;
+        const int ngroups = (ntile + TPS - 1) / TPS;
         // (the previous segment ended with every stage read and every DMA landed)
         int ops_in_flight = 0;   // this wave's DMA ops of the newest group issued
         if (ngroups > 0) fill_group(t_begin, 0, ntile);
@@ -344,11 +356,11 @@ __global__ __launch_bounds__(512, 2) void wv_bf_h16_kernel(H16Params p) {
             need_mask = tile_ok(tile_lds(0), t_begin, okw);
         }
         for (int t = 0; t < ntile; ++t) {
-            const int g = t / H_TPS;
+            const int g = t / TPS;
 #ifndef WV_H16_ABLATE_NO_FILL
             // group g + 2 goes to stage (g + 2) % 3 = (g - 1) % 3, last read in
             // group g - 1, before its closing barrier
-            if (t % H_TPS == 0) ops_in_flight = g + 2 < ngroups ? fill_group(t_begin, g + 2, ntile) : 0;
+            if (t % TPS == 0) ops_in_flight = g + 2 < ngroups ? fill_group(t_begin, g + 2, ntile) : 0;
 #endif
             const uint4* img = tile_lds(t);
             const uint32_t rb0 = (uint32_t)((t_begin + t) * (uint64_t)p.tile_stride * H_BN) + 4 * khalf;
@@ -376,7 +388,7 @@ __global__ __launch_bounds__(512, 2) void wv_bf_h16_kernel(H16Params p) {
             }
             // ---- C (last tile of a group): group g + 1 has landed (g + 2 may
             // stay in flight); every wave is done reading group g's stage ----
-            if (t % H_TPS == H_TPS - 1 || t == ntile - 1) {
+            if (t % TPS == TPS - 1 || t == ntile - 1) {
                 if (g + 1 < ngroups) vm_wait(ops_in_flight);
                 block_barrier();
             }
@@ -497,8 +509,8 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16w_kernel(H16Params p) {
                 const int bb = isb ? b - St::A_U4 / 64 : b;      // (group, step) block
                 const int grp = bb / HW_KC, st = bb % HW_KC;
                 const uint64_t G = isb ? (uint64_t)qb * (HW_BQ / 32) + grp : tile * (HW_BN / 32) + grp;
-                const uint4* src = (isb ? Qg : X) + ((G * ns + (uint64_t)c * HW_KC + st) * 64 + lane);
-                glds16(src, dst + (uint32_t)(b * 1024));
+                const uint4* src = (isb ? Qg : X) + (G * ns + (uint64_t)c * HW_KC + st) * 64;
+                glds16s(src, (uint32_t)(lane * 16), dst + (uint32_t)(b * 1024));
                 ++n;
             }
             if (c == 0) {
@@ -631,7 +643,7 @@ __global__ __launch_bounds__(64) void wv_h16_seed_kernel(H16SeedParams p) {
     const int q = blockIdx.x;
     const int lane = threadIdx.x;
     if (q >= p.nq) return;
-    const int n = bf_slots_of((uint64_t)(q / H_BQ), p.ntiles, p.units_per_block) * H_PROD;
+    const int n = bf_slots_of((uint64_t)(q / p.bq), p.ntiles, p.units_per_block) * H_PROD;
     const float* m = p.minima + (size_t)q * p.n_slots * H_PROD;
     const float inv_s = 1.0f / (p.sx * p.qscale[0]);
     // k rounds of a wave-wide minimum over the lanes' shares
@@ -790,24 +802,29 @@ hipError_t wv_launch_h16_xns(const float* xnorm, uint64_t n, float sx, const flo
     return hipGetLastError();
 }
 
-hipError_t wv_launch_bf_h16(const wv::H16Params* p, int ns, int seed, hipStream_t s) {
+hipError_t wv_launch_bf_h16(const wv::H16Params* p, int ns, int seed, int waves, hipStream_t s) {
     const uint64_t total = (uint64_t)p->n_qblocks * p->ntiles;
     const unsigned nb = (unsigned)((total + p->units_per_block - 1) / p->units_per_block);
     if (nb == 0) return hipSuccess;
-    if (ns < 1 || ns > wv::H_NS_MAX || !p->X || !p->Q || !p->excl || !p->qscale || p->tile_stride < 1)
+    if (ns < 1 || ns > wv::H_NS_MAX || !p->X || !p->Q || !p->excl || !p->qscale || p->tile_stride < 1 ||
+        (waves != 8 && waves != 4))
         return hipErrorInvalidValue;
     const bool l2 = p->metric == WV_METRIC_L2;
     if (l2 && !p->xns) return hipErrorInvalidValue;
+    const int tps = waves == 8 ? 2 : 1;
     // the stages, then (key pass with a running threshold) the per-lane list scratch
-    const size_t lds = (size_t)wv::H_STAGES * wv::H_TPS * (2 * ns * 64 + 17) * 16 +
-                       (seed ? 0 : (size_t)wv::H_WAVES * 64 * 2 * wv::BF_KP * 4);
-#define WV_H16_LAUNCH(NS)                                                                                      \
-    if (seed) {                                                                                                \
-        if (l2) hipLaunchKernelGGL((wv::wv_bf_h16_kernel<NS, true, true>), dim3(nb), dim3(512), lds, s, *p);   \
-        else hipLaunchKernelGGL((wv::wv_bf_h16_kernel<NS, false, true>), dim3(nb), dim3(512), lds, s, *p);     \
-    } else {                                                                                                   \
-        if (l2) hipLaunchKernelGGL((wv::wv_bf_h16_kernel<NS, true, false>), dim3(nb), dim3(512), lds, s, *p);  \
-        else hipLaunchKernelGGL((wv::wv_bf_h16_kernel<NS, false, false>), dim3(nb), dim3(512), lds, s, *p);    \
+    const size_t lds = (size_t)wv::H_STAGES * tps * (2 * ns * 64 + 17) * 16 +
+                       (seed ? 0 : (size_t)waves * 64 * 2 * wv::BF_KP * 4);
+#define WV_H16_GO(NS, L, S)                                                                                    \
+    if (waves == 8) hipLaunchKernelGGL((wv::wv_bf_h16_kernel<NS, L, S, 8, 2>), dim3(nb), dim3(512), lds, s, *p); \
+    else hipLaunchKernelGGL((wv::wv_bf_h16_kernel<NS, L, S, 4, 1>), dim3(nb), dim3(256), lds, s, *p);
+#define WV_H16_LAUNCH(NS)                     \
+    if (seed) {                               \
+        if (l2) { WV_H16_GO(NS, true, true) } \
+        else { WV_H16_GO(NS, false, true) }   \
+    } else {                                  \
+        if (l2) { WV_H16_GO(NS, true, false) } \
+        else { WV_H16_GO(NS, false, false) }  \
     }
     switch (ns) {
         case 1: WV_H16_LAUNCH(1) break;
@@ -820,13 +837,7 @@ hipError_t wv_launch_bf_h16(const wv::H16Params* p, int ns, int seed, hipStream_
         default: WV_H16_LAUNCH(8) break;
     }
 #undef WV_H16_LAUNCH
-    return hipGetLastError();
-}
-
-hipError_t wv_launch_h16_gtau(const unsigned int* gtau, int nq, float sx, const float* qscale, float* tau,
-                              hipStream_t s) {
-    if (nq == 0) return hipSuccess;
-    hipLaunchKernelGGL(wv::wv_h16_gtau_kernel, dim3((nq + 255) / 256), dim3(256), 0, s, gtau, nq, sx, qscale, tau);
+#undef WV_H16_GO
     return hipGetLastError();
 }
 
@@ -835,6 +846,13 @@ hipError_t wv_launch_h16_margin(int metric, int D, const float* qnorm, const flo
     if (nq == 0) return hipSuccess;
     hipLaunchKernelGGL(wv::wv_h16_margin_kernel, dim3((nq + 255) / 256), dim3(256), 0, s, metric, D, qnorm, qres,
                        xnorm_max, ex_max, sx, qscale, nq, marg);
+    return hipGetLastError();
+}
+
+hipError_t wv_launch_h16_gtau(const unsigned int* gtau, int nq, float sx, const float* qscale, float* tau,
+                              hipStream_t s) {
+    if (nq == 0) return hipSuccess;
+    hipLaunchKernelGGL(wv::wv_h16_gtau_kernel, dim3((nq + 255) / 256), dim3(256), 0, s, gtau, nq, sx, qscale, tau);
     return hipGetLastError();
 }
 

@@ -180,6 +180,7 @@ struct H16SeedParams {
     const float* qres;
     float* tau;               // [nq] out: threshold in true key units (+inf: none)
     unsigned int* gtau;       // [nq] out (nullable): h16_key_enc(tau * s), the running threshold's start
+    int bq;                   // queries per block of the pre-pass
 };
 
 struct BfFinParams {
