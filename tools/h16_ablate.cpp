@@ -8,6 +8,9 @@
 #include <vector>
 #include "../include/wvgpu.h"
 
+// debug builds (-DWV_BF_DBG_ITERS) export wave-level counts: tiles, extraction rounds
+extern "C" void wv_dbg_read(unsigned long long* out) __attribute__((weak));
+
 int main(int argc, char** argv) {
     const uint64_t N = argc > 1 ? atoll(argv[1]) : 1000000;
     const int nq = argc > 2 ? atoi(argv[2]) : 10000;
@@ -59,6 +62,12 @@ int main(int argc, char** argv) {
            name, (unsigned long long)N, nq, D, km / it, ks / it, kf / it, wall / it,
            2.0 * D * N * nq / (km / it * 1e-3) / 1e12, (unsigned long long)fb, (unsigned long long)ids[0],
            (unsigned long long)ids[1]);
+    if (wv_dbg_read) {
+        unsigned long long c[2] = {0, 0};
+        wv_dbg_read(c);
+        printf("%-16s wave-tiles %llu  extraction rounds %llu  (%.3f per wave-tile)\n", name, c[0], c[1],
+               c[0] ? (double)c[1] / (double)c[0] : 0.0);
+    }
     wv_index_destroy(ix);
     return 0;
 }

@@ -25,5 +25,4 @@ for f in $B/abl_*; do
 done
 WV_H16_NO_SEED=1 timeout -k 5 120 $B/abl_base ${N:-1000000} ${NQ:-10000} ${D:-128} base_noseed
 WV_H16_NO_RUNNING=1 timeout -k 5 120 $B/abl_base ${N:-1000000} ${NQ:-10000} ${D:-128} base_norunning
-WV_H16_WAVES=4 timeout -k 5 120 $B/abl_base ${N:-1000000} ${NQ:-10000} ${D:-128} base_4waves
-WV_H16_WAVES=4 timeout -k 5 120 $B/abl_pure ${N:-1000000} ${NQ:-10000} ${D:-128} pure_4waves
+
