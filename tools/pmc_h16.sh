@@ -31,4 +31,24 @@ for f in glob.glob("gpurun_out/pmc_h16/trace/run_kernel_stats.csv"):
         print(r["Name"][:70], r["Calls"], r["AverageNs"])
 print(json.dumps(out, indent=1))
 json.dump(out, open("gpurun_out/pmc_h16/summary.json", "w"), indent=1)
+# the bench's roofline.traffic source (bench.py attach_traffic): HBM bytes per
+# launch of the key pass, FETCH_SIZE doubled (gfx950 half-count correction)
+import os
+avg_ns = None
+for f in glob.glob("gpurun_out/pmc_h16/trace/run_kernel_stats.csv"):
+    for r in csv.DictReader(open(f)):
+        if "h16_kernel<8, true, false>" in r["Name"]:
+            avg_ns = float(r["AverageNs"])
+if "FETCH_SIZE" in out:
+    rd = 2.0 * out["FETCH_SIZE"] * 1024
+    js = {"kernel": "wv_bf_h16_kernel", "N": int(os.environ.get("N", 1000000)), "nq": int(os.environ.get("NQ", 10000)),
+          "dim": int(os.environ.get("D", 128)), "data": "uniform", "avg_kernel_ns": avg_ns,
+          "hbm_read_bytes_per_launch": rd, "hbm_bytes_per_launch": rd,
+          "algorithmic_bytes_per_launch": None,
+          "sq": {k: v for k, v in out.items() if k.startswith("SQ_") or k.startswith("GRBM")},
+          "note": "read = 2*FETCH_SIZE*1024 (gfx950 half-count correction); U[0,1) corpus/queries of the "
+                  "tools/h16_ablate.cpp harness (same shape as bench.py's configs[1]); write traffic is the "
+                  "candidate lists only (not collected)",
+          "source": "profiles/pmc_wv_bf_h16_kernel.json (tools/pmc_h16.sh)"}
+    json.dump(js, open("gpurun_out/pmc_h16/pmc_wv_bf_h16_kernel.json", "w"), indent=1)
 PY

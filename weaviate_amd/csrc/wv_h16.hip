@@ -88,15 +88,8 @@ struct H16Stage {
     static constexpr int IMG_U4 = 2 * NS * 64;
     static constexpr int U4 = IMG_U4 + 16 + 1;
 };
-#ifndef WV_H16_LDS_LISTS
-#define WV_H16_LDS_LISTS 0
-#endif
-// WV_H16_LDS_LISTS: the key pass keeps its candidate lists in LDS (lane-major,
-// read and written only by the rare extraction) and only the list tails in
-// registers; one tile per stage then (LDS budget)
-constexpr int H_TPS8 = WV_H16_LDS_LISTS ? 1 : 2;
+constexpr int H_TPS8 = 2;
 constexpr int H_STAGES = 3;   // a stage holds H_TPS tiles; stage p % 3 computes while p + 1, p + 2 land
-constexpr int H_TPS = 2;      // tiles per stage: one barrier per H_TPS tiles
 
 // SEED: the pre-pass over every H_SAMPLE-th tile keeps only each lane's
 // running minimum per query column (distinct rows per (slot, lane half)),
@@ -207,8 +200,6 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
 #pragma unroll
         for (int st = 0; st < NS; ++st) asm volatile("" ::"v"(bq0[st].x), "v"(bq1[st].x));
         asm volatile("" ::"v"(tau0), "v"(tau1), "v"(marg0), "v"(marg1));
-        constexpr bool LL = !SEED && WV_H16_LDS_LISTS;
-        // register lists (LL: only [BF_KP - 1], the tail, is kept up to date)
         float l0d[BF_KP], l1d[BF_KP];
         uint32_t l0i[BF_KP], l1i[BF_KP];
 #pragma unroll
@@ -216,40 +207,10 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
             l0d[i] = FLT_MAX; l1d[i] = FLT_MAX;
             l0i[i] = WV_NIL; l1i[i] = WV_NIL;
         }
-        // LL: list j (0: column jq0 keys, 1: jq1 keys, 2 / 3: their ids), entry
-        // i of this lane at LL_base[(j * BF_KP + i) * 64]
-        float* LL_base = reinterpret_cast<float*>(lds + H_STAGES * TPS * St::U4) + wave * 4 * BF_KP * 64 + lane;
-        if constexpr (LL) {
-#pragma unroll
-            for (int i = 0; i < BF_KP; ++i) {
-                LL_base[i * 64] = FLT_MAX;
-                LL_base[(BF_KP + i) * 64] = FLT_MAX;
-                LL_base[(2 * BF_KP + i) * 64] = __uint_as_float(WV_NIL);
-                LL_base[(3 * BF_KP + i) * 64] = __uint_as_float(WV_NIL);
-            }
-        }
         // extraction of a half tile's keys into list c (0 / 1)
         auto extract = [&](float& m, floatx16& acc, int c, float pt, uint32_t rb) {
-            if constexpr (LL) {
-                float ld[BF_KP];
-                uint32_t li[BF_KP];
-#pragma unroll
-                for (int i = 0; i < BF_KP; ++i) {
-                    ld[i] = LL_base[(c * BF_KP + i) * 64];
-                    li[i] = __float_as_uint(LL_base[((2 + c) * BF_KP + i) * 64]);
-                }
-                split_extract16(m, acc, ld, li, pt, rb);
-#pragma unroll
-                for (int i = 0; i < BF_KP; ++i) {
-                    LL_base[(c * BF_KP + i) * 64] = ld[i];
-                    LL_base[((2 + c) * BF_KP + i) * 64] = __uint_as_float(li[i]);
-                }
-                if (c == 0) l0d[BF_KP - 1] = ld[BF_KP - 1];
-                else l1d[BF_KP - 1] = ld[BF_KP - 1];
-            } else {
-                if (c == 0) split_extract16(m, acc, l0d, l0i, pt, rb);
-                else split_extract16(m, acc, l1d, l1i, pt, rb);
-            }
+            if (c == 0) split_extract16(m, acc, l0d, l0i, pt, rb);
+            else split_extract16(m, acc, l1d, l1i, pt, rb);
         };
         // Two-phase software pipeline over half tiles (rows 0-31: H0 =
         // acc00/acc01, rows 32-63: H1 = acc10/acc11).  Iteration t:
@@ -359,29 +320,23 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
         refresh_pt();
         // running threshold: k of the pair's list entries bound the k-th key
         // (ia from this lane's list, ib from the partner's), + 2 eps
-        // (the lists pass through a per-lane LDS scratch after the stages:
-        // a uniform index into register arrays would hold one mask per entry
-        // in SGPRs for the whole loop)
+        // (entries picked by select chains over an opaque VGPR index: a
+        // uniform index into register arrays would hold one SGPR mask per
+        // entry for the whole loop; the partner's entries arrive by shuffle)
         const int ia = (p.kth + 1) >> 1, ib = p.kth >> 1;
-        float* scr_all = reinterpret_cast<float*>(lds + H_STAGES * TPS * St::U4);
-        float* scr = scr_all + (wave * 64 + lane) * (2 * BF_KP);
-        const float* pscr = scr_all + (wave * 64 + (lane ^ 32)) * (2 * BF_KP);
         auto publish = [&] {
-            float a0, a1, b0, b1;
-            if constexpr (LL) {
-                const float* P = LL_base + ((lane ^ 32) - lane);
-                a0 = ia > 0 ? LL_base[(ia - 1) * 64] : -FLT_MAX;
-                a1 = ia > 0 ? LL_base[(BF_KP + ia - 1) * 64] : -FLT_MAX;
-                b0 = ib > 0 ? P[(ib - 1) * 64] : -FLT_MAX;
-                b1 = ib > 0 ? P[(BF_KP + ib - 1) * 64] : -FLT_MAX;
-            } else {
+            int va = ia - 1, vb = ib - 1;
+            asm volatile("" : "+v"(va), "+v"(vb));
+            float a0 = -FLT_MAX, a1 = -FLT_MAX, b0 = -FLT_MAX, b1 = -FLT_MAX;
 #pragma unroll
-                for (int i = 0; i < BF_KP; ++i) { scr[i] = l0d[i]; scr[BF_KP + i] = l1d[i]; }
-                a0 = ia > 0 ? scr[ia - 1] : -FLT_MAX;
-                a1 = ia > 0 ? scr[BF_KP + ia - 1] : -FLT_MAX;
-                b0 = ib > 0 ? pscr[ib - 1] : -FLT_MAX;
-                b1 = ib > 0 ? pscr[BF_KP + ib - 1] : -FLT_MAX;
+            for (int i = 0; i < BF_KP; ++i) {
+                a0 = va == i ? l0d[i] : a0;
+                a1 = va == i ? l1d[i] : a1;
+                b0 = vb == i ? l0d[i] : b0;
+                b1 = vb == i ? l1d[i] : b1;
             }
+            b0 = __shfl_xor(b0, 32, 64);
+            b1 = __shfl_xor(b1, 32, 64);
             const float k0 = fmaxf(a0, b0), k1 = fmaxf(a1, b1);
             if (khalf == 0) {
                 const float u4 = 4.f * 5.9604645e-08f;
@@ -436,7 +391,13 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
 #ifdef WV_H16_ABLATE_NO_EXTRACT
                 if (m0 == 1234.5f) l0d[0] = m1 + pt0 + pt1;
 #else
+#ifdef WV_H16_ABLATE_EXT_NEVER
+                float never = -INF;
+                asm volatile("" : "+v"(never));
+                const bool x0 = m0 <= never, x1 = m1 <= never;
+#else
                 const bool x0 = m0 <= fminf(l0d[BF_KP - 1], pt0), x1 = m1 <= fminf(l1d[BF_KP - 1], pt1);
+#endif
                 // one wave-uniform (rarely taken) branch around the extraction
                 grew = __any(x0 || x1);
                 if (__builtin_expect(grew, 0)) {
@@ -468,7 +429,13 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
 #ifdef WV_H16_ABLATE_NO_EXTRACT
                 if (m0 == 1234.5f) l0d[0] = m1 + pt0 + pt1;
 #else
+#ifdef WV_H16_ABLATE_EXT_NEVER
+                float never = -INF;
+                asm volatile("" : "+v"(never));
+                const bool x0 = m0 <= never, x1 = m1 <= never;
+#else
                 const bool x0 = m0 <= fminf(l0d[BF_KP - 1], pt0), x1 = m1 <= fminf(l1d[BF_KP - 1], pt1);
+#endif
                 const bool any1 = __any(x0 || x1);
                 if (__builtin_expect(any1, 0)) {
                     if (x0) extract(m0, acc10, 0, pt0, rb0 + 32);
@@ -485,15 +452,6 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
             if (jq0 < p.nq) p.out_d[((size_t)jq0 * p.n_slots + slot) * H_PROD + khalf] = l0d[0];
             if (jq1 < p.nq) p.out_d[((size_t)jq1 * p.n_slots + slot) * H_PROD + khalf] = l1d[0];
             continue;
-        }
-        if constexpr (LL) {
-#pragma unroll
-            for (int i = 0; i < BF_KP; ++i) {
-                l0d[i] = LL_base[i * 64];
-                l1d[i] = LL_base[(BF_KP + i) * 64];
-                l0i[i] = __float_as_uint(LL_base[(2 * BF_KP + i) * 64]);
-                l1i[i] = __float_as_uint(LL_base[(3 * BF_KP + i) * 64]);
-            }
         }
         const size_t per_q = (size_t)p.n_slots * H_PROD * BF_KP;
         if (jq0 < p.nq) {
@@ -883,10 +841,7 @@ hipError_t wv_launch_bf_h16(const wv::H16Params* p, int ns, int seed, int waves,
     const bool l2 = p->metric == WV_METRIC_L2;
     if (l2 && !p->xns) return hipErrorInvalidValue;
     const int tps = waves == 8 ? wv::H_TPS8 : 1;
-    // the stages, then (the key pass) the per-lane list scratch of the running
-    // threshold, or (WV_H16_LDS_LISTS) the lists themselves
-    const size_t lds = (size_t)wv::H_STAGES * tps * (2 * ns * 64 + 17) * 16 +
-                       (seed ? 0 : (size_t)waves * 64 * (WV_H16_LDS_LISTS ? 4 : 2) * wv::BF_KP * 4);
+    const size_t lds = (size_t)wv::H_STAGES * tps * (2 * ns * 64 + 17) * 16;
 #define WV_H16_GO(NS, L, S)                                                                                    \
     if (waves == 8) hipLaunchKernelGGL((wv::wv_bf_h16_kernel<NS, L, S, 8, wv::H_TPS8>), dim3(nb), dim3(512), lds, s, *p); \
     else hipLaunchKernelGGL((wv::wv_bf_h16_kernel<NS, L, S, 4, 1>), dim3(nb), dim3(256), lds, s, *p);
