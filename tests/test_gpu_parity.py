@@ -83,24 +83,40 @@ def test_bruteforce_mfma_ids_identical(metric):
 
 
 def test_bruteforce_integer_data_with_ties_uses_exact_fallback():
-    """SIFT-shaped integer data (many equal distances): the certificate cannot
-    separate ties at the boundary, so the batched exact fallback answers; the
-    result must equal the restatement up to the order among equal distances."""
+    """SIFT-shaped integer data (many equal distances): when the candidate lists
+    hold tied keys at the boundary the certificate cannot separate them and the
+    batched exact fallback answers; the result must equal the restatement up to
+    the order among equal distances, with (dist, id) order among ties.
+
+    Without the running threshold (WV_H16_NO_RUNNING) the lists fill with the
+    tied keys deterministically, so the fallback must run.  With it (default:
+    corpora too small for the seed pass) whether a query certifies depends on
+    when the shared threshold tightens -- both outcomes are exact, which the
+    default run checks."""
+    import os
     rng = np.random.default_rng(21)
     base = rng.integers(0, 3, (20000, 16)).astype(np.float32)
     qs = rng.integers(0, 3, (200, 16)).astype(np.float32)
-    ix = W.GPUVectorIndex(16, "l2-squared", capacity=20000)
-    ix.upload_vectors(base)
-    ids, ds, n = ix.search_batch(qs, 10, mode="exact")
     oi, od, on = O.flat_scan(O.L2, base, qs, 10)
-    assert ix.last_batch_stats()["fallbacks"] > 0
-    for i in range(len(qs)):
-        _same_tie_aware(ids[i], ds[i], oi[i], od[i])
-        # (dist, id) order: among equal distances the smallest ids win
-        full = ((base.astype(np.float64) - qs[i].astype(np.float64)) ** 2).sum(1)
-        order = np.lexsort((np.arange(len(base)), full))[:10]
-        assert ids[i].tolist() == order.tolist()
-    ix.close()
+    for env in ({"WV_H16_NO_RUNNING": "1"}, {}):
+        os.environ.update(env)
+        try:
+            ix = W.GPUVectorIndex(16, "l2-squared", capacity=20000)
+            ix.upload_vectors(base)
+            ids, ds, n = ix.search_batch(qs, 10, mode="exact")
+            fb = ix.last_batch_stats()["fallbacks"]
+            ix.close()
+        finally:
+            for key in env:
+                os.environ.pop(key, None)
+        if env:
+            assert fb > 0
+        for i in range(len(qs)):
+            _same_tie_aware(ids[i], ds[i], oi[i], od[i])
+            # (dist, id) order: among equal distances the smallest ids win
+            full = ((base.astype(np.float64) - qs[i].astype(np.float64)) ** 2).sum(1)
+            order = np.lexsort((np.arange(len(base)), full))[:10]
+            assert ids[i].tolist() == order.tolist()
 
 
 def test_bruteforce_ragged_sizes_and_small_batches():

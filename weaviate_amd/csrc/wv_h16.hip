@@ -88,7 +88,10 @@ struct H16Stage {
     static constexpr int IMG_U4 = 2 * NS * 64;
     static constexpr int U4 = IMG_U4 + 16 + 1;
 };
-constexpr int H_TPS8 = 2;
+#ifndef WV_H16_TPS
+#define WV_H16_TPS 2
+#endif
+constexpr int H_TPS8 = WV_H16_TPS;   // tiles per LDS stage (8-wave kernel): one barrier per H_TPS8 tiles
 constexpr int H_STAGES = 3;   // a stage holds H_TPS tiles; stage p % 3 computes while p + 1, p + 2 land
 
 // SEED: the pre-pass over every H_SAMPLE-th tile keeps only each lane's
