@@ -63,10 +63,13 @@ int main(int argc, char** argv) {
            2.0 * D * N * nq / (km / it * 1e-3) / 1e12, (unsigned long long)fb, (unsigned long long)ids[0],
            (unsigned long long)ids[1]);
     if (wv_dbg_read) {
-        unsigned long long c[2] = {0, 0};
+        // (summed over the 2 warm-up + `it` timed batches)
+        unsigned long long c[4] = {0, 0, 0, 0};
         wv_dbg_read(c);
-        printf("%-16s wave-tiles %llu  extraction rounds %llu  (%.3f per wave-tile)\n", name, c[0], c[1],
-               c[0] ? (double)c[1] / (double)c[0] : 0.0);
+        const double nb = 2.0 + it;
+        printf("%-16s per batch: wave-tiles %.0f  extraction calls %.0f  wave rounds %.0f  lane rounds %.0f  "
+               "(calls per wave-tile %.3f, lanes per round %.2f)\n", name, c[0] / nb, c[3] / nb, c[1] / nb, c[2] / nb,
+               c[0] ? (double)c[3] / (double)c[0] : 0.0, c[1] ? (double)c[2] / (double)c[1] : 0.0);
     }
     wv_index_destroy(ix);
     return 0;

@@ -49,11 +49,12 @@ hipError_t wv_launch_split_rows(const float* in, int ld_in, const uint64_t* ids,
                                 float scale, void* out, int ld_out, uint64_t out_row0, hipStream_t s);
 hipError_t wv_launch_h16_rows(const float* in, int ld_in, const uint64_t* ids, uint64_t n, int D, int ns, float sign,
                               float scale, const unsigned int* scale_from_max, void* out, uint64_t out_row0,
-                              unsigned int* res_max_bits, float* res_out, hipStream_t s);
+                              unsigned int* res_max_bits, float* res_out, int quad, hipStream_t s);
 hipError_t wv_launch_absmax(const float* in, int ld, uint64_t n, int D, unsigned int* max_bits, hipStream_t s);
 hipError_t wv_launch_h16_qscale(const unsigned int* max_bits, float bsign, float* qscale, hipStream_t s);
 hipError_t wv_launch_h16_xns(const float* xnorm, uint64_t n, float sx, const float* qscale, float* xns, hipStream_t s);
 hipError_t wv_launch_bf_h16(const wv::H16Params* p, int ns, int seed, int waves, hipStream_t s);
+hipError_t wv_launch_bf_h16q(const wv::H16Params* p, int ns32, int seed, hipStream_t s);
 hipError_t wv_launch_bf_h16w(const wv::H16Params* p, hipStream_t s);
 hipError_t wv_launch_h16_seed(const wv::H16SeedParams* p, hipStream_t s);
 hipError_t wv_launch_h16_margin(int metric, int D, const float* qnorm, const float* qres, float xnorm_max,
@@ -226,6 +227,7 @@ struct wv_index {
     // norm |x - f16(s_x x) / s_x| over the rows (rounded up), both host-cached
     bool use_h16 = false;
     bool h16_wide = false;  // D > 128: wv_bf_h16w_kernel (both operands through LDS, 128-row tiles)
+    bool h16_quad = false;  // D <= 128, even 16-k steps: wv_bf_h16q_kernel (16x16x32 MFMA, h16q_index images)
     int h16_ns = 0;
     float h16_sx = 0.f, h16_ex = 0.f;
     DevBuf ximg16, xns, qimg16, qres, qmax, qscale, tau, gtau, marg, allow_pad, ex_bits;
@@ -483,12 +485,14 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
             uint64_t* d_out_ids, float* d_out_d, int32_t* d_out_n, hipStream_t s, std::vector<int32_t>& fails) {
     const int ns = ix->h16_ns;
     const bool wd = ix->h16_wide;   // D > 128: the wide-D kernel
+    const bool quad = ix->h16_quad;   // the 16x16x32 kernel (8 waves, HQ_KP-entry lists)
     // D <= 128: 8-wave (512-query) workgroups, one per CU; WV_H16_WAVES=4:
     // 4-wave (256-query) workgroups, two independent ones per CU
-    const int waves = std::getenv("WV_H16_WAVES") && std::atoi(std::getenv("WV_H16_WAVES")) == 4 ? 4 : 8;
+    const int waves = !quad && std::getenv("WV_H16_WAVES") && std::atoi(std::getenv("WV_H16_WAVES")) == 4 ? 4 : 8;
     const int wg_per_cu = wd ? 1 : 8 / waves;
     const int tile_rows = wd ? wv::HW_BN : wv::H_BN, bq = wd ? wv::HW_BQ : waves * 64;
-    const int prod = wd ? wv::HW_PROD : wv::H_PROD;
+    const int prod = wd ? wv::HW_PROD : (quad ? wv::HQ_PROD : wv::H_PROD);
+    const int kp = quad ? wv::HQ_KP : wv::BF_KP;   // entries per list
     const uint64_t ntl = (N + tile_rows - 1) / tile_rows;
     const uint64_t words = ntl * (uint64_t)(tile_rows / 64);   // allow words the kernel reads
     const uint64_t* allow = d_allow;
@@ -516,7 +520,7 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     HIP_TRY(wv_launch_absmax(d_q, ix->dpad, nq, ix->dim, ix->qmax.as<unsigned int>(), s));
     HIP_TRY(wv_launch_h16_qscale(ix->qmax.as<unsigned int>(), bsign, ix->qscale.as<float>(), s));
     HIP_TRY(wv_launch_h16_rows(d_q, ix->dpad, nullptr, nq, ix->dim, ns, bsign, 1.f, ix->qmax.as<unsigned int>(),
-                               ix->qimg16.p, 0, nullptr, ix->qres.as<float>(), s));
+                               ix->qimg16.p, 0, nullptr, ix->qres.as<float>(), quad, s));
     if (ix->metric == WV_L2_SQUARED)
         HIP_TRY(wv_launch_h16_xns(ix->xnorm.as<float>(), ntl * tile_rows, ix->h16_sx, ix->qscale.as<float>(),
                                   ix->xns.as<float>(), s));
@@ -553,6 +557,7 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     fp.fail_thr = ix->fail_thr.as<float>();
     fp.bq = bq;
     fp.prod = prod;
+    fp.kp = kp;
     fp.h16 = 1;
     hp.ns = ns;
     fp.qscale = ix->qscale.as<float>();
@@ -575,7 +580,7 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     if (seed) {
         const uint64_t nts = (ntl + wv::H_SAMPLE - 1) / wv::H_SAMPLE;
         const wv::BfSchedule ss = wv::bf_schedule(nq, nts * wv::H_BN, target(nts), bq, wv::H_BN);
-        HIP_TRY(ix->cand_d.ensure((size_t)nq * ss.n_slots * wv::H_PROD * 4));
+        HIP_TRY(ix->cand_d.ensure((size_t)nq * ss.n_slots * prod * 4));
         hp.ntiles = ss.ntiles;
         hp.units_per_block = ss.units_per_block;
         hp.n_slots = ss.n_slots;
@@ -584,7 +589,7 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
         hp.out_d = ix->cand_d.as<float>();
         hp.out_id = nullptr;
         TREC(6);
-        HIP_TRY(wv_launch_bf_h16(&hp, ns, 1, waves, s));
+        HIP_TRY(quad ? wv_launch_bf_h16q(&hp, ns / 2, 1, s) : wv_launch_bf_h16(&hp, ns, 1, waves, s));
         wv::H16SeedParams sp{};
         sp.minima = ix->cand_d.as<float>();
         sp.n_slots = ss.n_slots;
@@ -603,14 +608,15 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
         sp.tau = ix->tau.as<float>();
         sp.gtau = ix->gtau.as<unsigned int>();
         sp.bq = bq;
+        sp.prod = prod;
         HIP_TRY(wv_launch_h16_seed(&sp, s));
         TREC(7);
     }
     const wv::BfSchedule sch = wv::bf_schedule(nq, N, target(ntl), bq, tile_rows);
-    if (wide && (uint64_t)sch.n_slots * prod * wv::BF_KP > (uint64_t)wv::FINW_NE)
+    if (wide && (uint64_t)sch.n_slots * prod * kp > (uint64_t)wv::FINW_NE)
         return fail(WV_ESTATE, "run_h16: too many lists for the wide finalize");
-    HIP_TRY(ix->cand_d.ensure((size_t)nq * sch.n_slots * prod * wv::BF_KP * 4));
-    HIP_TRY(ix->cand_id.ensure((size_t)nq * sch.n_slots * prod * wv::BF_KP * 4));
+    HIP_TRY(ix->cand_d.ensure((size_t)nq * sch.n_slots * prod * kp * 4));
+    HIP_TRY(ix->cand_id.ensure((size_t)nq * sch.n_slots * prod * kp * 4));
     hp.ntiles = sch.ntiles;
     hp.units_per_block = sch.units_per_block;
     hp.n_slots = sch.n_slots;
@@ -622,7 +628,7 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     // (with the seed's threshold the running one only adds work: measured
     // 3.048 vs 3.092 ms per 1M x 10k key pass; without a seed -- corpora below
     // 64 * H_SAMPLE tiles -- it cuts the pass 4.13 -> 3.43 ms at 1M)
-    hp.kth = k <= 2 * wv::BF_KP && !seed && !wd && !std::getenv("WV_H16_NO_RUNNING") ? k : 0;
+    hp.kth = k <= prod * kp && !seed && !wd && !std::getenv("WV_H16_NO_RUNNING") ? k : 0;
     if (hp.kth) {
         HIP_TRY(ix->marg.ensure((size_t)nq * 4));
         HIP_TRY(wv_launch_h16_margin(ix->metric, ix->dim, ix->q_nrm2.as<float>(), ix->qres.as<float>(),
@@ -633,7 +639,8 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     hp.out_d = ix->cand_d.as<float>();
     hp.out_id = ix->cand_id.as<uint32_t>();
     TREC(0);
-    HIP_TRY(wd ? wv_launch_bf_h16w(&hp, s) : wv_launch_bf_h16(&hp, ns, 0, waves, s));
+    HIP_TRY(wd ? wv_launch_bf_h16w(&hp, s)
+               : (quad ? wv_launch_bf_h16q(&hp, ns / 2, 0, s) : wv_launch_bf_h16(&hp, ns, 0, waves, s)));
     TREC(1);
     fp.cand_d = ix->cand_d.as<float>();
     fp.cand_id = ix->cand_id.as<uint32_t>();
@@ -1328,6 +1335,10 @@ int wv_index_create(int dim, int metric, const wv_config* cfg, uint64_t capacity
         // D > 128: the wide-D kernel, whose chunks are HW_KC 16-k steps
         ix->h16_wide = dim > 16 * wv::H_NS_MAX;
         ix->h16_ns = ix->h16_wide ? (dim + 16 * wv::HW_KC - 1) / (16 * wv::HW_KC) * wv::HW_KC : (dim + 15) / 16;
+        // 16x16x32 pass when D fills whole 32-k steps up to the 16-k granule
+        // (D = 100: 7 steps of 16 stay on the 32x32x16 pass, 112 vs 128)
+        const char* eq = std::getenv("WV_H16_QUAD");
+        ix->h16_quad = !ix->h16_wide && ix->h16_ns % 2 == 0 && !(eq && std::atoi(eq) == 0);
         const size_t ibytes = cap_rows * (size_t)ix->h16_ns * 16 * 2;
         if (ix->ximg16.ensure(ibytes) != hipSuccess || ix->xns.ensure(cap_rows * 4) != hipSuccess ||
             ix->ex_bits.ensure(4) != hipSuccess || ix->qmax.ensure(4) != hipSuccess ||
@@ -1412,14 +1423,14 @@ static int rows_written(wv_index* ix, const uint64_t* d_ids, uint64_t n, uint64_
     if (rebuild) {
         HIP_TRY(hipMemsetAsync(exb, 0, 4, ix->stream));
         HIP_TRY(wv_launch_h16_rows(ix->vecs.as<float>(), ix->ldx, nullptr, ix->n_rows, ix->dim, ix->h16_ns, 1.f,
-                                   ix->h16_sx, nullptr, ix->ximg16.p, 0, exb, nullptr, ix->stream));
+                                   ix->h16_sx, nullptr, ix->ximg16.p, 0, exb, nullptr, ix->h16_quad, ix->stream));
     } else if (d_ids) {
         HIP_TRY(wv_launch_h16_rows(ix->vecs.as<float>(), ix->ldx, d_ids, n, ix->dim, ix->h16_ns, 1.f, ix->h16_sx,
-                                   nullptr, ix->ximg16.p, 0, exb, nullptr, ix->stream));
+                                   nullptr, ix->ximg16.p, 0, exb, nullptr, ix->h16_quad, ix->stream));
     } else {
         HIP_TRY(wv_launch_h16_rows(ix->vecs.as<float>() + first_id * ix->ldx, ix->ldx, nullptr, n, ix->dim,
                                    ix->h16_ns, 1.f, ix->h16_sx, nullptr, ix->ximg16.p, first_id, exb, nullptr,
-                                   ix->stream));
+                                   ix->h16_quad, ix->stream));
     }
     unsigned int eb = 0;
     HIP_TRY(hipMemcpyAsync(&eb, exb, 4, hipMemcpyDeviceToHost, ix->stream));

@@ -1072,16 +1072,17 @@ template <int METRIC>
 __device__ void finalize_one(const BfFinParams& p, int q, float* sd, uint32_t* si, float* qv) {
     const int lane = threadIdx.x & 63;
     const int n_lists = bf_slots_of((uint64_t)(q / p.bq), p.ntiles, p.units_per_block) * p.prod;
-    const int n_ent = n_lists * BF_KP;
-    const float* cd = p.cand_d + (size_t)q * p.n_slots * p.prod * BF_KP;
-    const uint32_t* ci = p.cand_id + (size_t)q * p.n_slots * p.prod * BF_KP;
+    const int kp = p.kp ? p.kp : BF_KP;   // entries per list
+    const int n_ent = n_lists * kp;
+    const float* cd = p.cand_d + (size_t)q * p.n_slots * p.prod * kp;
+    const uint32_t* ci = p.cand_id + (size_t)q * p.n_slots * p.prod * kp;
 
     // bound from the producers' last entries: anything a producer dropped is >= its KP-th key
     float bound = FLT_MAX;
     uint32_t bound_id = WV_NIL;
     for (int l = lane; l < n_lists; l += 64) {
-        const float d = cd[l * BF_KP + BF_KP - 1];
-        const uint32_t i = ci[l * BF_KP + BF_KP - 1];
+        const float d = cd[l * kp + kp - 1];
+        const uint32_t i = ci[l * kp + kp - 1];
         if (key_less(d, i, bound, bound_id)) { bound = d; bound_id = i; }
     }
     for (int m = 32; m >= 1; m >>= 1) {
@@ -1282,15 +1283,16 @@ __device__ void finalize_wide(const BfFinParams& p, int q, float* qv, float* sd,
                               uint32_t* red_i, int* cnt) {
     const int tid = threadIdx.x, nt = blockDim.x;
     const int n_lists = bf_slots_of((uint64_t)(q / p.bq), p.ntiles, p.units_per_block) * p.prod;
-    const int n_ent = n_lists * BF_KP;
-    const float* cd = p.cand_d + (size_t)q * p.n_slots * p.prod * BF_KP;
-    const uint32_t* ci = p.cand_id + (size_t)q * p.n_slots * p.prod * BF_KP;
+    const int kp = p.kp ? p.kp : BF_KP;   // entries per list
+    const int n_ent = n_lists * kp;
+    const float* cd = p.cand_d + (size_t)q * p.n_slots * p.prod * kp;
+    const uint32_t* ci = p.cand_id + (size_t)q * p.n_slots * p.prod * kp;
     // smallest full-list tail: everything a list dropped is >= its tail
     float bound = FLT_MAX;
     uint32_t bound_id = WV_NIL;
     for (int l = tid; l < n_lists; l += nt) {
-        const float d = cd[l * BF_KP + BF_KP - 1];
-        const uint32_t i = ci[l * BF_KP + BF_KP - 1];
+        const float d = cd[l * kp + kp - 1];
+        const uint32_t i = ci[l * kp + kp - 1];
         if (key_less(d, i, bound, bound_id)) { bound = d; bound_id = i; }
     }
     for (int m = 32; m >= 1; m >>= 1) {
@@ -1953,7 +1955,8 @@ hipError_t wv_launch_bf_finalize(const wv::BfFinParams* p, hipStream_t s) {
 
 hipError_t wv_launch_bf_finalize_wide(const wv::BfFinParams* p, hipStream_t s) {
     if (p->nq == 0) return hipSuccess;
-    if (p->k < 1 || p->k > wv::BF_WIDE_KMAX || (uint64_t)p->n_slots * p->prod * wv::BF_KP > 4ull * wv::FINW_NE)
+    if (p->k < 1 || p->k > wv::BF_WIDE_KMAX ||
+        (uint64_t)p->n_slots * p->prod * (p->kp ? p->kp : wv::BF_KP) > 4ull * wv::FINW_NE)
         return hipErrorInvalidValue;
     const size_t lds = (((p->D + 3) & ~3) + 2 * wv::FINW_NE + 9) * sizeof(float);
     hipLaunchKernelGGL(wv::wv_bf_finalize_wide_kernel, dim3(p->nq), dim3(256), lds, s, *p);

@@ -32,6 +32,7 @@
 namespace wv {
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 // LDS-DMA (global_load_lds_dword{,x4}) as inline asm: the destination is the
 // wave-uniform LDS byte address in M0 (+ lane * size).  Written as asm so the
@@ -404,6 +405,7 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
                 // one wave-uniform (rarely taken) branch around the extraction
                 grew = __any(x0 || x1);
                 if (__builtin_expect(grew, 0)) {
+                    WV_DBG_COUNT(3)
                     if (x0) extract(m0, acc00, 0, pt0, rb0);
                     if (x1) extract(m1, acc01, 1, pt1, rb0);
                 }
@@ -441,6 +443,7 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
 #endif
                 const bool any1 = __any(x0 || x1);
                 if (__builtin_expect(any1, 0)) {
+                    WV_DBG_COUNT(3)
                     if (x0) extract(m0, acc10, 0, pt0, rb0 + 32);
                     if (x1) extract(m1, acc11, 1, pt1, rb0 + 32);
                 }
@@ -466,6 +469,358 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
             const size_t base = (size_t)jq1 * per_q + ((size_t)slot * H_PROD + khalf) * BF_KP;
 #pragma unroll
             for (int i = 0; i < BF_KP; ++i) { p.out_d[base + i] = l1d[i]; p.out_id[base + i] = l1i[i]; }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// The same key pass on v_mfma_f32_16x16x32_f16 (NS32 32-k steps, D <= 128 with
+// an even number of 16-k steps).  The chip holds a higher clock on this shape
+// under an MFMA-dense load: a bare loop at the same 64 x 64 tile per wave and
+// two waves per SIMD ran 1.92 PF/s vs 1.67 PF/s for 32x32x16
+// (tools/mfma_shape_bench.cpp, MI355X_MICROARCH.md 'DVFS give-back' item 7).
+// Structure as wv_bf_h16_kernel (LDS-DMA'd 64-row tiles, 3 stages of 2 tiles,
+// the wave's 64 queries as B operands in registers, a half-tile software
+// pipeline); per wave and tile 4 row groups x 4 query groups of 16 x 16
+// accumulators.  Keys: acc[rg][qg][r] is row 16 rg + 4 (lane / 16) + r x query
+// 16 qg + lane % 16, so a lane owns 4 query columns with 8 keys per half tile
+// each, and the 4 lanes of a column (lane % 16 equal) keep HQ_KP-entry lists
+// of disjoint rows; the extraction threshold of a list is the smallest tail of
+// the other three (and the seed / running threshold).
+//
+// Extraction of one column's 8 keys of a half tile (values v: rows rb + 16 (v
+// / 4) + v % 4) into a HQ_KP list, as split_extract16.
+__device__ __forceinline__ void quad_extract8(float& M, floatx4& A, floatx4& B, float (&ld)[HQ_KP],
+                                              uint32_t (&li)[HQ_KP], float pt, uint32_t rb) {
+    const float INF = __builtin_inff();
+    while (M <= fminf(ld[HQ_KP - 1], pt)) {
+        WV_DBG_COUNT(1)
+        // position of M: a descending scan, so among equal keys the lowest row wins
+        uint32_t sel = 0;
+#pragma unroll
+        for (int r = 3; r >= 0; --r) sel = B[r] == M ? 4u + r : sel;
+#pragma unroll
+        for (int r = 3; r >= 0; --r) sel = A[r] == M ? (uint32_t)r : sel;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            A[r] = sel == (uint32_t)r ? INF : A[r];
+            B[r] = sel == 4u + r ? INF : B[r];
+        }
+        uint32_t rbo = rb;   // opaque: the row ids stay in this rare loop
+        asm volatile("" : "+v"(rbo));
+        if (!(M < ld[HQ_KP - 1])) break;
+        uint32_t id = rbo + (sel & 3u) + 16u * (sel >> 2);
+        float d = M;
+#pragma unroll
+        for (int i = 0; i < HQ_KP; ++i) {
+            const bool lt = d < ld[i];
+            const float td = ld[i];
+            const uint32_t ti = li[i];
+            ld[i] = lt ? d : td;
+            li[i] = lt ? id : ti;
+            d = lt ? td : d;
+            id = lt ? ti : id;
+        }
+        M = fminf(fminf(fminf(A[0], A[1]), fminf(A[2], A[3])), fminf(fminf(B[0], B[1]), fminf(B[2], B[3])));
+    }
+}
+
+template <int NS32, bool L2, bool SEED>
+__global__ __launch_bounds__(512, 1) void wv_bf_h16q_kernel(H16Params p) {
+    constexpr int BQ = 512;
+    constexpr int TPS = 2;
+    extern __shared__ uint4 lds[];
+    using St = H16Stage<2 * NS32>;   // same stage bytes: 4 row groups x NS32 32-k steps
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lq = lane >> 4;        // lane quarter: rows 4 lq .. 4 lq + 3 of each 16-row group
+    const int l15 = lane & 15;
+    const uint4* __restrict__ X = reinterpret_cast<const uint4*>(p.X);
+    const uint4* __restrict__ Qg = reinterpret_cast<const uint4*>(p.Q);
+    const bool has_allow = p.allow != nullptr;
+    const float s = p.sx * p.qscale[0];
+    int lb = (int)blockIdx.x;
+    if ((p.locality & 1) && gridDim.x >= 8) {   // bijective XCD remap (blocks b, b + 8, ... share an XCD)
+        const int nwg = (int)gridDim.x, q8 = nwg / 8, r8 = nwg % 8, xcd = (int)blockIdx.x % 8;
+        lb = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (int)blockIdx.x / 8;
+    }
+    const uint64_t u_first = (uint64_t)lb * p.units_per_block;
+    uint64_t u_last = u_first + p.units_per_block;
+    if (u_last > (uint64_t)p.n_qblocks * p.ntiles) u_last = (uint64_t)p.n_qblocks * p.ntiles;
+    const uint32_t lds0 = lds_addr(lds);
+    const int n_ops = (wave < St::IMG_U4 / 64 ? (St::IMG_U4 / 64 - 1 - wave) / 8 + 1 : 0) + ((wave == 0 && L2) ? 1 : 0) +
+                      (wave == 1 ? 1 : 0);
+    auto fill = [&](uint64_t t, int st) {
+        const uint64_t tile = t * (uint64_t)p.tile_stride;
+        const uint32_t dst = lds0 + (uint32_t)(st * St::U4 * 16);
+        const uint4* src = X + tile * St::IMG_U4;
+#pragma unroll
+        for (int i = wave; i < St::IMG_U4 / 64; i += 8) glds16s(src, (uint32_t)(i * 1024 + lane * 16), dst + i * 1024);
+        if (wave == 0) {
+            if (L2) glds4(p.xns + tile * H_BN + lane, dst + St::IMG_U4 * 16);
+        } else if (wave == 1) {
+            const uint32_t* w = lane < 2 ? reinterpret_cast<const uint32_t*>(p.excl + tile) + lane
+                                         : reinterpret_cast<const uint32_t*>(p.allow + tile) + (lane - 2);
+            if (lane < 2 || (lane < 4 && has_allow)) glds4(w, dst + (St::IMG_U4 + 16) * 16);
+        }
+    };
+    auto fill_group = [&](uint64_t t_begin, int g, int ntile) {
+        const int st = g % H_STAGES;
+        int n = 0;
+#pragma unroll
+        for (int j = 0; j < TPS; ++j) {
+            const int t = g * TPS + j;
+            if (t < ntile) { fill(t_begin + t, st * TPS + j); ++n; }
+        }
+        return n * n_ops;
+    };
+    auto tile_lds = [&](int t) { return lds + ((t / TPS) % H_STAGES * TPS + t % TPS) * St::U4; };
+
+    for (uint64_t u = u_first; u < u_last;) {
+        const int qb = (int)(u / p.ntiles);
+        const uint64_t t_begin = u % p.ntiles;
+        uint64_t t_end = t_begin + (u_last - u);
+        if (t_end > p.ntiles) t_end = p.ntiles;
+        u += t_end - t_begin;
+        const int slot = lb - bf_first_block(qb, p.ntiles, p.units_per_block);
+        const int ntile = (int)(t_end - t_begin);
+        int jq[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) jq[g] = qb * BQ + wave * 64 + 16 * g + l15;
+
+        // the wave's 64 queries (4 groups of 16) as B operands
+        uint4 bq[4][NS32];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const uint64_t G = (uint64_t)qb * (BQ / 16) + 4 * wave + g;
+#pragma unroll
+            for (int kk = 0; kk < NS32; ++kk) bq[g][kk] = Qg[(G * NS32 + kk) * 64 + lane];
+        }
+        float tau[4], marg[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            tau[g] = FLT_MAX;
+            marg[g] = 0.f;
+            if (jq[g] < p.nq) {
+                if (!SEED && p.gtau) tau[g] = fminf(FLT_MAX, h16_key_dec(p.gtau[jq[g]]));
+                else if (p.tau) tau[g] = fminf(FLT_MAX, p.tau[jq[g]] * s);
+                if (!SEED && p.kth) marg[g] = p.marg[jq[g]];
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+            for (int kk = 0; kk < NS32; ++kk) asm volatile("" ::"v"(bq[g][kk].x));
+#pragma unroll
+        for (int g = 0; g < 4; ++g) asm volatile("" ::"v"(tau[g]), "v"(marg[g]));
+        float ld[4][HQ_KP];
+        uint32_t li[4][HQ_KP];
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+            for (int i = 0; i < HQ_KP; ++i) { ld[g][i] = FLT_MAX; li[g][i] = WV_NIL; }
+
+        const float INF = __builtin_inff();
+        floatx4 acc[4][4];   // [row group][query group]
+        // one half tile's MFMAs (row groups 2 h, 2 h + 1), the C-in and A
+        // fragments read from LDS first, `between` VALU interleaved
+        auto mfma_half = [&](const uint4* img, int h, auto&& between) {
+            floatx4 xc[2];
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                if (L2) {
+                    const float* xn = reinterpret_cast<const float*>(img + St::IMG_U4) + 16 * (2 * h + r) + 4 * lq;
+                    const float4 v = *reinterpret_cast<const float4*>(xn);
+                    xc[r] = floatx4{v.x, v.y, v.z, v.w};
+                } else {
+                    xc[r] = floatx4{0.f, 0.f, 0.f, 0.f};
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            uint4 a[2][NS32];
+#pragma unroll
+            for (int kk = 0; kk < NS32; ++kk)
+#pragma unroll
+                for (int r = 0; r < 2; ++r) a[r][kk] = img[((2 * h + r) * NS32 + kk) * 64 + lane];
+            between();
+#pragma unroll
+            for (int kk = 0; kk < NS32; ++kk)
+#pragma unroll
+                for (int r = 0; r < 2; ++r)
+#pragma unroll
+                    for (int g = 0; g < 4; ++g)
+                        acc[2 * h + r][g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+                            __builtin_bit_cast(half8, a[r][kk]), __builtin_bit_cast(half8, bq[g][kk]),
+                            kk == 0 ? xc[r] : acc[2 * h + r][g], 0, 0, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 2 * NS32, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+#pragma unroll
+            for (int i = 0; i < 8 * NS32; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+            }
+        };
+        auto tile_ok = [&](const uint4* img, uint64_t t, uint64_t& okw) -> bool {
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(img + St::IMG_U4 + 16);
+            const uint64_t ex = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+            const uint64_t al = has_allow ? ((uint64_t)w[2] | ((uint64_t)w[3] << 32)) : ~0ull;
+            okw = ~ex & al;
+            const uint64_t row0 = t * (uint64_t)p.tile_stride * H_BN;
+            if (row0 + H_BN > p.N) okw &= p.N > row0 ? ((1ull << (p.N - row0)) - 1) : 0ull;
+            return okw != ~0ull || (qb + 1) * BQ > p.nq;
+        };
+        // ineligible keys of half h to +inf (row 16 rg + 4 lq + r of the tile)
+        auto mask_half = [&](int h, uint64_t okw) {
+            uint32_t ow[4];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) ow[g] = (uint32_t)((jq[g] < p.nq ? okw : 0ull) >> (32 * h + 4 * lq));
+            constexpr uint32_t LANE_ROWS = 0x000F000Fu;   // bits r and 16 + r, r < 4
+            bool all = true;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) all = all && (ow[g] & LANE_ROWS) == LANE_ROWS;
+            if (__all(all)) return;
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+#pragma unroll
+                for (int r = 0; r < 2; ++r)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        acc[2 * h + r][g][e] = (ow[g] >> (16 * r + e)) & 1u ? acc[2 * h + r][g][e] : INF;
+        };
+        auto min8 = [&](int h, int g) {
+            const floatx4& A = acc[2 * h][g];
+            const floatx4& B = acc[2 * h + 1][g];
+            return fminf(fminf(fminf(A[0], A[1]), fminf(A[2], A[3])), fminf(fminf(B[0], B[1]), fminf(B[2], B[3])));
+        };
+        // extraction thresholds: min(the other three lanes' tails, tau)
+        float pt[4];
+        auto refresh_pt = [&] {
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const float t = ld[g][HQ_KP - 1];
+                pt[g] = fminf(fminf(__shfl_xor(t, 16, 64), __shfl_xor(t, 32, 64)),
+                              fminf(__shfl_xor(t, 48, 64), tau[g]));
+            }
+        };
+        refresh_pt();
+        // running threshold: entry e - 1 of each of the column's 4 lists, e =
+        // ceil(k / 4): 4 e >= k distinct rows with keys <= their maximum
+        const int ie = (p.kth + 3) >> 2;
+        auto publish = [&] {
+            int ve = ie - 1;
+            asm volatile("" : "+v"(ve));
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                float v = -FLT_MAX;
+#pragma unroll
+                for (int i = 0; i < HQ_KP; ++i) v = ve == i ? ld[g][i] : v;
+                v = fmaxf(v, __shfl_xor(v, 16, 64));
+                v = fmaxf(v, __shfl_xor(v, 32, 64));
+                if (lq == 0 && jq[g] < p.nq && v < FLT_MAX) {
+                    const float u4 = 4.f * 5.9604645e-08f;
+                    atomicMin(&p.gtau[jq[g]], h16_key_enc(v + marg[g] + u4 * (fabsf(v) + marg[g])));
+                }
+            }
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+                if (jq[g] < p.nq) tau[g] = fminf(tau[g], h16_key_dec(__atomic_load_n(&p.gtau[jq[g]], __ATOMIC_RELAXED)));
+            refresh_pt();
+        };
+        const bool running = !SEED && p.kth > 0 && p.gtau != nullptr;
+        // the epilogue of half h of tile t: minima (already in m[]), extraction
+        auto epilogue = [&](int h, const float (&m)[4], uint32_t rb) -> bool {
+            if constexpr (SEED) {
+#pragma unroll
+                for (int g = 0; g < 4; ++g) ld[g][0] = fminf(ld[g][0], m[g]);
+                return false;
+            } else {
+                bool x[4], anyx = false;
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    x[g] = m[g] <= fminf(ld[g][HQ_KP - 1], pt[g]);
+                    anyx = anyx || x[g];
+                }
+                const bool grew = __any(anyx);
+                if (__builtin_expect(grew, 0)) {
+                    WV_DBG_COUNT(3)
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        float mm = m[g];
+                        if (x[g]) quad_extract8(mm, acc[2 * h][g], acc[2 * h + 1][g], ld[g], li[g], pt[g], rb);
+                    }
+                }
+                return grew;
+            }
+        };
+
+        uint64_t okw = 0;
+        bool need_mask = false;
+        const int ngroups = (ntile + TPS - 1) / TPS;
+        int ops_in_flight = 0;
+        if (ngroups > 0) fill_group(t_begin, 0, ntile);
+        if (ngroups > 1) ops_in_flight = fill_group(t_begin, 1, ntile);
+        vm_wait(ops_in_flight);
+        block_barrier();
+        if (ntile > 0) {
+            mfma_half(tile_lds(0), 0, [] {});
+            need_mask = tile_ok(tile_lds(0), t_begin, okw);
+        }
+        for (int t = 0; t < ntile; ++t) {
+            WV_DBG_COUNT(0)
+            const int g = t / TPS;
+            if (t % TPS == 0) ops_in_flight = g + 2 < ngroups ? fill_group(t_begin, g + 2, ntile) : 0;
+            const uint4* img = tile_lds(t);
+            const uint32_t rb0 = (uint32_t)((t_begin + t) * (uint64_t)p.tile_stride * H_BN) + 4 * lq;
+            const bool mask_t = need_mask;
+            const uint64_t mo = okw;
+            // ---- A: H1(t) MFMAs, H0(t) minima ----
+            if (mask_t) mask_half(0, mo);
+            float m[4];
+            mfma_half(img, 1, [&] {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) m[q] = min8(0, q);
+            });
+            // ---- B ----
+            bool grew = epilogue(0, m, rb0);
+            // ---- C: group g + 1 landed; every wave done with group g's stage ----
+            if (t % TPS == TPS - 1 || t == ntile - 1) {
+                if (g + 1 < ngroups) vm_wait(ops_in_flight);
+                block_barrier();
+            }
+            // ---- E: H0(t + 1) MFMAs, H1(t) minima ----
+            if (mask_t) mask_half(1, mo);
+            if (t + 1 < ntile) {
+                mfma_half(tile_lds(t + 1), 0, [&] {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) m[q] = min8(1, q);
+                });
+                need_mask = tile_ok(tile_lds(t + 1), t_begin + t + 1, okw);
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) m[q] = min8(1, q);
+            }
+            // ---- F ----
+            grew = epilogue(1, m, rb0 + 32) || grew;
+            if constexpr (!SEED) {
+                if (running && (t & 15) == 15) publish();
+                else if (grew) refresh_pt();
+            }
+        }
+
+        if constexpr (SEED) {
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+                if (jq[g] < p.nq) p.out_d[((size_t)jq[g] * p.n_slots + slot) * HQ_PROD + lq] = ld[g][0];
+            continue;
+        }
+        const size_t per_q = (size_t)p.n_slots * HQ_PROD * HQ_KP;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            if (jq[g] >= p.nq) continue;
+            const size_t base = (size_t)jq[g] * per_q + ((size_t)slot * HQ_PROD + lq) * HQ_KP;
+#pragma unroll
+            for (int i = 0; i < HQ_KP; ++i) { p.out_d[base + i] = ld[g][i]; p.out_id[base + i] = li[g][i]; }
         }
     }
 }
@@ -675,8 +1030,9 @@ __global__ __launch_bounds__(64) void wv_h16_seed_kernel(H16SeedParams p) {
     const int q = blockIdx.x;
     const int lane = threadIdx.x;
     if (q >= p.nq) return;
-    const int n = bf_slots_of((uint64_t)(q / p.bq), p.ntiles, p.units_per_block) * H_PROD;
-    const float* m = p.minima + (size_t)q * p.n_slots * H_PROD;
+    const int prod = p.prod ? p.prod : H_PROD;
+    const int n = bf_slots_of((uint64_t)(q / p.bq), p.ntiles, p.units_per_block) * prod;
+    const float* m = p.minima + (size_t)q * p.n_slots * prod;
     const float inv_s = 1.0f / (p.sx * p.qscale[0]);
     // k rounds of a wave-wide minimum over the lanes' shares
     float taken = -__builtin_inff();
@@ -745,7 +1101,7 @@ __device__ __forceinline__ float pow2_scale_for(float maxabs) {
 
 __global__ void wv_h16_rows_kernel(const float* in, int ld_in, const uint64_t* ids, uint64_t n, int D, int ns,
                                    float sign, float scale, const unsigned int* scale_from_max, uint16_t* out,
-                                   uint64_t out_row0, unsigned int* res_max_bits, float* res_out) {
+                                   uint64_t out_row0, unsigned int* res_max_bits, float* res_out, int quad) {
     const uint64_t r = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (r >= n) return;
@@ -759,7 +1115,8 @@ __global__ void wv_h16_rows_kernel(const float* in, int ld_in, const uint64_t* i
         const float back = (float)h / scale;
         const float e = x - back;           // exact (Sterbenz) unless h overflowed
         acc = __builtin_fmaf(e, e, acc);
-        out[h16_index(out_row0 + row, k, ns)] = __builtin_bit_cast(uint16_t, h);
+        out[quad ? h16q_index(out_row0 + row, k, ns >> 1) : h16_index(out_row0 + row, k, ns)] =
+            __builtin_bit_cast(uint16_t, h);
     }
     for (int m = 32; m >= 1; m >>= 1) acc += __shfl_xor(acc, m, 64);
     if (lane == 0) {
@@ -806,11 +1163,12 @@ float wv_h16_pow2_scale(float maxabs) {
 
 hipError_t wv_launch_h16_rows(const float* in, int ld_in, const uint64_t* ids, uint64_t n, int D, int ns, float sign,
                               float scale, const unsigned int* scale_from_max, void* out, uint64_t out_row0,
-                              unsigned int* res_max_bits, float* res_out, hipStream_t s) {
+                              unsigned int* res_max_bits, float* res_out, int quad, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    if (ns < 1 || ns > wv::HW_NS_MAX || D > ns * 16) return hipErrorInvalidValue;
+    if (ns < 1 || ns > wv::HW_NS_MAX || D > ns * 16 || (quad && ns % 2)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(wv::wv_h16_rows_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, in, ld_in, ids, n, D,
-                       ns, sign, scale, scale_from_max, static_cast<uint16_t*>(out), out_row0, res_max_bits, res_out);
+                       ns, sign, scale, scale_from_max, static_cast<uint16_t*>(out), out_row0, res_max_bits, res_out,
+                       quad);
     return hipGetLastError();
 }
 
@@ -868,6 +1226,35 @@ hipError_t wv_launch_bf_h16(const wv::H16Params* p, int ns, int seed, int waves,
     }
 #undef WV_H16_LAUNCH
 #undef WV_H16_GO
+    return hipGetLastError();
+}
+
+hipError_t wv_launch_bf_h16q(const wv::H16Params* p, int ns32, int seed, hipStream_t s) {
+    const uint64_t total = (uint64_t)p->n_qblocks * p->ntiles;
+    const unsigned nb = (unsigned)((total + p->units_per_block - 1) / p->units_per_block);
+    if (nb == 0) return hipSuccess;
+    if (ns32 < 1 || ns32 > wv::H_NS_MAX / 2 || !p->X || !p->Q || !p->excl || !p->qscale || p->tile_stride < 1)
+        return hipErrorInvalidValue;
+    const bool l2 = p->metric == WV_METRIC_L2;
+    if (l2 && !p->xns) return hipErrorInvalidValue;
+    const size_t lds = (size_t)wv::H_STAGES * 2 * (4 * ns32 * 64 + 17) * 16;
+#define WV_H16Q_GO(NS, L, S) hipLaunchKernelGGL((wv::wv_bf_h16q_kernel<NS, L, S>), dim3(nb), dim3(512), lds, s, *p);
+#define WV_H16Q_LAUNCH(NS)                     \
+    if (seed) {                                \
+        if (l2) { WV_H16Q_GO(NS, true, true) } \
+        else { WV_H16Q_GO(NS, false, true) }   \
+    } else {                                   \
+        if (l2) { WV_H16Q_GO(NS, true, false) } \
+        else { WV_H16Q_GO(NS, false, false) }  \
+    }
+    switch (ns32) {
+        case 1: WV_H16Q_LAUNCH(1) break;
+        case 2: WV_H16Q_LAUNCH(2) break;
+        case 3: WV_H16Q_LAUNCH(3) break;
+        default: WV_H16Q_LAUNCH(4) break;
+    }
+#undef WV_H16Q_LAUNCH
+#undef WV_H16Q_GO
     return hipGetLastError();
 }
 

@@ -111,6 +111,24 @@ inline uint64_t h16_index(uint64_t row, int k, int ns) {
     return (block * 64 + lane) * 8 + (uint64_t)(k & 7);
 }
 
+// ---- f16 key pass on v_mfma_f32_16x16x32_f16 (wv_bf_h16q_kernel) ------------
+// The same 64-row tiles and 512-query blocks as wv_bf_h16_kernel, in the
+// 16x16x32 operand layout (h16q_index: per 16-row group and 32-k step a 1 KiB
+// block, lane (h, r) holding k 8h .. 8h + 7 of row r).  A lane's keys cover 4
+// query columns (16 q + lane % 16) and rows 4 (lane / 16) ...; the four lanes
+// of a column keep a list of HQ_KP entries each.
+constexpr int HQ_PROD = 4;    // lists per query per slot (the four lane quarters)
+constexpr int HQ_KP = 4;      // entries per list
+
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+inline uint64_t h16q_index(uint64_t row, int k, int ns32) {
+    const uint64_t block = (row >> 4) * (uint64_t)ns32 + (uint64_t)(k >> 5);   // (16-row group, 32-k step)
+    const uint64_t lane = (uint64_t)(((k >> 3) & 3) * 16) + (row & 15);
+    return (block * 64 + lane) * 8 + (uint64_t)(k & 7);
+}
+
 struct H16Params {
     const void* X;            // corpus image (h16_index), rows padded to whole tiles (zeros)
     const void* Q;            // query image (h16_index over query rows), padded to whole H_BQ blocks
@@ -181,6 +199,7 @@ struct H16SeedParams {
     float* tau;               // [nq] out: threshold in true key units (+inf: none)
     unsigned int* gtau;       // [nq] out (nullable): h16_key_enc(tau * s), the running threshold's start
     int bq;                   // queries per block of the pre-pass
+    int prod;                 // minima per query per slot (0: H_PROD)
 };
 
 struct BfFinParams {
@@ -202,6 +221,7 @@ struct BfFinParams {
     int split;              // approximate keys came from the bf16x3 pass (wider eps)
     int bq;                 // queries per block of the key pass (BfParams.bq)
     int prod;               // producers per query per slot (BfParams.prod)
+    int kp;                 // entries per list (0: BF_KP; the 16x16x32 f16 pass: HQ_KP)
     // f16 key pass (h16 = 1): keys are scaled by s = sx * qscale[0]; eps adds
     // ex_max * |B| + xnorm_max * qres[q] (the f16 rounding of corpus and query)
     int h16;

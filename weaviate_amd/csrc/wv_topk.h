@@ -13,10 +13,19 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 // v_min3_f32 without the IEEE canonicalisation hipcc wraps around fminf of
 // MFMA results (a NaN key never wins a comparison either way)
 #ifdef WV_BF_DBG_ITERS
-// ablation builds only: wave-level counts of tiles (0) and extract-loop iterations (1)
-__device__ unsigned long long wv_dbg_counts[2];
-#define WV_DBG_COUNT(i) if (__lane_id() == 0) atomicAdd(&wv_dbg_counts[i], 1ull);
-extern "C" void wv_dbg_read(unsigned long long* out) { hipMemcpyFromSymbol(out, HIP_SYMBOL(wv_dbg_counts), 16); }
+// ablation builds only: wave-level counts of tiles (0), extract-loop rounds
+// (1), lanes that ran a round (2) and extraction calls (3); counted by the
+// first active lane (the loops are divergent)
+__device__ unsigned long long wv_dbg_counts[4];
+#define WV_DBG_COUNT(i)                                                                        \
+    {                                                                                          \
+        const uint64_t dbg_b = __ballot(1);                                                    \
+        if (__lane_id() == __builtin_ctzll(dbg_b)) {                                           \
+            atomicAdd(&wv_dbg_counts[i], 1ull);                                                \
+            if ((i) == 1) atomicAdd(&wv_dbg_counts[2], (unsigned long long)__popcll(dbg_b));   \
+        }                                                                                      \
+    }
+extern "C" void wv_dbg_read(unsigned long long* out) { hipMemcpyFromSymbol(out, HIP_SYMBOL(wv_dbg_counts), 32); }
 #else
 #define WV_DBG_COUNT(i)
 #endif
