@@ -273,8 +273,12 @@ def exact_roofline(args, ix, kern_ms, stats, D, n_allowed, n_local, NQ):
         kind = "h16" if 8 * n_allowed >= n_local else "fp32"
     else:
         kind = "fp32"
-    peak, kname, kp = {"h16": (F16_MFMA_PEAK_TF, "wv_bf_h16_kernel" if D <= 128 else "wv_bf_h16w_kernel",
-                               "f16 MFMA keys (peak = f16 dense)"),
+    # WV_H16_QUAD=1, D <= 128 with an even number of 16-k steps: the 16x16x32 kernel (wv_api.hip h16_quad)
+    # (k <= 32; wider k runs the 32x32x16 kernel)
+    quad = D <= 128 and ((D + 15) // 16) % 2 == 0 and os.environ.get("WV_H16_QUAD", "0") == "1" and args.k <= 32
+    peak, kname, kp = {"h16": (F16_MFMA_PEAK_TF,
+                               "wv_bf_h16w_kernel" if D > 128 else ("wv_bf_h16q_kernel" if quad else "wv_bf_h16_kernel"),
+                               "f16 MFMA keys (%s; peak = f16 dense)" % ("16x16x32" if quad else "32x32x16")),
                        "split": (BF16_MFMA_PEAK_TF / 3, "wv_bf_split_kernel", "bf16x3 (peak = bf16 dense / 3)"),
                        "fp32": (FP32_MFMA_PEAK_TF, "wv_bf_mfma_kernel", "fp32 MFMA")}[kind]
     roof = {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 2), "peak": round(peak, 1),

@@ -54,6 +54,11 @@ int main(int argc, char** argv) {
         hipEventElapsedTime(&w, a, b);
         km += m; kf += f; ks += sd; wall += w;
     }
+    // one more batch with the fallback on: WV_ABLATE_NO_FALLBACK skips (and
+    // does not count) the uncertified queries
+    unsetenv("WV_ABLATE_NO_FALLBACK");
+    wv_search_batch_device(ix, dq, nq, 10, 0, nullptr, 0, 0, WV_MODE_EXACT, di, dd, dn, s);
+    hipStreamSynchronize(s);
     uint64_t de, ex, fb;
     wv_last_batch_stats(ix, &de, &ex, &fb);
     std::vector<uint64_t> ids(10);
@@ -63,10 +68,10 @@ int main(int argc, char** argv) {
            2.0 * D * N * nq / (km / it * 1e-3) / 1e12, (unsigned long long)fb, (unsigned long long)ids[0],
            (unsigned long long)ids[1]);
     if (wv_dbg_read) {
-        // (summed over the 2 warm-up + `it` timed batches)
+        // (summed over the 2 warm-up + `it` timed batches + the fallback-counting one)
         unsigned long long c[4] = {0, 0, 0, 0};
         wv_dbg_read(c);
-        const double nb = 2.0 + it;
+        const double nb = 3.0 + it;
         printf("%-16s per batch: wave-tiles %.0f  extraction calls %.0f  wave rounds %.0f  lane rounds %.0f  "
                "(calls per wave-tile %.3f, lanes per round %.2f)\n", name, c[0] / nb, c[3] / nb, c[1] / nb, c[2] / nb,
                c[0] ? (double)c[3] / (double)c[0] : 0.0, c[1] ? (double)c[2] / (double)c[1] : 0.0);

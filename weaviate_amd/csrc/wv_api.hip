@@ -54,7 +54,7 @@ hipError_t wv_launch_absmax(const float* in, int ld, uint64_t n, int D, unsigned
 hipError_t wv_launch_h16_qscale(const unsigned int* max_bits, float bsign, float* qscale, hipStream_t s);
 hipError_t wv_launch_h16_xns(const float* xnorm, uint64_t n, float sx, const float* qscale, float* xns, hipStream_t s);
 hipError_t wv_launch_bf_h16(const wv::H16Params* p, int ns, int seed, int waves, hipStream_t s);
-hipError_t wv_launch_bf_h16q(const wv::H16Params* p, int ns32, int seed, hipStream_t s);
+hipError_t wv_launch_bf_h16q(const wv::H16Params* p, int ns32, int seed, int waves, hipStream_t s);
 hipError_t wv_launch_bf_h16w(const wv::H16Params* p, hipStream_t s);
 hipError_t wv_launch_h16_seed(const wv::H16SeedParams* p, hipStream_t s);
 hipError_t wv_launch_h16_margin(int metric, int D, const float* qnorm, const float* qres, float xnorm_max,
@@ -231,6 +231,7 @@ struct wv_index {
     int h16_ns = 0;
     float h16_sx = 0.f, h16_ex = 0.f;
     DevBuf ximg16, xns, qimg16, qres, qmax, qscale, tau, gtau, marg, allow_pad, ex_bits;
+    DevBuf ximg16q;         // the corpus image in the 16x16x32 layout (h16_quad), beside ximg16
     float maxnorm_host = 0.f;   // max |x| (rounded up), cached after every row write
     DevBuf xnorm;           // [capacity]
     DevBuf maxnorm;         // unsigned bits of max |x|
@@ -485,10 +486,13 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
             uint64_t* d_out_ids, float* d_out_d, int32_t* d_out_n, hipStream_t s, std::vector<int32_t>& fails) {
     const int ns = ix->h16_ns;
     const bool wd = ix->h16_wide;   // D > 128: the wide-D kernel
-    const bool quad = ix->h16_quad;   // the 16x16x32 kernel (8 waves, HQ_KP-entry lists)
+    // the 16x16x32 kernel (HQ_KP-entry lists) for k <= FIN_KF; wider k on the
+    // 32x32x16 kernel, whose 8-entry lists keep the certificate's fallback
+    // rate low at k = 100..256 (4-entry lists fill with top-k keys too often)
+    const bool quad = ix->h16_quad && k <= wv::FIN_KF;
     // D <= 128: 8-wave (512-query) workgroups, one per CU; WV_H16_WAVES=4:
     // 4-wave (256-query) workgroups, two independent ones per CU
-    const int waves = !quad && std::getenv("WV_H16_WAVES") && std::atoi(std::getenv("WV_H16_WAVES")) == 4 ? 4 : 8;
+    const int waves = std::getenv("WV_H16_WAVES") && std::atoi(std::getenv("WV_H16_WAVES")) == 4 ? 4 : 8;
     const int wg_per_cu = wd ? 1 : 8 / waves;
     const int tile_rows = wd ? wv::HW_BN : wv::H_BN, bq = wd ? wv::HW_BQ : waves * 64;
     const int prod = wd ? wv::HW_PROD : (quad ? wv::HQ_PROD : wv::H_PROD);
@@ -525,7 +529,7 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
         HIP_TRY(wv_launch_h16_xns(ix->xnorm.as<float>(), ntl * tile_rows, ix->h16_sx, ix->qscale.as<float>(),
                                   ix->xns.as<float>(), s));
     wv::H16Params hp{};
-    hp.X = ix->ximg16.p;
+    hp.X = quad ? ix->ximg16q.p : ix->ximg16.p;
     hp.Q = ix->qimg16.p;
     hp.xns = ix->xns.as<float>();
     hp.excl = ix->excl.as<uint64_t>();
@@ -589,7 +593,7 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
         hp.out_d = ix->cand_d.as<float>();
         hp.out_id = nullptr;
         TREC(6);
-        HIP_TRY(quad ? wv_launch_bf_h16q(&hp, ns / 2, 1, s) : wv_launch_bf_h16(&hp, ns, 1, waves, s));
+        HIP_TRY(quad ? wv_launch_bf_h16q(&hp, ns / 2, 1, waves, s) : wv_launch_bf_h16(&hp, ns, 1, waves, s));
         wv::H16SeedParams sp{};
         sp.minima = ix->cand_d.as<float>();
         sp.n_slots = ss.n_slots;
@@ -628,7 +632,9 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     // (with the seed's threshold the running one only adds work: measured
     // 3.048 vs 3.092 ms per 1M x 10k key pass; without a seed -- corpora below
     // 64 * H_SAMPLE tiles -- it cuts the pass 4.13 -> 3.43 ms at 1M)
-    hp.kth = k <= prod * kp && !seed && !wd && !std::getenv("WV_H16_NO_RUNNING") ? k : 0;
+    hp.kth = k <= prod * kp && (!seed || std::getenv("WV_H16_RUN_SEED")) && !wd && !std::getenv("WV_H16_NO_RUNNING")
+                 ? k
+                 : 0;
     if (hp.kth) {
         HIP_TRY(ix->marg.ensure((size_t)nq * 4));
         HIP_TRY(wv_launch_h16_margin(ix->metric, ix->dim, ix->q_nrm2.as<float>(), ix->qres.as<float>(),
@@ -640,7 +646,7 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     hp.out_id = ix->cand_id.as<uint32_t>();
     TREC(0);
     HIP_TRY(wd ? wv_launch_bf_h16w(&hp, s)
-               : (quad ? wv_launch_bf_h16q(&hp, ns / 2, 0, s) : wv_launch_bf_h16(&hp, ns, 0, waves, s)));
+               : (quad ? wv_launch_bf_h16q(&hp, ns / 2, 0, waves, s) : wv_launch_bf_h16(&hp, ns, 0, waves, s)));
     TREC(1);
     fp.cand_d = ix->cand_d.as<float>();
     fp.cand_id = ix->cand_id.as<uint32_t>();
@@ -1335,18 +1341,22 @@ int wv_index_create(int dim, int metric, const wv_config* cfg, uint64_t capacity
         // D > 128: the wide-D kernel, whose chunks are HW_KC 16-k steps
         ix->h16_wide = dim > 16 * wv::H_NS_MAX;
         ix->h16_ns = ix->h16_wide ? (dim + 16 * wv::HW_KC - 1) / (16 * wv::HW_KC) * wv::HW_KC : (dim + 15) / 16;
-        // 16x16x32 pass when D fills whole 32-k steps up to the 16-k granule
-        // (D = 100: 7 steps of 16 stay on the 32x32x16 pass, 112 vs 128)
+        // opt-in 16x16x32 pass (WV_H16_QUAD=1) when D fills whole 32-k steps:
+        // 4.3 % faster key pass, but its 4-entry lists fail the certificate
+        // for ~0.3 % of the queries (31 of 10k at 1M x 128), whose device
+        // fallback costs more than the pass gains
         const char* eq = std::getenv("WV_H16_QUAD");
-        ix->h16_quad = !ix->h16_wide && ix->h16_ns % 2 == 0 && !(eq && std::atoi(eq) == 0);
+        ix->h16_quad = !ix->h16_wide && ix->h16_ns % 2 == 0 && eq && std::atoi(eq) == 1;
         const size_t ibytes = cap_rows * (size_t)ix->h16_ns * 16 * 2;
         if (ix->ximg16.ensure(ibytes) != hipSuccess || ix->xns.ensure(cap_rows * 4) != hipSuccess ||
+            (ix->h16_quad && ix->ximg16q.ensure(ibytes) != hipSuccess) ||
             ix->ex_bits.ensure(4) != hipSuccess || ix->qmax.ensure(4) != hipSuccess ||
             ix->qscale.ensure(4) != hipSuccess) {
             wv_index_destroy(ix);
             return fail(WV_EOOM, "wv_index_create: device allocation failed");
         }
         (void)hipMemsetAsync(ix->ximg16.p, 0, ibytes, ix->stream);
+        if (ix->h16_quad) (void)hipMemsetAsync(ix->ximg16q.p, 0, ibytes, ix->stream);
         (void)hipMemsetAsync(ix->xns.p, 0, cap_rows * 4, ix->stream);
         (void)hipMemsetAsync(ix->ex_bits.p, 0, 4, ix->stream);
     }
@@ -1376,7 +1386,7 @@ int wv_index_destroy(wv_index* ix) {
                       &ix->sort_tmp, &ix->g_idx, &ix->g_q, &ix->g_allow, &ix->g_ids, &ix->g_d, &ix->g_n, &ix->g_cnt,
                       &ix->out_ids, &ix->out_d, &ix->out_n, &ix->stage, &ix->fail_thr, &ix->fb_idx, &ix->fb_d, &ix->fb_i, &ix->fb_n, &ix->fb_of,
                       &ix->ac_cnt, &ix->ac_off, &ix->rowidx, &ix->pq_cent, &ix->pq_codes, &ix->pk_key,
-                      &ix->pk_dist, &ix->pk_val, &ix->pk_skey, &ix->pk_sval, &ix->pk_off, &ix->ximg16, &ix->xns,
+                      &ix->pk_dist, &ix->pk_val, &ix->pk_skey, &ix->pk_sval, &ix->pk_off, &ix->ximg16, &ix->ximg16q, &ix->xns,
                       &ix->qimg16, &ix->qres, &ix->qmax, &ix->qscale, &ix->tau, &ix->gtau, &ix->marg, &ix->allow_pad, &ix->ex_bits,
                       &ix->delta, &ix->dmask, &ix->dl_ids, &ix->dl_d, &ix->dl_n, &ix->dq_tmp, &ix->b_tgt, &ix->b_ci,
                       &ix->b_cd, &ix->b_cn, &ix->b_cnt0, &ix->b_cntu, &ix->b_rk, &ix->b_rn, &ix->b_rk2, &ix->b_rn2,
@@ -1420,17 +1430,21 @@ static int rows_written(wv_index* ix, const uint64_t* d_ids, uint64_t n, uint64_
     const bool rebuild = ix->h16_sx != 0.f && sx < ix->h16_sx;
     if (ix->h16_sx == 0.f || rebuild) ix->h16_sx = sx;
     unsigned int* exb = ix->ex_bits.as<unsigned int>();
-    if (rebuild) {
-        HIP_TRY(hipMemsetAsync(exb, 0, 4, ix->stream));
-        HIP_TRY(wv_launch_h16_rows(ix->vecs.as<float>(), ix->ldx, nullptr, ix->n_rows, ix->dim, ix->h16_ns, 1.f,
-                                   ix->h16_sx, nullptr, ix->ximg16.p, 0, exb, nullptr, ix->h16_quad, ix->stream));
-    } else if (d_ids) {
-        HIP_TRY(wv_launch_h16_rows(ix->vecs.as<float>(), ix->ldx, d_ids, n, ix->dim, ix->h16_ns, 1.f, ix->h16_sx,
-                                   nullptr, ix->ximg16.p, 0, exb, nullptr, ix->h16_quad, ix->stream));
-    } else {
-        HIP_TRY(wv_launch_h16_rows(ix->vecs.as<float>() + first_id * ix->ldx, ix->ldx, nullptr, n, ix->dim,
-                                   ix->h16_ns, 1.f, ix->h16_sx, nullptr, ix->ximg16.p, first_id, exb, nullptr,
-                                   ix->h16_quad, ix->stream));
+    if (rebuild) HIP_TRY(hipMemsetAsync(exb, 0, 4, ix->stream));
+    // both layouts: 32x32x16 (ximg16) and, with h16_quad, 16x16x32 (ximg16q)
+    for (int quad = 0; quad <= (ix->h16_quad ? 1 : 0); ++quad) {
+        void* img = quad ? ix->ximg16q.p : ix->ximg16.p;
+        if (rebuild) {
+            HIP_TRY(wv_launch_h16_rows(ix->vecs.as<float>(), ix->ldx, nullptr, ix->n_rows, ix->dim, ix->h16_ns, 1.f,
+                                       ix->h16_sx, nullptr, img, 0, exb, nullptr, quad, ix->stream));
+        } else if (d_ids) {
+            HIP_TRY(wv_launch_h16_rows(ix->vecs.as<float>(), ix->ldx, d_ids, n, ix->dim, ix->h16_ns, 1.f, ix->h16_sx,
+                                       nullptr, img, 0, exb, nullptr, quad, ix->stream));
+        } else {
+            HIP_TRY(wv_launch_h16_rows(ix->vecs.as<float>() + first_id * ix->ldx, ix->ldx, nullptr, n, ix->dim,
+                                       ix->h16_ns, 1.f, ix->h16_sx, nullptr, img, first_id, exb, nullptr, quad,
+                                       ix->stream));
+        }
     }
     unsigned int eb = 0;
     HIP_TRY(hipMemcpyAsync(&eb, exb, 4, hipMemcpyDeviceToHost, ix->stream));

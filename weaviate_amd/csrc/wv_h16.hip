@@ -525,10 +525,13 @@ __device__ __forceinline__ void quad_extract8(float& M, floatx4& A, floatx4& B, 
     }
 }
 
-template <int NS32, bool L2, bool SEED>
-__global__ __launch_bounds__(512, 1) void wv_bf_h16q_kernel(H16Params p) {
-    constexpr int BQ = 512;
-    constexpr int TPS = 2;
+// WAVES = 8: one 512-query workgroup per CU, 2 tiles per LDS stage; WAVES = 4:
+// two independent 256-query workgroups per CU (their own barriers), 1 tile
+// per stage.
+template <int NS32, bool L2, bool SEED, int WAVES>
+__global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16q_kernel(H16Params p) {
+    constexpr int BQ = WAVES * 64;
+    constexpr int TPS = WAVES == 8 ? 2 : 1;
     extern __shared__ uint4 lds[];
     using St = H16Stage<2 * NS32>;   // same stage bytes: 4 row groups x NS32 32-k steps
     const int tid = threadIdx.x;
@@ -549,14 +552,14 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16q_kernel(H16Params p) {
     uint64_t u_last = u_first + p.units_per_block;
     if (u_last > (uint64_t)p.n_qblocks * p.ntiles) u_last = (uint64_t)p.n_qblocks * p.ntiles;
     const uint32_t lds0 = lds_addr(lds);
-    const int n_ops = (wave < St::IMG_U4 / 64 ? (St::IMG_U4 / 64 - 1 - wave) / 8 + 1 : 0) + ((wave == 0 && L2) ? 1 : 0) +
-                      (wave == 1 ? 1 : 0);
+    const int n_ops = (wave < St::IMG_U4 / 64 ? (St::IMG_U4 / 64 - 1 - wave) / WAVES + 1 : 0) +
+                      ((wave == 0 && L2) ? 1 : 0) + (wave == 1 ? 1 : 0);
     auto fill = [&](uint64_t t, int st) {
         const uint64_t tile = t * (uint64_t)p.tile_stride;
         const uint32_t dst = lds0 + (uint32_t)(st * St::U4 * 16);
         const uint4* src = X + tile * St::IMG_U4;
 #pragma unroll
-        for (int i = wave; i < St::IMG_U4 / 64; i += 8) glds16s(src, (uint32_t)(i * 1024 + lane * 16), dst + i * 1024);
+        for (int i = wave; i < St::IMG_U4 / 64; i += WAVES) glds16s(src, (uint32_t)(i * 1024 + lane * 16), dst + i * 1024);
         if (wave == 0) {
             if (L2) glds4(p.xns + tile * H_BN + lane, dst + St::IMG_U4 * 16);
         } else if (wave == 1) {
@@ -691,7 +694,11 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16q_kernel(H16Params p) {
         auto min8 = [&](int h, int g) {
             const floatx4& A = acc[2 * h][g];
             const floatx4& B = acc[2 * h + 1][g];
-            return fminf(fminf(fminf(A[0], A[1]), fminf(A[2], A[3])), fminf(fminf(B[0], B[1]), fminf(B[2], B[3])));
+#ifdef WV_H16_ABLATE_NO_MIN
+            return fminf(A[0], B[0]);   // (both accumulators stay live)
+#endif
+            // 4 VALU: two independent v_min3, one v_min, a final v_min3
+            return min3_raw(min3_raw(A[0], A[1], A[2]), min3_raw(A[3], B[0], B[1]), fminf(B[2], B[3]));
         };
         // extraction thresholds: min(the other three lanes' tails, tau)
         float pt[4];
@@ -735,6 +742,10 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16q_kernel(H16Params p) {
                 for (int g = 0; g < 4; ++g) ld[g][0] = fminf(ld[g][0], m[g]);
                 return false;
             } else {
+#ifdef WV_H16_ABLATE_NO_EXTRACT
+                if (m[0] == 1234.5f) ld[0][0] = m[1] + m[2] + m[3] + pt[0];
+                return false;
+#endif
                 bool x[4], anyx = false;
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
@@ -769,7 +780,9 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16q_kernel(H16Params p) {
         for (int t = 0; t < ntile; ++t) {
             WV_DBG_COUNT(0)
             const int g = t / TPS;
+#ifndef WV_H16_ABLATE_NO_FILL
             if (t % TPS == 0) ops_in_flight = g + 2 < ngroups ? fill_group(t_begin, g + 2, ntile) : 0;
+#endif
             const uint4* img = tile_lds(t);
             const uint32_t rb0 = (uint32_t)((t_begin + t) * (uint64_t)p.tile_stride * H_BN) + 4 * lq;
             const bool mask_t = need_mask;
@@ -1229,7 +1242,7 @@ hipError_t wv_launch_bf_h16(const wv::H16Params* p, int ns, int seed, int waves,
     return hipGetLastError();
 }
 
-hipError_t wv_launch_bf_h16q(const wv::H16Params* p, int ns32, int seed, hipStream_t s) {
+hipError_t wv_launch_bf_h16q(const wv::H16Params* p, int ns32, int seed, int waves, hipStream_t s) {
     const uint64_t total = (uint64_t)p->n_qblocks * p->ntiles;
     const unsigned nb = (unsigned)((total + p->units_per_block - 1) / p->units_per_block);
     if (nb == 0) return hipSuccess;
@@ -1237,8 +1250,11 @@ hipError_t wv_launch_bf_h16q(const wv::H16Params* p, int ns32, int seed, hipStre
         return hipErrorInvalidValue;
     const bool l2 = p->metric == WV_METRIC_L2;
     if (l2 && !p->xns) return hipErrorInvalidValue;
-    const size_t lds = (size_t)wv::H_STAGES * 2 * (4 * ns32 * 64 + 17) * 16;
-#define WV_H16Q_GO(NS, L, S) hipLaunchKernelGGL((wv::wv_bf_h16q_kernel<NS, L, S>), dim3(nb), dim3(512), lds, s, *p);
+    if (waves != 8 && waves != 4) return hipErrorInvalidValue;
+    const size_t lds = (size_t)wv::H_STAGES * (waves == 8 ? 2 : 1) * (4 * ns32 * 64 + 17) * 16;
+#define WV_H16Q_GO(NS, L, S)                                                                                  \
+    if (waves == 8) hipLaunchKernelGGL((wv::wv_bf_h16q_kernel<NS, L, S, 8>), dim3(nb), dim3(512), lds, s, *p); \
+    else hipLaunchKernelGGL((wv::wv_bf_h16q_kernel<NS, L, S, 4>), dim3(nb), dim3(256), lds, s, *p);
 #define WV_H16Q_LAUNCH(NS)                     \
     if (seed) {                                \
         if (l2) { WV_H16Q_GO(NS, true, true) } \
