@@ -36,7 +36,8 @@ hipError_t wv_launch_rownorm(const float* X, uint64_t N, int D, int ldx, float* 
                              hipStream_t s);
 hipError_t wv_launch_normalize(const float* in, float* out, uint64_t n, int D, int ld, hipStream_t s);
 hipError_t wv_launch_scale(const float* in, float* out, uint64_t n, float scale, hipStream_t s);
-hipError_t wv_launch_qnorm(const float* Q, int nq, int D, int ldq, int metric, float* out, hipStream_t s);
+hipError_t wv_launch_qnorm(const float* Q, int nq, int D, int ldq, int metric, float* out, unsigned int* absmax_bits,
+                           hipStream_t s);
 hipError_t wv_launch_hnsw(const wv::HnswParams* p, int waves_per_block, hipStream_t s);
 hipError_t wv_launch_build_search(const wv::BuildParams* b, int waves_per_block, hipStream_t s);
 hipError_t wv_launch_build_select(const wv::BuildParams* b, hipStream_t s);
@@ -516,12 +517,13 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     HIP_TRY(ix->q_nrm2.ensure((size_t)nq * 4));
     HIP_TRY(ix->fail.ensure((size_t)nq * 4));
     HIP_TRY(ix->fail_thr.ensure((size_t)nq * 4));
-    HIP_TRY(wv_launch_qnorm(d_q, nq, ix->dim, ix->dpad, ix->metric, ix->q_nrm2.as<float>(), s));
-    // B = f16(s_q b), b = -2q (L2) or -q; s_q from the batch's max |b|
+    // |q|^2 and, in the same pass, the batch's max |q_i|; B = f16(s_q b),
+    // b = -2q (L2) or -q, s_q from max |b|
     const float bsign = ix->metric == WV_L2_SQUARED ? -2.f : -1.f;
     HIP_TRY(hipMemsetAsync(ix->qmax.p, 0, 4, s));
+    HIP_TRY(wv_launch_qnorm(d_q, nq, ix->dim, ix->dpad, ix->metric, ix->q_nrm2.as<float>(),
+                            ix->qmax.as<unsigned int>(), s));
     HIP_TRY(hipMemsetAsync(ix->qimg16.p, 0, qbytes, s));
-    HIP_TRY(wv_launch_absmax(d_q, ix->dpad, nq, ix->dim, ix->qmax.as<unsigned int>(), s));
     HIP_TRY(wv_launch_h16_qscale(ix->qmax.as<unsigned int>(), bsign, ix->qscale.as<float>(), s));
     HIP_TRY(wv_launch_h16_rows(d_q, ix->dpad, nullptr, nq, ix->dim, ns, bsign, 1.f, ix->qmax.as<unsigned int>(),
                                ix->qimg16.p, 0, nullptr, ix->qres.as<float>(), quad, s));
@@ -779,7 +781,7 @@ int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
         HIP_TRY(ix->cand_id.ensure((size_t)nq * n_lists * wv::BF_KP * 4));
         HIP_TRY(ix->q_nrm2.ensure((size_t)nq * 4));
         HIP_TRY(ix->fail.ensure((size_t)nq * 4));
-        HIP_TRY(wv_launch_qnorm(d_q, nq, ix->dim, ix->dpad, ix->metric, ix->q_nrm2.as<float>(), s));
+        HIP_TRY(wv_launch_qnorm(d_q, nq, ix->dim, ix->dpad, ix->metric, ix->q_nrm2.as<float>(), nullptr, s));
         // B operand in whole bq-row query blocks, zero rows past nq: -2q
         // (L2) or -q, as fp32 rows or (split key pass: whole-corpus or shared
         // allow list scans) as the native bf16 hi/lo image

@@ -1859,14 +1859,37 @@ __global__ void wv_scale_rows_kernel(const float* in, float* out, uint64_t n, fl
 }
 
 // |q|^2 for L2, |q| for dot/cosine (feeds eps only)
-__global__ void wv_qnorm_kernel(const float* Q, int nq, int D, int ldq, int metric, float* out) {
-    const int r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= nq) return;
-    float s = 0.f;
-    for (int i = 0; i < D; ++i) s = __builtin_fmaf(Q[(size_t)r * ldq + i], Q[(size_t)r * ldq + i], s);
+// |q|^2 (L2) or |q| per query row: one wave per row (coalesced), optionally
+// the batch's max |q_i| (absmax_bits: float bits, one atomicMax per block).
+// The summation order is the wave's tree: the certificate's eps bounds the
+// rounding of any order (D u sum q_i^2).
+__global__ __launch_bounds__(256) void wv_qnorm_kernel(const float* Q, int nq, int D, int ldq, int metric, float* out,
+                                                       unsigned int* absmax_bits) {
+    __shared__ float wmax[4];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int r = blockIdx.x * 4 + w;
+    float s = 0.f, m = 0.f;
+    if (r < nq) {
+        const float* q = Q + (size_t)r * ldq;
+        for (int i = lane; i < D; i += 64) {
+            const float v = q[i];
+            s = __builtin_fmaf(v, v, s);
+            m = fmaxf(m, fabsf(v));
+        }
+    }
+    for (int o = 32; o >= 1; o >>= 1) {
+        s += __shfl_xor(s, o, 64);
+        m = fmaxf(m, __shfl_xor(m, o, 64));
+    }
     // L2: |q|^2 enters the bound additively (no inflation; eps covers its
     // rounding).  dot/cosine: |q| only scales eps, so it is rounded up.
-    out[r] = metric == WV_METRIC_L2 ? s : sqrtf(s * (1.0f + 1e-6f)) * (1.0f + 1e-6f);
+    if (r < nq && lane == 0) out[r] = metric == WV_METRIC_L2 ? s : sqrtf(s * (1.0f + 1e-6f)) * (1.0f + 1e-6f);
+    if (absmax_bits) {
+        if (lane == 0) wmax[w] = m;
+        __syncthreads();
+        if (threadIdx.x == 0)
+            atomicMax(absmax_bits, __float_as_uint(fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]))));
+    }
 }
 
 }  // namespace wv
@@ -2040,9 +2063,11 @@ hipError_t wv_launch_scale(const float* in, float* out, uint64_t n, float scale,
     return hipGetLastError();
 }
 
-hipError_t wv_launch_qnorm(const float* Q, int nq, int D, int ldq, int metric, float* out, hipStream_t s) {
+hipError_t wv_launch_qnorm(const float* Q, int nq, int D, int ldq, int metric, float* out, unsigned int* absmax_bits,
+                           hipStream_t s) {
     if (nq == 0) return hipSuccess;
-    hipLaunchKernelGGL(wv::wv_qnorm_kernel, dim3((nq + 255) / 256), dim3(256), 0, s, Q, nq, D, ldq, metric, out);
+    hipLaunchKernelGGL(wv::wv_qnorm_kernel, dim3((nq + 3) / 4), dim3(256), 0, s, Q, nq, D, ldq, metric, out,
+                       absmax_bits);
     return hipGetLastError();
 }
 
