@@ -1068,7 +1068,10 @@ __global__ __launch_bounds__(768, 1) void wv_bf_split3_kernel(BfParams p) {
 // ---------------------------------------------------------------------------
 // Finalize: one wave per query.
 
-template <int METRIC>
+// FAST: every query has <= 256 list entries (n_slots * prod * kp): the
+// bitonic selection; otherwise per-lane top-KF runs and a KF-round merge
+// (separate instantiations: one kernel holding both needs 210 VGPRs)
+template <int METRIC, bool FAST>
 __device__ void finalize_one(const BfFinParams& p, int q, float* sd, uint32_t* si, float* qv) {
     const int lane = threadIdx.x & 63;
     const int n_lists = bf_slots_of((uint64_t)(q / p.bq), p.ntiles, p.units_per_block) * p.prod;
@@ -1091,49 +1094,102 @@ __device__ void finalize_one(const BfFinParams& p, int q, float* sd, uint32_t* s
         if (key_less(od, oi, bound, bound_id)) { bound = od; bound_id = oi; }
     }
 
-    // select the FIN_KF smallest keys among all entries: repeated wave-wide
-    // tournament over per-lane sorted runs would be faster; this keeps a
-    // sorted top-KF list in LDS, one candidate per lane per round.
-    if (lane < FIN_KF) { sd[lane] = FLT_MAX; si[lane] = WV_NIL; }
-    __builtin_amdgcn_wave_barrier();
-    // each lane scans its share and keeps a private top-KF in LDS-free registers
-    float td[FIN_KF];
-    uint32_t ti[FIN_KF];
+    // select the FIN_KF smallest (key, id) among all entries
+    if constexpr (FAST) {
+        // a wave-wide bitonic sort of the (<= 256) entries, element i = 64 j +
+        // lane in register j: strides >= 64 inside the lane, smaller ones by
+        // shuffles; the FIN_KF smallest end in lanes 0 .. FIN_KF - 1 of j = 0
+        float kd[4];
+        uint32_t ki[4];
 #pragma unroll
-    for (int i = 0; i < FIN_KF; ++i) { td[i] = FLT_MAX; ti[i] = WV_NIL; }
-    for (int e = lane; e < n_ent; e += 64) {
-        float d = cd[e];
-        uint32_t id = ci[e];
-        if (id == WV_NIL) continue;
-        if (!key_less(d, id, td[FIN_KF - 1], ti[FIN_KF - 1])) continue;
-#pragma unroll
-        for (int i = 0; i < FIN_KF; ++i) {
-            const bool lt = key_less(d, id, td[i], ti[i]);
-            const float a = td[i];
-            const uint32_t b = ti[i];
-            td[i] = lt ? d : td[i];
-            ti[i] = lt ? id : ti[i];
-            d = lt ? a : d;
-            id = lt ? b : id;
+        for (int j = 0; j < 4; ++j) {
+            const int e = 64 * j + lane;
+            kd[j] = FLT_MAX;
+            ki[j] = WV_NIL;
+            if (e < n_ent) {
+                ki[j] = ci[e];
+                if (ki[j] != WV_NIL) kd[j] = cd[e];
+            }
         }
-    }
-    // wave merge: FIN_KF rounds of argmin over the lane heads
-    int head = 0;
-    for (int r = 0; r < FIN_KF; ++r) {
-        float hd = FLT_MAX;
-        uint32_t hi = WV_NIL;
 #pragma unroll
-        for (int i = 0; i < FIN_KF; ++i)
-            if (i == head) { hd = td[i]; hi = ti[i]; }
-        float md = hd;
-        uint32_t mi = hi;
-        for (int m = 32; m >= 1; m >>= 1) {
-            const float od = __shfl_xor(md, m, 64);
-            const uint32_t oi = __shfl_xor(mi, m, 64);
-            if (key_less(od, oi, md, mi)) { md = od; mi = oi; }
+        for (int k = 2; k <= 256; k <<= 1) {
+#pragma unroll
+            for (int jj = k >> 1; jj > 0; jj >>= 1) {
+                if (jj >= 64) {
+                    const int m = jj >> 6;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int pj = j ^ m;
+                        if (pj <= j) continue;
+                        const bool up = ((64 * j + lane) & k) == 0;   // element j is the lower index
+                        const bool sw = up ? key_less(kd[pj], ki[pj], kd[j], ki[j]) : key_less(kd[j], ki[j], kd[pj], ki[pj]);
+                        const float td = kd[j];
+                        const uint32_t ti = ki[j];
+                        kd[j] = sw ? kd[pj] : kd[j];
+                        ki[j] = sw ? ki[pj] : ki[j];
+                        kd[pj] = sw ? td : kd[pj];
+                        ki[pj] = sw ? ti : ki[pj];
+                    }
+                } else {
+                    const bool lower = (lane & jj) == 0;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const float pd = __shfl_xor(kd[j], jj, 64);
+                        const uint32_t pi = __shfl_xor(ki[j], jj, 64);
+                        const bool up = ((64 * j + lane) & k) == 0;
+                        // the lower index of an ascending pair keeps the min
+                        const bool take = (lower == up) ? key_less(pd, pi, kd[j], ki[j]) : key_less(kd[j], ki[j], pd, pi);
+                        kd[j] = take ? pd : kd[j];
+                        ki[j] = take ? pi : ki[j];
+                    }
+                }
+            }
         }
-        if (hi == mi && hd == md && mi != WV_NIL) head++;
-        if (lane == 0) { sd[r] = md; si[r] = mi; }
+        if (lane < FIN_KF) { sd[lane] = kd[0]; si[lane] = ki[0]; }
+    } else {
+        // more entries: each lane keeps a private sorted top-KF of its share,
+        // then KF rounds of a wave-wide argmin over the lane heads
+        if (lane < FIN_KF) { sd[lane] = FLT_MAX; si[lane] = WV_NIL; }
+        __builtin_amdgcn_wave_barrier();
+        // each lane scans its share and keeps a private top-KF in LDS-free registers
+        float td[FIN_KF];
+        uint32_t ti[FIN_KF];
+#pragma unroll
+        for (int i = 0; i < FIN_KF; ++i) { td[i] = FLT_MAX; ti[i] = WV_NIL; }
+        for (int e = lane; e < n_ent; e += 64) {
+            float d = cd[e];
+            uint32_t id = ci[e];
+            if (id == WV_NIL) continue;
+            if (!key_less(d, id, td[FIN_KF - 1], ti[FIN_KF - 1])) continue;
+#pragma unroll
+            for (int i = 0; i < FIN_KF; ++i) {
+                const bool lt = key_less(d, id, td[i], ti[i]);
+                const float a = td[i];
+                const uint32_t b = ti[i];
+                td[i] = lt ? d : td[i];
+                ti[i] = lt ? id : ti[i];
+                d = lt ? a : d;
+                id = lt ? b : id;
+            }
+        }
+        // wave merge: FIN_KF rounds of argmin over the lane heads
+        int head = 0;
+        for (int r = 0; r < FIN_KF; ++r) {
+            float hd = FLT_MAX;
+            uint32_t hi = WV_NIL;
+#pragma unroll
+            for (int i = 0; i < FIN_KF; ++i)
+                if (i == head) { hd = td[i]; hi = ti[i]; }
+            float md = hd;
+            uint32_t mi = hi;
+            for (int m = 32; m >= 1; m >>= 1) {
+                const float od = __shfl_xor(md, m, 64);
+                const uint32_t oi = __shfl_xor(mi, m, 64);
+                if (key_less(od, oi, md, mi)) { md = od; mi = oi; }
+            }
+            if (hi == mi && hd == md && mi != WV_NIL) head++;
+            if (lane == 0) { sd[r] = md; si[r] = mi; }
+        }
     }
     __builtin_amdgcn_wave_barrier();
     // the KF-th approx key bounds every entry not selected
@@ -1240,6 +1296,7 @@ __device__ void finalize_one(const BfFinParams& p, int q, float* sd, uint32_t* s
     }
 }
 
+template <bool FAST>
 __global__ __launch_bounds__(64) void wv_bf_finalize_kernel(BfFinParams p) {
     // one dynamic region: query (16-byte aligned base), then the KF keys
     extern __shared__ float qv[];
@@ -1248,9 +1305,9 @@ __global__ __launch_bounds__(64) void wv_bf_finalize_kernel(BfFinParams p) {
     uint32_t* si = reinterpret_cast<uint32_t*>(sd + FIN_KF);
     const int q = blockIdx.x;
     if (q >= p.nq) return;
-    if (p.metric == WV_METRIC_L2) finalize_one<WV_METRIC_L2>(p, q, sd, si, qv);
-    else if (p.metric == WV_METRIC_DOT) finalize_one<WV_METRIC_DOT>(p, q, sd, si, qv);
-    else finalize_one<WV_METRIC_COSINE>(p, q, sd, si, qv);
+    if (p.metric == WV_METRIC_L2) finalize_one<WV_METRIC_L2, FAST>(p, q, sd, si, qv);
+    else if (p.metric == WV_METRIC_DOT) finalize_one<WV_METRIC_DOT, FAST>(p, q, sd, si, qv);
+    else finalize_one<WV_METRIC_COSINE, FAST>(p, q, sd, si, qv);
 }
 
 // ---------------------------------------------------------------------------
@@ -1972,7 +2029,9 @@ hipError_t wv_launch_split_rows(const float* in, int ld_in, const uint64_t* ids,
 
 hipError_t wv_launch_bf_finalize(const wv::BfFinParams* p, hipStream_t s) {
     const size_t lds = (((p->D + 3) & ~3) + 2 * wv::FIN_KF) * sizeof(float);
-    hipLaunchKernelGGL(wv::wv_bf_finalize_kernel, dim3(p->nq), dim3(64), lds, s, *p);
+    const bool fast = (uint64_t)p->n_slots * p->prod * (p->kp ? p->kp : wv::BF_KP) <= 256;
+    if (fast) hipLaunchKernelGGL(wv::wv_bf_finalize_kernel<true>, dim3(p->nq), dim3(64), lds, s, *p);
+    else hipLaunchKernelGGL(wv::wv_bf_finalize_kernel<false>, dim3(p->nq), dim3(64), lds, s, *p);
     return hipGetLastError();
 }
 
