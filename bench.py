@@ -34,6 +34,10 @@ HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 FP32_MFMA_PEAK_TF = 157.3    # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
 BF16_MFMA_PEAK_TF = 2500.0   # MI355X_MICROARCH.md: bf16 dense MFMA peak (no sparsity)
 F16_MFMA_PEAK_TF = 2500.0    # MI355X_MICROARCH.md: f16 MFMA runs at the bf16 rate (same cycles per instruction)
+# measured on the box: a bare f16 MFMA loop (operands in registers, 64x64 per
+# wave, two waves per SIMD, random data) at the clock the chip holds under it
+# (tools/mfma_shape_bench.cpp, profiles/r02_mfma_shape_bench.log)
+F16_MFMA_BARE_LOOP_TF = {"32x32x16": 1670.0, "16x16x32": 1920.0}
 
 
 def _par_rows(fn, seed: int, row0: int, nrows: int, dim: int, chunk: int = 1 << 16) -> np.ndarray:
@@ -287,6 +291,9 @@ def exact_roofline(args, ix, kern_ms, stats, D, n_allowed, n_local, NQ):
             "finalize_ms": round(float(np.mean([k["bf_finalize_ms"] for k in kern_ms])), 3),
             "fallback_queries": stats["fallbacks"]}
     if kind == "h16":
+        shape = "16x16x32" if kname == "wv_bf_h16q_kernel" else "32x32x16"
+        roof["frac_of_bare_mfma_loop"] = round(achieved / F16_MFMA_BARE_LOOP_TF[shape], 4)
+        roof["bare_mfma_loop_tf"] = F16_MFMA_BARE_LOOP_TF[shape]
         roof["seed_pass_ms"] = round(seed_ms, 3)
         roof["achieved_incl_seed_pass"] = round(flops / ((mfma_ms + seed_ms) * 1e-3) / 1e12, 2)
     return roof, kind
