@@ -1136,7 +1136,7 @@ __global__ void wv_h16_rows_kernel(const float* in, int ld_in, const uint64_t* i
         // inflate for the fp32 sum (D terms) and the sqrt
         const float res = acc == 0.f ? 0.f : sqrtf(acc * (1.0f + 2e-5f)) * (1.0f + 1e-6f) + 1e-30f;
         if (res_max_bits) atomicMax(res_max_bits, __float_as_uint(res));
-        if (res_out) res_out[row] = res;
+        if (res_out) res_out[out_row0 + row] = res;
     }
 }
 
@@ -1178,6 +1178,7 @@ hipError_t wv_launch_h16_rows(const float* in, int ld_in, const uint64_t* ids, u
                               float scale, const unsigned int* scale_from_max, void* out, uint64_t out_row0,
                               unsigned int* res_max_bits, float* res_out, int quad, hipStream_t s) {
     if (n == 0) return hipSuccess;
+    // quad: 0 = h16_index, 1 = h16q_index (ns even)
     if (ns < 1 || ns > wv::HW_NS_MAX || D > ns * 16 || (quad && ns % 2)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(wv::wv_h16_rows_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, in, ld_in, ids, n, D,
                        ns, sign, scale, scale_from_max, static_cast<uint16_t*>(out), out_row0, res_max_bits, res_out,
