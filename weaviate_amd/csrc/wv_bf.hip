@@ -1344,6 +1344,7 @@ __device__ void finalize_wide(const BfFinParams& p, int q, float* qv, float* sd,
     const int n_ent = n_lists * kp;
     const float* cd = p.cand_d + (size_t)q * p.n_slots * p.prod * kp;
     const uint32_t* ci = p.cand_id + (size_t)q * p.n_slots * p.prod * kp;
+    const int NE = p.finw_ne ? p.finw_ne : FINW_NE;   // LDS entry capacity
     // smallest full-list tail: everything a list dropped is >= its tail
     float bound = FLT_MAX;
     uint32_t bound_id = WV_NIL;
@@ -1367,11 +1368,11 @@ __device__ void finalize_wide(const BfFinParams& p, int q, float* qv, float* sd,
         const uint32_t id = ci[e];
         if (id == WV_NIL) continue;
         const int pos = atomicAdd(cnt, 1);
-        if (pos < FINW_NE) { sd[pos] = cd[e]; si[pos] = id; }
+        if (pos < NE) { sd[pos] = cd[e]; si[pos] = id; }
     }
     __syncthreads();
     const int n_all = *cnt;
-    const int n = n_all < FINW_NE ? n_all : FINW_NE;
+    const int n = n_all < NE ? n_all : NE;
     int len = 1;
     while (len < n) len <<= 1;
     for (int i = n + tid; i < len; i += nt) { sd[i] = FLT_MAX; si[i] = WV_NIL; }
@@ -1414,7 +1415,7 @@ __device__ void finalize_wide(const BfFinParams& p, int q, float* qv, float* sd,
         if (kf > FINW_KF) kf = FINW_KF;
         if (kf < n && key_less(sd[kf], si[kf], bound, bound_id)) { bound = sd[kf]; bound_id = si[kf]; }
     }
-    if (n_all > FINW_NE) bound = -FLT_MAX;   // entries were lost: never certify
+    if (n_all > NE) bound = -FLT_MAX;   // entries were lost: never certify
     if (p.h16 && bound != FLT_MAX && bound != -FLT_MAX) bound *= 1.0f / ks;
     if (p.tau_in) bound = fminf(bound, p.tau_in[q]);
     __syncthreads();
@@ -1461,8 +1462,9 @@ __global__ __launch_bounds__(256) void wv_bf_finalize_wide_kernel(BfFinParams p)
     const int dpad = (p.D + 3) & ~3;
     float* qv = lds_w;
     float* sd = qv + dpad;
-    uint32_t* si = reinterpret_cast<uint32_t*>(sd + FINW_NE);
-    float* red_d = reinterpret_cast<float*>(si + FINW_NE);
+    const int NE = p.finw_ne ? p.finw_ne : FINW_NE;
+    uint32_t* si = reinterpret_cast<uint32_t*>(sd + NE);
+    float* red_d = reinterpret_cast<float*>(si + NE);
     uint32_t* red_i = reinterpret_cast<uint32_t*>(red_d + 4);
     int* cnt = reinterpret_cast<int*>(red_i + 4);
     const int q = blockIdx.x;
@@ -2040,7 +2042,16 @@ hipError_t wv_launch_bf_finalize_wide(const wv::BfFinParams* p, hipStream_t s) {
     if (p->k < 1 || p->k > wv::BF_WIDE_KMAX ||
         (uint64_t)p->n_slots * p->prod * (p->kp ? p->kp : wv::BF_KP) > 4ull * wv::FINW_NE)
         return hipErrorInvalidValue;
-    const size_t lds = (((p->D + 3) & ~3) + 2 * wv::FINW_NE + 9) * sizeof(float);
+    // LDS sized by the entries the lists can hold (a power of two, at least
+    // the re-rank's FINW_KF): 2048 entries are 17 KB, so 8 workgroups share a
+    // CU instead of the 2 that FINW_NE's 64 KB allowed
+    const uint64_t ent = (uint64_t)p->n_slots * p->prod * (p->kp ? p->kp : wv::BF_KP);
+    int ne = wv::FINW_KF;
+    while ((uint64_t)ne < ent && ne < wv::FINW_NE) ne <<= 1;
+    wv::BfFinParams pp = *p;
+    pp.finw_ne = ne;
+    p = &pp;
+    const size_t lds = (((p->D + 3) & ~3) + 2 * (size_t)ne + 9) * sizeof(float);
     hipLaunchKernelGGL(wv::wv_bf_finalize_wide_kernel, dim3(p->nq), dim3(256), lds, s, *p);
     return hipGetLastError();
 }

@@ -1047,28 +1047,68 @@ __global__ __launch_bounds__(64) void wv_h16_seed_kernel(H16SeedParams p) {
     const int n = bf_slots_of((uint64_t)(q / p.bq), p.ntiles, p.units_per_block) * prod;
     const float* m = p.minima + (size_t)q * p.n_slots * prod;
     const float inv_s = 1.0f / (p.sx * p.qscale[0]);
-    // k rounds of a wave-wide minimum over the lanes' shares
-    float taken = -__builtin_inff();
-    int n_taken = 0;
     float mk = __builtin_inff();
-    for (int r = 0; r < p.k; ++r) {
-        float best = __builtin_inff();
-        int where = 0x7FFFFFFF;
-        for (int i = lane; i < n; i += 64) {
-            const float v = m[i];
-            // strictly after the last taken (value, index) in (value, index) order
-            const bool after = v > taken || (v == taken && i > n_taken);
-            if (after && v < __builtin_inff() && (v < best || (v == best && i < where))) { best = v; where = i; }
+    if (n <= 256) {
+        // the k-th smallest by a wave-wide bitonic sort of the (<= 256)
+        // minima, element i = 64 j + lane in register j
+        float v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = 64 * j + lane < n ? m[64 * j + lane] : __builtin_inff();
+#pragma unroll
+        for (int kk = 2; kk <= 256; kk <<= 1) {
+#pragma unroll
+            for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+                if (jj >= 64) {
+                    const int mm = jj >> 6;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int pj = j ^ mm;
+                        if (pj <= j) continue;
+                        const bool up = ((64 * j + lane) & kk) == 0;
+                        const float lo = fminf(v[j], v[pj]), hi = fmaxf(v[j], v[pj]);
+                        v[j] = up ? lo : hi;
+                        v[pj] = up ? hi : lo;
+                    }
+                } else {
+                    const bool lower = (lane & jj) == 0;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const float o = __shfl_xor(v[j], jj, 64);
+                        const bool up = ((64 * j + lane) & kk) == 0;
+                        v[j] = (lower == up) ? fminf(v[j], o) : fmaxf(v[j], o);
+                    }
+                }
+            }
         }
-        for (int o = 32; o >= 1; o >>= 1) {
-            const float ob = __shfl_xor(best, o, 64);
-            const int ow = __shfl_xor(where, o, 64);
-            if (ob < best || (ob == best && ow < where)) { best = ob; where = ow; }
+        // element k - 1 (k <= 256): register (k - 1) / 64 of lane (k - 1) % 64
+        const int e = p.k - 1;
+        float sel = v[0];
+#pragma unroll
+        for (int j = 1; j < 4; ++j) sel = (e >> 6) == j ? v[j] : sel;
+        mk = __shfl(sel, e & 63, 64);
+    } else {
+        // k rounds of a wave-wide minimum over the lanes' shares
+        float taken = -__builtin_inff();
+        int n_taken = 0;
+        for (int r = 0; r < p.k; ++r) {
+            float best = __builtin_inff();
+            int where = 0x7FFFFFFF;
+            for (int i = lane; i < n; i += 64) {
+                const float v = m[i];
+                // strictly after the last taken (value, index) in (value, index) order
+                const bool after = v > taken || (v == taken && i > n_taken);
+                if (after && v < __builtin_inff() && (v < best || (v == best && i < where))) { best = v; where = i; }
+            }
+            for (int o = 32; o >= 1; o >>= 1) {
+                const float ob = __shfl_xor(best, o, 64);
+                const int ow = __shfl_xor(where, o, 64);
+                if (ob < best || (ob == best && ow < where)) { best = ob; where = ow; }
+            }
+            if (!(best < __builtin_inff())) { mk = __builtin_inff(); break; }
+            taken = best;
+            n_taken = where;
+            mk = best;
         }
-        if (!(best < __builtin_inff())) { mk = __builtin_inff(); break; }
-        taken = best;
-        n_taken = where;
-        mk = best;
     }
     if (lane == 0) {
         float tau = __builtin_inff();

@@ -222,6 +222,7 @@ struct BfFinParams {
     int bq;                 // queries per block of the key pass (BfParams.bq)
     int prod;               // producers per query per slot (BfParams.prod)
     int kp;                 // entries per list (0: BF_KP; the 16x16x32 f16 pass: HQ_KP)
+    int finw_ne;            // wide finalize: LDS entry capacity (a power of two >= FINW_KF; 0: FINW_NE)
     // f16 key pass (h16 = 1): keys are scaled by s = sx * qscale[0]; eps adds
     // ex_max * |B| + xnorm_max * qres[q] (the f16 rounding of corpus and query)
     int h16;
