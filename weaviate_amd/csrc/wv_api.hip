@@ -36,7 +36,7 @@ hipError_t wv_launch_rownorm(const float* X, uint64_t N, int D, int ldx, float* 
                              hipStream_t s);
 hipError_t wv_launch_normalize(const float* in, float* out, uint64_t n, int D, int ld, hipStream_t s);
 hipError_t wv_launch_scale(const float* in, float* out, uint64_t n, float scale, hipStream_t s);
-hipError_t wv_launch_qnorm(const float* Q, int nq, int D, int ldq, int metric, float* out, unsigned int* absmax_bits,
+hipError_t wv_launch_qnorm(const float* Q, int nq, int D, int ldq, int metric, float* out, float* absmax_part,
                            hipStream_t s);
 hipError_t wv_launch_hnsw(const wv::HnswParams* p, int waves_per_block, hipStream_t s);
 hipError_t wv_launch_build_search(const wv::BuildParams* b, int waves_per_block, hipStream_t s);
@@ -52,7 +52,8 @@ hipError_t wv_launch_h16_rows(const float* in, int ld_in, const uint64_t* ids, u
                               float scale, const unsigned int* scale_from_max, void* out, uint64_t out_row0,
                               unsigned int* res_max_bits, float* res_out, int quad, hipStream_t s);
 hipError_t wv_launch_absmax(const float* in, int ld, uint64_t n, int D, unsigned int* max_bits, hipStream_t s);
-hipError_t wv_launch_h16_qscale(const unsigned int* max_bits, float bsign, float* qscale, hipStream_t s);
+hipError_t wv_launch_h16_qscale(const float* part, int nparts, unsigned int* max_bits, float bsign, float* qscale,
+                                hipStream_t s);
 hipError_t wv_launch_h16_xns(const float* xnorm, uint64_t n, float sx, const float* qscale, float* xns, hipStream_t s);
 hipError_t wv_launch_bf_h16(const wv::H16Params* p, int ns, int seed, int waves, hipStream_t s);
 hipError_t wv_launch_bf_h16q(const wv::H16Params* p, int ns32, int seed, int waves, hipStream_t s);
@@ -233,6 +234,7 @@ struct wv_index {
     float h16_sx = 0.f, h16_ex = 0.f;
     DevBuf ximg16, xns, qimg16, qres, qmax, qscale, tau, gtau, marg, allow_pad, ex_bits;
     DevBuf ximg16q;         // the corpus image in the 16x16x32 layout (h16_quad), beside ximg16
+    DevBuf qmax_part;       // per-block max |q_i| of the query-norm pass
     float maxnorm_host = 0.f;   // max |x| (rounded up), cached after every row write
     DevBuf xnorm;           // [capacity]
     DevBuf maxnorm;         // unsigned bits of max |x|
@@ -520,11 +522,12 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     // |q|^2 and, in the same pass, the batch's max |q_i|; B = f16(s_q b),
     // b = -2q (L2) or -q, s_q from max |b|
     const float bsign = ix->metric == WV_L2_SQUARED ? -2.f : -1.f;
-    HIP_TRY(hipMemsetAsync(ix->qmax.p, 0, 4, s));
-    HIP_TRY(wv_launch_qnorm(d_q, nq, ix->dim, ix->dpad, ix->metric, ix->q_nrm2.as<float>(),
-                            ix->qmax.as<unsigned int>(), s));
+    HIP_TRY(ix->qmax_part.ensure((size_t)((nq + 3) / 4) * 4));
+    HIP_TRY(wv_launch_qnorm(d_q, nq, ix->dim, ix->dpad, ix->metric, ix->q_nrm2.as<float>(), ix->qmax_part.as<float>(),
+                            s));
     HIP_TRY(hipMemsetAsync(ix->qimg16.p, 0, qbytes, s));
-    HIP_TRY(wv_launch_h16_qscale(ix->qmax.as<unsigned int>(), bsign, ix->qscale.as<float>(), s));
+    HIP_TRY(wv_launch_h16_qscale(ix->qmax_part.as<float>(), (nq + 3) / 4, ix->qmax.as<unsigned int>(), bsign,
+                                 ix->qscale.as<float>(), s));
     HIP_TRY(wv_launch_h16_rows(d_q, ix->dpad, nullptr, nq, ix->dim, ns, bsign, 1.f, ix->qmax.as<unsigned int>(),
                                ix->qimg16.p, 0, nullptr, ix->qres.as<float>(), quad, s));
     if (ix->metric == WV_L2_SQUARED)
@@ -1388,7 +1391,7 @@ int wv_index_destroy(wv_index* ix) {
                       &ix->sort_tmp, &ix->g_idx, &ix->g_q, &ix->g_allow, &ix->g_ids, &ix->g_d, &ix->g_n, &ix->g_cnt,
                       &ix->out_ids, &ix->out_d, &ix->out_n, &ix->stage, &ix->fail_thr, &ix->fb_idx, &ix->fb_d, &ix->fb_i, &ix->fb_n, &ix->fb_of,
                       &ix->ac_cnt, &ix->ac_off, &ix->rowidx, &ix->pq_cent, &ix->pq_codes, &ix->pk_key,
-                      &ix->pk_dist, &ix->pk_val, &ix->pk_skey, &ix->pk_sval, &ix->pk_off, &ix->ximg16, &ix->ximg16q, &ix->xns,
+                      &ix->pk_dist, &ix->pk_val, &ix->pk_skey, &ix->pk_sval, &ix->pk_off, &ix->ximg16, &ix->ximg16q, &ix->qmax_part, &ix->xns,
                       &ix->qimg16, &ix->qres, &ix->qmax, &ix->qscale, &ix->tau, &ix->gtau, &ix->marg, &ix->allow_pad, &ix->ex_bits,
                       &ix->delta, &ix->dmask, &ix->dl_ids, &ix->dl_d, &ix->dl_n, &ix->dq_tmp, &ix->b_tgt, &ix->b_ci,
                       &ix->b_cd, &ix->b_cn, &ix->b_cnt0, &ix->b_cntu, &ix->b_rk, &ix->b_rn, &ix->b_rk2, &ix->b_rn2,

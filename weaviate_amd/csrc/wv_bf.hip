@@ -1599,30 +1599,34 @@ __global__ __launch_bounds__(1024) void wv_fb_select_kernel(FbParams p) {
 //     collection -- the result of a full sort, as exact_full computes it.
 __global__ __launch_bounds__(1024) void wv_fbd_compact_kernel(const int32_t* __restrict__ flags, int nq,
                                                               int32_t* __restrict__ list, int32_t* __restrict__ count,
-                                                              unsigned long long* total) {
+                                                              unsigned long long* total, uint32_t* __restrict__ cand_n) {
+    // each thread owns a contiguous run of flags; one block-wide exclusive
+    // scan of the runs' counts places them (two barriers in all)
     __shared__ int wsum[16];
-    __shared__ int base;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    if (tid == 0) base = 0;
-    __syncthreads();
-    for (int c0 = 0; c0 < nq; c0 += 1024) {
-        const int q = c0 + tid;
-        const bool f = q < nq && flags[q] != 0;
-        const uint64_t b = __ballot(f);
-        const int r = __popcll(b & ((1ull << lane) - 1ull));
-        if (lane == 0) wsum[w] = __popcll(b);
-        __syncthreads();
-        int off = base;
-        for (int i = 0; i < w; ++i) off += wsum[i];
-        if (f) list[off + r] = q;
-        __syncthreads();
-        if (tid == 0)
-            for (int i = 0; i < 16; ++i) base += wsum[i];
-        __syncthreads();
+    const int per = (nq + 1023) / 1024;
+    const int q0 = tid * per, q1 = min(nq, q0 + per);
+    int c = 0;
+    for (int q = q0; q < q1; ++q) c += flags[q] != 0;
+    int incl = c;   // inclusive scan over the wave
+    for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += v;
     }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    int off = incl - c, all = 0;
+    for (int i = 0; i < 16; ++i) {
+        if (i < w) off += wsum[i];
+        all += wsum[i];
+    }
+    for (int q = q0; q < q1; ++q)
+        if (flags[q] != 0) list[off++] = q;
+    // the filter's per-slot candidate counters start at zero
+    for (int i = tid; i < all; i += 1024) cand_n[i] = 0;
     if (tid == 0) {
-        *count = base;
-        if (total) atomicAdd(total, (unsigned long long)base);
+        *count = all;
+        if (total && all) atomicAdd(total, (unsigned long long)all);
     }
 }
 
@@ -1919,11 +1923,11 @@ __global__ void wv_scale_rows_kernel(const float* in, float* out, uint64_t n, fl
 
 // |q|^2 for L2, |q| for dot/cosine (feeds eps only)
 // |q|^2 (L2) or |q| per query row: one wave per row (coalesced), optionally
-// the batch's max |q_i| (absmax_bits: float bits, one atomicMax per block).
+// each block's max |q_i| (absmax_part[block], 4 rows per block).
 // The summation order is the wave's tree: the certificate's eps bounds the
 // rounding of any order (D u sum q_i^2).
 __global__ __launch_bounds__(256) void wv_qnorm_kernel(const float* Q, int nq, int D, int ldq, int metric, float* out,
-                                                       unsigned int* absmax_bits) {
+                                                       float* absmax_part) {
     __shared__ float wmax[4];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int r = blockIdx.x * 4 + w;
@@ -1943,11 +1947,12 @@ __global__ __launch_bounds__(256) void wv_qnorm_kernel(const float* Q, int nq, i
     // L2: |q|^2 enters the bound additively (no inflation; eps covers its
     // rounding).  dot/cosine: |q| only scales eps, so it is rounded up.
     if (r < nq && lane == 0) out[r] = metric == WV_METRIC_L2 ? s : sqrtf(s * (1.0f + 1e-6f)) * (1.0f + 1e-6f);
-    if (absmax_bits) {
+    if (absmax_part) {
+        // one partial per block (wv_h16_qscale_kernel reduces them): atomics
+        // on one address from thousands of blocks serialise (25 us at 10k)
         if (lane == 0) wmax[w] = m;
         __syncthreads();
-        if (threadIdx.x == 0)
-            atomicMax(absmax_bits, __float_as_uint(fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]))));
+        if (threadIdx.x == 0) absmax_part[blockIdx.x] = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
     }
 }
 
@@ -2076,9 +2081,7 @@ hipError_t wv_launch_fbd(const int32_t* flags, int nq, const wv::FbParams* fb, h
     if (nq == 0) return hipSuccess;
     if (fb->k < 1 || fb->k > wv::FBD_K || !fb->d_nf || !fb->scratch || fb->n_scr < 1) return hipErrorInvalidValue;
     hipLaunchKernelGGL(wv::wv_fbd_compact_kernel, dim3(1), dim3(1024), 0, s, flags, nq, const_cast<int32_t*>(fb->qidx),
-                       const_cast<int32_t*>(fb->d_nf), fb->fb_total);
-    hipError_t e = hipMemsetAsync(fb->cand_n, 0, (size_t)nq * 4, s);
-    if (e != hipSuccess) return e;
+                       const_cast<int32_t*>(fb->d_nf), fb->fb_total, fb->cand_n);
     uint64_t blocks = (fb->N + 255) / 256;
     if (blocks > 512) blocks = 512;
     if (blocks == 0) blocks = 1;
@@ -2133,11 +2136,11 @@ hipError_t wv_launch_scale(const float* in, float* out, uint64_t n, float scale,
     return hipGetLastError();
 }
 
-hipError_t wv_launch_qnorm(const float* Q, int nq, int D, int ldq, int metric, float* out, unsigned int* absmax_bits,
+hipError_t wv_launch_qnorm(const float* Q, int nq, int D, int ldq, int metric, float* out, float* absmax_part,
                            hipStream_t s) {
     if (nq == 0) return hipSuccess;
     hipLaunchKernelGGL(wv::wv_qnorm_kernel, dim3((nq + 3) / 4), dim3(256), 0, s, Q, nq, D, ldq, metric, out,
-                       absmax_bits);
+                       absmax_part);
     return hipGetLastError();
 }
 

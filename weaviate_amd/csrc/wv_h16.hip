@@ -1193,8 +1193,23 @@ __global__ void wv_absmax_kernel(const float* in, int ld, uint64_t n, int D, uns
 }
 
 // s_q from the batch max, and s * |x|^2 for the L2 C-in
-__global__ void wv_h16_qscale_kernel(const unsigned int* max_bits, float bsign, float* qscale) {
-    if (threadIdx.x == 0 && blockIdx.x == 0) qscale[0] = pow2_scale_for(__uint_as_float(*max_bits) * fabsf(bsign));
+// s_q from the batch max: the qnorm pass's per-block partials (nparts, or a
+// single precomputed max when part == nullptr), reduced here; the max is also
+// left in max_bits for the query image kernel
+__global__ __launch_bounds__(256) void wv_h16_qscale_kernel(const float* part, int nparts, unsigned int* max_bits,
+                                                            float bsign, float* qscale) {
+    __shared__ float wm[4];
+    float m = 0.f;
+    if (part)
+        for (int i = threadIdx.x; i < nparts; i += blockDim.x) m = fmaxf(m, part[i]);
+    for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float mx = part ? fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3])) : __uint_as_float(*max_bits);
+        if (part) *max_bits = __float_as_uint(mx);
+        qscale[0] = pow2_scale_for(mx * fabsf(bsign));
+    }
 }
 __global__ void wv_h16_xns_kernel(const float* xnorm, uint64_t n, float sx, const float* qscale, float* xns) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1234,8 +1249,9 @@ hipError_t wv_launch_absmax(const float* in, int ld, uint64_t n, int D, unsigned
     return hipGetLastError();
 }
 
-hipError_t wv_launch_h16_qscale(const unsigned int* max_bits, float bsign, float* qscale, hipStream_t s) {
-    hipLaunchKernelGGL(wv::wv_h16_qscale_kernel, dim3(1), dim3(64), 0, s, max_bits, bsign, qscale);
+hipError_t wv_launch_h16_qscale(const float* part, int nparts, unsigned int* max_bits, float bsign, float* qscale,
+                                hipStream_t s) {
+    hipLaunchKernelGGL(wv::wv_h16_qscale_kernel, dim3(1), dim3(256), 0, s, part, nparts, max_bits, bsign, qscale);
     return hipGetLastError();
 }
 
