@@ -489,17 +489,18 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
             uint64_t* d_out_ids, float* d_out_d, int32_t* d_out_n, hipStream_t s, std::vector<int32_t>& fails) {
     const int ns = ix->h16_ns;
     const bool wd = ix->h16_wide;   // D > 128: the wide-D kernel
-    // the 16x16x32 kernel (HQ_KP-entry lists) for k <= FIN_KF; wider k on the
-    // 32x32x16 kernel, whose 8-entry lists keep the certificate's fallback
-    // rate low at k = 100..256 (4-entry lists fill with top-k keys too often)
+    // the 16x16x32 kernel (one 16-entry list per column and slot) for k <=
+    // FIN_KF; wider k on the 32x32x16 kernel
     const bool quad = ix->h16_quad && k <= wv::FIN_KF;
     // D <= 128: 8-wave (512-query) workgroups, one per CU; WV_H16_WAVES=4:
     // 4-wave (256-query) workgroups, two independent ones per CU
     const int waves = std::getenv("WV_H16_WAVES") && std::atoi(std::getenv("WV_H16_WAVES")) == 4 ? 4 : 8;
     const int wg_per_cu = wd ? 1 : 8 / waves;
     const int tile_rows = wd ? wv::HW_BN : wv::H_BN, bq = wd ? wv::HW_BQ : waves * 64;
-    const int prod = wd ? wv::HW_PROD : (quad ? wv::HQ_PROD : wv::H_PROD);
-    const int kp = quad ? wv::HQ_KP : wv::BF_KP;   // entries per list
+    // seed minima per query and slot; lists per query and slot, entries per list
+    const int seed_prod = wd ? wv::HW_PROD : (quad ? wv::HQ_PROD : wv::H_PROD);
+    const int prod = quad ? 1 : seed_prod;
+    const int kp = quad ? wv::HQ_PROD * wv::HQ_KP : wv::BF_KP;
     const uint64_t ntl = (N + tile_rows - 1) / tile_rows;
     const uint64_t words = ntl * (uint64_t)(tile_rows / 64);   // allow words the kernel reads
     const uint64_t* allow = d_allow;
@@ -589,7 +590,7 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     if (seed) {
         const uint64_t nts = (ntl + wv::H_SAMPLE - 1) / wv::H_SAMPLE;
         const wv::BfSchedule ss = wv::bf_schedule(nq, nts * wv::H_BN, target(nts), bq, wv::H_BN);
-        HIP_TRY(ix->cand_d.ensure((size_t)nq * ss.n_slots * prod * 4));
+        HIP_TRY(ix->cand_d.ensure((size_t)nq * ss.n_slots * seed_prod * 4));
         hp.ntiles = ss.ntiles;
         hp.units_per_block = ss.units_per_block;
         hp.n_slots = ss.n_slots;
@@ -617,7 +618,7 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
         sp.tau = ix->tau.as<float>();
         sp.gtau = ix->gtau.as<unsigned int>();
         sp.bq = bq;
-        sp.prod = prod;
+        sp.prod = seed_prod;
         HIP_TRY(wv_launch_h16_seed(&sp, s));
         TREC(7);
     }

@@ -484,16 +484,28 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
 // pipeline); per wave and tile 4 row groups x 4 query groups of 16 x 16
 // accumulators.  Keys: acc[rg][qg][r] is row 16 rg + 4 (lane / 16) + r x query
 // 16 qg + lane % 16, so a lane owns 4 query columns with 8 keys per half tile
-// each, and the 4 lanes of a column (lane % 16 equal) keep HQ_KP-entry lists
-// of disjoint rows; the extraction threshold of a list is the smallest tail of
-// the other three (and the seed / running threshold).
+// each; the 4 lanes of a column (lane % 16 equal) share the column's sorted
+// list of HQ_PROD * HQ_KP = 16 entries, lane quarter q holding entries
+// 4 q .. 4 q + 3 (a 16-entry list per column and slot, so the certificate's
+// list tails lie well beyond the top k).
 //
-// Extraction of one column's 8 keys of a half tile (values v: rows rb + 16 (v
-// / 4) + v % 4) into a HQ_KP list, as split_extract16.
-__device__ __forceinline__ void quad_extract8(float& M, floatx4& A, floatx4& B, float (&ld)[HQ_KP],
-                                              uint32_t (&li)[HQ_KP], float pt, uint32_t rb) {
+// Extraction of one query group's keys of a half tile (a lane's 8 values v:
+// rows rb + 16 (v / 4) + v % 4) into the column lists, in wave-uniform rounds:
+// every lane whose smallest remaining key is <= its column's threshold (the
+// list's tail, the seed / running threshold) takes it out; the candidates of
+// each lane quarter in turn are broadcast to the column's four lanes, which
+// merge them into their entries (entry j becomes med3(e[j - 1], d, e[j]),
+// e[-1] the previous quarter's last entry).  Keys equal to the tail are taken
+// out without entering.
+__device__ __forceinline__ void qcol_extract(float M, floatx4& A, floatx4& B, float (&ld)[HQ_KP],
+                                             uint32_t (&li)[HQ_KP], float& thr, float tau, uint32_t rb, int lane) {
     const float INF = __builtin_inff();
-    while (M <= fminf(ld[HQ_KP - 1], pt)) {
+    const int l15 = lane & 15;
+    const int prev = (lane + 48) & 63;   // the same column's previous lane quarter
+    for (;;) {
+        const bool has = M <= thr;
+        const uint64_t hb = __ballot(has);
+        if (!hb) break;
         WV_DBG_COUNT(1)
         // position of M: a descending scan, so among equal keys the lowest row wins
         uint32_t sel = 0;
@@ -501,6 +513,7 @@ __device__ __forceinline__ void quad_extract8(float& M, floatx4& A, floatx4& B, 
         for (int r = 3; r >= 0; --r) sel = B[r] == M ? 4u + r : sel;
 #pragma unroll
         for (int r = 3; r >= 0; --r) sel = A[r] == M ? (uint32_t)r : sel;
+        sel = has ? sel : 8u;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             A[r] = sel == (uint32_t)r ? INF : A[r];
@@ -508,19 +521,26 @@ __device__ __forceinline__ void quad_extract8(float& M, floatx4& A, floatx4& B, 
         }
         uint32_t rbo = rb;   // opaque: the row ids stay in this rare loop
         asm volatile("" : "+v"(rbo));
-        if (!(M < ld[HQ_KP - 1])) break;
-        uint32_t id = rbo + (sel & 3u) + 16u * (sel >> 2);
-        float d = M;
+        const uint32_t id = rbo + (sel & 3u) + 16u * ((sel >> 2) & 1u);
+        const float d = has ? M : INF;
 #pragma unroll
-        for (int i = 0; i < HQ_KP; ++i) {
-            const bool lt = d < ld[i];
-            const float td = ld[i];
-            const uint32_t ti = li[i];
-            ld[i] = lt ? d : td;
-            li[i] = lt ? id : ti;
-            d = lt ? td : d;
-            id = lt ? ti : id;
+        for (int q = 0; q < HQ_PROD; ++q) {
+            if (!((hb >> (16 * q)) & 0xFFFFull)) continue;   // (wave-uniform)
+            const float cd = __shfl(d, l15 + 16 * q, 64);
+            const uint32_t cid = __shfl(id, l15 + 16 * q, 64);
+            float pk = __shfl(ld[HQ_KP - 1], prev, 64);
+            const uint32_t pi = __shfl(li[HQ_KP - 1], prev, 64);
+            pk = lane < 16 ? -INF : pk;
+#pragma unroll
+            for (int i = HQ_KP - 1; i >= 0; --i) {
+                const float lo = i ? ld[i - 1] : pk;
+                const uint32_t loi = i ? li[i - 1] : pi;
+                const bool a = cd < lo, b = cd < ld[i];
+                li[i] = a ? loi : (b ? cid : li[i]);
+                ld[i] = __builtin_amdgcn_fmed3f(lo, cd, ld[i]);
+            }
         }
+        thr = fminf(__shfl(ld[HQ_KP - 1], l15 + 48, 64), tau);
         M = fminf(fminf(fminf(A[0], A[1]), fminf(A[2], A[3])), fminf(fminf(B[0], B[1]), fminf(B[2], B[3])));
     }
 }
@@ -700,30 +720,26 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16q_kernel(H16Pa
             // 4 VALU: two independent v_min3, one v_min, a final v_min3
             return min3_raw(min3_raw(A[0], A[1], A[2]), min3_raw(A[3], B[0], B[1]), fminf(B[2], B[3]));
         };
-        // extraction thresholds: min(the other three lanes' tails, tau)
+        // extraction thresholds: min(the column list's tail, tau)
         float pt[4];
         auto refresh_pt = [&] {
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const float t = ld[g][HQ_KP - 1];
-                pt[g] = fminf(fminf(__shfl_xor(t, 16, 64), __shfl_xor(t, 32, 64)),
-                              fminf(__shfl_xor(t, 48, 64), tau[g]));
-            }
+            for (int g = 0; g < 4; ++g) pt[g] = fminf(__shfl(ld[g][HQ_KP - 1], l15 + 48, 64), tau[g]);
         };
         refresh_pt();
-        // running threshold: entry e - 1 of each of the column's 4 lists, e =
-        // ceil(k / 4): 4 e >= k distinct rows with keys <= their maximum
-        const int ie = (p.kth + 3) >> 2;
+        // running threshold: entry k - 1 of the column list (k distinct rows
+        // with keys <= it), held by lane quarter (k - 1) / 4
+        const int ke = p.kth > 0 ? p.kth - 1 : 0;
+        const int ksrc = l15 + 16 * (ke >> 2);
         auto publish = [&] {
-            int ve = ie - 1;
+            int ve = ke & 3;
             asm volatile("" : "+v"(ve));
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-                float v = -FLT_MAX;
+                float v = FLT_MAX;
 #pragma unroll
                 for (int i = 0; i < HQ_KP; ++i) v = ve == i ? ld[g][i] : v;
-                v = fmaxf(v, __shfl_xor(v, 16, 64));
-                v = fmaxf(v, __shfl_xor(v, 32, 64));
+                v = __shfl(v, ksrc, 64);
                 if (lq == 0 && jq[g] < p.nq && v < FLT_MAX) {
                     const float u4 = 4.f * 5.9604645e-08f;
                     atomicMin(&p.gtau[jq[g]], h16_key_enc(v + marg[g] + u4 * (fabsf(v) + marg[g])));
@@ -749,19 +765,17 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16q_kernel(H16Pa
                 bool x[4], anyx = false;
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
-                    x[g] = m[g] <= fminf(ld[g][HQ_KP - 1], pt[g]);
+                    x[g] = m[g] <= pt[g];
                     anyx = anyx || x[g];
                 }
-                const bool grew = __any(anyx);
-                if (__builtin_expect(grew, 0)) {
+                if (__builtin_expect(__any(anyx), 0)) {
                     WV_DBG_COUNT(3)
 #pragma unroll
-                    for (int g = 0; g < 4; ++g) {
-                        float mm = m[g];
-                        if (x[g]) quad_extract8(mm, acc[2 * h][g], acc[2 * h + 1][g], ld[g], li[g], pt[g], rb);
-                    }
+                    for (int g = 0; g < 4; ++g)
+                        if (__any(x[g]))
+                            qcol_extract(m[g], acc[2 * h][g], acc[2 * h + 1][g], ld[g], li[g], pt[g], tau[g], rb, lane);
                 }
-                return grew;
+                return false;   // (the thresholds are current)
             }
         };
 
@@ -827,11 +841,12 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16q_kernel(H16Pa
                 if (jq[g] < p.nq) p.out_d[((size_t)jq[g] * p.n_slots + slot) * HQ_PROD + lq] = ld[g][0];
             continue;
         }
+        // one 16-entry list per query and slot, lane quarter lq's entries at 4 lq
         const size_t per_q = (size_t)p.n_slots * HQ_PROD * HQ_KP;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             if (jq[g] >= p.nq) continue;
-            const size_t base = (size_t)jq[g] * per_q + ((size_t)slot * HQ_PROD + lq) * HQ_KP;
+            const size_t base = (size_t)jq[g] * per_q + (size_t)slot * HQ_PROD * HQ_KP + lq * HQ_KP;
 #pragma unroll
             for (int i = 0; i < HQ_KP; ++i) { p.out_d[base + i] = ld[g][i]; p.out_id[base + i] = li[g][i]; }
         }

@@ -116,9 +116,11 @@ inline uint64_t h16_index(uint64_t row, int k, int ns) {
 // 16x16x32 operand layout (h16q_index: per 16-row group and 32-k step a 1 KiB
 // block, lane (h, r) holding k 8h .. 8h + 7 of row r).  A lane's keys cover 4
 // query columns (16 q + lane % 16) and rows 4 (lane / 16) ...; the four lanes
-// of a column keep a list of HQ_KP entries each.
-constexpr int HQ_PROD = 4;    // lists per query per slot (the four lane quarters)
-constexpr int HQ_KP = 4;      // entries per list
+// of a column share one sorted list of HQ_PROD * HQ_KP entries per slot, lane
+// quarter q holding entries HQ_KP q ...; the seed pass keeps one minimum per
+// lane quarter (HQ_PROD per query and slot).
+constexpr int HQ_PROD = 4;    // lane quarters per column
+constexpr int HQ_KP = 4;      // list entries per lane quarter
 
 #if defined(__HIPCC__)
 __host__ __device__
@@ -221,7 +223,7 @@ struct BfFinParams {
     int split;              // approximate keys came from the bf16x3 pass (wider eps)
     int bq;                 // queries per block of the key pass (BfParams.bq)
     int prod;               // producers per query per slot (BfParams.prod)
-    int kp;                 // entries per list (0: BF_KP; the 16x16x32 f16 pass: HQ_KP)
+    int kp;                 // entries per list (0: BF_KP; the 16x16x32 f16 pass: HQ_PROD * HQ_KP)
     int finw_ne;            // wide finalize: LDS entry capacity (a power of two >= FINW_KF; 0: FINW_NE)
     // f16 key pass (h16 = 1): keys are scaled by s = sx * qscale[0]; eps adds
     // ex_max * |B| + xnorm_max * qres[q] (the f16 rounding of corpus and query)
