@@ -64,6 +64,51 @@ __global__ __launch_bounds__(512, 1) void k16(int iters, float* out) {
     out[seed] = s;
 }
 
+// as k16, the A operands (64 rows x 128 k per tile, h16q-style 1 KiB blocks)
+// read from LDS each tile: 8 ds_read_b128 per 16 MFMAs of a half tile, like
+// wv_bf_h16q_kernel's mfma_half; BAR: a workgroup barrier every 2 tiles
+template <bool BAR, bool FENCE = false>
+__global__ __launch_bounds__(512, 1) void k16lds(int iters, float* out) {
+    __shared__ uint4 img[4][8][64];   // 3 stages' worth is not needed: one static tile
+    const int lane = threadIdx.x & 63;
+    const uint32_t seed = blockIdx.x * 512 + threadIdx.x;
+    for (int i = threadIdx.x; i < 4 * 8 * 64; i += 512) {
+        half8 h = rnd8(i * 7 + 3);
+        (&img[0][0][0])[i] = __builtin_bit_cast(uint4, h);
+    }
+    __syncthreads();
+    half8 b[4][4];
+    for (int i = 0; i < 4; ++i)
+        for (int k = 0; k < 4; ++k) b[i][k] = rnd8(seed * 17 + i * 4 + k + 99);
+    floatx4 c[4][4];
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) c[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            if (FENCE) __builtin_amdgcn_sched_barrier(0);   // no hoisting of the next half's reads
+            uint4 a[2][4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int r = 0; r < 2; ++r) a[r][k] = img[2 * h + r][(k + it) & 7][lane];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int r = 0; r < 2; ++r)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        c[2 * h + r][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, a[r][k]), b[j][k],
+                                                                                  c[2 * h + r][j], 0, 0, 0);
+        }
+        if (BAR && (it & 1)) __syncthreads();
+    }
+    float s = 0.f;
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) s += c[i][j][0] + c[i][j][1] + c[i][j][2] + c[i][j][3];
+    out[seed] = s;
+}
+
 int main(int argc, char** argv) {
     const int iters = argc > 1 ? atoi(argv[1]) : 20000;
     int dev = 0, cus = 0;
@@ -76,15 +121,19 @@ int main(int argc, char** argv) {
     hipEventCreate(&e1);
     const double flop = 2.0 * 64 * 64 * 128 * (double)iters * 8 * nb;   // 8 waves x 64x64x128 per iter
     for (int rep = 0; rep < 3; ++rep) {
-        for (int shape = 0; shape < 2; ++shape) {
-            hipLaunchKernelGGL(shape ? k16 : k32, dim3(nb), dim3(512), 0, 0, iters / 10, out);   // warm
+        for (int shape = 0; shape < 6; ++shape) {
+            void (*kf)(int, float*) = shape == 0 ? k32 : shape == 1 ? k16 : shape == 2 ? k16lds<false> : shape == 3 ? k16lds<true>
+                                    : shape == 4 ? k16lds<false, true> : k16lds<true, true>;
+            const char* nm[6] = {"32x32x16_f16", "16x16x32_f16", "16x16x32_f16 A from LDS", "16x16x32_f16 A from LDS + barrier/2 tiles",
+                                 "16x16x32_f16 A from LDS, reads fenced per half", "16x16x32_f16 A from LDS, fenced + barrier/2 tiles"};
+            hipLaunchKernelGGL(kf, dim3(nb), dim3(512), 0, 0, iters / 10, out);   // warm
             hipEventRecord(e0);
-            hipLaunchKernelGGL(shape ? k16 : k32, dim3(nb), dim3(512), 0, 0, iters, out);
+            hipLaunchKernelGGL(kf, dim3(nb), dim3(512), 0, 0, iters, out);
             hipEventRecord(e1);
             hipEventSynchronize(e1);
             float ms;
             hipEventElapsedTime(&ms, e0, e1);
-            printf("%s  %.3f ms  %.1f TF/s\n", shape ? "16x16x32_f16" : "32x32x16_f16", ms, flop / (ms * 1e-3) / 1e12);
+            printf("%s  %.3f ms  %.1f TF/s\n", nm[shape], ms, flop / (ms * 1e-3) / 1e12);
         }
     }
     hipFree(out);

@@ -586,15 +586,17 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
         if (wide) t = std::max<uint64_t>(t, (uint64_t)nqb * std::min<uint64_t>(tiles, (uint64_t)k + 2));
         return (int)std::min<uint64_t>(t, 1u << 30);
     };
-    const bool seed = !wd && ntl >= 64 * (uint64_t)wv::H_SAMPLE && !std::getenv("WV_H16_NO_SEED");
+    int sample = wv::H_SAMPLE;   // (WV_H16_SAMPLE: the seed's tile stride, for measurements)
+    if (const char* e = std::getenv("WV_H16_SAMPLE")) sample = std::max(1, std::atoi(e));
+    const bool seed = !wd && ntl >= 64 * (uint64_t)sample && !std::getenv("WV_H16_NO_SEED");
     if (seed) {
-        const uint64_t nts = (ntl + wv::H_SAMPLE - 1) / wv::H_SAMPLE;
+        const uint64_t nts = (ntl + sample - 1) / sample;
         const wv::BfSchedule ss = wv::bf_schedule(nq, nts * wv::H_BN, target(nts), bq, wv::H_BN);
         HIP_TRY(ix->cand_d.ensure((size_t)nq * ss.n_slots * seed_prod * 4));
         hp.ntiles = ss.ntiles;
         hp.units_per_block = ss.units_per_block;
         hp.n_slots = ss.n_slots;
-        hp.tile_stride = wv::H_SAMPLE;
+        hp.tile_stride = sample;
         hp.tau = nullptr;
         hp.out_d = ix->cand_d.as<float>();
         hp.out_id = nullptr;
