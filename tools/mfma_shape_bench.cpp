@@ -109,6 +109,78 @@ __global__ __launch_bounds__(512, 1) void k16lds(int iters, float* out) {
     out[seed] = s;
 }
 
+// the kernel's half-tile structure (wv_bf_h16q_kernel's mfma_half): each half
+// tile's accumulators restart from a C-in read from LDS, and the 8-key minima
+// of the other half (MIN) are interleaved 1:1 with this half's MFMAs by
+// sched_group_barrier, as in the kernel
+template <bool MIN>
+__global__ __launch_bounds__(512, 1) void k16half(int iters, float* out) {
+    __shared__ uint4 img[4][8][64];
+    __shared__ float xn[64];
+    const int lane = threadIdx.x & 63;
+    const uint32_t seed = blockIdx.x * 512 + threadIdx.x;
+    for (int i = threadIdx.x; i < 4 * 8 * 64; i += 512) {
+        half8 h = rnd8(i * 7 + 3);
+        (&img[0][0][0])[i] = __builtin_bit_cast(uint4, h);
+    }
+    if (threadIdx.x < 64) xn[threadIdx.x] = (float)threadIdx.x;
+    __syncthreads();
+    half8 b[4][4];
+    for (int i = 0; i < 4; ++i)
+        for (int k = 0; k < 4; ++k) b[i][k] = rnd8(seed * 17 + i * 4 + k + 99);
+    floatx4 c[4][4];
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) c[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    float sink = 0.f;
+    const int lq = lane >> 4;
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            floatx4 xc[2];
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                const float4 v = *reinterpret_cast<const float4*>(&xn[16 * (2 * h + r) + 4 * lq]);
+                xc[r] = floatx4{v.x, v.y, v.z, v.w};
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            uint4 a[2][4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int r = 0; r < 2; ++r) a[r][k] = img[2 * h + r][(k + it) & 7][lane];
+            if (MIN) {
+                const int o = 1 - h;
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const floatx4& A = c[2 * o][g];
+                    const floatx4& B = c[2 * o + 1][g];
+                    sink = fminf(sink, fminf(fminf(fminf(A[0], A[1]), fminf(A[2], A[3])), fminf(fminf(B[0], B[1]), fminf(B[2], B[3]))));
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int r = 0; r < 2; ++r)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        c[2 * h + r][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, a[r][k]), b[j][k],
+                                                                                  k == 0 ? xc[r] : c[2 * h + r][j], 0, 0, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+#pragma unroll
+            for (int i = 0; i < 32; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+            }
+        }
+        if (it & 1) __syncthreads();
+    }
+    float s = sink;
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) s += c[i][j][0] + c[i][j][1] + c[i][j][2] + c[i][j][3];
+    out[seed] = s;
+}
+
 int main(int argc, char** argv) {
     const int iters = argc > 1 ? atoi(argv[1]) : 20000;
     int dev = 0, cus = 0;
@@ -121,11 +193,14 @@ int main(int argc, char** argv) {
     hipEventCreate(&e1);
     const double flop = 2.0 * 64 * 64 * 128 * (double)iters * 8 * nb;   // 8 waves x 64x64x128 per iter
     for (int rep = 0; rep < 3; ++rep) {
-        for (int shape = 0; shape < 6; ++shape) {
+        for (int shape = 0; shape < 8; ++shape) {
             void (*kf)(int, float*) = shape == 0 ? k32 : shape == 1 ? k16 : shape == 2 ? k16lds<false> : shape == 3 ? k16lds<true>
-                                    : shape == 4 ? k16lds<false, true> : k16lds<true, true>;
-            const char* nm[6] = {"32x32x16_f16", "16x16x32_f16", "16x16x32_f16 A from LDS", "16x16x32_f16 A from LDS + barrier/2 tiles",
-                                 "16x16x32_f16 A from LDS, reads fenced per half", "16x16x32_f16 A from LDS, fenced + barrier/2 tiles"};
+                                    : shape == 4 ? k16lds<false, true> : shape == 5 ? k16lds<true, true>
+                                    : shape == 6 ? k16half<false> : k16half<true>;
+            const char* nm[8] = {"32x32x16_f16", "16x16x32_f16", "16x16x32_f16 A from LDS", "16x16x32_f16 A from LDS + barrier/2 tiles",
+                                 "16x16x32_f16 A from LDS, reads fenced per half", "16x16x32_f16 A from LDS, fenced + barrier/2 tiles",
+                                 "16x16x32_f16 kernel half-tile structure (C-in restart), no minima",
+                                 "16x16x32_f16 kernel half-tile structure + minima of the other half"};
             hipLaunchKernelGGL(kf, dim3(nb), dim3(512), 0, 0, iters / 10, out);   // warm
             hipEventRecord(e0);
             hipLaunchKernelGGL(kf, dim3(nb), dim3(512), 0, 0, iters, out);
