@@ -82,6 +82,22 @@ __device__ __forceinline__ void block_barrier() {
 #endif
 }
 
+// Eligibility of a tile's 64 rows (bit r: row r is not excluded, is allowed,
+// and is < N), read with scalar loads: the tile index is wave-uniform, so
+// the words come through the constant address space (s_load), which neither
+// waits behind the LDS operand reads (a word staged in LDS cost 0.31 ms per
+// 1M x 10k pass: its read stalled the wave at every tile) nor counts against
+// the LDS-DMA's vmcnt.
+__device__ __forceinline__ uint64_t tile_okw(const H16Params& p, uint64_t tile, bool has_allow) {
+    typedef const __attribute__((address_space(4))) uint64_t cu64;
+    const uint32_t tl = __builtin_amdgcn_readfirstlane((uint32_t)tile);
+    uint64_t okw = ~((cu64*)p.excl)[tl];
+    if (has_allow) okw &= ((cu64*)p.allow)[tl];
+    const uint64_t row0 = (uint64_t)tl * H_BN;
+    if (row0 + H_BN > p.N) okw &= p.N > row0 ? ((1ull << (p.N - row0)) - 1) : 0ull;
+    return okw;
+}
+
 // LDS stage: [2 row blocks][ns k-steps][64 lanes] uint4 image, then 64 floats
 // of s|x|^2, then the exclusion and allow words of the tile.
 template <int NS>
@@ -133,7 +149,7 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
 #endif
     // this wave's LDS-DMA ops per tile (the counted waits below)
     const int n_ops = (wave < St::IMG_U4 / 64 ? (St::IMG_U4 / 64 - 1 - wave) / WAVES + 1 : 0) +
-                      ((wave == 0 && L2) ? 1 : 0) + (wave == 1 ? 1 : 0);
+                      ((wave == 0 && L2) ? 1 : 0);
     auto fill = [&](uint64_t t, int st) {
         const uint64_t tile = t * (uint64_t)p.tile_stride;
         const uint32_t dst = lds0 + (uint32_t)(st * St::U4 * 16);
@@ -141,14 +157,7 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
 #pragma unroll
         for (int i = wave; i < St::IMG_U4 / 64; i += WAVES)
             glds16s(src, (uint32_t)(i * 1024 + lane * 16), dst + i * 1024);
-        if (wave == 0) {
-            if (L2) glds4(p.xns + tile * H_BN + lane, dst + St::IMG_U4 * 16);
-        } else if (wave == 1) {
-            // lanes 0-1: exclusion word, 2-3: allow word (dword halves)
-            const uint32_t* w = lane < 2 ? reinterpret_cast<const uint32_t*>(p.excl + tile) + lane
-                                         : reinterpret_cast<const uint32_t*>(p.allow + tile) + (lane - 2);
-            if (lane < 2 || (lane < 4 && has_allow)) glds4(w, dst + (St::IMG_U4 + 16) * 16);
-        }
+        if (wave == 0 && L2) glds4(p.xns + tile * H_BN + lane, dst + St::IMG_U4 * 16);
     };
 
     // the tiles of stage-group g (TPS consecutive tiles) into LDS stage g % 3
@@ -279,13 +288,8 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
         // eligibility of a tile's 64 rows for this lane's two columns (bits of
         // rows 4 khalf + ..., low word: rows 0-31, high word: rows 32-63)
         // (the lane-dependent shifts happen only when a tile needs the mask)
-        auto tile_ok = [&](const uint4* img, uint64_t t, uint64_t& okw) -> bool {
-            const uint32_t* w = reinterpret_cast<const uint32_t*>(img + St::IMG_U4 + 16);
-            const uint64_t ex = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
-            const uint64_t al = has_allow ? ((uint64_t)w[2] | ((uint64_t)w[3] << 32)) : ~0ull;
-            okw = ~ex & al;
-            const uint64_t row0 = t * (uint64_t)p.tile_stride * H_BN;
-            if (row0 + H_BN > p.N) okw &= p.N > row0 ? ((1ull << (p.N - row0)) - 1) : 0ull;
+        auto tile_ok = [&](uint64_t t, uint64_t& okw) -> bool {
+            okw = tile_okw(p, t * (uint64_t)p.tile_stride, has_allow);
             return okw != ~0ull || (qb + 1) * BQ > p.nq;
         };
         auto lane_ok = [&](uint64_t okw, int jq) -> uint64_t { return (jq < p.nq ? okw : 0ull) >> (4 * khalf); };
@@ -367,7 +371,7 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
         block_barrier();          // everyone's
         if (ntile > 0) {
             mfma_half(tile_lds(0), 0, acc00, acc01, [] {});
-            need_mask = tile_ok(tile_lds(0), t_begin, okw);
+            need_mask = tile_ok(t_begin, okw);
         }
         for (int t = 0; t < ntile; ++t) {
             WV_DBG_COUNT(0)
@@ -421,7 +425,7 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
             if (mask_t) mask_half(acc10, acc11, (uint32_t)(mo0 >> 32), (uint32_t)(mo1 >> 32));
             if (t + 1 < ntile) {
                 mfma_half(tile_lds(t + 1), 0, acc00, acc01, [&] { m0 = min16(acc10); m1 = min16(acc11); });
-                need_mask = tile_ok(tile_lds(t + 1), t_begin + t + 1, okw);
+                need_mask = tile_ok(t_begin + t + 1, okw);
             } else {
                 m0 = min16(acc10);
                 m1 = min16(acc11);
@@ -573,20 +577,14 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16q_kernel(H16Pa
     if (u_last > (uint64_t)p.n_qblocks * p.ntiles) u_last = (uint64_t)p.n_qblocks * p.ntiles;
     const uint32_t lds0 = lds_addr(lds);
     const int n_ops = (wave < St::IMG_U4 / 64 ? (St::IMG_U4 / 64 - 1 - wave) / WAVES + 1 : 0) +
-                      ((wave == 0 && L2) ? 1 : 0) + (wave == 1 ? 1 : 0);
+                      ((wave == 0 && L2) ? 1 : 0);
     auto fill = [&](uint64_t t, int st) {
         const uint64_t tile = t * (uint64_t)p.tile_stride;
         const uint32_t dst = lds0 + (uint32_t)(st * St::U4 * 16);
         const uint4* src = X + tile * St::IMG_U4;
 #pragma unroll
         for (int i = wave; i < St::IMG_U4 / 64; i += WAVES) glds16s(src, (uint32_t)(i * 1024 + lane * 16), dst + i * 1024);
-        if (wave == 0) {
-            if (L2) glds4(p.xns + tile * H_BN + lane, dst + St::IMG_U4 * 16);
-        } else if (wave == 1) {
-            const uint32_t* w = lane < 2 ? reinterpret_cast<const uint32_t*>(p.excl + tile) + lane
-                                         : reinterpret_cast<const uint32_t*>(p.allow + tile) + (lane - 2);
-            if (lane < 2 || (lane < 4 && has_allow)) glds4(w, dst + (St::IMG_U4 + 16) * 16);
-        }
+        if (wave == 0 && L2) glds4(p.xns + tile * H_BN + lane, dst + St::IMG_U4 * 16);
     };
     auto fill_group = [&](uint64_t t_begin, int g, int ntile) {
         const int st = g % H_STAGES;
@@ -684,13 +682,8 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16q_kernel(H16Pa
                 __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
             }
         };
-        auto tile_ok = [&](const uint4* img, uint64_t t, uint64_t& okw) -> bool {
-            const uint32_t* w = reinterpret_cast<const uint32_t*>(img + St::IMG_U4 + 16);
-            const uint64_t ex = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
-            const uint64_t al = has_allow ? ((uint64_t)w[2] | ((uint64_t)w[3] << 32)) : ~0ull;
-            okw = ~ex & al;
-            const uint64_t row0 = t * (uint64_t)p.tile_stride * H_BN;
-            if (row0 + H_BN > p.N) okw &= p.N > row0 ? ((1ull << (p.N - row0)) - 1) : 0ull;
+        auto tile_ok = [&](uint64_t t, uint64_t& okw) -> bool {
+            okw = tile_okw(p, t * (uint64_t)p.tile_stride, has_allow);
             return okw != ~0ull || (qb + 1) * BQ > p.nq;
         };
         // ineligible keys of half h to +inf (row 16 rg + 4 lq + r of the tile)
@@ -789,7 +782,7 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16q_kernel(H16Pa
         block_barrier();
         if (ntile > 0) {
             mfma_half(tile_lds(0), 0, [] {});
-            need_mask = tile_ok(tile_lds(0), t_begin, okw);
+            need_mask = tile_ok(t_begin, okw);
         }
         for (int t = 0; t < ntile; ++t) {
             WV_DBG_COUNT(0)
@@ -812,7 +805,9 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16q_kernel(H16Pa
             bool grew = epilogue(0, m, rb0);
             // ---- C: group g + 1 landed; every wave done with group g's stage ----
             if (t % TPS == TPS - 1 || t == ntile - 1) {
+#ifndef WV_H16_ABLATE_NO_VMWAIT
                 if (g + 1 < ngroups) vm_wait(ops_in_flight);
+#endif
                 block_barrier();
             }
             // ---- E: H0(t + 1) MFMAs, H1(t) minima ----
@@ -822,7 +817,9 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16q_kernel(H16Pa
 #pragma unroll
                     for (int q = 0; q < 4; ++q) m[q] = min8(1, q);
                 });
-                need_mask = tile_ok(tile_lds(t + 1), t_begin + t + 1, okw);
+#ifndef WV_H16_ABLATE_NO_TILEOK
+                need_mask = tile_ok(t_begin + t + 1, okw);
+#endif
             } else {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) m[q] = min8(1, q);
