@@ -764,7 +764,8 @@ def test_split_pass_query_blocks_multi_segment(dim, metric):
 def test_h16_key_pass_seeded_equals_unseeded_and_fp32(dim, metric):
     """The f16 key pass at a corpus size that runs the seed pre-pass (>= 64k
     rows): seeded (default), unseeded (WV_H16_NO_SEED), without the XCD remap
-    (WV_BF_LOCALITY=0) and the fp32 pass return the same ids and distances,
+    (WV_BF_LOCALITY=0), the 16x16x32 kernel seeded and unseeded (WV_H16_QUAD)
+    and the fp32 pass return the same ids and distances,
     with tombstones, a shared allow list kept in the epilogue and a partial
     last query block -- and equal the restatement up to tie order.  D=100 is
     GloVe-shaped (7 k-steps of 16: 112, not 128)."""
@@ -776,7 +777,10 @@ def test_h16_key_pass_seeded_equals_unseeded_and_fp32(dim, metric):
     allow_ids = np.nonzero(rng.random(n) < 0.6)[0]
     al = W.AllowList.from_ids(allow_ids, n)
     runs = []
-    for env in ({}, {"WV_H16_NO_SEED": "1"}, {"WV_BF_LOCALITY": "0"}, {"WV_BF_FP32": "1"}):
+    # WV_H16_QUAD: the 16x16x32 kernel (shared column lists) where D allows
+    # it (128: 4 32-k steps; at 100 the 32x32x16 kernel runs regardless)
+    for env in ({}, {"WV_H16_NO_SEED": "1"}, {"WV_BF_LOCALITY": "0"}, {"WV_BF_FP32": "1"}, {"WV_H16_QUAD": "1"},
+                {"WV_H16_QUAD": "1", "WV_H16_NO_SEED": "1"}):
         os.environ.update(env)
         try:
             ix = W.GPUVectorIndex(dim, METRIC_NAMES[metric], capacity=n)
