@@ -1,0 +1,12 @@
+#!/bin/bash
+# previous kernel (abl_old) vs the current one without and with the
+# cross-slot threshold, alternated in one call
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+: > gpurun_out/xslot2.log
+for r in 1 2; do
+  timeout -k 5 120 build/h16/abl_old 1000000 10000 128 old >> gpurun_out/xslot2.log 2>&1 || exit $?
+  WV_H16_XSLOT=0 timeout -k 5 120 build/h16/abl_base 1000000 10000 128 xslot0 >> gpurun_out/xslot2.log 2>&1 || exit $?
+  WV_H16_XSLOT=1 timeout -k 5 120 build/h16/abl_base 1000000 10000 128 xslot1 >> gpurun_out/xslot2.log 2>&1 || exit $?
+done
+cat gpurun_out/xslot2.log

@@ -232,7 +232,7 @@ struct wv_index {
     bool h16_quad = false;  // D <= 128, even 16-k steps: wv_bf_h16q_kernel (16x16x32 MFMA, h16q_index images)
     int h16_ns = 0;
     float h16_sx = 0.f, h16_ex = 0.f;
-    DevBuf ximg16, xns, qimg16, qres, qmax, qscale, tau, gtau, marg, allow_pad, ex_bits;
+    DevBuf ximg16, xns, qimg16, qres, qmax, qscale, tau, gtau, marg, allow_pad, ex_bits, gslot;
     DevBuf ximg16q;         // the corpus image in the 16x16x32 layout (h16_quad), beside ximg16
     DevBuf qmax_part;       // per-block max |q_i| of the query-norm pass
     float maxnorm_host = 0.f;   // max |x| (rounded up), cached after every row write
@@ -643,6 +643,16 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     hp.kth = k <= prod * kp && (!seed || std::getenv("WV_H16_RUN_SEED")) && !wd && !std::getenv("WV_H16_NO_RUNNING")
                  ? k
                  : 0;
+    // cross-slot threshold (32x32x16 pass, <= 32 list heads per query)
+    const char* xe = std::getenv("WV_H16_XSLOT");
+    if (xe && std::atoi(xe) == 1 && !quad && !wd && 2 * sch.n_slots <= 32 && k <= 2 * sch.n_slots) {
+        const size_t gb = (size_t)nq * 2 * sch.n_slots * 4;
+        HIP_TRY(ix->gslot.ensure(gb));
+        HIP_TRY(hipMemsetAsync(ix->gslot.p, 0x7F, gb, s));   // 3.4e38: no head yet
+        hp.gslot = ix->gslot.as<float>();
+        hp.xslot = 1;
+        hp.kth = k;
+    }
     if (hp.kth) {
         HIP_TRY(ix->marg.ensure((size_t)nq * 4));
         HIP_TRY(wv_launch_h16_margin(ix->metric, ix->dim, ix->q_nrm2.as<float>(), ix->qres.as<float>(),
@@ -1395,7 +1405,7 @@ int wv_index_destroy(wv_index* ix) {
                       &ix->out_ids, &ix->out_d, &ix->out_n, &ix->stage, &ix->fail_thr, &ix->fb_idx, &ix->fb_d, &ix->fb_i, &ix->fb_n, &ix->fb_of,
                       &ix->ac_cnt, &ix->ac_off, &ix->rowidx, &ix->pq_cent, &ix->pq_codes, &ix->pk_key,
                       &ix->pk_dist, &ix->pk_val, &ix->pk_skey, &ix->pk_sval, &ix->pk_off, &ix->ximg16, &ix->ximg16q, &ix->qmax_part, &ix->xns,
-                      &ix->qimg16, &ix->qres, &ix->qmax, &ix->qscale, &ix->tau, &ix->gtau, &ix->marg, &ix->allow_pad, &ix->ex_bits,
+                      &ix->qimg16, &ix->qres, &ix->qmax, &ix->qscale, &ix->tau, &ix->gtau, &ix->marg, &ix->allow_pad, &ix->ex_bits, &ix->gslot,
                       &ix->delta, &ix->dmask, &ix->dl_ids, &ix->dl_d, &ix->dl_n, &ix->dq_tmp, &ix->b_tgt, &ix->b_ci,
                       &ix->b_cd, &ix->b_cn, &ix->b_cnt0, &ix->b_cntu, &ix->b_rk, &ix->b_rn, &ix->b_rk2, &ix->b_rn2,
                       &ix->b_uk, &ix->b_ul, &ix->b_uo, &ix->b_nr, &ix->b_tmp, &ix->stat_acc, &ix->fbd_list,

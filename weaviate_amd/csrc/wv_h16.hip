@@ -117,7 +117,7 @@ constexpr int H_STAGES = 3;   // a stage holds H_TPS tiles; stage p % 3 computes
 // WAVES = 8: one 512-query workgroup per CU (two waves per SIMD, kept in
 // phase by the stage barrier); WAVES = 4: two independent 256-query
 // workgroups per CU (one wave per SIMD each), TPS tiles per LDS stage.
-template <int NS, bool L2, bool SEED, int WAVES, int TPS>
+template <int NS, bool L2, bool SEED, int WAVES, int TPS, bool XS = false>
 __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Params p) {
     constexpr int BQ = WAVES * 64;
     extern __shared__ uint4 lds[];
@@ -361,7 +361,61 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
             if (jq1 < p.nq) tau1 = fminf(tau1, h16_key_dec(__atomic_load_n(&p.gtau[jq1], __ATOMIC_RELAXED)));
             refresh_pt();
         };
-        const bool running = !SEED && p.kth > 0 && p.gtau != nullptr;
+        const bool running = !SEED && p.kth > 0 && p.gtau != nullptr && !p.xslot;
+        // cross-slot threshold: the slots of a query block run side by side
+        // over equal tile ranges, so at a fraction f of the segment the heads
+        // of all 2 n_slots lists are the minima of disjoint row sets covering
+        // f of the corpus; their k-th smallest (+ 2 eps) bounds the k-th key
+        // at rank ~ k / f instead of the seed's ~ k H_SAMPLE.  Stored at 1/8,
+        // 1/4, 1/2 of the segment, read at 1/4, 1/2, 3/4 (the values the
+        // other slots stored one step earlier).  Lane half 0 selects for
+        // jq0, lane half 1 for jq1.
+        const bool xs = XS && !SEED && p.kth > 0;   // (its own instantiation: the code costs SGPRs)
+        auto xslot_step = [&](bool rd, bool wr) {
+            const int nv = 2 * p.n_slots;
+            if (rd) {
+                const int jq = khalf ? jq1 : jq0;
+                float v[32];
+#pragma unroll
+                for (int i = 0; i < 32; ++i)
+                    v[i] = (i < nv && jq < p.nq) ? __hip_atomic_load(p.gslot + (size_t)jq * nv + i, __ATOMIC_RELAXED,
+                                                                    __HIP_MEMORY_SCOPE_AGENT)
+                                                 : FLT_MAX;
+                // ascending bitonic network over the 32 values, then entry k - 1
+#pragma unroll
+                for (int size = 2; size <= 32; size <<= 1)
+#pragma unroll
+                    for (int stride = size >> 1; stride > 0; stride >>= 1)
+#pragma unroll
+                        for (int i = 0; i < 32; ++i) {
+                            const int j = i ^ stride;
+                            if (j > i) {
+                                const float a = v[i], b = v[j];
+                                const bool up = (i & size) == 0;
+                                v[i] = up ? fminf(a, b) : fmaxf(a, b);
+                                v[j] = up ? fmaxf(a, b) : fminf(a, b);
+                            }
+                        }
+                float kv = FLT_MAX;
+#pragma unroll
+                for (int i = 0; i < 32; ++i) kv = i == p.kth - 1 ? v[i] : kv;
+                const float mg = khalf ? marg1 : marg0;
+                const float u4 = 4.f * 5.9604645e-08f;
+                float b = kv < 1e30f ? kv + mg + u4 * (fabsf(kv) + mg) : FLT_MAX;
+                const float bo = __shfl_xor(b, 32, 64);   // the other half's query
+                tau0 = fminf(tau0, khalf ? bo : b);
+                tau1 = fminf(tau1, khalf ? b : bo);
+                refresh_pt();
+            }
+            if (wr) {
+                const int s2 = 2 * slot + khalf;
+                if (jq0 < p.nq && l0d[0] < FLT_MAX)
+                    __hip_atomic_store(p.gslot + (size_t)jq0 * nv + s2, l0d[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (jq1 < p.nq && l1d[0] < FLT_MAX)
+                    __hip_atomic_store(p.gslot + (size_t)jq1 * nv + s2, l1d[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        };
+        const int xs1 = ntile / 8, xs2 = ntile / 4, xs3 = ntile / 2, xs4 = (3 * ntile) / 4;
         const int ngroups = (ntile + TPS - 1) / TPS;
         // (the previous segment ended with every stage read and every DMA landed)
         int ops_in_flight = 0;   // this wave's DMA ops of the newest group issued
@@ -455,6 +509,8 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
 #endif
                 if (running && (t & 15) == 15) publish();
                 else if (grew) refresh_pt();
+                if constexpr (XS)
+                    if (xs && (t == xs1 || t == xs2 || t == xs3 || t == xs4)) xslot_step(t != xs1, t != xs4);
             }
         }
 
@@ -1286,7 +1342,9 @@ hipError_t wv_launch_bf_h16(const wv::H16Params* p, int ns, int seed, int waves,
     const int tps = waves == 8 ? wv::H_TPS8 : 1;
     const size_t lds = (size_t)wv::H_STAGES * tps * (2 * ns * 64 + 17) * 16;
 #define WV_H16_GO(NS, L, S)                                                                                    \
-    if (waves == 8) hipLaunchKernelGGL((wv::wv_bf_h16_kernel<NS, L, S, 8, wv::H_TPS8>), dim3(nb), dim3(512), lds, s, *p); \
+    if (waves == 8 && !S && p->xslot)                                                                          \
+        hipLaunchKernelGGL((wv::wv_bf_h16_kernel<NS, L, false, 8, wv::H_TPS8, true>), dim3(nb), dim3(512), lds, s, *p); \
+    else if (waves == 8) hipLaunchKernelGGL((wv::wv_bf_h16_kernel<NS, L, S, 8, wv::H_TPS8>), dim3(nb), dim3(512), lds, s, *p); \
     else hipLaunchKernelGGL((wv::wv_bf_h16_kernel<NS, L, S, 4, 1>), dim3(nb), dim3(256), lds, s, *p);
 #define WV_H16_LAUNCH(NS)                     \
     if (seed) {                               \

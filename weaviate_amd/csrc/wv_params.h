@@ -155,6 +155,11 @@ struct H16Params {
     unsigned int* gtau;       // [nq] (nullable)
     int kth;                  // k (0: no running threshold)
     const float* marg;        // [nq] 2 eps in scaled key units, rounded up (wv_h16_margin_kernel)
+    // cross-slot threshold (xslot, 32x32x16 pass): each slot stores its lists'
+    // heads in gslot[q][2 slot + lane half] at a few points of its segment and
+    // reads the others', whose k-th smallest + 2 eps bounds the k-th key
+    float* gslot;             // [nq][2 n_slots] (xslot)
+    int xslot;                // 1: use gslot instead of the gtau publish
     int ns;                   // 16-k steps of the images (the wide-D kernel: a multiple of HW_KC)
 };
 
