@@ -826,16 +826,16 @@ def test_h16_integer_data_keys_exact():
 
 
 def test_h16_cross_slot_threshold_equals_default():
-    """The opt-in cross-slot threshold (WV_H16_XSLOT=1) only rejects keys above
-    a certified bound on the k-th key, so the results equal the default pass
-    bit for bit.  8 300 queries over 70k rows make 17 query blocks, so a
+    """The cross-slot threshold (default; WV_H16_XSLOT=0 turns it off) only
+    rejects keys above a certified bound on the k-th key, so the results equal
+    the pass without it bit for bit.  8 300 queries over 70k rows make 17 query blocks, so a
     query block has <= 16 slots (<= 32 list heads), where it engages."""
     import os
     n, d, nq = 70001, 128, 8300
     base, qs = _data(n, d, nq, seed=91)
     tomb_ids = np.nonzero(np.random.default_rng(92).random(n) < 0.01)[0]
     runs = []
-    for env in ({}, {"WV_H16_XSLOT": "1"}):
+    for env in ({}, {"WV_H16_XSLOT": "0"}):
         os.environ.update(env)
         try:
             ix = W.GPUVectorIndex(d, "l2-squared", capacity=n)

@@ -375,12 +375,13 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
             const int nv = 2 * p.n_slots;
             if (rd) {
                 const int jq = khalf ? jq1 : jq0;
+                int nvv = jq < p.nq ? nv : 0;   // (opaque VGPR, as ve below)
+                asm volatile("" : "+v"(nvv));
+                const float* g = p.gslot + (size_t)jq * nv;
                 float v[32];
 #pragma unroll
                 for (int i = 0; i < 32; ++i)
-                    v[i] = (i < nv && jq < p.nq) ? __hip_atomic_load(p.gslot + (size_t)jq * nv + i, __ATOMIC_RELAXED,
-                                                                    __HIP_MEMORY_SCOPE_AGENT)
-                                                 : FLT_MAX;
+                    v[i] = i < nvv ? __hip_atomic_load(g + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : FLT_MAX;
                 // ascending bitonic network over the 32 values, then entry k - 1
 #pragma unroll
                 for (int size = 2; size <= 32; size <<= 1)
@@ -396,9 +397,13 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
                                 v[j] = up ? fmaxf(a, b) : fminf(a, b);
                             }
                         }
+                // (an opaque VGPR index: a uniform one would keep 32 SGPR
+                // masks live across the tile loop)
+                int ve = p.kth - 1;
+                asm volatile("" : "+v"(ve));
                 float kv = FLT_MAX;
 #pragma unroll
-                for (int i = 0; i < 32; ++i) kv = i == p.kth - 1 ? v[i] : kv;
+                for (int i = 0; i < 32; ++i) kv = i == ve ? v[i] : kv;
                 const float mg = khalf ? marg1 : marg0;
                 const float u4 = 4.f * 5.9604645e-08f;
                 float b = kv < 1e30f ? kv + mg + u4 * (fabsf(kv) + mg) : FLT_MAX;
