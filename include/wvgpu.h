@@ -189,8 +189,10 @@ int wv_search_batch(wv_index *ix, const float *queries, int nq, int k, int ef, c
 /* Device-resident variant: every pointer is device memory.  d_queries holds
  * nq rows at a stride of wv_index_query_ld(ix) floats (dim rounded up to 4;
  * the pad columns are ignored).  The work is queued on `stream` (a
- * hipStream_t, NULL = the index's own stream) and ordered after every earlier
- * call on the index; later calls on the index are ordered after it.  The
+ * hipStream_t, NULL = the index's own stream, then also ordered after the work
+ * already queued on the legacy default stream, where a caller may have just
+ * written d_queries) and ordered after every earlier call on the index; later
+ * calls on the index are ordered after it.  The
  * results are complete when the stream reaches the end of the queued work.
  * Exact searches (k <= 256 on the f16 key pass, k <= 32 otherwise) and HNSW
  * searches without an allow list queue everything, certificate fallbacks

@@ -102,3 +102,37 @@ def test_device_fallback_on_sift_like_ties_matches_restatement():
     for i in range(len(qs)):
         same_tie_aware(gi[i], gd[i], oi[i], od[i])
     ix.close()
+
+
+def test_null_stream_call_orders_after_default_stream_writes():
+    """stream=NULL queues on the index's own non-blocking stream; the query
+    rows a torch kernel has just written on the legacy default stream must
+    still be read complete (the call records an event on stream 0 and waits
+    for it).  The queries are produced by a chain of default-stream kernels
+    that takes far longer than the launch, so a missing wait reads zeros."""
+    n, d, nq, k = 200_000, 128, 4096, 10
+    rng = np.random.default_rng(5)
+    base = rng.random((n, d), dtype=np.float32)
+    qs = rng.random((nq, d), dtype=np.float32)
+    ix = W.GPUVectorIndex(d, "l2-squared", capacity=n)
+    ix.upload_vectors(base)
+    dev = torch.device("cuda:0")
+    ld = ix.query_ld()
+    src = torch.zeros((nq, ld), dtype=torch.float32, device=dev)
+    src[:, :d] = torch.from_numpy(qs).to(dev)
+    ids = torch.empty((nq, k), dtype=torch.int64, device=dev)
+    ds = torch.empty((nq, k), dtype=torch.float32, device=dev)
+    cnt = torch.empty(nq, dtype=torch.int32, device=dev)
+    big = torch.randn(4096, 4096, device=dev)
+    for _ in range(3):
+        q = torch.zeros_like(src)
+        torch.cuda.synchronize()
+        assert torch.cuda.current_stream().cuda_stream == 0
+        for _ in range(20):          # ~ms of default-stream work ahead of the query write
+            big = torch.tanh(big @ big)
+        q.copy_(src)                 # the query rows land only after that
+        ix.search_batch_device(q.data_ptr(), nq, k, ids.data_ptr(), ds.data_ptr(), cnt.data_ptr(), mode="exact")
+        torch.cuda.synchronize()
+        hi, hd, hn = ix.search_batch(qs[:256], k, mode="exact")
+        assert ids.cpu().numpy()[:256].view(np.uint64).tolist() == hi.tolist()
+    ix.close()

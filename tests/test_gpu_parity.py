@@ -849,3 +849,48 @@ def test_h16_cross_slot_threshold_equals_default():
     for (ai, ad, an), (bi, bd, bn) in zip(runs[0], runs[1]):
         assert an.tolist() == bn.tolist()
         _same(ai, ad, bi, bd)
+    # and the default (cross-slot threshold engaged) against the restatement
+    tb = O.bits_from_ids(tomb_ids, n)
+    for k, (gi, gd, gn) in zip((10, 32), runs[0]):
+        oi, od, on = O.flat_scan(O.L2, base, qs, k, tomb_bits=tb, threads=16)
+        assert gn.tolist() == on.tolist()
+        for i in range(nq):
+            _same_tie_aware(gi[i], gd[i], oi[i], od[i])
+
+
+@pytest.mark.parametrize("data", ["uniform", "integer"])
+def test_h16_cross_slot_threshold_without_seed_equals_restatement(data):
+    """The cross-slot threshold where no seed pre-pass runs (40k rows: 625
+    tiles, under the 64 x H_SAMPLE cutoff) and the running threshold is off:
+    certification then rests on the list tails and on the bounds the cross
+    slot exchange published to gtau (the finalize's tau_in).  17 query blocks
+    (<= 16 slots each), uniform and tie-heavy integer data, k = 10 and 32:
+    on == off == the restatement (tie-aware)."""
+    import os
+    n, d, nq = 40000, 128, 8700
+    if data == "uniform":
+        base, qs = _data(n, d, nq, seed=93)
+    else:
+        rng = np.random.default_rng(94)
+        base = rng.integers(0, 4, (n, d)).astype(np.float32)
+        qs = rng.integers(0, 4, (nq, d)).astype(np.float32)
+    tomb_ids = np.nonzero(np.random.default_rng(95).random(n) < 0.01)[0]
+    runs = []
+    for env in ({}, {"WV_H16_XSLOT": "0"}):
+        os.environ.update(env)
+        try:
+            ix = W.GPUVectorIndex(d, "l2-squared", capacity=n)
+            ix.upload_vectors(base)
+            ix.set_tombstones(tomb_ids)
+            runs.append([ix.search_batch(qs, k, mode="exact") for k in (10, 32)])
+            ix.close()
+        finally:
+            for key in env:
+                os.environ.pop(key, None)
+    tb = O.bits_from_ids(tomb_ids, n)
+    for k, (a, b) in zip((10, 32), zip(runs[0], runs[1])):
+        oi, od, on = O.flat_scan(O.L2, base, qs, k, tomb_bits=tb, threads=16)
+        for gi, gd, gn in (a, b):
+            assert gn.tolist() == on.tolist()
+            for i in range(nq):
+                _same_tie_aware(gi[i], gd[i], oi[i], od[i])

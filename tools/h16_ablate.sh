@@ -13,10 +13,17 @@ if [ "$1" == "build" ]; then
   rm -f $B/abl_*
   for v in $VARIANTS; do
     name=${v%%=*}; defs=${v#*=}; defs=${defs//:/ }
-    /opt/rocm/bin/hipcc $HF -fno-honor-nans $defs -c $C/wv_h16.hip -o $B/h16_$name.o
-    /opt/rocm/bin/hipcc --offload-arch=gfx950 -pthread $B/main.o $B/h16_$name.o $C/wv_bf.o $C/wv_hnsw.o $C/wv_pq.o \
+    (
+    # the variant's defines apply to the one-wave-per-SIMD pass (wv_h16s.hip,
+    # WV_H16_SOLO=1 at run time) unless SOLO_ONLY=0 also builds wv_h16.hip with them
+    if [ "${SOLO_ONLY:-1}" == "1" ]; then cp $C/wv_h16.o $B/h16_$name.o; else
+      /opt/rocm/bin/hipcc $HF -fno-honor-nans $defs -c $C/wv_h16.hip -o $B/h16_$name.o; fi
+    /opt/rocm/bin/hipcc $HF -fno-honor-nans -mllvm -amdgpu-mfma-vgpr-form $defs -c $C/wv_h16s.hip -o $B/h16s_$name.o
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -pthread $B/main.o $B/h16_$name.o $B/h16s_$name.o $C/wv_bf.o $C/wv_hnsw.o $C/wv_pq.o \
         $C/wv_api.o $C/wv_batcher.o $C/wv_commitlog.o $C/wv_group.o -L/opt/rocm/lib -lrccl -o $B/abl_$name
+    ) &
   done
+  wait
   exit 0
 fi
 export WV_ABLATE_NO_FALLBACK=1

@@ -57,6 +57,7 @@ hipError_t wv_launch_h16_qscale(const float* part, int nparts, unsigned int* max
 hipError_t wv_launch_h16_xns(const float* xnorm, uint64_t n, float sx, const float* qscale, float* xns, hipStream_t s);
 hipError_t wv_launch_bf_h16(const wv::H16Params* p, int ns, int seed, int waves, hipStream_t s);
 hipError_t wv_launch_bf_h16q(const wv::H16Params* p, int ns32, int seed, int waves, hipStream_t s);
+hipError_t wv_launch_bf_h16s(const wv::H16Params* p, int ns32, int seed, hipStream_t s);
 hipError_t wv_launch_bf_h16w(const wv::H16Params* p, hipStream_t s);
 hipError_t wv_launch_h16_seed(const wv::H16SeedParams* p, hipStream_t s);
 hipError_t wv_launch_h16_margin(int metric, int D, const float* qnorm, const float* qres, float xnorm_max,
@@ -230,6 +231,7 @@ struct wv_index {
     bool use_h16 = false;
     bool h16_wide = false;  // D > 128: wv_bf_h16w_kernel (both operands through LDS, 128-row tiles)
     bool h16_quad = false;  // D <= 128, even 16-k steps: wv_bf_h16q_kernel (16x16x32 MFMA, h16q_index images)
+    bool h16_solo = false;  // D <= 128, even 16-k steps: wv_bf_h16s_kernel (one wave per SIMD, h16q_index images)
     int h16_ns = 0;
     float h16_sx = 0.f, h16_ex = 0.f;
     DevBuf ximg16, xns, qimg16, qres, qmax, qscale, tau, gtau, marg, allow_pad, ex_bits, gslot;
@@ -293,6 +295,7 @@ struct wv_index {
     // then waits for the call, so the scratch and state buffers the call reads
     // are never rewritten by a later call while it is still queued
     hipEvent_t ev_in = nullptr, ev_out = nullptr;
+    hipEvent_t ev_null = nullptr;   // a NULL-stream call: the legacy default stream's work so far
     // optional kernel timing (hipEvents on the launch stream): each batch
     // records into its own event set (pairs 0-1 key pass, 2-3 finalize, 4-5
     // HNSW, 6-7 seed pass); the sets are read -- after a sync -- only when the
@@ -491,12 +494,17 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     const bool wd = ix->h16_wide;   // D > 128: the wide-D kernel
     // the 16x16x32 kernel (one 16-entry list per column and slot) for k <=
     // FIN_KF; wider k on the 32x32x16 kernel
-    const bool quad = ix->h16_quad && k <= wv::FIN_KF;
+    // k <= FIN_KF: the one-wave-per-SIMD 16x16x32 kernel (h16_solo) or the
+    // opt-in two-waves-per-SIMD one (h16_quad) -- one 16-entry list per
+    // column and slot; wider k on the 32x32x16 kernel
+    const bool solo = ix->h16_solo && k <= wv::FIN_KF;
+    const bool quad = (ix->h16_quad || solo) && k <= wv::FIN_KF;
     // D <= 128: 8-wave (512-query) workgroups, one per CU; WV_H16_WAVES=4:
-    // 4-wave (256-query) workgroups, two independent ones per CU
-    const int waves = std::getenv("WV_H16_WAVES") && std::atoi(std::getenv("WV_H16_WAVES")) == 4 ? 4 : 8;
-    const int wg_per_cu = wd ? 1 : 8 / waves;
-    const int tile_rows = wd ? wv::HW_BN : wv::H_BN, bq = wd ? wv::HW_BQ : waves * 64;
+    // 4-wave (256-query) workgroups, two independent ones per CU; solo: one
+    // 4-wave 512-query workgroup per CU
+    const int waves = solo ? 4 : std::getenv("WV_H16_WAVES") && std::atoi(std::getenv("WV_H16_WAVES")) == 4 ? 4 : 8;
+    const int wg_per_cu = wd || solo ? 1 : 8 / waves;
+    const int tile_rows = wd ? wv::HW_BN : wv::H_BN, bq = wd ? wv::HW_BQ : solo ? wv::HS_BQ : waves * 64;
     // seed minima per query and slot; lists per query and slot, entries per list
     const int seed_prod = wd ? wv::HW_PROD : (quad ? wv::HQ_PROD : wv::H_PROD);
     const int prod = quad ? 1 : seed_prod;
@@ -601,7 +609,8 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
         hp.out_d = ix->cand_d.as<float>();
         hp.out_id = nullptr;
         TREC(6);
-        HIP_TRY(quad ? wv_launch_bf_h16q(&hp, ns / 2, 1, waves, s) : wv_launch_bf_h16(&hp, ns, 1, waves, s));
+        HIP_TRY(solo ? wv_launch_bf_h16s(&hp, ns / 2, 1, s)
+                     : quad ? wv_launch_bf_h16q(&hp, ns / 2, 1, waves, s) : wv_launch_bf_h16(&hp, ns, 1, waves, s));
         wv::H16SeedParams sp{};
         sp.minima = ix->cand_d.as<float>();
         sp.n_slots = ss.n_slots;
@@ -647,7 +656,7 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     // unless WV_H16_XSLOT=0): 2.87-2.91 vs 2.98-3.00 ms per 1M x 10k key pass
     const char* xe = std::getenv("WV_H16_XSLOT");
     const bool xs_on = !xe || std::atoi(xe) != 0;
-    if (xs_on && !quad && !wd && 2 * sch.n_slots <= 32 && k <= 2 * sch.n_slots) {
+    if (xs_on && (!quad || solo) && !wd && 2 * sch.n_slots <= 32 && k <= 2 * sch.n_slots) {
         const size_t gb = (size_t)nq * 2 * sch.n_slots * 4;
         HIP_TRY(ix->gslot.ensure(gb));
         HIP_TRY(hipMemsetAsync(ix->gslot.p, 0x7F, gb, s));   // 3.4e38: no head yet
@@ -666,6 +675,7 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     hp.out_id = ix->cand_id.as<uint32_t>();
     TREC(0);
     HIP_TRY(wd ? wv_launch_bf_h16w(&hp, s)
+               : solo ? wv_launch_bf_h16s(&hp, ns / 2, 0, s)
                : (quad ? wv_launch_bf_h16q(&hp, ns / 2, 0, waves, s) : wv_launch_bf_h16(&hp, ns, 0, waves, s)));
     TREC(1);
     fp.cand_d = ix->cand_d.as<float>();
@@ -1367,16 +1377,19 @@ int wv_index_create(int dim, int metric, const wv_config* cfg, uint64_t capacity
         // fallback costs more than the pass gains
         const char* eq = std::getenv("WV_H16_QUAD");
         ix->h16_quad = !ix->h16_wide && ix->h16_ns % 2 == 0 && eq && std::atoi(eq) == 1;
+        // the one-wave-per-SIMD 16x16x32 kernel (WV_H16_SOLO=1)
+        const char* es = std::getenv("WV_H16_SOLO");
+        ix->h16_solo = !ix->h16_wide && ix->h16_ns % 2 == 0 && es && std::atoi(es) == 1;
         const size_t ibytes = cap_rows * (size_t)ix->h16_ns * 16 * 2;
         if (ix->ximg16.ensure(ibytes) != hipSuccess || ix->xns.ensure(cap_rows * 4) != hipSuccess ||
-            (ix->h16_quad && ix->ximg16q.ensure(ibytes) != hipSuccess) ||
+            ((ix->h16_quad || ix->h16_solo) && ix->ximg16q.ensure(ibytes) != hipSuccess) ||
             ix->ex_bits.ensure(4) != hipSuccess || ix->qmax.ensure(4) != hipSuccess ||
             ix->qscale.ensure(4) != hipSuccess) {
             wv_index_destroy(ix);
             return fail(WV_EOOM, "wv_index_create: device allocation failed");
         }
         (void)hipMemsetAsync(ix->ximg16.p, 0, ibytes, ix->stream);
-        if (ix->h16_quad) (void)hipMemsetAsync(ix->ximg16q.p, 0, ibytes, ix->stream);
+        if (ix->h16_quad || ix->h16_solo) (void)hipMemsetAsync(ix->ximg16q.p, 0, ibytes, ix->stream);
         (void)hipMemsetAsync(ix->xns.p, 0, cap_rows * 4, ix->stream);
         (void)hipMemsetAsync(ix->ex_bits.p, 0, 4, ix->stream);
     }
@@ -1419,6 +1432,7 @@ int wv_index_destroy(wv_index* ix) {
             if (e) (void)hipEventDestroy(e);
     if (ix->ev_in) (void)hipEventDestroy(ix->ev_in);
     if (ix->ev_out) (void)hipEventDestroy(ix->ev_out);
+    if (ix->ev_null) (void)hipEventDestroy(ix->ev_null);
     if (ix->stream) (void)hipStreamDestroy(ix->stream);
     delete ix;
     return WV_OK;
@@ -1452,7 +1466,7 @@ static int rows_written(wv_index* ix, const uint64_t* d_ids, uint64_t n, uint64_
     unsigned int* exb = ix->ex_bits.as<unsigned int>();
     if (rebuild) HIP_TRY(hipMemsetAsync(exb, 0, 4, ix->stream));
     // both layouts: 32x32x16 (ximg16) and, with h16_quad, 16x16x32 (ximg16q)
-    for (int quad = 0; quad <= (ix->h16_quad ? 1 : 0); ++quad) {
+    for (int quad = 0; quad <= (ix->h16_quad || ix->h16_solo ? 1 : 0); ++quad) {
         void* img = quad ? ix->ximg16q.p : ix->ximg16.p;
         if (rebuild) {
             HIP_TRY(wv_launch_h16_rows(ix->vecs.as<float>(), ix->ldx, nullptr, ix->n_rows, ix->dim, ix->h16_ns, 1.f,
@@ -2120,6 +2134,13 @@ int wv_search_batch_device(wv_index* ix, const float* d_queries, int nq, int k, 
         }
         HIP_TRY(hipEventRecord(ix->ev_in, ix->stream));
         HIP_TRY(hipStreamWaitEvent(s, ix->ev_in, 0));
+    } else {
+        // NULL: the index's own (non-blocking) stream, which would not wait
+        // for work the caller queued on the legacy default stream -- e.g. a
+        // torch kernel that just wrote d_queries: order after it explicitly
+        if (!ix->ev_null) HIP_TRY(hipEventCreateWithFlags(&ix->ev_null, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(ix->ev_null, nullptr));
+        HIP_TRY(hipStreamWaitEvent(s, ix->ev_null, 0));
     }
     const float* dq = d_queries;
     int rc = WV_OK;

@@ -78,6 +78,27 @@ struct DBuf {
     }
 };
 
+// pinned host staging: an async copy from it is truly asynchronous, and it
+// outlives the call, so nothing has to wait for a copy before the call returns
+struct HBuf {
+    void* p = nullptr;
+    size_t n = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= n) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        n = 0;
+        hipError_t e = hipHostMalloc(&p, std::max<size_t>(bytes, 64), hipHostMallocDefault);
+        if (e == hipSuccess) n = std::max<size_t>(bytes, 64);
+        return e;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
 struct Member {
     wv_index* ix = nullptr;
     int dev = 0;
@@ -85,6 +106,7 @@ struct Member {
     hipEvent_t done = nullptr;
     uint64_t base = 0, cap = 0, rows = 0;   // global ids [base, base + cap); rows written below base + rows
     DBuf q, allow, ids, d, n;
+    HBuf h_allow;                           // this member's slice of the allow list
     int rc = WV_OK;
     std::string err;
 };
@@ -98,6 +120,7 @@ struct wv_group {
     std::vector<Member> m;
     std::vector<ncclComm_t> comms;   // empty: copy path
     DBuf r_ids, r_d, r_n, o_ids, o_d, o_n;   // on the root (member 0's device)
+    HBuf h_q;                                // the batch, staged once for every member's upload
     std::mutex mu;
 };
 
@@ -144,100 +167,119 @@ std::vector<Span> spans(const wv_group* g, uint64_t lo, uint64_t hi) {
     return out;
 }
 
+// wait for every member's stream (error paths: the pinned staging must be
+// idle before a later call rewrites it)
+void drain_members(wv_group* g) {
+    for (auto& mb : g->m) {
+        if (hipSetDevice(mb.dev) == hipSuccess && mb.s) (void)hipStreamSynchronize(mb.s);
+    }
+}
+
 int search_shards(wv_group* g, const float* queries, int nq, int k, int ef, const uint64_t* allow_bits,
                   uint64_t allow_nbits, uint64_t allow_stride, int mode, uint64_t* out_ids, float* out_d,
                   int32_t* out_n) {
     const int n = (int)g->m.size();
     const size_t nk = (size_t)nq * k;
+    // 0. the batch into pinned staging once (a previous call's copies from
+    // it have landed: every call ends with its members' streams drained)
+    G_HIP(g->h_q.ensure((size_t)nq * g->dim * 4));
+    std::memcpy(g->h_q.p, queries, (size_t)nq * g->dim * 4);
     // 1. every member: its queries, its slice of the allow list, its search
+    // (queued, not waited for: the staging is pinned and owned by the group)
     int rc = each_member(g, [&](int i) -> int {
         Member& mb = g->m[i];
         G_HIP(mb.q.ensure((size_t)nq * g->ld * 4));
         G_HIP(mb.ids.ensure(nk * 8));
         G_HIP(mb.d.ensure(nk * 4));
         G_HIP(mb.n.ensure((size_t)nq * 4));
-        G_HIP(hipMemcpy2DAsync(mb.q.p, (size_t)g->ld * 4, queries, (size_t)g->dim * 4, (size_t)g->dim * 4, nq,
+        G_HIP(hipMemcpy2DAsync(mb.q.p, (size_t)g->ld * 4, g->h_q.p, (size_t)g->dim * 4, (size_t)g->dim * 4, nq,
                                hipMemcpyHostToDevice, mb.s));
         const uint64_t* d_allow = nullptr;
         uint64_t nbits = 0, stride = 0;
-        std::vector<uint64_t> slice;
         if (allow_bits) {
             // global bits [base, base + cap) -> local bits [0, cap); base % 64 == 0
             nbits = allow_nbits > mb.base ? std::min(allow_nbits - mb.base, mb.cap) : 0;
             const uint64_t w = (nbits + 63) / 64, w0 = mb.base / 64;
             const uint64_t gw = allow_stride ? allow_stride : (allow_nbits + 63) / 64;
             const int rows_a = allow_stride ? nq : 1;
-            stride = allow_stride ? std::max<uint64_t>(w, 1) : 0;
-            slice.assign((size_t)rows_a * std::max<uint64_t>(w, 1), 0);
+            const uint64_t ws = std::max<uint64_t>(w, 1);
+            stride = allow_stride ? ws : 0;
+            G_HIP(mb.h_allow.ensure((size_t)rows_a * ws * 8));
+            auto* slice = static_cast<uint64_t*>(mb.h_allow.p);
             for (int r = 0; r < rows_a; ++r)
-                for (uint64_t j = 0; j < w && w0 + j < gw; ++j)
-                    slice[(size_t)r * std::max<uint64_t>(w, 1) + j] = allow_bits[(size_t)r * gw + w0 + j];
-            G_HIP(mb.allow.ensure(slice.size() * 8));
-            G_HIP(hipMemcpyAsync(mb.allow.p, slice.data(), slice.size() * 8, hipMemcpyHostToDevice, mb.s));
+                for (uint64_t j = 0; j < ws; ++j)
+                    slice[(size_t)r * ws + j] = j < w && w0 + j < gw ? allow_bits[(size_t)r * gw + w0 + j] : 0;
+            G_HIP(mb.allow.ensure((size_t)rows_a * ws * 8));
+            G_HIP(hipMemcpyAsync(mb.allow.p, slice, (size_t)rows_a * ws * 8, hipMemcpyHostToDevice, mb.s));
             d_allow = static_cast<const uint64_t*>(mb.allow.p);
         }
-        int r = wv_search_batch_device(mb.ix, static_cast<const float*>(mb.q.p), nq, k, ef, d_allow, nbits, stride,
-                                       mode, static_cast<uint64_t*>(mb.ids.p), static_cast<float*>(mb.d.p),
-                                       static_cast<int32_t*>(mb.n.p), mb.s);
-        if (r) return r;
-        // the staging buffers (slice) die with this call: let the copies land
-        G_HIP(hipStreamSynchronize(mb.s));
-        return WV_OK;
+        return wv_search_batch_device(mb.ix, static_cast<const float*>(mb.q.p), nq, k, ef, d_allow, nbits, stride,
+                                      mode, static_cast<uint64_t*>(mb.ids.p), static_cast<float*>(mb.d.p),
+                                      static_cast<int32_t*>(mb.n.p), mb.s);
     });
-    if (rc) return rc;
-    // 2. gather the per-shard lists on the root
-    Member& root = g->m[0];
-    G_HIP(hipSetDevice(root.dev));
-    G_HIP(g->r_ids.ensure((size_t)n * nk * 8));
-    G_HIP(g->r_d.ensure((size_t)n * nk * 4));
-    G_HIP(g->r_n.ensure((size_t)n * nq * 4));
-    G_HIP(g->o_ids.ensure(nk * 8));
-    G_HIP(g->o_d.ensure(nk * 4));
-    G_HIP(g->o_n.ensure((size_t)nq * 4));
-    auto* rid = static_cast<uint64_t*>(g->r_ids.p);
-    auto* rd = static_cast<float*>(g->r_d.p);
-    auto* rn = static_cast<int32_t*>(g->r_n.p);
-    if (!g->comms.empty()) {
-        G_NCCL(ncclGroupStart());
-        for (int i = 0; i < n; ++i) {
-            Member& mb = g->m[i];
-            const bool is_root = i == 0;
-            G_NCCL(ncclGather(mb.ids.p, is_root ? rid : nullptr, nk, ncclUint64, 0, g->comms[i], mb.s));
-            G_NCCL(ncclGather(mb.d.p, is_root ? rd : nullptr, nk, ncclFloat32, 0, g->comms[i], mb.s));
-            G_NCCL(ncclGather(mb.n.p, is_root ? rn : nullptr, (size_t)nq, ncclInt32, 0, g->comms[i], mb.s));
-        }
-        G_NCCL(ncclGroupEnd());
-        for (int i = 1; i < n; ++i) {   // senders done before their buffers are reused
-            G_HIP(hipSetDevice(g->m[i].dev));
-            G_HIP(hipStreamSynchronize(g->m[i].s));
-        }
-        G_HIP(hipSetDevice(root.dev));
-    } else {
-        for (int i = 0; i < n; ++i) {
-            Member& mb = g->m[i];
-            G_HIP(hipSetDevice(mb.dev));
-            G_HIP(hipMemcpyPeerAsync(rid + (size_t)i * nk, root.dev, mb.ids.p, mb.dev, nk * 8, mb.s));
-            G_HIP(hipMemcpyPeerAsync(rd + (size_t)i * nk, root.dev, mb.d.p, mb.dev, nk * 4, mb.s));
-            G_HIP(hipMemcpyPeerAsync(rn + (size_t)i * nq, root.dev, mb.n.p, mb.dev, (size_t)nq * 4, mb.s));
-            G_HIP(hipEventRecord(mb.done, mb.s));
-        }
-        G_HIP(hipSetDevice(root.dev));
-        for (int i = 1; i < n; ++i) G_HIP(hipStreamWaitEvent(root.s, g->m[i].done, 0));
+    if (rc) {
+        drain_members(g);   // no copy from the staging may still be in flight
+        return rc;
     }
-    // 3. merge on the root (index.go:1030-1043), results to the host
-    rc = wv_merge_shards_device(rd, rid, rn, n, nq, k, static_cast<float*>(g->o_d.p),
-                                static_cast<uint64_t*>(g->o_ids.p), static_cast<int32_t*>(g->o_n.p), root.s);
-    if (rc) return rc;
-    G_HIP(hipMemcpyAsync(out_ids, g->o_ids.p, nk * 8, hipMemcpyDeviceToHost, root.s));
-    G_HIP(hipMemcpyAsync(out_d, g->o_d.p, nk * 4, hipMemcpyDeviceToHost, root.s));
-    G_HIP(hipMemcpyAsync(out_n, g->o_n.p, (size_t)nq * 4, hipMemcpyDeviceToHost, root.s));
-    G_HIP(hipStreamSynchronize(root.s));
-    if (g->comms.empty())
-        for (int i = 1; i < n; ++i) {
-            G_HIP(hipSetDevice(g->m[i].dev));
-            G_HIP(hipStreamSynchronize(g->m[i].s));
+    // 2.-3. gather on the root, merge, results to the host; on an error every
+    // member's stream is drained before returning
+    rc = [&]() -> int {
+        // 2. gather the per-shard lists on the root
+        Member& root = g->m[0];
+        G_HIP(hipSetDevice(root.dev));
+        G_HIP(g->r_ids.ensure((size_t)n * nk * 8));
+        G_HIP(g->r_d.ensure((size_t)n * nk * 4));
+        G_HIP(g->r_n.ensure((size_t)n * nq * 4));
+        G_HIP(g->o_ids.ensure(nk * 8));
+        G_HIP(g->o_d.ensure(nk * 4));
+        G_HIP(g->o_n.ensure((size_t)nq * 4));
+        auto* rid = static_cast<uint64_t*>(g->r_ids.p);
+        auto* rd = static_cast<float*>(g->r_d.p);
+        auto* rn = static_cast<int32_t*>(g->r_n.p);
+        if (!g->comms.empty()) {
+            G_NCCL(ncclGroupStart());
+            for (int i = 0; i < n; ++i) {
+                Member& mb = g->m[i];
+                const bool is_root = i == 0;
+                G_NCCL(ncclGather(mb.ids.p, is_root ? rid : nullptr, nk, ncclUint64, 0, g->comms[i], mb.s));
+                G_NCCL(ncclGather(mb.d.p, is_root ? rd : nullptr, nk, ncclFloat32, 0, g->comms[i], mb.s));
+                G_NCCL(ncclGather(mb.n.p, is_root ? rn : nullptr, (size_t)nq, ncclInt32, 0, g->comms[i], mb.s));
+            }
+            G_NCCL(ncclGroupEnd());
+            for (int i = 1; i < n; ++i) {   // senders done before their buffers are reused
+                G_HIP(hipSetDevice(g->m[i].dev));
+                G_HIP(hipStreamSynchronize(g->m[i].s));
+            }
+            G_HIP(hipSetDevice(root.dev));
+        } else {
+            for (int i = 0; i < n; ++i) {
+                Member& mb = g->m[i];
+                G_HIP(hipSetDevice(mb.dev));
+                G_HIP(hipMemcpyPeerAsync(rid + (size_t)i * nk, root.dev, mb.ids.p, mb.dev, nk * 8, mb.s));
+                G_HIP(hipMemcpyPeerAsync(rd + (size_t)i * nk, root.dev, mb.d.p, mb.dev, nk * 4, mb.s));
+                G_HIP(hipMemcpyPeerAsync(rn + (size_t)i * nq, root.dev, mb.n.p, mb.dev, (size_t)nq * 4, mb.s));
+                G_HIP(hipEventRecord(mb.done, mb.s));
+            }
+            G_HIP(hipSetDevice(root.dev));
+            for (int i = 1; i < n; ++i) G_HIP(hipStreamWaitEvent(root.s, g->m[i].done, 0));
         }
-    return WV_OK;
+        // 3. merge on the root (index.go:1030-1043), results to the host
+        int rc = wv_merge_shards_device(rd, rid, rn, n, nq, k, static_cast<float*>(g->o_d.p),
+                                    static_cast<uint64_t*>(g->o_ids.p), static_cast<int32_t*>(g->o_n.p), root.s);
+        if (rc) return rc;
+        G_HIP(hipMemcpyAsync(out_ids, g->o_ids.p, nk * 8, hipMemcpyDeviceToHost, root.s));
+        G_HIP(hipMemcpyAsync(out_d, g->o_d.p, nk * 4, hipMemcpyDeviceToHost, root.s));
+        G_HIP(hipMemcpyAsync(out_n, g->o_n.p, (size_t)nq * 4, hipMemcpyDeviceToHost, root.s));
+        G_HIP(hipStreamSynchronize(root.s));
+        if (g->comms.empty())
+            for (int i = 1; i < n; ++i) {
+                G_HIP(hipSetDevice(g->m[i].dev));
+                G_HIP(hipStreamSynchronize(g->m[i].s));
+            }
+        return WV_OK;
+    }();
+    if (rc) drain_members(g);
+    return rc;
 }
 
 int search_replicas(wv_group* g, const float* queries, int nq, int k, int ef, const uint64_t* allow_bits,
@@ -260,6 +302,7 @@ void destroy_members(wv_group* g) {
     for (auto& mb : g->m) {
         (void)hipSetDevice(mb.dev);
         for (DBuf* b : {&mb.q, &mb.allow, &mb.ids, &mb.d, &mb.n}) b->release();
+        mb.h_allow.release();
         if (mb.done) (void)hipEventDestroy(mb.done);
         if (mb.s) (void)hipStreamDestroy(mb.s);
         if (mb.ix) wv_index_destroy(mb.ix);
@@ -268,6 +311,7 @@ void destroy_members(wv_group* g) {
         (void)hipSetDevice(g->m[0].dev);
         for (DBuf* b : {&g->r_ids, &g->r_d, &g->r_n, &g->o_ids, &g->o_d, &g->o_n}) b->release();
     }
+    g->h_q.release();
     g->m.clear();
 }
 
@@ -280,6 +324,9 @@ int wv_group_create(const int* devices, int n_devices, int dim, int metric, cons
     if (!devices || n_devices < 1 || dim < 1 || !cfg || !out || capacity == 0 ||
         (layout != WV_GROUP_SHARD && layout != WV_GROUP_REPLICA))
         return gfail(WV_EINVAL, "wv_group_create: bad argument");
+    // the device merge (wv_merge_shards_device) takes at most 16 shard lists
+    if (layout == WV_GROUP_SHARD && n_devices > 16)
+        return gfail(WV_EINVAL, "wv_group_create: at most 16 shard members");
     int n_vis = 0;
     G_HIP(hipGetDeviceCount(&n_vis));
     for (int i = 0; i < n_devices; ++i)

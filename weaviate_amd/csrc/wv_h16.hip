@@ -29,87 +29,10 @@
 
 #include <float.h>
 
+#include "wv_h16_dev.h"
+
 namespace wv {
 
-typedef _Float16 half8 __attribute__((ext_vector_type(8)));
-typedef float floatx4 __attribute__((ext_vector_type(4)));
-
-// LDS-DMA (global_load_lds_dword{,x4}) as inline asm: the destination is the
-// wave-uniform LDS byte address in M0 (+ lane * size).  Written as asm so the
-// compiler's waitcnt pass does not see them: for a builtin LDS-DMA it waits
-// vmcnt(0) before every LDS read it cannot prove disjoint -- the prefetch of
-// the next tiles would be drained before the current one is read.  The
-// kernel places the (counted) vmcnt waits itself.
-__device__ __forceinline__ uint32_t lds_addr(const void* p) {
-    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
-}
-__device__ __forceinline__ void glds16(const void* src, uint32_t lds_wave_base) {
-    uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(src), "s"(lds_wave_base) : "memory");
-}
-// the same from a wave-uniform base (SGPR pair) + a per-lane 32-bit byte
-// offset: a tile's address update is scalar work, no per-lane 64-bit adds
-__device__ __forceinline__ void glds16s(const void* sbase, uint32_t voff, uint32_t lds_wave_base) {
-    uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds_wave_base) : "memory");
-}
-__device__ __forceinline__ void glds4(const void* src, uint32_t lds_wave_base) {
-    uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(src), "s"(lds_wave_base) : "memory");
-}
-// wait until at most n of this wave's vector-memory ops are outstanding
-__device__ __forceinline__ void vm_wait(int n) {
-    switch (n) {
-        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-        case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
-        case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-        case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
-        case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-        case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
-        case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-        case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
-        default: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-    }
-}
-__device__ __forceinline__ void block_barrier() {
-#ifdef WV_H16_ABLATE_NO_BARRIER
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#else
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#endif
-}
-
-// Eligibility of a tile's 64 rows (bit r: row r is not excluded, is allowed,
-// and is < N), read with scalar loads: the tile index is wave-uniform, so
-// the words come through the constant address space (s_load), which neither
-// waits behind the LDS operand reads (a word staged in LDS cost 0.31 ms per
-// 1M x 10k pass: its read stalled the wave at every tile) nor counts against
-// the LDS-DMA's vmcnt.
-__device__ __forceinline__ uint64_t tile_okw(const H16Params& p, uint64_t tile, bool has_allow) {
-    typedef const __attribute__((address_space(4))) uint64_t cu64;
-    const uint32_t tl = __builtin_amdgcn_readfirstlane((uint32_t)tile);
-    uint64_t okw = ~((cu64*)p.excl)[tl];
-    if (has_allow) okw &= ((cu64*)p.allow)[tl];
-    const uint64_t row0 = (uint64_t)tl * H_BN;
-    if (row0 + H_BN > p.N) okw &= p.N > row0 ? ((1ull << (p.N - row0)) - 1) : 0ull;
-    return okw;
-}
-
-// LDS stage: [2 row blocks][ns k-steps][64 lanes] uint4 image, then 64 floats
-// of s|x|^2, then the exclusion and allow words of the tile.
-template <int NS>
-struct H16Stage {
-    static constexpr int IMG_U4 = 2 * NS * 64;
-    static constexpr int U4 = IMG_U4 + 16 + 1;
-};
-#ifndef WV_H16_TPS
-#define WV_H16_TPS 2
-#endif
-constexpr int H_TPS8 = WV_H16_TPS;   // tiles per LDS stage (8-wave kernel): one barrier per H_TPS8 tiles
-constexpr int H_STAGES = 3;   // a stage holds H_TPS tiles; stage p % 3 computes while p + 1, p + 2 land
 
 // SEED: the pre-pass over every H_SAMPLE-th tile keeps only each lane's
 // running minimum per query column (distinct rows per (slot, lane half)),
@@ -407,6 +330,9 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
                 const float mg = khalf ? marg1 : marg0;
                 const float u4 = 4.f * 5.9604645e-08f;
                 float b = kv < 1e30f ? kv + mg + u4 * (fabsf(kv) + mg) : FLT_MAX;
+                // publish it: the finalize's tau_in (wv_h16_gtau_kernel) must
+                // be <= every threshold a key was dropped above
+                if (jq < p.nq && b < FLT_MAX) atomicMin(&p.gtau[jq], h16_key_enc(b));
                 const float bo = __shfl_xor(b, 32, 64);   // the other half's query
                 tau0 = fminf(tau0, khalf ? bo : b);
                 tau1 = fminf(tau1, khalf ? b : bo);
@@ -554,62 +480,6 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
 // 4 q .. 4 q + 3 (a 16-entry list per column and slot, so the certificate's
 // list tails lie well beyond the top k).
 //
-// Extraction of one query group's keys of a half tile (a lane's 8 values v:
-// rows rb + 16 (v / 4) + v % 4) into the column lists, in wave-uniform rounds:
-// every lane whose smallest remaining key is <= its column's threshold (the
-// list's tail, the seed / running threshold) takes it out; the candidates of
-// each lane quarter in turn are broadcast to the column's four lanes, which
-// merge them into their entries (entry j becomes med3(e[j - 1], d, e[j]),
-// e[-1] the previous quarter's last entry).  Keys equal to the tail are taken
-// out without entering.
-__device__ __forceinline__ void qcol_extract(float M, floatx4& A, floatx4& B, float (&ld)[HQ_KP],
-                                             uint32_t (&li)[HQ_KP], float& thr, float tau, uint32_t rb, int lane) {
-    const float INF = __builtin_inff();
-    const int l15 = lane & 15;
-    const int prev = (lane + 48) & 63;   // the same column's previous lane quarter
-    for (;;) {
-        const bool has = M <= thr;
-        const uint64_t hb = __ballot(has);
-        if (!hb) break;
-        WV_DBG_COUNT(1)
-        // position of M: a descending scan, so among equal keys the lowest row wins
-        uint32_t sel = 0;
-#pragma unroll
-        for (int r = 3; r >= 0; --r) sel = B[r] == M ? 4u + r : sel;
-#pragma unroll
-        for (int r = 3; r >= 0; --r) sel = A[r] == M ? (uint32_t)r : sel;
-        sel = has ? sel : 8u;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            A[r] = sel == (uint32_t)r ? INF : A[r];
-            B[r] = sel == 4u + r ? INF : B[r];
-        }
-        uint32_t rbo = rb;   // opaque: the row ids stay in this rare loop
-        asm volatile("" : "+v"(rbo));
-        const uint32_t id = rbo + (sel & 3u) + 16u * ((sel >> 2) & 1u);
-        const float d = has ? M : INF;
-#pragma unroll
-        for (int q = 0; q < HQ_PROD; ++q) {
-            if (!((hb >> (16 * q)) & 0xFFFFull)) continue;   // (wave-uniform)
-            const float cd = __shfl(d, l15 + 16 * q, 64);
-            const uint32_t cid = __shfl(id, l15 + 16 * q, 64);
-            float pk = __shfl(ld[HQ_KP - 1], prev, 64);
-            const uint32_t pi = __shfl(li[HQ_KP - 1], prev, 64);
-            pk = lane < 16 ? -INF : pk;
-#pragma unroll
-            for (int i = HQ_KP - 1; i >= 0; --i) {
-                const float lo = i ? ld[i - 1] : pk;
-                const uint32_t loi = i ? li[i - 1] : pi;
-                const bool a = cd < lo, b = cd < ld[i];
-                li[i] = a ? loi : (b ? cid : li[i]);
-                ld[i] = __builtin_amdgcn_fmed3f(lo, cd, ld[i]);
-            }
-        }
-        thr = fminf(__shfl(ld[HQ_KP - 1], l15 + 48, 64), tau);
-        M = fminf(fminf(fminf(A[0], A[1]), fminf(A[2], A[3])), fminf(fminf(B[0], B[1]), fminf(B[2], B[3])));
-    }
-}
-
 // WAVES = 8: one 512-query workgroup per CU, 2 tiles per LDS stage; WAVES = 4:
 // two independent 256-query workgroups per CU (their own barriers), 1 tile
 // per stage.

@@ -121,6 +121,11 @@ inline uint64_t h16_index(uint64_t row, int k, int ns) {
 // lane quarter (HQ_PROD per query and slot).
 constexpr int HQ_PROD = 4;    // lane quarters per column
 constexpr int HQ_KP = 4;      // list entries per lane quarter
+// one-wave-per-SIMD variant (wv_bf_h16s_kernel): 4-wave workgroups, one per
+// CU, 8 query groups of 16 per wave; h16q images and lists
+constexpr int HS_QG = 8;      // query groups per wave
+constexpr int HS_BQ = 512;    // queries per block: 4 waves x 8 groups x 16
+constexpr int HS_TPS = 2;     // tiles per LDS stage
 
 #if defined(__HIPCC__)
 __host__ __device__
