@@ -112,6 +112,36 @@ def counter_sift(seed: int, row0: int, nrows: int, dim: int) -> np.ndarray:
     return np.maximum(np.rint(x), 0).astype(np.float32)
 
 
+GLOVE_DESC = ("GloVe-100-shaped (4096 Zipf-weighted clusters of a 24-d latent family + full-rank noise, "
+              "log-normal row norms before the cosine normalisation)")
+
+
+def counter_glove(seed: int, row0: int, nrows: int, dim: int) -> np.ndarray:
+    """GloVe-100-shaped data (BASELINE configs[2]): word vectors are
+    clustered with heavily skewed cluster sizes (word frequency), live near a
+    low-dimensional family of directions, keep a sizeable full-rank residual,
+    and have heavy-tailed norms -- which the cosine distancer normalises away
+    (insert.go:56-60), so only the directions matter for the search.  I.i.d.
+    Gaussians (round 1's C3 data) have none of this structure and no HNSW
+    operating point (recall@10 0.15-0.39 for ef 32-256); this data has one in
+    the reference's range.  Counter-based per row like counter_uniform."""
+    if nrows > (1 << 16):
+        return _par_rows(counter_glove, seed, row0, nrows, dim)
+    C, L = 4096, 24
+    centres = counter_gauss(81, 0, C, L) * np.float32(np.sqrt(L))          # cluster centres in the latent space
+    basis = counter_gauss(82, 0, dim, L) * np.float32(np.sqrt(L))          # latent -> ambient
+    u = counter_uniform(seed + 2000, row0, nrows, 1)[:, 0].astype(np.float64)
+    cid = np.minimum((C * u ** 3).astype(np.int64), C - 1)                 # Zipf-like cluster sizes
+    z = centres[cid] + np.float32(0.55) * counter_gauss(seed + 3000, row0, nrows, L) * np.float32(np.sqrt(L))
+    e = counter_gauss(seed + 4000, row0, nrows, dim) * np.float32(np.sqrt(dim))
+    x = (z @ basis.T) / np.float32(np.sqrt(L)) + np.float32(GLOVE_NOISE) * e
+    s = np.exp(np.float32(0.6) * counter_gauss(seed + 5000, row0, nrows, 1) * np.float32(1.0))
+    return (x * s).astype(np.float32)
+
+
+GLOVE_NOISE = 0.45
+
+
 def parity_stats(gi, gd, oi, od):
     """ids position-equal / distances bitwise equal / identical up to the
     order among equal distances (the reference orders ties by heap layout,
@@ -320,7 +350,7 @@ def run_exact(args, ctx, W):
     N, D, NQ, K = args.rows, args.dim, args.nq, args.k
     ws, rank = ctx.ws, ctx.rank
     split = args.split
-    gen = {"uniform": counter_uniform, "gauss": counter_gauss, "sift": counter_sift}[args.data]
+    gen = {"uniform": counter_uniform, "gauss": counter_gauss, "sift": counter_sift, "glove": counter_glove}[args.data]
     lo, hi = (N * rank // ws, N * (rank + 1) // ws) if split == "corpus" else (0, N)
     n_local = hi - lo
     base = gen(1, lo, n_local, D)
@@ -509,77 +539,140 @@ def build_hnsw_graph(args, ctx, ix, base, n_local, O):
 
 
 def run_hnsw(args, ctx, W, with_cpu):
-    """configs[0]: hnsw beam search (knnSearchByVector) at ef on SIFT-shaped
-    data; query split over the ranks (each rank holds the graph and answers
-    its own batch).  Recall@10 against exact truths from the exact path
-    (bit-identical to the restatement's flatSearch); on rank 0 at N = 1 also
+    """configs[0] / configs[4]: hnsw beam search (knnSearchByVector) at ef.
+    query split (default at N > 1 for 1M rows): every rank holds the whole
+    graph and answers its own batch (weak scaling).  corpus split (the
+    north-star layout, default for configs[4]-shaped runs): rank r owns ids
+    [r N/W, (r+1) N/W) and the graph of those rows (built on its GPU), every
+    rank searches the same batch over its shard graph, the per-shard top-k are
+    all-gathered over RCCL and merged on the device (index.go:967-1044).
+    Recall@10 against exact truths from the exact path (bit-identical to the
+    restatement's flatSearch; sharded the same way); on rank 0 at N = 1 also
     the restatement's recall on the same graph and its CPU throughput."""
     torch = ctx.torch
     N, D, NQ, K = args.rows, args.dim, args.nq, args.k
+    ws, rank = ctx.ws, ctx.rank
+    corpus = args.split == "corpus" and ws > 1
     data = args.hnsw_data
-    gen = {"uniform": counter_uniform, "gauss": counter_gauss, "sift": counter_sift}[data]
-    base = gen(1, 0, N, D)
-    queries = gen(2, ctx.rank * NQ, NQ, D)
-    ix = W.GPUVectorIndex(D, args.metric, capacity=N, device=ctx.gpu, max_connections=args.M)
+    gen = {"uniform": counter_uniform, "gauss": counter_gauss, "sift": counter_sift, "glove": counter_glove}[data]
+    lo, hi = (N * rank // ws, N * (rank + 1) // ws) if corpus else (0, N)
+    n_local = hi - lo
+    base = gen(1, lo, n_local, D)
+    queries = gen(2, 0 if corpus else rank * NQ, NQ, D)
+    ix = W.GPUVectorIndex(D, args.metric, capacity=n_local, device=ctx.gpu, max_connections=args.M, id_base=lo)
     ix.upload_vectors(base)
     O = _oracle() if (with_cpu or args.graph_build != "gpu") else None
-    graph = build_hnsw_graph(args, ctx, ix, base, N, O)
+    graph = build_hnsw_graph(args, ctx, ix, base, n_local, O)
     graph["max_level"] = int(ix.graph_info()["max_level"])
     dpad = ix.query_ld()
     qt = _query_tensor(ctx, queries, dpad)
     out_ids, out_d, out_n = _out_tensors(ctx, NQ, K)
+    if corpus:
+        g_ids = torch.empty((ws, NQ, K), dtype=torch.int64, device=ctx.dev)
+        g_d = torch.empty((ws, NQ, K), dtype=torch.float32, device=ctx.dev)
+        g_n = torch.empty((ws, NQ), dtype=torch.int32, device=ctx.dev)
+        m_ids, m_d, m_n = _out_tensors(ctx, NQ, K)
+
+    def merge():
+        ctx.allgather(g_ids, out_ids)
+        ctx.allgather(g_d, out_d)
+        ctx.allgather(g_n, out_n)
+        W.merge_shards_device(g_d.data_ptr(), g_ids.data_ptr(), g_n.data_ptr(), ws, NQ, K, m_d.data_ptr(),
+                              m_ids.data_ptr(), m_n.data_ptr(), stream=ctx.stream)
+
     kern_ms, stats = [], []
 
     def step(timed):
         ix.search_batch_device(qt.data_ptr(), NQ, K, out_ids.data_ptr(), out_d.data_ptr(), out_n.data_ptr(),
                                ef=args.ef, mode="hnsw", stream=ctx.stream)
+        if corpus:
+            merge()
 
     ix.set_timing(True)
     elapsed = ctx.time_steps(step, args.steps, args.warmup, before_timed=ix.last_kernel_times)
     kern_ms.append(ix.last_kernel_times())   # per-batch averages over the timed steps
     stats.append(ix.last_batch_stats())
-    hi_ids = out_ids.cpu().numpy().view(np.uint64)
-    hi_d = out_d.cpu().numpy()
+    fin = (m_ids, m_d) if corpus else (out_ids, out_d)
+    hi_ids = fin[0].cpu().numpy().view(np.uint64).copy()
+    hi_d = fin[1].cpu().numpy().copy()
+    shard_ids = out_ids.cpu().numpy().view(np.uint64).copy()   # this rank's own shard answer
+    shard_d = out_d.cpu().numpy().copy()
     # exact truths on the same queries (the exact path: ids bit-identical to
-    # flatSearch), timed once: SIFT-shaped data is integer-valued, so equal
-    # distances at the k boundary send queries to the certificate's fallback
+    # flatSearch; per shard + the same merge in the corpus layout), timed
+    # once: SIFT-shaped data is integer-valued, so equal distances at the k
+    # boundary send queries to the certificate's fallback
     ix.set_timing(False)
     torch.cuda.synchronize(ctx.dev)
     t0 = time.perf_counter()
     ix.search_batch_device(qt.data_ptr(), NQ, K, out_ids.data_ptr(), out_d.data_ptr(), out_n.data_ptr(), ef=0,
                            mode="exact", stream=ctx.stream)
+    if corpus:
+        merge()
     torch.cuda.synchronize(ctx.dev)
     exact_ms = 1000 * (time.perf_counter() - t0)
     exact_fb = ix.last_batch_stats()["fallbacks"]
-    truth = out_ids.cpu().numpy().view(np.uint64)
+    truth = (m_ids if corpus else out_ids).cpu().numpy().view(np.uint64)
     rec = float(np.mean([len(set(a) & set(b)) / K for a, b in zip(hi_ids.tolist(), truth.tolist())]))
     hnsw_ms = float(np.mean([k["hnsw_ms"] for k in kern_ms]))
     e, x = stats[-1]["dist_evals"], stats[-1]["expansions"]
     by = 4.0 * D * e + 4.0 * 2 * args.M * x   # 4*D*E + 4*deg_slots*X (deg0 = 2M)
     achieved = by / (hnsw_ms * 1e-3) / 1e9
+    sweep = {}
+    for ef in args.ef_sweep:   # the configs[2] ef sweep on the same graph and queries
+        def step_e(timed, ef=ef):
+            ix.search_batch_device(qt.data_ptr(), NQ, K, out_ids.data_ptr(), out_d.data_ptr(), out_n.data_ptr(),
+                                   ef=ef, mode="hnsw", stream=ctx.stream)
+            if corpus:
+                merge()
+        ix.set_timing(True)
+        el = ctx.time_steps(step_e, args.steps, 1, before_timed=ix.last_kernel_times)
+        km = ix.last_kernel_times()["hnsw_ms"]
+        se = ix.last_batch_stats()
+        got = (m_ids if corpus else out_ids).cpu().numpy().view(np.uint64)
+        r_e = float(np.mean([len(set(a) & set(b)) / K for a, b in zip(got.tolist(), truth.tolist())]))
+        b_e = 4.0 * D * se["dist_evals"] + 4.0 * 2 * args.M * se["expansions"]
+        sweep[str(ef)] = {"value": round(NQ * (1 if corpus else ws) * args.steps / el, 1),
+                          "ms_per_step": round(1000 * el / args.steps, 3), "recall@10": round(r_e, 4),
+                          "kernel_ms": round(km, 3),
+                          "hbm_frac_gpu_counts": round(b_e / (km * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                          "dist_evals_per_query": round(se["dist_evals"] / NQ, 1)}
+    ix.set_timing(False)
+    if args.dump_ids:   # the shard's graph and answers, for the multi-rank parity test
+        np.savez(args.dump_ids % {"rank": rank} if "%(rank)" in args.dump_ids else args.dump_ids,
+                 ids=hi_ids, dists=hi_d, shard_ids=shard_ids, shard_dists=shard_d, lo=lo, n_local=n_local,
+                 **{"g_" + k: np.asarray(v) for k, v in ix.download_graph().items()})
+    units = NQ * (1 if corpus else ws)
     res = {
-        "metric": METRIC, "value": round(NQ * ctx.ws * args.steps / elapsed, 1), "unit": "queries/s",
+        "metric": METRIC, "value": round(units * args.steps / elapsed, 1), "unit": "queries/s",
         "ms_per_step": round(1000 * elapsed / args.steps, 3), "recall@10": round(rec, 4),
         "recall_truth": "exact path on the same queries (all of them)",
-        "scaling": "weak",
-        "workload": "hnsw knnSearchByVector ef=%d, %s x %d-d %s, %d-query batch per GPU (BASELINE configs[0] "
-                    "parameters M=%d, efConstruction=%d)" % (args.ef, f"{N:,}", D, args.metric, NQ, args.M, args.efc),
+        "scaling": "strong" if corpus else "weak",
+        "workload": "hnsw knnSearchByVector ef=%d, %s x %d-d %s, %d-query batch%s (M=%d, efConstruction=%d)"
+                    % (args.ef, f"{N:,}", D, args.metric, NQ, "" if corpus else " per GPU", args.M, args.efc),
+        "parallelism": (f"corpus sharded over {ws} GPU(s) by id range ({n_local:,} rows and their own graph per GPU), "
+                        f"RCCL all-gather of per-shard top-k + device merge" if corpus else
+                        f"{ws} GPU(s), each holding the graph and answering its own batch"),
         "data": {"sift": "SIFT-shaped (1024 centres + 24-d latent + noise, non-negative integers)",
-                 "uniform": "U[0,1)", "gauss": "N(0,1)/sqrt(D)"}[data],
+                 "uniform": "U[0,1)", "gauss": "N(0,1)/sqrt(D)", "glove": GLOVE_DESC}[data],
         "graph": graph,
         "exact_same_data": {"ms_one_batch": round(exact_ms, 2), "fallback_queries": exact_fb,
-                            "note": "the exact path on these (tie-heavy, integer-valued) queries, one untimed-loop "
-                                    "call after the hnsw steps"},
+                            "note": "the exact path on these queries, one untimed-loop call after the hnsw steps"},
         "roofline": {"bound": "hbm", "kernel": "wv_hnsw_kernel", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": None, "kernel_ms": round(hnsw_ms, 3), "counts_from": "GPU counters",
                      "dist_evals_per_query": round(e / NQ, 1), "expansions_per_query": round(x / NQ, 1),
                      "fallback_queries": stats[-1]["fallbacks"]},
     }
-    attach_traffic(res["roofline"], N, NQ, D, data)
+    attach_traffic(res["roofline"], n_local, NQ, D, data)
+    if sweep:
+        res["ef_sweep"] = sweep
     if with_cpu:
         ref = O.Index(D, args.metric, args.M, args.efc, capacity=N, seed=1)
         ref.import_graph(base, ix.download_graph())   # the restatement searches the very same graph
+        for ef, line in sweep.items():
+            ri = ref.search_batch(queries, K, int(ef), threads=args.cpu_threads)[0]
+            line["recall@10_cpu_restatement"] = round(
+                float(np.mean([len(set(a) & set(b)) / K for a, b in zip(ri.tolist(), truth.tolist())])), 4)
         probe = min(NQ, 500)
         t0 = time.perf_counter()
         ref.search_batch(queries[:probe], K, args.ef, threads=args.cpu_threads)
@@ -625,7 +718,7 @@ def group_leg(args):
     import weaviate_amd as W
     devs = [int(x) for x in args.group_devices.split(",")]
     N, D, NQ, K = args.rows, args.dim, args.nq, args.k
-    gen = {"uniform": counter_uniform, "gauss": counter_gauss, "sift": counter_sift}[args.data]
+    gen = {"uniform": counter_uniform, "gauss": counter_gauss, "sift": counter_sift, "glove": counter_glove}[args.data]
     base = gen(1, 0, N, D)
     queries = gen(2, 0, NQ, D)
     g = W.GPUGroup(devs, D, args.metric, capacity=N, layout="shard")
@@ -678,6 +771,7 @@ def run_group_leg_child(args, ws, final_ids, final_d):
 
 
 def main():
+    global GLOVE_NOISE
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -691,11 +785,15 @@ def main():
     ap.add_argument("--nq", type=int, default=10_000, help="queries per batch (per GPU with --split query)")
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--ef", type=int, default=64)
+    ap.add_argument("--ef-sweep", default="", help="hnsw: comma-separated ef values timed after the main line "
+                                                   "(configs[2]: 32,64,128,256)")
     ap.add_argument("--metric", default="l2-squared")
-    ap.add_argument("--data", choices=["auto", "uniform", "gauss", "sift"], default="auto",
+    ap.add_argument("--data", choices=["auto", "uniform", "gauss", "sift", "glove"], default="auto",
                     help="uniform: U[0,1) (tie-free, configs[1]); gauss: N(0,1)/sqrt(D) (GloVe/Deep/C4-shaped); "
                          "sift: clustered non-negative integers (SIFT-shaped, configs[0]); "
                          "auto: uniform for exact, sift for hnsw")
+    ap.add_argument("--glove-noise", type=float, default=GLOVE_NOISE,
+                    help="glove data: full-rank residual relative to the latent part")
     ap.add_argument("--allow-frac", type=float, default=0.0,
                     help="exact mode: shared allow list, Bernoulli(p) over ids (seed 3, BASELINE configs[3])")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time (T=all)")
@@ -723,6 +821,8 @@ def main():
     ap.add_argument("--group-leg", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--group-devices", default="0", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    args.ef_sweep = [int(x) for x in args.ef_sweep.split(",") if x]
+    GLOVE_NOISE = args.glove_noise
     if args.group_leg:
         if args.data == "auto":
             args.data = "uniform"
@@ -736,7 +836,12 @@ def main():
                                    f"{args.gpus} or without a launcher"}), flush=True)
         sys.exit(2)
     if not args.split:
-        args.split = "query" if ws > 1 else "corpus"
+        # the north-star layout (id-range shards + RCCL merge) for the
+        # sharded configs -- configs[3] (10M x 768 dot) and configs[4] (100M x
+        # 96 hnsw) -- and for any corpus past 8M rows; the query split for
+        # configs[0]/[1]'s 1M rows, which one GPU holds whole
+        sharded_cfg = args.rows >= 8_000_000 or (args.dim >= 512 and args.metric == "dot")
+        args.split = "corpus" if (ws == 1 or sharded_cfg) else "query"
     if args.data == "auto":
         args.data = "sift" if args.workload == "hnsw" else "uniform"
     args.hnsw_data = args.data if args.workload == "hnsw" else "sift"
@@ -749,13 +854,13 @@ def main():
         h = run_hnsw(args, ctx, W, with_cpu)
         result = {"metric": METRIC, "value": h["value"], "unit": "queries/s", "n_gpus": ws,
                   "devices": ctx.n_devices, "steps": args.steps, "warmup": args.warmup,
-                  "ms_per_step": h["ms_per_step"], "higher_is_better": True, "scaling": "weak",
+                  "ms_per_step": h["ms_per_step"], "higher_is_better": True, "scaling": h["scaling"],
                   "vs_baseline": None, "dtype": "f32", "data": "synthetic: counter-based " + h["data"],
                   "config": {"workload": h["workload"], "N": args.rows, "dim": args.dim, "nq": args.nq,
-                             "k": args.k, "metric": args.metric, "mode": "hnsw",
-                             "parallelism": f"{ws} GPU(s), each holding the graph and answering its own batch"},
+                             "k": args.k, "metric": args.metric, "mode": "hnsw", "split": args.split,
+                             "parallelism": h["parallelism"]},
                   "recall@10": h["recall@10"], "graph": h["graph"], "roofline": h["roofline"]}
-        for key in ("parity_sample", "cpu_baseline"):
+        for key in ("parity_sample", "cpu_baseline", "ef_sweep"):
             if key in h:
                 result[key] = h[key]
     else:
@@ -766,7 +871,7 @@ def main():
             "scaling": e["scaling"], "vs_baseline": None,
             "dtype": e["dtype"],
             "data": "synthetic: counter-based %s float32 corpus (seed 1) and queries (seed 2)" % {
-                "uniform": "U[0,1)", "gauss": "N(0,1)/sqrt(D)",
+                "uniform": "U[0,1)", "gauss": "N(0,1)/sqrt(D)", "glove": GLOVE_DESC,
                 "sift": "SIFT-shaped (1024 centres + 24-d latent + noise, non-negative integers)"}[args.data],
             "config": {"workload": e["workload"], "N": args.rows, "dim": args.dim, "nq": args.nq, "k": args.k,
                        "metric": args.metric, "mode": "exact", "recall@10": 1.0, "split": args.split,

@@ -3,29 +3,43 @@
 // Package gpu serves Weaviate's VectorIndex search path from libwvgpu.so, the
 // MI355X engine of this repository, behind the reference's own interface
 // (adapters/repos/db/vector_index.go:23-40).  It is the file a maintainer
-// commits as adapters/repos/db/vector/gpu/gpu.go; the one-line factory change
-// in adapters/repos/db/shard.go:134-172 is shown in INTEGRATION.md.
+// commits as adapters/repos/db/vector/gpu/gpu.go; the factory change in
+// adapters/repos/db/shard.go:134-172 is shown in INTEGRATION.md.
 //
-// The decorator owns a GPU mirror of one shard's hnsw index and delegates
-// persistence (commit log, snapshots), maintenance and every write to the CPU
-// index it wraps, then propagates the write to the mirror:
+// The decorator wraps the shard's CPU hnsw index.  The CPU index keeps
+// persistence (commit log, snapshots), maintenance and every write; each
+// write is then propagated to a GPU mirror (wv_mirror_* in include/wvgpu.h),
+// whose whole lifecycle lives in the library so that the native replay
+// harness (tests/native/mirror_replay.cpp) tests exactly the calls below:
 //
-//	Add(id, vec)     -> cpu.Add, then wv_index_add            (insert.go:43-65)
-//	Delete(ids...)   -> cpu.Delete, then wv_index_add_tombstones (delete.go:29-84)
-//	SearchByVector   -> wv_batcher_search (concurrent callers coalesced into
-//	                    one GPU batch; search.go:64-79 dispatch inside)
-//	SearchByVectorDistance -> wv_search_by_vector_distance   (search.go:90-158)
-//	UpdateUserConfig -> cpu.UpdateUserConfig, then wv_index_update_config
+//	New              -> wv_mirror_create (dims learnt lazily, insert.go:43-65)
+//	PostStartup      -> cpu.PostStartup, then wv_mirror_post_startup: the
+//	                    shard's commit log <RootPath>/<ID>.hnsw.commitlog.d
+//	                    replayed as restoreFromDisk does (startup.go:56-152),
+//	                    rows pulled through VectorForIDThunk (shard.go:165)
+//	Add(id, vec)     -> cpu.Add, then wv_mirror_add (the mirror grows like
+//	                    growIndexToAccomodateNode, maintainance.go:69-100)
+//	Delete(ids...)   -> cpu.Delete, then wv_mirror_delete (delete.go:29-84)
+//	SearchByVector   -> wv_mirror_search (micro-batched; search.go:64-79)
+//	SearchByVectorDistance -> wv_mirror_search_by_distance (search.go:90-158)
+//	UpdateUserConfig -> cpu.UpdateUserConfig, then wv_mirror_update_config
 //
-// A write the mirror cannot take (an id beyond its capacity, a device error)
-// marks the mirror stale: searches are then answered by the CPU index until
-// SyncFromCPU uploads a fresh snapshot, so a stale mirror never serves a
-// deleted id or misses an added one.
+// Rows added after the last graph snapshot are searched exactly beside the
+// graph; once wv_mirror_needs_compaction reports enough of them, a background
+// goroutine flushes the CPU index's commit log (hnsw.Flush, index.go:650-652)
+// and calls wv_mirror_compact, which re-snapshots the mirror's graph from the
+// log -- the CPU index's own graph.
 //
-// The Go toolchain is not part of the build image this engine is developed
-// in; tests/native/go_replay.cpp replays this file's C call sequence
-// (concurrent searches while adding and deleting) against the library on the
-// GPU and asserts both properties.
+// A write the mirror cannot take marks it stale (the library refuses reads
+// with WV_ESTALE): searches are then answered by the CPU index until a later
+// PostStartup resyncs it, so a stale mirror never serves a deleted id or
+// misses an added one.  Writes hold mu shared across the CPU write and its
+// propagation; compaction holds it exclusively while it flushes the log, so
+// every node the flushed log holds has reached the mirror.
+//
+// The Go toolchain is not part of the image this engine is developed in, so
+// this file has not been type-checked; tests/native/mirror_replay.cpp
+// replays its C call sequence against the library on the GPU.
 package gpu
 
 /*
@@ -33,11 +47,18 @@ package gpu
 #cgo LDFLAGS: -L${SRCDIR}/../../../weaviate_amd -lwvgpu -Wl,-rpath,${SRCDIR}/../../../weaviate_amd
 #include <stdlib.h>
 #include "wvgpu.h"
+
+// the exported Go thunk (below), as a wv_vector_source
+extern int wvgpuVectorForID(void *ctx, uint64_t id, float *out, int cap, int *len);
+static int wvgpu_post_startup(wv_mirror *m, void *ctx) {
+	return wv_mirror_post_startup(m, wvgpuVectorForID, ctx);
+}
 */
 import "C"
 
 import (
 	"context"
+	"runtime/cgo"
 	"sync"
 	"sync/atomic"
 	"unsafe"
@@ -45,6 +66,7 @@ import (
 	"github.com/pkg/errors"
 	"github.com/weaviate/weaviate/adapters/repos/db/helpers"
 	"github.com/weaviate/weaviate/entities/schema"
+	"github.com/weaviate/weaviate/entities/storobj"
 	ent "github.com/weaviate/weaviate/entities/vectorindex/hnsw"
 )
 
@@ -68,6 +90,10 @@ type cpuIndex interface {
 	ValidateBeforeInsert(vector []float32) error
 }
 
+// VectorForID is hnsw.VectorForID (hnsw/index.go): the shard's
+// vectorByIndexID (shard_read.go:145-161).
+type VectorForID func(ctx context.Context, id uint64) ([]float32, error)
+
 // Metric values of wv_metric (distancer.Provider.Type(), provider.go:14-24).
 const (
 	MetricL2Squared = C.WV_L2_SQUARED
@@ -78,24 +104,25 @@ const (
 // Index is a VectorIndex whose searches run on one MI355X.
 type Index struct {
 	cpuIndex
-	ix       *C.wv_index
-	b        *C.wv_batcher
-	dim      int
-	capacity uint64
-	device   int
-
-	// mu: searches and propagated writes hold it shared, SyncFromCPU and
-	// Shutdown exclusively (the ABI forbids uploads racing searches).
-	mu    sync.RWMutex
-	stale atomic.Bool
+	m          *C.wv_mirror
+	logDir     *C.char
+	vectorFor  VectorForID
+	device     int
+	mu         sync.RWMutex // calls shared; the log flush before a compaction, PostStartup and close exclusive
+	compacting atomic.Bool
+	closed     atomic.Bool
 }
 
-// Options sizes the mirror and its micro-batcher.
+// Options: the shard's paths and the mirror's sizes.
 type Options struct {
-	Device      int
-	Capacity    uint64 // local ids 0..Capacity-1 (docIDs are dense per shard)
-	MaxBatch    int    // queries per coalesced launch (default 1024)
-	MaxWaitUsec int    // batching window after the first waiting query (default 200)
+	Device       int
+	RootPath     string      // hnsw.Config.RootPath
+	ID           string      // hnsw.Config.ID: the log is RootPath/ID.hnsw.commitlog.d
+	VectorForID  VectorForID // hnsw.Config.VectorForIDThunk
+	MaxBatch     int         // queries per coalesced launch (0: 1024)
+	MaxWaitUsec  int         // batching window after the first waiting query (0: 200)
+	CompactRows  uint64      // delta rows that trigger a compaction (0: 8192)
+	InitialSize  uint64      // mirror capacity before growth (0: 25000)
 }
 
 func lastErr(op string, rc C.int) error {
@@ -115,133 +142,142 @@ func configOf(uc ent.UserConfig, device int) C.wv_config {
 	return cfg
 }
 
-// New creates the mirror; it serves searches once SyncFromCPU has uploaded
-// the CPU index's state (PostStartup).
-func New(cpu cpuIndex, dim int, metric int, uc ent.UserConfig, opt Options) (*Index, error) {
-	if opt.MaxBatch <= 0 {
-		opt.MaxBatch = 1024
-	}
-	if opt.MaxWaitUsec <= 0 {
-		opt.MaxWaitUsec = 200
+// New creates the mirror.  It serves searches after PostStartup.
+func New(cpu cpuIndex, metric int, uc ent.UserConfig, opt Options) (*Index, error) {
+	if opt.VectorForID == nil || opt.RootPath == "" || opt.ID == "" {
+		return nil, errors.New("wvgpu: RootPath, ID and VectorForID are required")
 	}
 	cfg := configOf(uc, opt.Device)
-	var ix *C.wv_index
-	if rc := C.wv_index_create(C.int(dim), C.int(metric), &cfg, C.uint64_t(opt.Capacity), &ix); rc != 0 {
+	g := &Index{cpuIndex: cpu, vectorFor: opt.VectorForID, device: opt.Device}
+	g.logDir = C.CString(opt.RootPath + "/" + opt.ID + ".hnsw.commitlog.d")
+	var mo C.wv_mirror_options
+	mo.initial_capacity = C.uint64_t(opt.InitialSize)
+	mo.max_batch = C.int(opt.MaxBatch)
+	mo.max_wait_us = C.int(opt.MaxWaitUsec)
+	mo.compact_rows = C.uint64_t(opt.CompactRows)
+	mo.commitlog_dir = g.logDir
+	if rc := C.wv_mirror_create(C.int(metric), &cfg, &mo, &g.m); rc != 0 {
+		C.free(unsafe.Pointer(g.logDir))
 		return nil, lastErr("create", rc)
 	}
-	var b *C.wv_batcher
-	if rc := C.wv_batcher_create(ix, C.int(dim), C.int(opt.MaxBatch), C.int(opt.MaxWaitUsec), &b); rc != 0 {
-		C.wv_index_destroy(ix)
-		return nil, lastErr("batcher", rc)
-	}
-	g := &Index{cpuIndex: cpu, ix: ix, b: b, dim: dim, capacity: opt.Capacity, device: opt.Device}
-	g.stale.Store(true)
 	return g, nil
 }
 
-// allowBits turns the sroar-backed AllowList (helpers/allow_list.go:19-118)
-// into the dense bitmap of the ABI: bit i of word i/64 <=> docID i allowed.
-func allowBits(allow helpers.AllowList) ([]uint64, uint64) {
-	if allow == nil {
-		return nil, 0
-	}
-	ids := allow.Slice() // ascending
-	var nbits uint64
-	if len(ids) > 0 {
-		nbits = ids[len(ids)-1] + 1
-	}
-	bits := make([]uint64, nbits/64+1)
-	for _, id := range ids {
-		bits[id>>6] |= 1 << (id & 63)
-	}
-	return bits, nbits
-}
-
-func (g *Index) markStale() {
-	g.stale.Store(true)
-}
-
-// Add mirrors hnsw.Add (insert.go:43-65): the CPU index persists the node,
-// then the row joins the GPU mirror (its delta set until the next snapshot),
-// findable by the next search.
-func (g *Index) Add(id uint64, vector []float32) error {
-	if err := g.cpuIndex.Add(id, vector); err != nil {
-		return err
-	}
-	g.mu.RLock()
-	defer g.mu.RUnlock()
-	if g.stale.Load() {
-		return nil
-	}
-	if id >= g.capacity || len(vector) != g.dim {
-		g.markStale() // grows past the mirror: serve from the CPU until a resync
-		return nil
-	}
-	ids := [1]uint64{id}
-	if rc := C.wv_index_add(g.ix, (*C.uint64_t)(unsafe.Pointer(&ids[0])),
-		(*C.float)(unsafe.Pointer(&vector[0])), 1); rc != 0 {
-		g.markStale()
-	}
-	return nil
-}
-
-// Delete mirrors hnsw.Delete (delete.go:29-84): tombstones, applied to the
-// mirror before Delete returns, so no later search returns the ids.
-func (g *Index) Delete(ids ...uint64) error {
-	if err := g.cpuIndex.Delete(ids...); err != nil {
-		return err
-	}
-	if len(ids) == 0 {
-		return nil
-	}
-	g.mu.RLock()
-	defer g.mu.RUnlock()
-	if g.stale.Load() {
-		return nil
-	}
-	in := make([]uint64, 0, len(ids))
-	for _, id := range ids {
-		if id < g.capacity {
-			in = append(in, id)
+//export wvgpuVectorForID
+func wvgpuVectorForID(ctx unsafe.Pointer, id C.uint64_t, out *C.float, capacity C.int, length *C.int) C.int {
+	g := cgo.Handle(*(*C.uintptr_t)(ctx)).Value().(*Index)
+	vec, err := g.vectorFor(context.Background(), uint64(id))
+	if err != nil {
+		var nf storobj.ErrNotFound
+		if errors.As(err, &nf) {
+			return C.WV_ENOTFOUND // search.go's handleDeletedNode path
 		}
+		return C.WV_EINVAL
 	}
-	if len(in) == 0 {
-		return nil
+	*length = C.int(len(vec))
+	if len(vec) > 0 && len(vec) <= int(capacity) {
+		dst := unsafe.Slice((*float32)(unsafe.Pointer(out)), len(vec))
+		copy(dst, vec)
 	}
-	if rc := C.wv_index_add_tombstones(g.ix, (*C.uint64_t)(unsafe.Pointer(&in[0])), C.uint64_t(len(in))); rc != 0 {
-		g.markStale()
+	return C.WV_OK
+}
+
+// PostStartup: the CPU index's own routines, then the mirror is loaded from
+// the shard's commit log and object store (startup.go:169-205).
+func (g *Index) PostStartup() {
+	g.cpuIndex.PostStartup()
+	g.mu.Lock() // no write slips between the log read and serving
+	defer g.mu.Unlock()
+	if err := g.cpuIndex.Flush(); err != nil {
+		return // the mirror stays stale: the CPU index serves
+	}
+	h := cgo.NewHandle(g)
+	defer h.Delete()
+	ctx := (*C.uintptr_t)(C.malloc(C.size_t(unsafe.Sizeof(C.uintptr_t(0)))))
+	defer C.free(unsafe.Pointer(ctx))
+	*ctx = C.uintptr_t(h)
+	C.wvgpu_post_startup(g.m, unsafe.Pointer(ctx)) // non-zero: stale, CPU serves
+}
+
+// Add mirrors hnsw.Add (insert.go:43-65).
+func (g *Index) Add(id uint64, vector []float32) error {
+	g.mu.RLock()
+	if err := g.cpuIndex.Add(id, vector); err != nil {
+		g.mu.RUnlock()
+		return err
+	}
+	if len(vector) > 0 && !g.closed.Load() {
+		C.wv_mirror_add(g.m, C.uint64_t(id), (*C.float)(unsafe.Pointer(&vector[0])), C.int(len(vector)))
+	}
+	g.mu.RUnlock()
+	g.maybeCompact()
+	return nil
+}
+
+// Delete mirrors hnsw.Delete (delete.go:29-84): tombstones reach the mirror
+// before Delete returns.
+func (g *Index) Delete(ids ...uint64) error {
+	g.mu.RLock()
+	defer g.mu.RUnlock()
+	if err := g.cpuIndex.Delete(ids...); err != nil || g.closed.Load() {
+		return err
+	}
+	if len(ids) > 0 {
+		C.wv_mirror_delete(g.m, (*C.uint64_t)(unsafe.Pointer(&ids[0])), C.uint64_t(len(ids)))
 	}
 	return nil
 }
 
-// SearchByVector replaces hnsw.SearchByVector (search.go:64-79).  Concurrent
-// callers are coalesced by the library's micro-batcher into one launch.
+// maybeCompact re-snapshots the mirror's graph from the flushed commit log
+// once the delta has grown past Options.CompactRows.
+func (g *Index) maybeCompact() {
+	if C.wv_mirror_needs_compaction(g.m) == 0 || !g.compacting.CompareAndSwap(false, true) {
+		return
+	}
+	go func() {
+		defer g.compacting.Store(false)
+		g.mu.Lock()
+		err := g.cpuIndex.Flush()
+		g.mu.Unlock()
+		g.mu.RLock() // (close waits for it)
+		if err == nil && !g.closed.Load() {
+			C.wv_mirror_compact(g.m) // the log is read without blocking searches
+		}
+		g.mu.RUnlock()
+	}()
+}
+
+func allowIDs(allow helpers.AllowList) (*C.uint64_t, C.uint64_t, C.int) {
+	if allow == nil {
+		return nil, 0, 0
+	}
+	ids := allow.Slice() // ascending (sroar bitmap)
+	if len(ids) == 0 {
+		return nil, 0, 1
+	}
+	return (*C.uint64_t)(unsafe.Pointer(&ids[0])), C.uint64_t(len(ids)), 1
+}
+
+// SearchByVector replaces hnsw.SearchByVector (search.go:64-79).
 func (g *Index) SearchByVector(vector []float32, k int, allow helpers.AllowList) ([]uint64, []float32, error) {
 	g.mu.RLock()
-	if g.stale.Load() || len(vector) != g.dim || k <= 0 {
-		g.mu.RUnlock()
+	defer g.mu.RUnlock()
+	if len(vector) == 0 || k <= 0 || g.closed.Load() {
 		return g.cpuIndex.SearchByVector(vector, k, allow)
 	}
-	bits, nbits := allowBits(allow)
 	ids := make([]uint64, k)
 	dists := make([]float32, k)
 	var n C.int32_t
-	var bp *C.uint64_t
-	if bits != nil {
-		bp = (*C.uint64_t)(unsafe.Pointer(&bits[0]))
-	}
-	rc := C.wv_batcher_search(g.b, (*C.float)(unsafe.Pointer(&vector[0])), C.int(k), bp, C.uint64_t(nbits),
-		(*C.uint64_t)(unsafe.Pointer(&ids[0])), (*C.float)(unsafe.Pointer(&dists[0])), &n)
-	g.mu.RUnlock()
-	if rc == C.WV_EDELETED {
+	ap, an, filtered := allowIDs(allow)
+	rc := C.wv_mirror_search(g.m, (*C.float)(unsafe.Pointer(&vector[0])), C.int(len(vector)), C.int(k), filtered,
+		ap, an, (*C.uint64_t)(unsafe.Pointer(&ids[0])), (*C.float)(unsafe.Pointer(&dists[0])), &n)
+	switch {
+	case rc == C.WV_EDELETED:
 		return nil, nil, errors.New("entrypoint was deleted in the object store, " +
 			"it has been flagged for cleanup and should be fixed in the next cleanup cycle")
-	}
-	if rc != 0 {
-		// device error: this call is answered by the CPU index (SURVEY §5)
+	case rc != 0: // stale mirror or device error: the CPU index answers
 		return g.cpuIndex.SearchByVector(vector, k, allow)
-	}
-	if n == 0 {
+	case n == 0:
 		return nil, nil, nil // empty index: search.go:463-465
 	}
 	return ids[:n], dists[:n], nil
@@ -249,17 +285,14 @@ func (g *Index) SearchByVector(vector []float32, k int, allow helpers.AllowList)
 
 // SearchByVectorDistance replaces hnsw.SearchByVectorDistance (search.go:90-158).
 func (g *Index) SearchByVectorDistance(vector []float32, dist float32, maxLimit int64,
-	allow helpers.AllowList) ([]uint64, []float32, error) {
+	allow helpers.AllowList,
+) ([]uint64, []float32, error) {
 	g.mu.RLock()
 	defer g.mu.RUnlock()
-	if g.stale.Load() || len(vector) != g.dim {
+	if len(vector) == 0 || g.closed.Load() {
 		return g.cpuIndex.SearchByVectorDistance(vector, dist, maxLimit, allow)
 	}
-	bits, nbits := allowBits(allow)
-	var bp *C.uint64_t
-	if bits != nil {
-		bp = (*C.uint64_t)(unsafe.Pointer(&bits[0]))
-	}
+	ap, an, filtered := allowIDs(allow)
 	capOut := int64(1 << 12)
 	if maxLimit > 0 && maxLimit < capOut {
 		capOut = maxLimit
@@ -268,8 +301,8 @@ func (g *Index) SearchByVectorDistance(vector []float32, dist float32, maxLimit 
 		ids := make([]uint64, capOut)
 		dists := make([]float32, capOut)
 		var n C.int64_t
-		rc := C.wv_search_by_vector_distance(g.ix, (*C.float)(unsafe.Pointer(&vector[0])), C.float(dist),
-			C.int64_t(maxLimit), bp, C.uint64_t(nbits), (*C.uint64_t)(unsafe.Pointer(&ids[0])),
+		rc := C.wv_mirror_search_by_distance(g.m, (*C.float)(unsafe.Pointer(&vector[0])), C.int(len(vector)),
+			C.float(dist), C.int64_t(maxLimit), filtered, ap, an, (*C.uint64_t)(unsafe.Pointer(&ids[0])),
 			(*C.float)(unsafe.Pointer(&dists[0])), C.int64_t(capOut), &n)
 		if rc != 0 {
 			return g.cpuIndex.SearchByVectorDistance(vector, dist, maxLimit, allow)
@@ -287,85 +320,24 @@ func (g *Index) UpdateUserConfig(updated schema.VectorIndexConfig, callback func
 	if err := g.cpuIndex.UpdateUserConfig(updated, callback); err != nil {
 		return err
 	}
-	uc, ok := updated.(ent.UserConfig)
-	if !ok {
-		return nil
+	g.mu.RLock()
+	defer g.mu.RUnlock()
+	if uc, ok := updated.(ent.UserConfig); ok && !g.closed.Load() {
+		cfg := configOf(uc, g.device)
+		C.wv_mirror_update_config(g.m, &cfg)
 	}
-	g.mu.Lock()
-	defer g.mu.Unlock()
-	cfg := configOf(uc, g.device)
-	if rc := C.wv_index_update_config(g.ix, &cfg); rc != 0 {
-		g.markStale()
-	}
-	return nil
-}
-
-// Snapshot is the CPU index's state in the ABI's CSR layout
-// (wv_index_upload_graph in include/wvgpu.h; wv_graph_export_csr builds it
-// from the commit log).
-type Snapshot struct {
-	Vectors    []float32 // [N][dim]
-	N          uint64
-	Levels     []int8   // [N], -1 nil
-	Layer0     []uint32 // [N][Deg0]
-	Deg0       int
-	UpperRow   []uint32 // [N]
-	Upper      []uint32 // [NUpper][MaxLevel][DegU]
-	NUpper     uint64
-	DegU       int
-	MaxLevel   int
-	Entrypoint uint64
-	Tombstones []uint64 // bitmap over ids
-}
-
-// SyncFromCPU uploads a snapshot (PostStartup, and after compaction /
-// tombstone cleanup, or to recover a stale mirror).  Rows added after the
-// snapshot must be re-applied with Add's propagation by the caller holding
-// the CPU index's insert lock.
-func (g *Index) SyncFromCPU(s *Snapshot) error {
-	g.mu.Lock()
-	defer g.mu.Unlock()
-	g.stale.Store(true)
-	if s.N > g.capacity {
-		return errors.Errorf("wvgpu: snapshot of %d nodes exceeds capacity %d", s.N, g.capacity)
-	}
-	if s.N > 0 {
-		if rc := C.wv_index_upload_vectors(g.ix, (*C.float)(unsafe.Pointer(&s.Vectors[0])), C.uint64_t(s.N), 0); rc != 0 {
-			return lastErr("upload vectors", rc)
-		}
-		var upper *C.uint32_t
-		if len(s.Upper) > 0 {
-			upper = (*C.uint32_t)(unsafe.Pointer(&s.Upper[0]))
-		}
-		if rc := C.wv_index_upload_graph(g.ix, C.uint64_t(s.N), (*C.int8_t)(unsafe.Pointer(&s.Levels[0])),
-			(*C.uint32_t)(unsafe.Pointer(&s.Layer0[0])), C.int(s.Deg0), (*C.uint32_t)(unsafe.Pointer(&s.UpperRow[0])),
-			upper, C.uint64_t(s.NUpper), C.int(s.DegU), C.int(s.MaxLevel), C.uint64_t(s.Entrypoint)); rc != 0 {
-			return lastErr("upload graph", rc)
-		}
-	}
-	var tb *C.uint64_t
-	if len(s.Tombstones) > 0 {
-		tb = (*C.uint64_t)(unsafe.Pointer(&s.Tombstones[0]))
-	}
-	if rc := C.wv_index_set_tombstones(g.ix, tb, C.uint64_t(len(s.Tombstones)*64)); rc != 0 {
-		return lastErr("tombstones", rc)
-	}
-	g.stale.Store(false)
 	return nil
 }
 
 func (g *Index) close() {
 	g.mu.Lock()
+	if g.closed.Swap(true) {
+		g.mu.Unlock()
+		return
+	}
 	defer g.mu.Unlock()
-	if g.b != nil {
-		C.wv_batcher_destroy(g.b) // drains waiting searches first
-		g.b = nil
-	}
-	if g.ix != nil {
-		C.wv_index_destroy(g.ix)
-		g.ix = nil
-	}
-	g.stale.Store(true)
+	C.wv_mirror_destroy(g.m) // waits for a running compaction, drains waiting searches
+	C.free(unsafe.Pointer(g.logDir))
 }
 
 func (g *Index) Shutdown(ctx context.Context) error {

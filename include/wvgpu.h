@@ -137,6 +137,12 @@ int wv_index_add(wv_index *ix, const uint64_t *ids, const float *rows, uint64_t 
 int wv_index_add_tombstones(wv_index *ix, const uint64_t *ids, uint64_t n);
 int wv_index_remove_tombstones(wv_index *ix, const uint64_t *ids, uint64_t n);
 int wv_index_delta_size(wv_index *ix, uint64_t *n);
+/* Capacity growth in place, every row, code, tombstone and the graph kept
+ * (hnsw grows its node array the same way: maintainance.go:31-100
+ * growIndexToAccomodateNode).  Waits for the queued work first; must not
+ * race with searches.  wv_index_capacity: the capacity and highest row + 1. */
+int wv_index_reserve(wv_index *ix, uint64_t capacity);
+int wv_index_capacity(const wv_index *ix, uint64_t *capacity, uint64_t *n_rows);
 
 /* Product quantization (ssdhelpers/product_quantization.go,
  * hnsw/compress.go:39-89).  The fitted quantizer crosses as its centroid
@@ -319,6 +325,74 @@ int wv_group_search_batch(wv_group *g, const float *queries, int nq, int k, int 
                           float *out_dists, int32_t *out_n);
 /* the micro-batcher over a group (wv_batcher_search / _stats / _destroy as above) */
 int wv_batcher_create_group(wv_group *g, int dim, int max_batch, int max_wait_us, wv_batcher **out);
+
+/* GPU mirror of one shard's hnsw index -- the whole lifecycle the cgo
+ * decorator (go/vector/gpu/gpu.go) drives, kept native so that the replay
+ * harness (tests/native/mirror_replay.cpp) tests the code Go calls:
+ *   startup   wv_mirror_post_startup: the shard's commit log
+ *             (<RootPath>/<ID>.hnsw.commitlog.d, replayed as restoreFromDisk,
+ *             startup.go:56-152) becomes the mirror's graph, its rows come
+ *             from the shard's VectorForIDThunk (shard.go:165,
+ *             shard_read.go:145-161) as PostStartup's cache prefill does
+ *             (startup.go:169-205); a node whose object is gone is skipped
+ *             as search.go's handleDeletedNode path skips it (a nil node);
+ *   writes    wv_mirror_add (hnsw.Add, insert.go:43-65: the dimension is
+ *             learnt from the first vector, capacity grows as
+ *             growIndexToAccomodateNode does, maintainance.go:22-24,69-100),
+ *             wv_mirror_delete (delete.go:29-84);
+ *   reads     wv_mirror_search (SearchByVector through the micro-batcher, the
+ *             allow list crossing as ascending ids, allow_list.go:19-118),
+ *             wv_mirror_search_by_distance;
+ *   compaction rows added since the last snapshot are searched exactly beside
+ *             the graph (the delta set); past opt.compact_rows
+ *             wv_mirror_needs_compaction turns true and wv_mirror_compact
+ *             re-snapshots the graph from the (flushed) commit log -- the CPU
+ *             index's own graph -- or, without a log directory, builds it on
+ *             the device (wv_index_build_graph).
+ * Any failed write marks the mirror stale: every read then returns
+ * WV_ESTALE (the decorator answers from the CPU index) until
+ * wv_mirror_post_startup runs again.  Reads and writes may run concurrently
+ * from many threads; growth, compaction and startup are exclusive. */
+typedef struct wv_mirror wv_mirror;
+enum { WV_ESTALE = 6,      /* mirror not serving: answer from the CPU index */
+       WV_ENOTFOUND = 7 }; /* vector source: no object for this doc id */
+typedef struct {
+    int dim;                   /* 0: learnt from the first vector */
+    uint64_t initial_capacity; /* 0: 25000 (maintainance.go:22 initialSize) */
+    int max_batch;             /* micro-batcher: queries per launch (0: 1024) */
+    int max_wait_us;           /* micro-batcher window (0: 200) */
+    uint64_t compact_rows;     /* delta rows that ask for a compaction (0: 8192) */
+    int ef_construction;       /* device-build compaction (0: 128) */
+    uint64_t build_seed;       /* device-build level draw */
+    const char *commitlog_dir; /* NULL: no commit log, compaction builds on the device */
+} wv_mirror_options;
+/* VectorForIDThunk for one doc id: WV_OK with *len = the vector's length
+ * (copied to out when *len <= cap), WV_ENOTFOUND for a deleted object, any
+ * other status is an error. */
+typedef int (*wv_vector_source)(void *ctx, uint64_t id, float *out, int cap, int *len);
+typedef struct {
+    int live;                  /* serving (not stale) */
+    int dim;
+    uint64_t capacity, n_rows, delta_rows, graph_nodes;
+    uint64_t growths, compactions, startup_rows, startup_missing;
+    uint64_t batcher_requests, batcher_batches;
+} wv_mirror_stats;
+int wv_mirror_create(int metric, const wv_config *cfg, const wv_mirror_options *opt, wv_mirror **out);
+int wv_mirror_post_startup(wv_mirror *m, wv_vector_source src, void *ctx);
+int wv_mirror_add(wv_mirror *m, uint64_t id, const float *vector, int len);
+int wv_mirror_delete(wv_mirror *m, const uint64_t *ids, uint64_t n);
+/* filtered != 0: allow_ids[n_allow] ascending doc ids (may be empty: nothing
+ * allowed); filtered == 0: no allow list */
+int wv_mirror_search(wv_mirror *m, const float *vector, int len, int k, int filtered, const uint64_t *allow_ids,
+                     uint64_t n_allow, uint64_t *out_ids, float *out_dists, int32_t *out_n);
+int wv_mirror_search_by_distance(wv_mirror *m, const float *vector, int len, float target_distance,
+                                 int64_t max_limit, int filtered, const uint64_t *allow_ids, uint64_t n_allow,
+                                 uint64_t *out_ids, float *out_dists, int64_t out_cap, int64_t *out_n);
+int wv_mirror_update_config(wv_mirror *m, const wv_config *cfg);
+int wv_mirror_needs_compaction(wv_mirror *m);
+int wv_mirror_compact(wv_mirror *m);
+int wv_mirror_get_stats(wv_mirror *m, wv_mirror_stats *st);
+int wv_mirror_destroy(wv_mirror *m);
 
 const char *wv_last_error(void);
 const char *wv_version(void);

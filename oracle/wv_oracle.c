@@ -768,6 +768,14 @@ int wvo_set_vector(wvo_index *h, uint64_t id, const float *vec) {
     return 0;
 }
 
+/* The object behind id left the object store (the shard deleted it): reads
+ * through VectorForIDThunk now fail (shard_read.go:155-158). */
+int wvo_clear_vector(wvo_index *h, uint64_t id) {
+    if (id >= h->cap) return -1;
+    h->has_vec[id] = 0;
+    return 0;
+}
+
 static inline const float *vec_of(wvo_index *h, uint64_t id) { return h->vecs + id * (uint64_t)h->dim; }
 
 /* distanceToFloatNode / distBetweenNodeAndVec (search.go:420-441,

@@ -75,6 +75,8 @@ void wvo_set_search_config(wvo_index *h, int64_t ef, int64_t ef_min,
  * in: VectorForIDThunk).  Cosine vectors are normalized as on read
  * (vector_cache.go:110-112). */
 int wvo_set_vector(wvo_index *h, uint64_t id, const float *vec);
+/* the object store lost id's object: later reads of its vector fail */
+int wvo_clear_vector(wvo_index *h, uint64_t id);
 /* Add (insert.go:43-65 / 103-217).  Levels are drawn from a counter-based
  * generator keyed by (seed, id) so the graph does not depend on thread
  * interleaving of the level draws. */

@@ -79,7 +79,22 @@ bool deleted_since(int nd_before, uint64_t id) {   // deleted while a search ran
     return false;
 }
 
-std::shared_mutex sync_mu;   // the decorator's RWMutex: searches shared, SyncFromCPU exclusive
+// the decorator's RWMutex: searches shared, SyncFromCPU exclusive.  Go's
+// sync.RWMutex is writer-preferring (a blocked Lock holds off new readers);
+// std::shared_mutex (glibc) is not, and 8 back-to-back searchers would starve
+// the resync forever -- so a gate gives the same semantics.
+struct GoRWMutex {
+    std::shared_mutex rw;
+    std::mutex gate;
+    void lock_shared() {
+        { std::lock_guard<std::mutex> g(gate); }
+        rw.lock_shared();
+    }
+    void unlock_shared() { rw.unlock_shared(); }
+    void lock() { gate.lock(); rw.lock(); }
+    void unlock() { rw.unlock(); gate.unlock(); }
+};
+GoRWMutex sync_mu;
 
 }  // namespace
 
@@ -128,7 +143,7 @@ int main(int argc, char** argv) {
             const uint64_t id = N0 + a;
             row(id, v.data());
             {
-                std::shared_lock<std::shared_mutex> l(sync_mu);
+                std::shared_lock<GoRWMutex> l(sync_mu);
                 if (wv_index_add(ix, &id, v.data(), 1)) violation(std::string("add: ") + wv_last_error());
             }
             n_added.store(a + 1, std::memory_order_release);
@@ -138,7 +153,7 @@ int main(int argc, char** argv) {
                 if (d % 10 == 9 && a > 8) del = N0 + (a - 8);   // delete a row added earlier
                 deleted_log[d] = del;
                 {
-                    std::shared_lock<std::shared_mutex> l(sync_mu);
+                    std::shared_lock<GoRWMutex> l(sync_mu);
                     if (wv_index_add_tombstones(ix, &del, 1))
                         violation(std::string("tombstone: ") + wv_last_error());
                 }
@@ -146,7 +161,7 @@ int main(int argc, char** argv) {
             }
             if (a == N_ADD / 2) {
                 // SyncFromCPU: exclusive, a fresh snapshot holding the added rows
-                std::unique_lock<std::shared_mutex> l(sync_mu);
+                std::unique_lock<GoRWMutex> l(sync_mu);
                 if (wv_index_build_graph(ix, 64, 7, 64)) violation(std::string("resync: ") + wv_last_error());
                 added_at_resync.store(a + 1, std::memory_order_release);
                 n_resync++;
@@ -181,7 +196,7 @@ int main(int argc, char** argv) {
             const bool filtered = it % 5 == 0;
             const bool by_dist = it % 17 == 0;
             int32_t n = 0;
-            std::shared_lock<std::shared_mutex> l(sync_mu);
+            std::shared_lock<GoRWMutex> l(sync_mu);
             if (by_dist) {
                 std::vector<uint64_t> di(4096);
                 std::vector<float> dd(4096);

@@ -1,0 +1,394 @@
+// mirror_replay.cpp -- the cgo decorator's lifecycle (go/vector/gpu/gpu.go
+// over wv_mirror_*) replayed natively against the CPU restatement as "the
+// shard's hnsw index": test infrastructure (links oracle/libwvoracle.so as the
+// checker and as the CPU index whose commit log the mirror reads).
+//
+//   startup    the restatement inserts N0 rows one by one, writing its commit
+//              log (commitlog/logger.go records, as insert.go writes them),
+//              tombstones 600 ids and loses 100 of their objects; the log goes
+//              to <dir>/main.hnsw.commitlog.d/<ts>.  wv_mirror_post_startup
+//              replays that directory and pulls rows through a
+//              VectorForIDThunk stand-in (no wv_index_build_graph shortcut).
+//              Check 1: searches (HNSW, flat and filtered-HNSW by the cutoff)
+//              equal the restatement's SearchByVector, ids and distances.
+//   serving    a writer adds N_ADD rows (the restatement's Add then
+//              wv_mirror_add, as the decorator does: the mirror grows past its
+//              25 000-row initial size) and deletes ids; a maintenance thread
+//              flushes the log and calls wv_mirror_compact whenever
+//              wv_mirror_needs_compaction; 8 searchers query through
+//              wv_mirror_search (allow lists as ascending ids) and assert that
+//              no id deleted before a search started is returned and that a
+//              row added before it started is found first while it sits in
+//              the delta set.  Check 2: the delta stays bounded.
+//   quiescent  final flush + compaction; check 3: searches equal the
+//              restatement's again, and the delta is empty.
+// Exit 0 with one JSON line, or 1 with the first violation.
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <random>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include <sys/stat.h>
+
+#include "../../include/wvgpu.h"
+#include "../../oracle/wv_oracle.h"
+
+namespace {
+
+constexpr int DIM = 32;
+constexpr uint64_t N0 = 20000;
+constexpr uint64_t N_ADD = 20000;
+constexpr uint64_t CAP = N0 + N_ADD;
+constexpr int M = 16, EFC = 64, EF = 64, K = 10;
+constexpr int64_t CUTOFF = 5000;
+constexpr uint64_t COMPACT_ROWS = 4096;
+constexpr int SEARCHERS = 8;
+constexpr int NQ_CHECK = 400;
+
+std::atomic<bool> failed{false};
+std::mutex err_mu;
+std::string first_err;
+void violation(const std::string& m) {
+    std::lock_guard<std::mutex> l(err_mu);
+    if (!failed.exchange(true)) first_err = m;
+}
+
+float urand(uint64_t id, int j) {
+    uint64_t x = id * 0x9E3779B97F4A7C15ull + (uint64_t)j * 0xBF58476D1CE4E5B9ull + 0x94D049BB133111EBull;
+    x ^= x >> 30; x *= 0xBF58476D1CE4E5B9ull; x ^= x >> 27; x *= 0x94D049BB133111EBull; x ^= x >> 31;
+    return (float)(x >> 40) * (1.0f / 16777216.0f);
+}
+void row(uint64_t id, float* out) { for (int j = 0; j < DIM; ++j) out[j] = urand(id, j); }
+
+// the shard's object store (VectorForIDThunk stand-in)
+std::vector<float> store(CAP * DIM);
+std::vector<uint8_t> in_store(CAP, 0);
+
+int vector_for_id(void*, uint64_t id, float* out, int cap, int* len) {
+    if (id >= CAP || !in_store[id]) return WV_ENOTFOUND;
+    *len = DIM;
+    if (cap >= DIM) std::memcpy(out, &store[id * DIM], DIM * sizeof(float));
+    return WV_OK;
+}
+
+// the CPU index and its commit log file
+std::mutex cpu_mu;
+wvo_index* cpu = nullptr;
+std::string log_file;
+uint64_t log_written = 0;
+
+void flush_log() {   // hnsw.Flush(): the buffered log reaches the file (cpu_mu held)
+    const uint64_t n = wvo_log_size(cpu);
+    std::vector<uint8_t> buf(n);
+    wvo_log_copy(cpu, buf.data(), n);
+    FILE* f = std::fopen(log_file.c_str(), "ab");
+    if (!f) { violation("cannot write " + log_file); return; }
+    std::fwrite(buf.data() + log_written, 1, n - log_written, f);
+    std::fclose(f);
+    log_written = n;
+}
+
+std::vector<uint64_t> allow_ids(std::mt19937_64& g, uint64_t n_ids, uint64_t range) {
+    std::vector<uint64_t> a;
+    a.reserve(n_ids);
+    for (uint64_t i = 0; i < n_ids; ++i) a.push_back(g() % range);
+    std::sort(a.begin(), a.end());
+    a.erase(std::unique(a.begin(), a.end()), a.end());
+    return a;
+}
+int exact_fallbacks = 0;   // filtered HNSW queries answered by the exact scan
+
+std::vector<uint64_t> to_bits(const std::vector<uint64_t>& ids, uint64_t range) {
+    std::vector<uint64_t> b((range + 63) / 64, 0);
+    for (uint64_t id : ids) b[id >> 6] |= 1ull << (id & 63);
+    return b;
+}
+
+// mirror vs restatement on NQ_CHECK queries (a third unfiltered, a third with
+// a small allow list -> flatSearch, a third with a large one -> filtered HNSW)
+int compare(wv_mirror* m, uint64_t range, int seed, const char* phase) {
+    std::mt19937_64 g(seed);
+    std::vector<float> q(DIM);
+    uint64_t oi[K], mi[K];
+    float od[K], md[K];
+    int diffs = 0;
+    for (int i = 0; i < NQ_CHECK; ++i) {
+        row(g() % range, q.data());
+        for (int j = 0; j < DIM; ++j) q[j] += 0.02f * (urand(g(), j) - 0.5f);
+        std::vector<uint64_t> al;
+        if (i % 3 == 1) al = allow_ids(g, 1500, range);
+        if (i % 3 == 2) al = allow_ids(g, 14000, range);
+        const std::vector<uint64_t> bits = to_bits(al, range);
+        int on = 0;
+        int32_t mn = 0;
+        {
+            std::lock_guard<std::mutex> l(cpu_mu);
+            wvo_search_by_vector(cpu, q.data(), K, i % 3 ? bits.data() : nullptr, i % 3 ? range : 0, oi, od, &on,
+                                 nullptr);
+        }
+        const int rc = wv_mirror_search(m, q.data(), DIM, K, i % 3 != 0, al.data(), al.size(), mi, md, &mn);
+        if (rc) { violation(std::string(phase) + ": mirror search: " + wv_last_error()); return -1; }
+        bool same = mn == on;
+        for (int j = 0; same && j < on; ++j) same = mi[j] == oi[j] && std::memcmp(&md[j], &od[j], 4) == 0;
+        if (!same && i % 3 == 2) {
+            // a filtered HNSW query whose side candidates outgrow the wave's
+            // LDS is answered by the exact filtered scan (a
+            // superset in quality): then it must equal flatSearch's answer
+            int fn = 0;
+            {
+                std::lock_guard<std::mutex> l(cpu_mu);
+                wvo_flat_search(cpu, q.data(), K, bits.data(), range, oi, od, &fn);
+            }
+            same = mn == fn;
+            for (int j = 0; same && j < fn; ++j) same = mi[j] == oi[j] && std::memcmp(&md[j], &od[j], 4) == 0;
+            if (same) ++exact_fallbacks;
+        }
+        if (!same) {
+            if (++diffs == 1)
+                std::fprintf(stderr, "%s: query %d differs (mirror n=%d id0=%llu, restatement n=%d id0=%llu)\n", phase, i,
+                             mn, (unsigned long long)(mn ? mi[0] : 0), on, (unsigned long long)(on ? oi[0] : 0));
+        }
+    }
+    return diffs;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    if (argc < 2) { std::fprintf(stderr, "usage: mirror_replay <dir> [device]\n"); return 2; }
+    const std::string root = argv[1];
+    const int device = argc > 2 ? std::atoi(argv[2]) : 0;
+    const std::string log_dir = root + "/main.hnsw.commitlog.d";
+    mkdir(root.c_str(), 0755);
+    mkdir(log_dir.c_str(), 0755);
+    log_file = log_dir + "/1700000000";
+    std::remove(log_file.c_str());
+
+    // ---- startup state: the CPU index as restoreFromDisk would find it ----
+    cpu = wvo_create(DIM, WVO_L2, M, EFC, CAP, 7);
+    wvo_set_search_config(cpu, EF, 100, 500, 8, CUTOFF, 0);
+    wvo_log_enable(cpu, 1);
+    std::vector<float> v(DIM);
+    for (uint64_t id = 0; id < N0; ++id) {
+        row(id, &store[id * DIM]);
+        in_store[id] = 1;
+        wvo_add(cpu, id, &store[id * DIM]);
+    }
+    std::mt19937_64 g0(5);
+    std::vector<uint64_t> deleted;   // append-only: ids deleted before each point in time
+    for (int i = 0; i < 600; ++i) {
+        const uint64_t id = 1 + g0() % (N0 - 1);
+        wvo_add_tombstone(cpu, id);
+        deleted.push_back(id);
+    }
+    uint64_t gone = 0;
+    for (int i = 0; i < 100; ++i) {   // objects deleted from the store as well
+        const uint64_t id = deleted[i];
+        uint64_t ns = 0, ep = 0, nu = 0;
+        int ml = 0;
+        wvo_graph_info(cpu, &ns, &ep, &ml, &nu);
+        if (id == ep || !in_store[id]) continue;
+        in_store[id] = 0;
+        wvo_clear_vector(cpu, id);
+        ++gone;
+    }
+    flush_log();
+
+    wv_config cfg;
+    wv_config_default(&cfg);
+    cfg.device = device;
+    cfg.max_connections = M;
+    cfg.ef = EF;
+    cfg.flat_search_cutoff = CUTOFF;
+    wv_mirror_options opt{};
+    opt.compact_rows = COMPACT_ROWS;
+    opt.max_batch = 256;
+    opt.commitlog_dir = log_dir.c_str();
+    wv_mirror* m = nullptr;
+    if (wv_mirror_create(WV_L2_SQUARED, &cfg, &opt, &m)) { std::fprintf(stderr, "create: %s\n", wv_last_error()); return 1; }
+    {
+        // before PostStartup the mirror does not serve: the CPU index answers
+        uint64_t i0[K]; float d0[K]; int32_t n0 = 0;
+        if (wv_mirror_search(m, &store[0], DIM, K, 0, nullptr, 0, i0, d0, &n0) != WV_ESTALE)
+            violation("a mirror serves before PostStartup");
+    }
+    const auto t_start = std::chrono::steady_clock::now();
+    if (wv_mirror_post_startup(m, vector_for_id, nullptr)) {
+        std::fprintf(stderr, "post_startup: %s\n", wv_last_error());
+        return 1;
+    }
+    const double startup_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
+    wv_mirror_stats st0;
+    wv_mirror_get_stats(m, &st0);
+    if (!st0.live || st0.dim != DIM || st0.startup_missing != gone || st0.startup_rows != N0 - gone ||
+        st0.graph_nodes != N0 || st0.delta_rows != 0 || st0.capacity != 25000)
+        violation("startup stats: live " + std::to_string(st0.live) + " dim " + std::to_string(st0.dim) + " rows " +
+                  std::to_string(st0.startup_rows) + " missing " + std::to_string(st0.startup_missing) + " nodes " +
+                  std::to_string(st0.graph_nodes) + " delta " + std::to_string(st0.delta_rows) + " capacity " +
+                  std::to_string(st0.capacity));
+    const int diffs_startup = failed ? -1 : compare(m, N0, 11, "startup");
+
+    // ---- serving: adds, deletes, compactions and searches at once ----
+    std::atomic<int> n_deleted{(int)deleted.size()};
+    deleted.resize(deleted.size() + N_ADD);   // (no reallocation while readers scan it)
+    std::atomic<uint64_t> n_added{0};
+    std::atomic<bool> writer_done{false}, stop_maint{false};
+    std::atomic<uint64_t> max_delta{0}, n_compact{0}, n_search{0}, n_added_checks{0}, n_filtered{0};
+    std::mutex in_graph_mu;
+    std::vector<uint8_t> compacted(CAP, 0);   // added rows that a compaction moved into the graph
+
+    auto writer = std::thread([&] {
+        std::mt19937_64 g(21);
+        for (uint64_t a = 0; a < N_ADD && !failed; ++a) {
+            const uint64_t id = N0 + a;
+            row(id, &store[id * DIM]);
+            in_store[id] = 1;
+            {
+                std::lock_guard<std::mutex> l(cpu_mu);
+                wvo_add(cpu, id, &store[id * DIM]);
+            }
+            const int rc = wv_mirror_add(m, id, &store[id * DIM], DIM);
+            if (rc) violation(std::string("add: ") + wv_last_error());
+            n_added.store(a + 1, std::memory_order_release);
+            if (a % 3 == 0) {
+                const uint64_t del = a % 9 == 0 && a > 16 ? N0 + a - 16 : g() % N0;
+                {
+                    std::lock_guard<std::mutex> l(cpu_mu);
+                    wvo_add_tombstone(cpu, del);
+                }
+                if (wv_mirror_delete(m, &del, 1)) violation(std::string("delete: ") + wv_last_error());
+                const int d = n_deleted.load();
+                deleted[d] = del;
+                n_deleted.store(d + 1, std::memory_order_release);
+            }
+            wv_mirror_stats s;
+            wv_mirror_get_stats(m, &s);
+            uint64_t md = max_delta.load();
+            while (s.delta_rows > md && !max_delta.compare_exchange_weak(md, s.delta_rows)) {}
+        }
+        writer_done = true;
+    });
+    auto maint = std::thread([&] {   // the decorator's compaction goroutine
+        while (!stop_maint && !failed) {
+            if (wv_mirror_needs_compaction(m)) {
+                const uint64_t na = n_added.load(std::memory_order_acquire);
+                {
+                    std::lock_guard<std::mutex> l(cpu_mu);
+                    flush_log();
+                }
+                if (wv_mirror_compact(m)) violation(std::string("compact: ") + wv_last_error());
+                {
+                    std::lock_guard<std::mutex> l(in_graph_mu);
+                    for (uint64_t a = 0; a < na; ++a) compacted[N0 + a] = 1;
+                }
+                n_compact++;
+            }
+            std::this_thread::sleep_for(std::chrono::microseconds(500));
+        }
+    });
+    auto searcher = [&](int t) {
+        std::mt19937_64 g(100 + t);
+        std::vector<float> q(DIM);
+        uint64_t ids[K];
+        float ds[K];
+        uint64_t it = 0;
+        while (!writer_done && !failed) {
+            ++it;
+            const int nd = n_deleted.load(std::memory_order_acquire);
+            const uint64_t na = n_added.load(std::memory_order_acquire);
+            std::vector<uint8_t> del_now(CAP, 0);
+            for (int i = 0; i < nd; ++i) del_now[deleted[i]] = 1;
+            uint64_t target = UINT64_MAX;
+            bool target_in_graph = false;
+            if (na > 0 && it % 2 == 0) {
+                target = N0 + g() % na;
+                row(target, q.data());
+                std::lock_guard<std::mutex> l(in_graph_mu);
+                target_in_graph = compacted[target];
+            } else {
+                row(g() % N0, q.data());
+                for (int j = 0; j < DIM; ++j) q[j] += 0.01f * urand(g(), j);
+            }
+            const bool filtered = it % 5 == 0;
+            std::vector<uint64_t> al;
+            if (filtered) {
+                al = allow_ids(g, 1500, N0 + na);
+                if (target != UINT64_MAX) {
+                    al.push_back(target);
+                    std::sort(al.begin(), al.end());
+                    al.erase(std::unique(al.begin(), al.end()), al.end());
+                }
+                n_filtered++;
+            }
+            int32_t n = 0;
+            const int rc = wv_mirror_search(m, q.data(), DIM, K, filtered, al.data(), al.size(), ids, ds, &n);
+            if (rc) { violation(std::string("search: ") + wv_last_error()); return; }
+            n_search++;
+            for (int i = 0; i < n; ++i) {
+                if (ids[i] >= CAP) violation("id out of range");
+                else if (del_now[ids[i]]) violation("search returned deleted id " + std::to_string(ids[i]));
+                if (filtered && !std::binary_search(al.begin(), al.end(), ids[i]))
+                    violation("filtered search returned a disallowed id");
+            }
+            if (target != UINT64_MAX && !del_now[target] && (filtered || !target_in_graph)) {
+                n_added_checks++;
+                bool deleted_since = false;
+                const int nd2 = n_deleted.load(std::memory_order_acquire);
+                for (int i = nd; i < nd2; ++i) deleted_since |= deleted[i] == target;
+                if (!(n > 0 && ids[0] == target && ds[0] == 0.f) && !deleted_since)
+                    violation("added id " + std::to_string(target) + " not found first");
+            }
+        }
+    };
+    std::vector<std::thread> ts;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int t = 0; t < SEARCHERS; ++t) ts.emplace_back(searcher, t);
+    writer.join();
+    for (auto& t : ts) t.join();
+    stop_maint = true;
+    maint.join();
+    const double serve_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+
+    // ---- quiescent: final flush + compaction, then the restatement again ----
+    {
+        std::lock_guard<std::mutex> l(cpu_mu);
+        flush_log();
+    }
+    if (!failed && wv_mirror_compact(m)) violation(std::string("final compact: ") + wv_last_error());
+    wv_mirror_stats st;
+    wv_mirror_get_stats(m, &st);
+    const int diffs_final = failed ? -1 : compare(m, CAP, 12, "final");
+    if (!failed && st.delta_rows != 0) violation("delta not empty after the final compaction");
+    if (!failed && max_delta > 2 * COMPACT_ROWS) violation("delta grew to " + std::to_string(max_delta.load()));
+    if (!failed && st.growths < 1) violation("the mirror never grew past its initial capacity");
+    if (!failed && n_compact < 2) violation("fewer than two compactions while serving");
+    if (!failed && (diffs_startup != 0 || diffs_final != 0))
+        violation("searches differ from the restatement: startup " + std::to_string(diffs_startup) + ", final " +
+                  std::to_string(diffs_final) + " of " + std::to_string(NQ_CHECK));
+    wv_mirror_destroy(m);
+    wvo_destroy(cpu);
+    if (failed) {
+        std::fprintf(stderr, "VIOLATION: %s\n", first_err.c_str());
+        return 1;
+    }
+    std::printf("{\"ok\": true, \"startup_rows\": %llu, \"startup_missing\": %llu, \"startup_s\": %.2f, "
+                "\"diffs_startup\": %d, \"diffs_final\": %d, \"exact_fallbacks\": %d, \"checked\": %d, \"adds\": %llu, \"deletes\": %d, "
+                "\"compactions\": %llu, \"max_delta\": %llu, \"capacity\": %llu, \"growths\": %llu, "
+                "\"searches\": %llu, \"added_checks\": %llu, \"filtered\": %llu, \"batcher_requests\": %llu, "
+                "\"batcher_batches\": %llu, \"serve_s\": %.2f}\n",
+                (unsigned long long)st0.startup_rows, (unsigned long long)st0.startup_missing, startup_s,
+                diffs_startup, diffs_final, exact_fallbacks, NQ_CHECK, (unsigned long long)n_added.load(), n_deleted.load(),
+                (unsigned long long)st.compactions, (unsigned long long)max_delta.load(),
+                (unsigned long long)st.capacity, (unsigned long long)st.growths, (unsigned long long)n_search.load(),
+                (unsigned long long)n_added_checks.load(), (unsigned long long)n_filtered.load(),
+                (unsigned long long)st.batcher_requests, (unsigned long long)st.batcher_batches, serve_s);
+    return 0;
+}

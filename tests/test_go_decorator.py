@@ -1,4 +1,4 @@
-"""The cgo decorator (go/vector/gpu/gpu.go) and its native replay harness.
+"""The cgo decorator (go/vector/gpu/gpu.go) and its native replay harnesses.
 
 The Go toolchain is absent from the build image, so the decorator's C call
 sequence is replayed by tests/native/go_replay.cpp (plain C++ over the C ABI,
@@ -31,19 +31,49 @@ def test_go_decorator_binds_only_header_symbols():
     assert used, "the decorator calls no C function"
     assert used <= _header_functions(), f"not in wvgpu.h: {used - _header_functions()}"
     # every write of the VectorIndex interface reaches the mirror
-    for method, call in (("Add", "wv_index_add"), ("Delete", "wv_index_add_tombstones"),
-                         ("SearchByVector", "wv_batcher_search"),
-                         ("SearchByVectorDistance", "wv_search_by_vector_distance"),
-                         ("UpdateUserConfig", "wv_index_update_config")):
+    for method, call in (("Add", "wv_mirror_add"), ("Delete", "wv_mirror_delete"),
+                         ("SearchByVector", "wv_mirror_search"),
+                         ("SearchByVectorDistance", "wv_mirror_search_by_distance"),
+                         ("UpdateUserConfig", "wv_mirror_update_config"),
+                         ("PostStartup", "wvgpu_post_startup")):
         body = re.search(r"func \(g \*Index\) %s\(.*?\n}\n" % method, src, re.S)
         assert body, method
         assert f"C.{call}(" in body.group(0), f"{method} does not call {call}"
+    # PostStartup goes live from the shard's commit log and VectorForIDThunk
+    assert "wv_mirror_post_startup(m, wvgpuVectorForID, ctx)" in src
+    assert '".hnsw.commitlog.d"' in src and "//export wvgpuVectorForID" in src
+    # compaction flushes the CPU index's log first
+    body = re.search(r"func \(g \*Index\) maybeCompact\(.*?\n}\n", src, re.S).group(0)
+    assert body.index("cpuIndex.Flush()") < body.index("C.wv_mirror_compact(")
 
 
 def test_replay_harness_binds_only_header_symbols():
-    src = open(os.path.join(ROOT, "tests", "native", "go_replay.cpp")).read()
-    used = set(re.findall(r"\b(wv_[a-z0-9_]+)\s*\(", src))
-    assert used <= _header_functions()
+    for f in ("go_replay.cpp", "mirror_replay.cpp"):
+        src = open(os.path.join(ROOT, "tests", "native", f)).read()
+        used = set(re.findall(r"\b(wv_[a-z0-9_]+)\s*\(", src))
+        assert used <= _header_functions(), f
+
+
+@pytest.mark.gpu
+def test_mirror_lifecycle_from_commit_log(tmp_path):
+    """The decorator's lifecycle over wv_mirror_*: startup from a commit-log
+    directory the restatement wrote (startup.go:56-205) with rows pulled
+    through the vector thunk, searches equal to the restatement's, then 20k
+    adds (capacity growth), deletes and log-driven compactions under 8
+    concurrent searchers, the delta bounded, and searches equal to the
+    restatement's again after the final compaction."""
+    binp = os.path.join(ROOT, "tests", "native", "mirror_replay")
+    assert os.path.exists(binp), "build tests/native first (__graft_entry__.build())"
+    p = subprocess.run([binp, str(tmp_path), "0"], capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:] + p.stdout[-2000:]
+    r = json.loads(p.stdout.strip().splitlines()[-1])
+    assert r["ok"] and r["diffs_startup"] == 0 and r["diffs_final"] == 0
+    assert r["startup_missing"] > 50 and r["startup_rows"] + r["startup_missing"] == 20000
+    assert r["adds"] == 20000 and r["growths"] >= 1 and r["capacity"] >= 40000
+    assert r["compactions"] >= 3 and r["max_delta"] <= 2 * 4096
+    assert r["added_checks"] > 100 and r["filtered"] > 50
+    assert r["batcher_batches"] < r["batcher_requests"]
+    print(r)
 
 
 @pytest.mark.gpu

@@ -607,6 +607,38 @@ def test_mutable_index_added_rows_are_searchable_until_the_next_snapshot():
     ix.close()
 
 
+def test_index_reserve_grows_in_place():
+    """wv_index_reserve (growIndexToAccomodateNode, maintainance.go:31-100):
+    rows, f16 images, tombstones and the graph survive the growth; rows added
+    past the old capacity are found at once (delta), exact search over every
+    row equals the restatement's."""
+    n0, n1, d, k, ef = 3000, 7000, 64, 10, 64
+    rng = np.random.default_rng(57)
+    base = rng.random((n1, d), dtype=np.float32)
+    qs = rng.random((200, d), dtype=np.float32)
+    ref = O.Index(d, "l2-squared", 16, 64, capacity=n1, seed=8)
+    ref.add_batch(base[:n0], threads=4)
+    ix = W.GPUVectorIndex(d, "l2-squared", capacity=n0, max_connections=16)
+    ix.upload_vectors(base[:n0])
+    ix.upload_graph(ref.export_graph())
+    dead = np.arange(5, 400, 7, dtype=np.uint64)
+    ix.add_tombstones(dead)
+    h0 = ix.search_batch(qs, k, ef=ef, mode="hnsw")
+    ix.reserve(n1)
+    assert ix.capacity_info() == (n1, n0)
+    h1 = ix.search_batch(qs, k, ef=ef, mode="hnsw")
+    _same(h1[0], h1[1], h0[0], h0[1])
+    ix.add(np.arange(n0, n1), base[n0:])
+    assert ix.delta_size() == n1 - n0
+    ei, ed, en = ix.search_batch(qs, k, mode="exact")
+    allow = np.ones(n1, bool)
+    allow[dead.astype(np.int64)] = False
+    sel = np.nonzero(allow)[0]
+    oi, od, on = O.flat_scan(O.L2, base[sel], qs, k)
+    _same(ei, ed, sel[oi.astype(np.int64)].astype(np.uint64), od)
+    ix.close()
+
+
 def test_mutable_index_delta_with_per_query_allow_lists():
     n0, n1, d, k = 3000, 3600, 24, 10
     rng = np.random.default_rng(52)

@@ -247,7 +247,7 @@ struct wv_index {
     uint64_t gn = 0;
     int deg0 = 0, degU = 0, max_level = 0;
     uint64_t n_upper = 0, entrypoint = 0;
-    std::vector<int8_t> levels_host;
+    std::vector<uint64_t> nil_host;   // graph nil nodes and ids >= gn, one bit per id
     DevBuf levels, layer0, upper_row, upper;
     // bitmaps
     std::vector<uint64_t> tomb_host;
@@ -329,17 +329,13 @@ int refresh_bitmaps(wv_index* ix) {
     std::vector<uint64_t> dl(words, 0);
     uint64_t dcount = 0;
     if (ix->has_graph) {
-        for (uint64_t i = 0; i < ix->capacity; ++i) {
-            const bool nil = i >= ix->gn || ix->levels_host[i] < 0;
-            const uint64_t bit = 1ull << (i & 63);
-            const bool pend = ix->pending_host[i >> 6] & bit;
-            // a nil node is skipped by flatSearch (flat_search.go:29-40) unless
-            // it was added after the graph snapshot: then it is live (delta)
-            if (nil && !pend) ex[i >> 6] |= bit;
-            if (nil && pend && (ix->has_vec[i >> 6] & bit) && !(ex[i >> 6] & bit)) {
-                dl[i >> 6] |= bit;
-                dcount++;
-            }
+        // a nil node is skipped by flatSearch (flat_search.go:29-40) unless
+        // it was added after the graph snapshot: then it is live (delta)
+        for (uint64_t w = 0; w < words; ++w) {
+            const uint64_t nil = ix->nil_host[w], pend = ix->pending_host[w];
+            dl[w] = nil & pend & ix->has_vec[w] & ~ex[w];
+            ex[w] |= nil & ~pend;
+            dcount += (uint64_t)__builtin_popcountll(dl[w]);
         }
     }
     ix->delta_count = dcount;
@@ -1593,11 +1589,12 @@ int wv_index_upload_graph(wv_index* ix, uint64_t n, const int8_t* levels, const 
                                ix->stream));
     }
     HIP_TRY(hipStreamSynchronize(ix->stream));
-    ix->levels_host.assign(levels, levels + n);
+    ix->nil_host.assign(ix->bm_words, ~0ull);
+    for (uint64_t i = 0; i < n; ++i)
+        if (levels[i] >= 0) ix->nil_host[i >> 6] &= ~(1ull << (i & 63));
     ix->any_nil = std::any_of(levels, levels + n, [](int8_t l) { return l < 0; });
     for (uint64_t i = 0; i < n; ++i)   // the new snapshot holds these added rows
         if (levels[i] >= 0) ix->pending_host[i >> 6] &= ~(1ull << (i & 63));
-    ix->levels_host.resize(ix->capacity, -1);
     ix->gn = n;
     ix->deg0 = deg0;
     ix->degU = max_level > 0 ? degU : 1;
@@ -1726,6 +1723,67 @@ int wv_index_delta_size(wv_index* ix, uint64_t* n) {
     int rc = refresh_bitmaps(ix);
     if (rc) return rc;
     *n = ix->delta_count;
+    return WV_OK;
+}
+
+// Re-home a capacity-sized device buffer at new_bytes: the first old_bytes
+// copied, the rest zeroed (an unused buffer stays unallocated).
+static hipError_t regrow(DevBuf& b, size_t old_bytes, size_t new_bytes, hipStream_t s) {
+    if (!b.p || new_bytes <= b.cap) return hipSuccess;
+    void* np = nullptr;
+    hipError_t e = hipMalloc(&np, new_bytes);
+    if (e != hipSuccess) return e;
+    old_bytes = std::min(old_bytes, b.cap);
+    if (old_bytes) e = hipMemcpyAsync(np, b.p, old_bytes, hipMemcpyDeviceToDevice, s);
+    if (e == hipSuccess) e = hipMemsetAsync(static_cast<char*>(np) + old_bytes, 0, new_bytes - old_bytes, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) { (void)hipFree(np); return e; }
+    (void)hipFree(b.p);
+    b.p = np;
+    b.cap = new_bytes;
+    return hipSuccess;
+}
+
+// Capacity growth in place (the mirror of a shard that outgrew its
+// allocation; hnsw grows its node array the same way,
+// maintainance.go:31-100 growIndexToAccomodateNode): every row, image, norm, code, tombstone and the
+// graph stay; the queued work is drained first.
+int wv_index_reserve(wv_index* ix, uint64_t capacity) {
+    if (check(ix) || capacity >= (1ull << 31)) return fail(WV_EINVAL, "wv_index_reserve: bad argument");
+    std::lock_guard<std::mutex> g(ix->mu);
+    if (capacity <= ix->capacity) return WV_OK;
+    HIP_TRY(hipSetDevice(ix->cfg.device));
+    hipStream_t s = ix->stream;
+    HIP_TRY(hipStreamSynchronize(s));
+    const uint64_t old_rows = (ix->capacity + wv::BF_BN - 1) / wv::BF_BN * wv::BF_BN;
+    const uint64_t cap_rows = (capacity + wv::BF_BN - 1) / wv::BF_BN * wv::BF_BN;
+    const size_t ld4 = (size_t)ix->ldx * 4, img = (size_t)ix->h16_ns * 16 * 2;
+    const uint64_t words = (capacity + 63) / 64;
+    HIP_TRY(regrow(ix->vecs, old_rows * ld4, cap_rows * ld4, s));
+    HIP_TRY(regrow(ix->xsplit, old_rows * ld4, cap_rows * ld4, s));
+    HIP_TRY(regrow(ix->xnorm, old_rows * 4, cap_rows * 4, s));
+    HIP_TRY(regrow(ix->xns, old_rows * 4, cap_rows * 4, s));
+    HIP_TRY(regrow(ix->ximg16, old_rows * img, cap_rows * img, s));
+    HIP_TRY(regrow(ix->ximg16q, old_rows * img, cap_rows * img, s));
+    HIP_TRY(regrow(ix->pq_codes, ix->capacity * ix->pq_stride, capacity * ix->pq_stride, s));
+    // bitmaps are rewritten from the host copies by the next refresh
+    HIP_TRY(ix->tomb.ensure(words * 8));
+    HIP_TRY(ix->excl.ensure((words + 2) * 8));
+    ix->has_vec.resize(words, 0);
+    ix->tomb_host.resize(words, 0);
+    ix->pending_host.resize(words, 0);
+    if (!ix->has_code.empty()) ix->has_code.resize(words, 0);
+    if (!ix->nil_host.empty()) ix->nil_host.resize(words, ~0ull);
+    ix->capacity = capacity;
+    ix->bm_words = words;
+    ix->bitmaps_dirty = true;
+    return WV_OK;
+}
+
+int wv_index_capacity(const wv_index* ix, uint64_t* capacity, uint64_t* n_rows) {
+    if (!ix) return fail(WV_EINVAL, "null index");
+    if (capacity) *capacity = ix->capacity;
+    if (n_rows) *n_rows = ix->n_rows;
     return WV_OK;
 }
 
@@ -1887,8 +1945,9 @@ int wv_index_build_graph(wv_index* ix, int ef_construction, uint64_t seed, int b
         done += nb;
     }
     HIP_TRY(hipStreamSynchronize(s));
-    ix->levels_host.assign(lv.begin(), lv.end());
-    ix->levels_host.resize(ix->capacity, -1);
+    ix->nil_host.assign(ix->bm_words, ~0ull);
+    for (uint64_t i = 0; i < lv.size(); ++i)
+        if (lv[i] >= 0) ix->nil_host[i >> 6] &= ~(1ull << (i & 63));
     ix->gn = n;
     ix->deg0 = M0;
     ix->degU = M;

@@ -218,6 +218,16 @@ class GPUVectorIndex:
         check(lib().wv_index_delta_size(self._h, C.byref(n)))
         return n.value
 
+    def reserve(self, capacity: int):
+        """Grow the index in place (growIndexToAccomodateNode, maintainance.go:31-100)."""
+        check(lib().wv_index_reserve(self._h, capacity))
+        self.capacity = max(self.capacity, capacity)
+
+    def capacity_info(self) -> tuple:
+        cap, n = C.c_uint64(), C.c_uint64()
+        check(lib().wv_index_capacity(self._h, C.byref(cap), C.byref(n)))
+        return cap.value, n.value
+
     # -- product quantization (compress.go:39-89) -------------------------------
     def set_pq(self, centroids, use_bits_encoding: bool = False, encoder: str = "kmeans"):
         """The fitted quantizer: centroids[segments][ks][dims/segments] =
