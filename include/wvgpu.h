@@ -283,12 +283,20 @@ int wv_graph_destroy(wv_graph *g);
  * dispatcher thread coalesces up to max_batch waiting requests (or those that
  * arrived within max_wait_us of the first) into one wv_search_batch with
  * per-query allow lists, then returns this caller's row: the same result as
- * wv_search_by_vector(ix, vector, k, allow_bits, allow_nbits, ...).  Destroy
- * the batcher before the index. */
+ * wv_search_by_vector(ix, vector, k, allow_bits, allow_nbits, ...).  Two
+ * workers alternate, so one batch is coalesced and queued while the previous
+ * one runs.  Destroy the batcher before the index. */
 typedef struct wv_batcher wv_batcher;
 int wv_batcher_create(wv_index *ix, int dim, int max_batch, int max_wait_us, wv_batcher **out);
 int wv_batcher_search(wv_batcher *b, const float *vector, int k, const uint64_t *allow_bits, uint64_t allow_nbits,
                       uint64_t *out_ids, float *out_dists, int32_t *out_n);
+/* The same with the AllowList as strictly ascending ids (its Slice(),
+ * helpers/allow_list.go:19-118): filtered == 0 means no list; filtered with
+ * n_allow == 0 allows nothing.  The ids go straight into the batch's bitmap
+ * row (no per-caller dense bitmap); a batch whose requests all carry the
+ * same list sends it once. */
+int wv_batcher_search_ids(wv_batcher *b, const float *vector, int k, int filtered, const uint64_t *allow_ids,
+                          uint64_t n_allow, uint64_t *out_ids, float *out_dists, int32_t *out_n);
 int wv_batcher_stats(wv_batcher *b, uint64_t *requests, uint64_t *batches);
 int wv_batcher_destroy(wv_batcher *b);
 

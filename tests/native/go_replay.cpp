@@ -147,6 +147,9 @@ int main(int argc, char** argv) {
                 if (wv_index_add(ix, &id, v.data(), 1)) violation(std::string("add: ") + wv_last_error());
             }
             n_added.store(a + 1, std::memory_order_release);
+            // an import's pace (a few thousand objects per second), so the
+            // searchers overlap every phase of the writer
+            std::this_thread::sleep_for(std::chrono::microseconds(400));
             // interleave deletes: ~3 per 2 adds
             for (int r = 0; r < 3 && a % 2 == 0 && d < N_DELETE; ++r, ++d) {
                 uint64_t del = deleted_log[d];

@@ -389,10 +389,34 @@ def test_batcher_concurrent_single_queries_equal_direct_calls():
     for t in th:
         t.join(120)
     st = b.stats()
+    # the AllowList as ascending ids (wv_batcher_search_ids): per-query lists,
+    # and one list shared by every caller (sent once per batch), from 8
+    # threads against the two workers
+    shared = np.nonzero(rng.random(n) < 0.2)[0].astype(np.uint64)
+    want_sh = [ix.search_by_vector(qs[i], 10, allow=W.AllowList.from_ids(shared, n)) for i in range(len(qs))]
+    got_ids, got_sh = [None] * len(qs), [None] * len(qs)
+
+    def worker_ids(t):
+        for i in range(t, len(qs), 8):
+            a = allows[i]
+            got_ids[i] = b.search_ids(qs[i], ks[i], None if a is None else np.nonzero(
+                np.unpackbits(a.words.view(np.uint8), bitorder="little")[:n])[0].astype(np.uint64))
+            got_sh[i] = b.search_ids(qs[i], 10, shared)
+
+    th = [threading.Thread(target=worker_ids, args=(t,)) for t in range(8)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    # an empty list allows nothing
+    e_ids, e_d = b.search_ids(qs[0], 10, np.zeros(0, np.uint64))
     b.close()
     ix.close()
     for i in range(len(qs)):
         _same(got[i][0], got[i][1], want[i][0], want[i][1])
+        _same(got_ids[i][0], got_ids[i][1], want[i][0], want[i][1])
+        _same(got_sh[i][0], got_sh[i][1], want_sh[i][0], want_sh[i][1])
+    assert len(e_ids) == 0
     assert st["requests"] == len(qs) and st["batches"] < len(qs), st
 
 

@@ -13,6 +13,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <condition_variable>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -101,10 +102,16 @@ struct DevBuf {
     size_t cap = 0;
     hipError_t ensure(size_t bytes) {
         if (bytes <= cap) return hipSuccess;
-        if (p) (void)hipFree(p);
+        // batches may still be queued that read the old buffer (several in
+        // flight on the index's stream, wv_search_batch): drain the device
+        // before it goes
+        size_t want = std::max<size_t>(bytes, 256);
+        // scratch that grows with the batch: geometric steps (bounded), so a
+        // stream of growing batches does not reallocate -- and drain -- each time
+        if (cap) want = std::max(want, std::min(cap + cap / 2, bytes + ((size_t)256 << 20)));
+        if (p) { (void)hipDeviceSynchronize(); (void)hipFree(p); }
         p = nullptr;
         cap = 0;
-        size_t want = std::max<size_t>(bytes, 256);
         hipError_t e = hipMalloc(&p, want);
         if (e == hipSuccess) cap = want;
         return e;
@@ -310,6 +317,20 @@ struct wv_index {
     // brute-force workgroups per launch: a whole number of resident waves of
     // workgroups (CUs x 2 per CU x WV_BF_ROUNDS)
     int bf_blocks = 512;
+    // host staging of wv_search_batch: pinned slots, so a batch's copies are
+    // asynchronous and the index mutex is released before the caller waits --
+    // the next batch (another batcher worker) is staged and queued while this
+    // one runs, and the GPU does not idle between batches
+    struct HostSlot {
+        void* pin = nullptr;
+        size_t cap = 0;
+        hipEvent_t done = nullptr;
+        bool busy = false;
+    };
+    std::mutex slot_mu;
+    std::condition_variable slot_cv;
+    std::array<HostSlot, 3> slots;
+    DevBuf allow_keep;   // per-query allow lists of an AUTO batch (the dispatch gathers into g_allow)
 };
 
 namespace {
@@ -1423,6 +1444,11 @@ int wv_index_destroy(wv_index* ix) {
                       &ix->fbd_nf, &ix->fbd_over, &ix->fbd_cd, &ix->fbd_ci, &ix->fbd_cn, &ix->fbd_scr})
         b->release();
     if (ix->stream) (void)hipStreamSynchronize(ix->stream);
+    ix->allow_keep.release();
+    for (auto& sl : ix->slots) {
+        if (sl.pin) (void)hipHostFree(sl.pin);
+        if (sl.done) (void)hipEventDestroy(sl.done);
+    }
     for (auto& set : ix->ev_pool)
         for (auto e : set)
             if (e) (void)hipEventDestroy(e);
@@ -2133,46 +2159,90 @@ int wv_index_set_compressed(wv_index* ix, int on) {
 int wv_search_time_ef(const wv_index* ix, int k) { return ix ? search_time_ef(ix->cfg, k) : -1; }
 int wv_config_search_time_ef(const wv_config* cfg, int k) { return cfg ? search_time_ef(*cfg, k) : -1; }
 
+namespace {
+// one pinned staging slot of wv_search_batch, returned when the call ends
+struct SlotLease {
+    wv_index* ix;
+    wv_index::HostSlot* sl = nullptr;
+    explicit SlotLease(wv_index* x) : ix(x) {
+        std::unique_lock<std::mutex> l(ix->slot_mu);
+        ix->slot_cv.wait(l, [&] {
+            for (auto& c : ix->slots)
+                if (!c.busy) return true;
+            return false;
+        });
+        for (auto& c : ix->slots)
+            if (!c.busy) { sl = &c; break; }
+        sl->busy = true;
+    }
+    ~SlotLease() {
+        std::lock_guard<std::mutex> l(ix->slot_mu);
+        sl->busy = false;
+        ix->slot_cv.notify_one();
+    }
+};
+}  // namespace
+
 int wv_search_batch(wv_index* ix, const float* queries, int nq, int k, int ef, const uint64_t* allow_bits,
                     uint64_t allow_nbits, uint64_t allow_stride_words, int mode, uint64_t* out_ids, float* out_dists,
                     int32_t* out_n) {
     if (check(ix) || nq < 0 || k <= 0 || (nq && (!queries || !out_ids || !out_dists || !out_n)))
         return fail(WV_EINVAL, "wv_search_batch: bad argument");
     if (nq == 0) return WV_OK;
-    std::lock_guard<std::mutex> g(ix->mu);
+    const uint64_t words = (allow_nbits + 63) / 64;
+    const uint64_t arows = allow_bits ? (allow_stride_words ? (uint64_t)nq : 1) : 0;
+    const uint64_t astride = allow_stride_words ? allow_stride_words : words;
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t qb = (size_t)nq * ix->dim * 4, ab = arows * astride * 8, ib = (size_t)nq * k * 8,
+                 db = (size_t)nq * k * 4, nb = (size_t)nq * 4;
+    const size_t o_a = al(qb), o_i = o_a + al(ab), o_d = o_i + al(ib), o_n = o_d + al(db), need = o_n + al(nb);
     HIP_TRY(hipSetDevice(ix->cfg.device));
-    hipStream_t s = ix->stream;
-    const float* dq = nullptr;
-    int rc = stage_queries(ix, queries, nq, &dq, s);
-    if (rc) return rc;
-    const uint64_t* dallow = nullptr;
-    if (allow_bits) {
-        const uint64_t words = (allow_nbits + 63) / 64;
-        const uint64_t rows = allow_stride_words ? (uint64_t)nq : 1;
-        const uint64_t stride = allow_stride_words ? allow_stride_words : words;
-        HIP_TRY(ix->g_allow.ensure(rows * stride * 8));
-        HIP_TRY(hipMemcpyAsync(ix->g_allow.p, allow_bits, rows * stride * 8, hipMemcpyHostToDevice, s));
-        dallow = ix->g_allow.as<uint64_t>();
+    SlotLease lease(ix);
+    wv_index::HostSlot& sl = *lease.sl;
+    if (sl.cap < need) {
+        if (sl.pin) HIP_TRY(hipHostFree(sl.pin));
+        sl.pin = nullptr;
+        sl.cap = 0;
+        const size_t want = std::max<size_t>(need + need / 4, 1 << 20);
+        HIP_TRY(hipHostMalloc(&sl.pin, want, hipHostMallocDefault));
+        sl.cap = want;
     }
-    HIP_TRY(ix->out_ids.ensure((size_t)nq * k * 8));
-    HIP_TRY(ix->out_d.ensure((size_t)nq * k * 4));
-    HIP_TRY(ix->out_n.ensure((size_t)nq * 4));
-    // an AUTO batch with per-query allow lists gathers into g_allow: keep the
-    // caller's bitmaps in their own buffer
-    DevBuf allow_copy;
-    if (dallow && allow_stride_words && mode == WV_MODE_AUTO) {
-        HIP_TRY(allow_copy.ensure((size_t)nq * allow_stride_words * 8));
-        HIP_TRY(hipMemcpyAsync(allow_copy.p, dallow, (size_t)nq * allow_stride_words * 8, hipMemcpyDeviceToDevice, s));
-        dallow = allow_copy.as<uint64_t>();
+    if (!sl.done) HIP_TRY(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+    char* pin = static_cast<char*>(sl.pin);
+    std::memcpy(pin, queries, qb);
+    if (ab) std::memcpy(pin + o_a, allow_bits, ab);
+    {
+        std::lock_guard<std::mutex> g(ix->mu);
+        HIP_TRY(hipSetDevice(ix->cfg.device));
+        hipStream_t s = ix->stream;
+        const float* dq = nullptr;
+        int rc = stage_queries(ix, reinterpret_cast<const float*>(pin), nq, &dq, s);
+        if (rc) return rc;
+        const uint64_t* dallow = nullptr;
+        if (ab) {
+            // an AUTO batch with per-query allow lists gathers into g_allow:
+            // keep the caller's bitmaps in their own buffer then
+            DevBuf& dst = allow_stride_words && mode == WV_MODE_AUTO ? ix->allow_keep : ix->g_allow;
+            HIP_TRY(dst.ensure(ab));
+            HIP_TRY(hipMemcpyAsync(dst.p, pin + o_a, ab, hipMemcpyHostToDevice, s));
+            dallow = dst.as<uint64_t>();
+        }
+        HIP_TRY(ix->out_ids.ensure(ib));
+        HIP_TRY(ix->out_d.ensure(db));
+        HIP_TRY(ix->out_n.ensure(nb));
+        rc = search_core(ix, dq, nq, k, ef, dallow, allow_nbits, allow_stride_words, mode, ix->out_ids.as<uint64_t>(),
+                         ix->out_d.as<float>(), ix->out_n.as<int32_t>(), s);
+        if (rc) return rc;
+        HIP_TRY(hipMemcpyAsync(pin + o_i, ix->out_ids.p, ib, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(pin + o_d, ix->out_d.p, db, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(pin + o_n, ix->out_n.p, nb, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipEventRecord(sl.done, s));
     }
-    rc = search_core(ix, dq, nq, k, ef, dallow, allow_nbits, allow_stride_words, mode, ix->out_ids.as<uint64_t>(),
-                     ix->out_d.as<float>(), ix->out_n.as<int32_t>(), s);
-    if (rc) { allow_copy.release(); return rc; }
-    HIP_TRY(hipMemcpyAsync(out_ids, ix->out_ids.p, (size_t)nq * k * 8, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(out_dists, ix->out_d.p, (size_t)nq * k * 4, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(out_n, ix->out_n.p, (size_t)nq * 4, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    allow_copy.release();
+    // the index is free for the next batch while this one finishes
+    HIP_TRY(hipEventSynchronize(sl.done));
+    std::memcpy(out_ids, pin + o_i, ib);
+    std::memcpy(out_dists, pin + o_d, db);
+    std::memcpy(out_n, pin + o_n, nb);
     return WV_OK;
 }
 

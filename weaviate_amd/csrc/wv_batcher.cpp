@@ -13,7 +13,14 @@
 // Requests are grouped by (k, filtered): searchTimeEF depends on k
 // (search.go:30-62), and a filtered group carries one allow bitmap per query
 // (allow_stride_words), so the AUTO dispatch of search.go:64-79 (flat vs HNSW
-// by allowList.Len()) is still decided per query inside the batch.
+// by allowList.Len()) is still decided per query inside the batch.  An allow
+// list crosses as a bitmap or as ascending ids (the AllowList's Slice(),
+// helpers/allow_list.go:19-118), written straight into the batch's row; a
+// group whose requests all carry the same list sends it once (shared).
+//
+// Two workers take batches off the queue: while one batch runs on the GPU
+// (wv_search_batch releases the index before it waits), the other coalesces
+// and queues the next, so the device does not idle between batches.
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
@@ -33,8 +40,11 @@ namespace {
 struct Request {
     const float* q;
     int k;
-    const uint64_t* allow;
+    const uint64_t* allow;        // bitmap, or
     uint64_t allow_nbits;
+    const uint64_t* allow_ids;    // ascending ids (filtered with either)
+    uint64_t n_ids = 0;
+    bool filtered = false;
     uint64_t* out_ids;
     float* out_d;
     int32_t* out_n;
@@ -55,27 +65,48 @@ struct wv_batcher {
     std::condition_variable cv_work, cv_done;
     std::deque<Request*> queue;
     bool stop = false;
-    std::thread th;
+    std::vector<std::thread> th;   // the workers
     uint64_t n_requests = 0, n_batches = 0, n_launch_rows = 0;
+
+    static uint64_t nbits_of(const Request* r) {
+        if (r->allow) return r->allow_nbits;
+        return r->n_ids ? r->allow_ids[r->n_ids - 1] + 1 : 0;
+    }
+    static bool same_list(const Request* a, const Request* b) {
+        if (a->allow || b->allow)
+            return a->allow && b->allow && a->allow_nbits == b->allow_nbits &&
+                   (a->allow == b->allow || std::memcmp(a->allow, b->allow, (a->allow_nbits + 63) / 64 * 8) == 0);
+        return a->n_ids == b->n_ids &&
+               (a->allow_ids == b->allow_ids || std::memcmp(a->allow_ids, b->allow_ids, a->n_ids * 8) == 0);
+    }
+    static void write_row(const Request* r, uint64_t* row) {
+        if (r->allow) {
+            const uint64_t w = (r->allow_nbits + 63) / 64;
+            std::memcpy(row, r->allow, w * 8);
+            if (r->allow_nbits & 63)   // bits past a request's own nbits are not allowed
+                row[w - 1] &= (1ull << (r->allow_nbits & 63)) - 1;
+        } else {
+            for (uint64_t i = 0; i < r->n_ids; ++i) row[r->allow_ids[i] >> 6] |= 1ull << (r->allow_ids[i] & 63);
+        }
+    }
 
     void run_group(std::vector<Request*>& g) {
         const int n = (int)g.size();
         const int k = g[0]->k;
-        const bool filtered = g[0]->allow != nullptr;
+        const bool filtered = g[0]->filtered;
         std::vector<float> q((size_t)n * dim);
         for (int i = 0; i < n; ++i) std::memcpy(q.data() + (size_t)i * dim, g[i]->q, sizeof(float) * dim);
         std::vector<uint64_t> bits;
         uint64_t nbits = 0, stride = 0;
         if (filtered) {
-            for (Request* r : g) nbits = std::max(nbits, r->allow_nbits);
-            stride = (nbits + 63) / 64;
-            bits.assign((size_t)n * std::max<uint64_t>(stride, 1), 0);
-            for (int i = 0; i < n; ++i) {
-                const uint64_t w = (g[i]->allow_nbits + 63) / 64;
-                std::memcpy(bits.data() + (size_t)i * stride, g[i]->allow, w * 8);
-                if (g[i]->allow_nbits & 63)   // bits past a request's own nbits are not allowed
-                    bits[(size_t)i * stride + w - 1] &= (1ull << (g[i]->allow_nbits & 63)) - 1;
-            }
+            bool shared = true;
+            for (int i = 1; i < n && shared; ++i) shared = same_list(g[0], g[i]);
+            for (Request* r : g) nbits = std::max(nbits, nbits_of(r));
+            nbits = std::max<uint64_t>(nbits, 1);   // (an empty list allows nothing)
+            const uint64_t words = (nbits + 63) / 64;
+            stride = shared ? 0 : words;
+            bits.assign((size_t)(shared ? 1 : n) * words, 0);
+            for (int i = 0; i < (shared ? 1 : n); ++i) write_row(g[i], bits.data() + (size_t)i * words);
         }
         std::vector<uint64_t> ids((size_t)n * k);
         std::vector<float> ds((size_t)n * k);
@@ -124,8 +155,7 @@ struct wv_batcher {
                 if (used[i]) continue;
                 std::vector<Request*> g;
                 for (size_t j = i; j < take.size(); ++j) {
-                    if (used[j] || take[j]->k != take[i]->k ||
-                        (take[j]->allow != nullptr) != (take[i]->allow != nullptr))
+                    if (used[j] || take[j]->k != take[i]->k || take[j]->filtered != take[i]->filtered)
                         continue;
                     used[j] = true;
                     g.push_back(take[j]);
@@ -150,7 +180,7 @@ static int create_batcher(wv_index* ix, wv_group* grp, int dim, int max_batch, i
     b->dim = dim;
     b->max_batch = max_batch;
     b->max_wait_us = max_wait_us;
-    b->th = std::thread([b] { b->loop(); });
+    for (int w = 0; w < 2; ++w) b->th.emplace_back([b] { b->loop(); });
     *out = b;
     return WV_OK;
 }
@@ -163,20 +193,7 @@ int wv_batcher_create_group(wv_group* g, int dim, int max_batch, int max_wait_us
     return create_batcher(nullptr, g, dim, max_batch, max_wait_us, out);
 }
 
-int wv_batcher_search(wv_batcher* b, const float* vector, int k, const uint64_t* allow_bits, uint64_t allow_nbits,
-                      uint64_t* out_ids, float* out_dists, int32_t* out_n) {
-    if (!b || !vector || k <= 0 || !out_ids || !out_dists || !out_n) {
-        wv_internal_set_error("wv_batcher_search: bad argument");
-        return WV_EINVAL;
-    }
-    Request r;
-    r.q = vector;
-    r.k = k;
-    r.allow = allow_bits;
-    r.allow_nbits = allow_bits ? allow_nbits : 0;
-    r.out_ids = out_ids;
-    r.out_d = out_dists;
-    r.out_n = out_n;
+static int submit(wv_batcher* b, Request& r) {
     {
         std::unique_lock<std::mutex> l(b->mu);
         if (b->stop) {
@@ -190,6 +207,50 @@ int wv_batcher_search(wv_batcher* b, const float* vector, int k, const uint64_t*
     }
     if (r.rc) wv_internal_set_error(r.err.c_str());
     return r.rc;
+}
+
+int wv_batcher_search(wv_batcher* b, const float* vector, int k, const uint64_t* allow_bits, uint64_t allow_nbits,
+                      uint64_t* out_ids, float* out_dists, int32_t* out_n) {
+    if (!b || !vector || k <= 0 || !out_ids || !out_dists || !out_n) {
+        wv_internal_set_error("wv_batcher_search: bad argument");
+        return WV_EINVAL;
+    }
+    Request r;
+    r.q = vector;
+    r.k = k;
+    r.allow = allow_bits;
+    r.allow_nbits = allow_bits ? allow_nbits : 0;
+    r.allow_ids = nullptr;
+    r.filtered = allow_bits != nullptr;
+    r.out_ids = out_ids;
+    r.out_d = out_dists;
+    r.out_n = out_n;
+    return submit(b, r);
+}
+
+int wv_batcher_search_ids(wv_batcher* b, const float* vector, int k, int filtered, const uint64_t* allow_ids,
+                          uint64_t n_allow, uint64_t* out_ids, float* out_dists, int32_t* out_n) {
+    if (!b || !vector || k <= 0 || !out_ids || !out_dists || !out_n || (n_allow && !allow_ids)) {
+        wv_internal_set_error("wv_batcher_search_ids: bad argument");
+        return WV_EINVAL;
+    }
+    for (uint64_t i = 1; i < n_allow; ++i)
+        if (allow_ids[i] <= allow_ids[i - 1]) {
+            wv_internal_set_error("wv_batcher_search_ids: allow ids must be strictly ascending");
+            return WV_EINVAL;
+        }
+    Request r;
+    r.q = vector;
+    r.k = k;
+    r.allow = nullptr;
+    r.allow_nbits = 0;
+    r.allow_ids = allow_ids;
+    r.n_ids = filtered ? n_allow : 0;
+    r.filtered = filtered != 0;
+    r.out_ids = out_ids;
+    r.out_d = out_dists;
+    r.out_n = out_n;
+    return submit(b, r);
 }
 
 int wv_batcher_stats(wv_batcher* b, uint64_t* requests, uint64_t* batches) {
@@ -207,7 +268,7 @@ int wv_batcher_destroy(wv_batcher* b) {
         b->stop = true;
     }
     b->cv_work.notify_all();
-    if (b->th.joinable()) b->th.join();   // drains the queue before it exits
+    for (auto& t : b->th) t.join();   // the workers drain the queue before they exit
     delete b;
     return WV_OK;
 }

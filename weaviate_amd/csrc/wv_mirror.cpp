@@ -390,10 +390,10 @@ int wv_mirror_search(wv_mirror* m, const float* vector, int len, int k, int filt
     if (!m->live) return err(WV_ESTALE, "wv_mirror: stale");
     if (!m->ix) { *out_n = 0; return WV_OK; }   // empty index (search.go:463-465)
     if (len != m->dim) return err(WV_ESTALE, "wv_mirror_search: vector length differs from the index's");
-    thread_local std::vector<uint64_t> bits;
-    uint64_t nbits = 0;
-    if (filtered) allow_bitmap(allow_ids, n_allow, m->capacity, bits, nbits);
-    return wv_batcher_search(m->b, vector, k, filtered ? bits.data() : nullptr, nbits, out_ids, out_dists, out_n);
+    // ids past the capacity hold no row: the list is cut there (ascending)
+    const uint64_t cap = m->capacity;
+    while (n_allow && allow_ids[n_allow - 1] >= cap) --n_allow;
+    return wv_batcher_search_ids(m->b, vector, k, filtered, allow_ids, n_allow, out_ids, out_dists, out_n);
 }
 
 int wv_mirror_search_by_distance(wv_mirror* m, const float* vector, int len, float target_distance,

@@ -507,6 +507,20 @@ class Batcher:
         check(lib().wv_batcher_search(self._h, _ptr(q), k, _ptr(bits), nb, _ptr(ids), _ptr(ds), _ptr(n)))
         return ids[: n[0]], ds[: n[0]]
 
+    def search_ids(self, vector, k: int, allow_ids=None):
+        """The same with the AllowList as ascending ids (wv_batcher_search_ids);
+        allow_ids None = no filter."""
+        q = np.ascontiguousarray(vector, dtype=np.float32)
+        if q.size != self.index.dim:
+            raise WvError(1, f"vector lengths don't match: {q.size} vs {self.index.dim}")
+        a = np.ascontiguousarray(np.zeros(0, np.uint64) if allow_ids is None else allow_ids, dtype=np.uint64)
+        ids = np.zeros(k, np.uint64)
+        ds = np.zeros(k, np.float32)
+        n = np.zeros(1, np.int32)
+        check(lib().wv_batcher_search_ids(self._h, _ptr(q), k, int(allow_ids is not None), _ptr(a), len(a), _ptr(ids),
+                                          _ptr(ds), _ptr(n)))
+        return ids[: n[0]], ds[: n[0]]
+
     def stats(self):
         a, b = C.c_uint64(), C.c_uint64()
         check(lib().wv_batcher_stats(self._h, C.byref(a), C.byref(b)))
