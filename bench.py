@@ -707,6 +707,29 @@ def run_hnsw(args, ctx, W, with_cpu):
                                "kind": "port", "value_t1": round(n1 / t1, 1), "cores_t1": 1,
                                "sample": f"all {NQ} queries x {reps} passes (T={args.cpu_threads}), {n1} queries "
                                          f"(T=1); knnSearchByVector restated in C on the same graph (oracle/)"}
+        if args.seq_build:
+            # north_star: recall within 0.5 pt of the reference index -- whose
+            # graph is built by inserting one node at a time (insert.go:103-217,
+            # here the restatement's concurrent build) -- on identical data and ef
+            del ref
+            t0 = time.time()
+            seq = O.Index(D, args.metric, args.M, args.efc, capacity=N, seed=1)
+            seq.add_batch(base, threads=args.hnsw_build_threads)
+            build_s = time.time() - t0
+            si = seq.search_batch(queries, K, args.ef, threads=args.cpu_threads)[0]
+            ix.upload_graph(seq.export_graph())
+            del seq
+            ix.search_batch_device(qt.data_ptr(), NQ, K, out_ids.data_ptr(), out_d.data_ptr(), out_n.data_ptr(),
+                                   ef=args.ef, mode="hnsw", stream=ctx.stream)
+            torch.cuda.synchronize(ctx.dev)
+            gs = out_ids.cpu().numpy().view(np.uint64)
+            r_seq = float(np.mean([len(set(a) & set(b)) / K for a, b in zip(si.tolist(), truth.tolist())]))
+            r_gs = float(np.mean([len(set(a) & set(b)) / K for a, b in zip(gs.tolist(), truth.tolist())]))
+            res["sequential_build"] = {
+                "recall@10_restatement_on_sequential_graph": round(r_seq, 4),
+                "recall@10_gpu_on_sequential_graph": round(r_gs, 4), "recall@10_gpu_built_graph": round(rec, 4),
+                "delta_pt_gpu_built_vs_sequential": round(100 * (rec - r_seq), 2),
+                "sequential_build_s": round(build_s, 1), "threads": args.hnsw_build_threads}
     ix.close()
     return res
 
@@ -843,6 +866,9 @@ def main():
                     help="skip the configs[0] hnsw line that the exact workload reports beside its value")
     ap.add_argument("--no-corpus-leg", action="store_true",
                     help="N>1 exact: skip the corpus-sharded (RCCL merge) leg reported beside the query split")
+    ap.add_argument("--seq-build", action="store_true",
+                    help="hnsw at N=1: also build the restatement's insert-by-insert graph and report its recall "
+                         "beside the GPU-built graph's (north_star's 0.5-pt criterion; ~40 s of CPU at 1M)")
     ap.add_argument("--no-c3-line", action="store_true",
                     help="skip the configs[2] GloVe-shaped hnsw ef-sweep line reported beside the default value")
     ap.add_argument("--hnsw-build-threads", type=int, default=16)
@@ -902,7 +928,7 @@ def main():
                              "k": args.k, "metric": args.metric, "mode": "hnsw", "split": args.split,
                              "parallelism": h["parallelism"]},
                   "recall@10": h["recall@10"], "graph": h["graph"], "roofline": h["roofline"]}
-        for key in ("parity_sample", "cpu_baseline", "ef_sweep", "concurrent_callers"):
+        for key in ("parity_sample", "cpu_baseline", "ef_sweep", "concurrent_callers", "sequential_build"):
             if key in h:
                 result[key] = h[key]
     else:

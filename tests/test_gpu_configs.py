@@ -45,6 +45,35 @@ def _unexplained(ref, qs, k, ef, gi, gd, oi, od):
     return bad
 
 
+def test_configs0_gpu_built_graph_recall_vs_sequential_build():
+    """north_star: HNSW recall@10 within 0.5 pt of the *reference* index on
+    identical data and ef -- the reference builds its graph by inserting one
+    node at a time (insert.go:103-217), here the restatement's build; the GPU
+    serves a graph it built itself in batches (wv_index_build_graph).  At
+    configs[0]'s parameters (SIFT-shaped 128-d, M=64, efConstruction=128,
+    ef=64), scaled to 100k rows; bench.py --seq-build reports the same at 1M."""
+    n, d, nq, k, ef = 100_000, 128, 1000, 10, 64
+    base = counter_sift(1, 0, n, d)
+    qs = counter_sift(2, 0, nq, d)
+    truth, _, _ = O.flat_scan(O.L2, base, qs, k, threads=THREADS)
+    ix = W.GPUVectorIndex(d, "l2-squared", capacity=n, max_connections=64)
+    ix.upload_vectors(base)
+    ix.build_graph(ef_construction=128, seed=1, batch_div=64)
+    gi, gd, gn = ix.search_batch(qs, k, ef=ef, mode="hnsw")
+    ref = O.Index(d, "l2-squared", 64, 128, capacity=n, seed=1)
+    ref.add_batch(base, threads=THREADS)
+    oi, od, on, _ = ref.search_batch(qs, k, ef, threads=THREADS)
+    r_gpu, r_ref = recall(gi, truth), recall(oi, truth)
+    # and the GPU searching the restatement's own graph answers as the restatement does
+    ix.upload_graph(ref.export_graph())
+    si, sd, sn = ix.search_batch(qs, k, ef=ef, mode="hnsw")
+    ix.close()
+    print(f"recall@10 GPU-built {r_gpu:.4f}, sequential build {r_ref:.4f}, GPU on the sequential graph "
+          f"{recall(si, truth):.4f}")
+    assert abs(r_gpu - r_ref) <= 0.005, (r_gpu, r_ref)
+    assert abs(recall(si, truth) - r_ref) <= 0.001
+
+
 def test_configs0_sift_hnsw_m64_efc128_ef64():
     """configs[0]: maxConnections=64 -> layer-0 lists of up to 128 ids, two per
     lane of the neighbour batch; recall within 0.5 pt of the restatement."""
