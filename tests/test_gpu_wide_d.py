@@ -72,3 +72,28 @@ def test_wide_d_allow_list_tombstones_and_large_k():
     for k in (64, 200):
         _check(ix, base, qs, k, O.DOT, tomb=tomb)
     ix.close()
+
+
+@pytest.mark.parametrize("d,metric", [(768, O.DOT), (128, O.L2), (100, O.COSINE)])
+def test_gathered_allow_list_pass_equals_restatement(d, metric):
+    """A shared allow list keeping under half the corpus: the f16 key pass
+    runs over an image of just the allowed rows (gathered on the device, ids
+    mapped back through the ascending row list before the re-rank) --
+    flatSearch's walk over the allow list (flat_search.go:25-58) at the f16
+    rate (configs[3]'s 1 / 10 % legs).  Bit-identical to the restatement, with
+    tombstones inside the list, k up to 200, a list that ends inside a tile."""
+    n = 50_001
+    base, qs = _gauss(n, d, 7), _gauss(400, d, 8)
+    ix = W.GPUVectorIndex(d, NAMES[metric], capacity=n)
+    ix.upload_vectors(base)
+    rng = np.random.default_rng(9)
+    dead = rng.choice(n, 1500, replace=False)
+    ix.add_tombstones(dead)
+    tomb = O.bits_from_ids(dead, n)
+    for frac in (0.01, 0.1, 0.4):
+        ids_a = np.nonzero(rng.random(n) < frac)[0]
+        al = W.AllowList.from_ids(ids_a, n)
+        for k in ((10, 64) if frac != 0.01 else (10, 200)):
+            st = _check(ix, base, qs, k, metric, allow_bits=al.words, allow=al, tomb=tomb)
+            assert st["fallbacks"] <= len(qs) // 50, (frac, k, st)
+    ix.close()

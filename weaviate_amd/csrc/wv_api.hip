@@ -52,6 +52,11 @@ hipError_t wv_launch_split_rows(const float* in, int ld_in, const uint64_t* ids,
 hipError_t wv_launch_h16_rows(const float* in, int ld_in, const uint64_t* ids, uint64_t n, int D, int ns, float sign,
                               float scale, const unsigned int* scale_from_max, void* out, uint64_t out_row0,
                               unsigned int* res_max_bits, float* res_out, int quad, hipStream_t s);
+hipError_t wv_launch_h16_rows_gather(const float* in, int ld_in, const uint32_t* gather, uint64_t n, int D, int ns,
+                                     float scale, void* out, hipStream_t s);
+hipError_t wv_launch_h16_compact_aux(const float* xnorm, const uint32_t* rowidx, uint64_t n, float* cxnorm,
+                                     uint64_t* excl, uint64_t excl_words, hipStream_t s);
+hipError_t wv_launch_remap_ids(uint32_t* ids, uint64_t n, const uint32_t* rowidx, hipStream_t s);
 hipError_t wv_launch_absmax(const float* in, int ld, uint64_t n, int D, unsigned int* max_bits, hipStream_t s);
 hipError_t wv_launch_h16_qscale(const float* part, int nparts, unsigned int* max_bits, float bsign, float* qscale,
                                 hipStream_t s);
@@ -331,6 +336,9 @@ struct wv_index {
     std::condition_variable slot_cv;
     std::array<HostSlot, 3> slots;
     DevBuf allow_keep;   // per-query allow lists of an AUTO batch (the dispatch gathers into g_allow)
+    // f16 key pass over a compacted shared allow list: the rows' image,
+    // their |x|^2 and the scan's exclusion bits (the last tile's padding)
+    DevBuf cimg16, cxnorm, cexcl;
 };
 
 namespace {
@@ -505,8 +513,13 @@ int run_pq_flat(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d
 // H_SAMPLE-th tile (its finalize yields per-query thresholds), the main pass
 // seeded with them, and the certifying finalize.  Appends uncertified queries
 // to `fails` (read back from the device).
+// rowidx (nullable): the ascending row list of a compacted shared allow list
+// (compact_allowed) -- the pass then runs over an f16 image of just those N
+// rows (gathered here) and the candidate ids are mapped back to rows before
+// the finalize; d_allow is then already applied
 int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_allow, uint64_t allow_nbits, uint64_t N,
-            uint64_t* d_out_ids, float* d_out_d, int32_t* d_out_n, hipStream_t s, std::vector<int32_t>& fails) {
+            uint64_t* d_out_ids, float* d_out_d, int32_t* d_out_n, hipStream_t s, std::vector<int32_t>& fails,
+            const uint32_t* rowidx = nullptr) {
     const int ns = ix->h16_ns;
     const bool wd = ix->h16_wide;   // D > 128: the wide-D kernel
     // the 16x16x32 kernel (one 16-entry list per column and slot) for k <=
@@ -514,8 +527,8 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     // k <= FIN_KF: the one-wave-per-SIMD 16x16x32 kernel (h16_solo) or the
     // opt-in two-waves-per-SIMD one (h16_quad) -- one 16-entry list per
     // column and slot; wider k on the 32x32x16 kernel
-    const bool solo = ix->h16_solo && k <= wv::FIN_KF;
-    const bool quad = (ix->h16_quad || solo) && k <= wv::FIN_KF;
+    const bool solo = ix->h16_solo && k <= wv::FIN_KF && !rowidx;
+    const bool quad = (ix->h16_quad || solo) && k <= wv::FIN_KF && !rowidx;   // (a gathered image: h16_index)
     // D <= 128: 8-wave (512-query) workgroups, one per CU; WV_H16_WAVES=4:
     // 4-wave (256-query) workgroups, two independent ones per CU; solo: one
     // 4-wave 512-query workgroup per CU
@@ -556,14 +569,35 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
                                  ix->qscale.as<float>(), s));
     HIP_TRY(wv_launch_h16_rows(d_q, ix->dpad, nullptr, nq, ix->dim, ns, bsign, 1.f, ix->qmax.as<unsigned int>(),
                                ix->qimg16.p, 0, nullptr, ix->qres.as<float>(), quad, s));
+    const void* ximg = quad ? ix->ximg16q.p : ix->ximg16.p;
+    const float* xnorm = ix->xnorm.as<float>();
+    const uint64_t* excl = ix->excl.as<uint64_t>();
+    if (rowidx) {
+        // the allowed rows' image in list order (whole tiles, zero padded),
+        // their |x|^2, and exclusion bits set only past N
+        const uint64_t rows = ntl * tile_rows, ew = rows / 64 + 2;
+        const size_t ib = rows * (size_t)ns * 16 * 2;
+        HIP_TRY(ix->cimg16.ensure(ib));
+        HIP_TRY(ix->cxnorm.ensure(rows * 4));
+        HIP_TRY(ix->cexcl.ensure(ew * 8));
+        HIP_TRY(hipMemsetAsync(ix->cimg16.p, 0, ib, s));
+        HIP_TRY(hipMemsetAsync(ix->cxnorm.p, 0, rows * 4, s));
+        HIP_TRY(wv_launch_h16_rows_gather(ix->vecs.as<float>(), ix->ldx, rowidx, N, ix->dim, ns, ix->h16_sx,
+                                          ix->cimg16.p, s));
+        HIP_TRY(wv_launch_h16_compact_aux(ix->xnorm.as<float>(), rowidx, N, ix->cxnorm.as<float>(),
+                                          ix->cexcl.as<uint64_t>(), ew, s));
+        ximg = ix->cimg16.p;
+        xnorm = ix->cxnorm.as<float>();
+        excl = ix->cexcl.as<uint64_t>();
+        allow = nullptr;
+    }
     if (ix->metric == WV_L2_SQUARED)
-        HIP_TRY(wv_launch_h16_xns(ix->xnorm.as<float>(), ntl * tile_rows, ix->h16_sx, ix->qscale.as<float>(),
-                                  ix->xns.as<float>(), s));
+        HIP_TRY(wv_launch_h16_xns(xnorm, ntl * tile_rows, ix->h16_sx, ix->qscale.as<float>(), ix->xns.as<float>(), s));
     wv::H16Params hp{};
-    hp.X = quad ? ix->ximg16q.p : ix->ximg16.p;
+    hp.X = ximg;
     hp.Q = ix->qimg16.p;
     hp.xns = ix->xns.as<float>();
-    hp.excl = ix->excl.as<uint64_t>();
+    hp.excl = excl;
     hp.allow = allow;
     hp.qscale = ix->qscale.as<float>();
     hp.sx = ix->h16_sx;
@@ -571,6 +605,7 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     hp.nq = nq;
     hp.metric = ix->metric;
     hp.n_qblocks = nqb;
+    hp.stagger = std::getenv("WV_H16_STAGGER") && std::atoi(std::getenv("WV_H16_STAGGER")) == 1;
     hp.locality = 1;
     if (const char* e = std::getenv("WV_BF_LOCALITY")) hp.locality = std::atoi(e);
     wv::BfFinParams fp{};
@@ -695,6 +730,7 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
                : solo ? wv_launch_bf_h16s(&hp, ns / 2, 0, s)
                : (quad ? wv_launch_bf_h16q(&hp, ns / 2, 0, waves, s) : wv_launch_bf_h16(&hp, ns, 0, waves, s)));
     TREC(1);
+    if (rowidx) HIP_TRY(wv_launch_remap_ids(ix->cand_id.as<uint32_t>(), (uint64_t)nq * sch.n_slots * prod * kp, rowidx, s));
     fp.cand_d = ix->cand_d.as<float>();
     fp.cand_id = ix->cand_id.as<uint32_t>();
     fp.n_slots = sch.n_slots;
@@ -791,8 +827,19 @@ int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
                 HIP_TRY(hipMemsetAsync(d_out_n, 0, sizeof(int32_t) * nq, s));
                 return WV_OK;
             }
-            // the f16 pass scans the whole corpus ~6x faster than the fp32
-            // pass over a row list: compact only very selective lists then
+            // a list keeping under half the corpus: the scan runs over its
+            // rows -- on the f16 pass over their gathered image (h16_ok), else
+            // on the fp32 pass over the row list
+            const bool compact = (2 * n_ok < N && !std::getenv("WV_BF_NO_COMPACT")) || d_rowmask;
+            if (compact && h16_ok && !std::getenv("WV_BF_H16_NO_GATHER")) {
+                std::vector<int32_t> none;
+                int rc2 = run_h16(ix, d_q, nq, k, nullptr, 0, n_ok, d_out_ids, d_out_d, d_out_n, s, none,
+                                  ix->rowidx.as<uint32_t>());
+                if (rc2) return rc2;
+                return queue_fbd(ix, d_q, nq, k, d_allow, allow_nbits, allow_stride, d_out_ids, d_out_d, d_out_n, s);
+            }
+            // (WV_BF_H16_NO_GATHER: round 2's rule -- the f16 pass masks the
+            // whole corpus unless the list keeps under 1/8 of it)
             const uint64_t frac = ix->use_h16 && !allow_stride ? 8 : 2;
             if (((frac * n_ok < N && !std::getenv("WV_BF_NO_COMPACT")) || d_rowmask) && k <= wv::BF_FAST_KMAX) {
                 n_scan = n_ok;
@@ -1445,6 +1492,9 @@ int wv_index_destroy(wv_index* ix) {
         b->release();
     if (ix->stream) (void)hipStreamSynchronize(ix->stream);
     ix->allow_keep.release();
+    ix->cimg16.release();
+    ix->cxnorm.release();
+    ix->cexcl.release();
     for (auto& sl : ix->slots) {
         if (sl.pin) (void)hipHostFree(sl.pin);
         if (sl.done) (void)hipEventDestroy(sl.done);

@@ -40,9 +40,18 @@ namespace wv {
 // WAVES = 8: one 512-query workgroup per CU (two waves per SIMD, kept in
 // phase by the stage barrier); WAVES = 4: two independent 256-query
 // workgroups per CU (one wave per SIMD each), TPS tiles per LDS stage.
-template <int NS, bool L2, bool SEED, int WAVES, int TPS, bool XS = false>
+// STG: stagger (8 waves only) -- waves 4-7 (the second wave of every SIMD)
+// run half a tile behind waves 0-3, so that one wave's half-tile boundary
+// (accumulator restart, fragment reads) falls inside its partner's MFMA run
+// instead of beside the partner's own boundary (MI355X_MICROARCH 'Two waves
+// per SIMD' item 9).  The lagging waves meet each group's barrier half a tile
+// earlier in their stream (before the group's last A phase), which a 4-stage
+// ring allows: a fill overwrites the stage of group g - 2, never one a
+// lagging wave still reads.
+template <int NS, bool L2, bool SEED, int WAVES, int TPS, bool XS = false, bool STG = false>
 __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Params p) {
     constexpr int BQ = WAVES * 64;
+    constexpr int NSTG = STG ? 4 : H_STAGES;
     extern __shared__ uint4 lds[];
     using St = H16Stage<NS>;
     const int tid = threadIdx.x;
@@ -85,7 +94,7 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
 
     // the tiles of stage-group g (TPS consecutive tiles) into LDS stage g % 3
     auto fill_group = [&](uint64_t t_begin, int g, int ntile) {
-        const int st = g % H_STAGES;
+        const int st = g % NSTG;
         int n = 0;
 #pragma unroll
         for (int j = 0; j < TPS; ++j) {
@@ -94,7 +103,7 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
         }
         return n * n_ops;   // this wave's DMA ops for the group
     };
-    auto tile_lds = [&](int t) { return lds + ((t / TPS) % H_STAGES * TPS + t % TPS) * St::U4; };
+    auto tile_lds = [&](int t) { return lds + ((t / TPS) % NSTG * TPS + t % TPS) * St::U4; };
 
     for (uint64_t u = u_first; u < u_last;) {
         const int qb = (int)(u / p.ntiles);
@@ -348,6 +357,7 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
         };
         const int xs1 = ntile / 8, xs2 = ntile / 4, xs3 = ntile / 2, xs4 = (3 * ntile) / 4;
         const int ngroups = (ntile + TPS - 1) / TPS;
+        const bool lag = STG && wave >= 4;
         // (the previous segment ended with every stage read and every DMA landed)
         int ops_in_flight = 0;   // this wave's DMA ops of the newest group issued
         if (ngroups > 0) fill_group(t_begin, 0, ntile);
@@ -368,6 +378,11 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
 #endif
             const uint4* img = tile_lds(t);
             const uint32_t rb0 = (uint32_t)((t_begin + t) * (uint64_t)p.tile_stride * H_BN) + 4 * khalf;
+            const bool group_end = t % TPS == TPS - 1 || t == ntile - 1;
+            if (lag && group_end) {   // (staggered waves: the group's barrier, half a tile early)
+                if (g + 1 < ngroups) vm_wait(ops_in_flight);
+                block_barrier();
+            }
             // lanes l and l ^ 32 keep lists for the same query column (see the split pass)
             const bool mask_t = need_mask;
             const uint64_t mo0 = mask_t ? lane_ok(okw, jq0) : 0ull, mo1 = mask_t ? lane_ok(okw, jq1) : 0ull;
@@ -402,7 +417,7 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
             }
             // ---- C (last tile of a group): group g + 1 has landed (g + 2 may
             // stay in flight); every wave is done reading group g's stage ----
-            if (t % TPS == TPS - 1 || t == ntile - 1) {
+            if (!lag && group_end) {
                 if (g + 1 < ngroups) vm_wait(ops_in_flight);
                 block_barrier();
             }
@@ -445,6 +460,9 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
             }
         }
 
+        // (staggered: everyone past the segment's last reads before the next
+        // segment's fills)
+        if constexpr (STG) block_barrier();
         if constexpr (SEED) {
             if (jq0 < p.nq) p.out_d[((size_t)jq0 * p.n_slots + slot) * H_PROD + khalf] = l0d[0];
             if (jq1 < p.nq) p.out_d[((size_t)jq1 * p.n_slots + slot) * H_PROD + khalf] = l1d[0];
@@ -1095,14 +1113,19 @@ __device__ __forceinline__ float pow2_scale_for(float maxabs) {
     return ldexpf(1.f, e);
 }
 
-__global__ void wv_h16_rows_kernel(const float* in, int ld_in, const uint64_t* ids, uint64_t n, int D, int ns,
-                                   float sign, float scale, const unsigned int* scale_from_max, uint16_t* out,
-                                   uint64_t out_row0, unsigned int* res_max_bits, float* res_out, int quad) {
+__global__ void wv_h16_rows_kernel(const float* in, int ld_in, const uint64_t* ids, const uint32_t* gather,
+                                   uint64_t n, int D, int ns, float sign, float scale,
+                                   const unsigned int* scale_from_max, uint16_t* out, uint64_t out_row0,
+                                   unsigned int* res_max_bits, float* res_out, int quad) {
     const uint64_t r = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (r >= n) return;
     if (scale_from_max) scale = pow2_scale_for(__uint_as_float(*scale_from_max) * fabsf(sign));
-    const uint64_t row = ids ? ids[r] : r;
+    // ids: row ids[r] to image row ids[r] (row writes); gather: row gather[r]
+    // to image row r (a compacted allow list's rows, in list order)
+    const uint64_t src = gather ? gather[r] : ids ? ids[r] : r;
+    const uint64_t row = gather ? r : src;
+    in += (src - row) * (uint64_t)ld_in;
     const int kmax = ns * 16;
     float acc = 0.f;
     for (int k = lane; k < kmax; k += 64) {
@@ -1178,9 +1201,56 @@ hipError_t wv_launch_h16_rows(const float* in, int ld_in, const uint64_t* ids, u
     if (n == 0) return hipSuccess;
     // quad: 0 = h16_index, 1 = h16q_index (ns even)
     if (ns < 1 || ns > wv::HW_NS_MAX || D > ns * 16 || (quad && ns % 2)) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(wv::wv_h16_rows_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, in, ld_in, ids, n, D,
-                       ns, sign, scale, scale_from_max, static_cast<uint16_t*>(out), out_row0, res_max_bits, res_out,
-                       quad);
+    hipLaunchKernelGGL(wv::wv_h16_rows_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, in, ld_in, ids,
+                       (const uint32_t*)nullptr, n, D, ns, sign, scale, scale_from_max, static_cast<uint16_t*>(out),
+                       out_row0, res_max_bits, res_out, quad);
+    return hipGetLastError();
+}
+
+// the image of rows gather[0..n) (ascending row ids of a compacted allow
+// list) as image rows 0..n (h16_index layout)
+hipError_t wv_launch_h16_rows_gather(const float* in, int ld_in, const uint32_t* gather, uint64_t n, int D, int ns,
+                                     float scale, void* out, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    if (ns < 1 || ns > wv::HW_NS_MAX || D > ns * 16 || !gather) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(wv::wv_h16_rows_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, in, ld_in,
+                       (const uint64_t*)nullptr, gather, n, D, ns, 1.f, scale, (const unsigned int*)nullptr,
+                       static_cast<uint16_t*>(out), (uint64_t)0, (unsigned int*)nullptr, (float*)nullptr, 0);
+    return hipGetLastError();
+}
+
+__global__ void wv_gather_f32_kernel(const float* src, const uint32_t* idx, uint64_t n, float* dst) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = src[idx[i]];
+}
+
+// candidate lists of a key pass over compacted rows: list positions -> row ids
+// (the map is increasing, so every (key, id) order is unchanged)
+__global__ void wv_remap_ids_kernel(uint32_t* ids, uint64_t n, const uint32_t* rowidx) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && ids[i] != WV_NIL) ids[i] = rowidx[ids[i]];
+}
+
+// exclusion bits of a compacted scan: rows >= n (the last tile's padding)
+__global__ void wv_excl_tail_kernel(uint64_t* excl, uint64_t n, uint64_t words) {
+    const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= words) return;
+    const uint64_t lo = w * 64;
+    excl[w] = lo >= n ? ~0ull : (n - lo >= 64 ? 0ull : ~0ull << (n - lo));
+}
+
+hipError_t wv_launch_h16_compact_aux(const float* xnorm, const uint32_t* rowidx, uint64_t n, float* cxnorm,
+                                     uint64_t* excl, uint64_t excl_words, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(wv_gather_f32_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, xnorm, rowidx, n,
+                              cxnorm);
+    hipLaunchKernelGGL(wv_excl_tail_kernel, dim3((unsigned)((excl_words + 255) / 256)), dim3(256), 0, s, excl, n,
+                       excl_words);
+    return hipGetLastError();
+}
+
+hipError_t wv_launch_remap_ids(uint32_t* ids, uint64_t n, const uint32_t* rowidx, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(wv_remap_ids_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, ids, n, rowidx);
     return hipGetLastError();
 }
 
@@ -1215,9 +1285,14 @@ hipError_t wv_launch_bf_h16(const wv::H16Params* p, int ns, int seed, int waves,
     const bool l2 = p->metric == WV_METRIC_L2;
     if (l2 && !p->xns) return hipErrorInvalidValue;
     const int tps = waves == 8 ? wv::H_TPS8 : 1;
-    const size_t lds = (size_t)wv::H_STAGES * tps * (2 * ns * 64 + 17) * 16;
+    const bool stg = waves == 8 && p->stagger;
+    const size_t lds = (size_t)(stg ? 4 : wv::H_STAGES) * tps * (2 * ns * 64 + 17) * 16;
 #define WV_H16_GO(NS, L, S)                                                                                    \
-    if (waves == 8 && !S && p->xslot)                                                                          \
+    if (stg && !S && p->xslot)                                                                                 \
+        hipLaunchKernelGGL((wv::wv_bf_h16_kernel<NS, L, false, 8, wv::H_TPS8, true, true>), dim3(nb), dim3(512), lds, s, *p); \
+    else if (stg)                                                                                              \
+        hipLaunchKernelGGL((wv::wv_bf_h16_kernel<NS, L, S, 8, wv::H_TPS8, false, true>), dim3(nb), dim3(512), lds, s, *p); \
+    else if (waves == 8 && !S && p->xslot)                                                                     \
         hipLaunchKernelGGL((wv::wv_bf_h16_kernel<NS, L, false, 8, wv::H_TPS8, true>), dim3(nb), dim3(512), lds, s, *p); \
     else if (waves == 8) hipLaunchKernelGGL((wv::wv_bf_h16_kernel<NS, L, S, 8, wv::H_TPS8>), dim3(nb), dim3(512), lds, s, *p); \
     else hipLaunchKernelGGL((wv::wv_bf_h16_kernel<NS, L, S, 4, 1>), dim3(nb), dim3(256), lds, s, *p);

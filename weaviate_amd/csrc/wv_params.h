@@ -165,6 +165,7 @@ struct H16Params {
     // reads the others', whose k-th smallest + 2 eps bounds the k-th key
     float* gslot;             // [nq][2 n_slots] (xslot)
     int xslot;                // 1: use gslot instead of the gtau publish
+    int stagger;              // 32x32x16 8-wave pass: waves 4-7 half a tile behind (4-stage ring)
     int ns;                   // 16-k steps of the images (the wide-D kernel: a multiple of HW_KC)
 };
 
