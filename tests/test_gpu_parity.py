@@ -891,7 +891,9 @@ def test_h16_cross_slot_threshold_equals_default():
     base, qs = _data(n, d, nq, seed=91)
     tomb_ids = np.nonzero(np.random.default_rng(92).random(n) < 0.01)[0]
     runs = []
-    for env in ({}, {"WV_H16_XSLOT": "0"}):
+    # (third run: the staggered 8-wave pass, WV_H16_STAGGER=1 -- same lists,
+    # another schedule)
+    for env in ({}, {"WV_H16_XSLOT": "0"}, {"WV_H16_STAGGER": "1"}):
         os.environ.update(env)
         try:
             ix = W.GPUVectorIndex(d, "l2-squared", capacity=n)
@@ -902,9 +904,10 @@ def test_h16_cross_slot_threshold_equals_default():
         finally:
             for key in env:
                 os.environ.pop(key, None)
-    for (ai, ad, an), (bi, bd, bn) in zip(runs[0], runs[1]):
-        assert an.tolist() == bn.tolist()
-        _same(ai, ad, bi, bd)
+    for other in (runs[1], runs[2]):
+        for (ai, ad, an), (bi, bd, bn) in zip(runs[0], other):
+            assert an.tolist() == bn.tolist()
+            _same(ai, ad, bi, bd)
     # and the default (cross-slot threshold engaged) against the restatement
     tb = O.bits_from_ids(tomb_ids, n)
     for k, (gi, gd, gn) in zip((10, 32), runs[0]):

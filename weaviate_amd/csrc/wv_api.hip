@@ -56,7 +56,8 @@ hipError_t wv_launch_h16_rows_gather(const float* in, int ld_in, const uint32_t*
                                      float scale, void* out, hipStream_t s);
 hipError_t wv_launch_h16_compact_aux(const float* xnorm, const uint32_t* rowidx, uint64_t n, float* cxnorm,
                                      uint64_t* excl, uint64_t excl_words, hipStream_t s);
-hipError_t wv_launch_remap_ids(uint32_t* ids, uint64_t n, const uint32_t* rowidx, hipStream_t s);
+hipError_t wv_launch_remap_ids(uint32_t* ids, int nq, int n_slots, int per_slot, int bq, uint64_t ntiles,
+                               uint64_t units_per_block, const uint32_t* rowidx, uint64_t n_rows, hipStream_t s);
 hipError_t wv_launch_absmax(const float* in, int ld, uint64_t n, int D, unsigned int* max_bits, hipStream_t s);
 hipError_t wv_launch_h16_qscale(const float* part, int nparts, unsigned int* max_bits, float bsign, float* qscale,
                                 hipStream_t s);
@@ -730,7 +731,9 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
                : solo ? wv_launch_bf_h16s(&hp, ns / 2, 0, s)
                : (quad ? wv_launch_bf_h16q(&hp, ns / 2, 0, waves, s) : wv_launch_bf_h16(&hp, ns, 0, waves, s)));
     TREC(1);
-    if (rowidx) HIP_TRY(wv_launch_remap_ids(ix->cand_id.as<uint32_t>(), (uint64_t)nq * sch.n_slots * prod * kp, rowidx, s));
+    if (rowidx)
+        HIP_TRY(wv_launch_remap_ids(ix->cand_id.as<uint32_t>(), nq, sch.n_slots, prod * kp, bq, sch.ntiles,
+                                    sch.units_per_block, rowidx, N, s));
     fp.cand_d = ix->cand_d.as<float>();
     fp.cand_id = ix->cand_id.as<uint32_t>();
     fp.n_slots = sch.n_slots;

@@ -1225,10 +1225,21 @@ __global__ void wv_gather_f32_kernel(const float* src, const uint32_t* idx, uint
 }
 
 // candidate lists of a key pass over compacted rows: list positions -> row ids
-// (the map is increasing, so every (key, id) order is unchanged)
-__global__ void wv_remap_ids_kernel(uint32_t* ids, uint64_t n, const uint32_t* rowidx) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n && ids[i] != WV_NIL) ids[i] = rowidx[ids[i]];
+// (the map is increasing, so every (key, id) order is unchanged).  Only the
+// lists a query's block really produced (bf_slots_of slots, as the finalize
+// reads them): the other entries of the [nq][n_slots][per_slot] array hold
+// stale words.  A position >= n_rows cannot come out of the pass; it would
+// become WV_NIL here rather than an out-of-range read.
+__global__ void wv_remap_ids_kernel(uint32_t* ids, int nq, int n_slots, int per_slot, int bq, uint64_t ntiles,
+                                    uint64_t units_per_block, const uint32_t* rowidx, uint64_t n_rows) {
+    const int q = blockIdx.x;
+    if (q >= nq) return;
+    const int n_valid = wv::bf_slots_of((uint64_t)(q / bq), ntiles, units_per_block) * per_slot;
+    uint32_t* e = ids + (size_t)q * n_slots * per_slot;
+    for (int i = threadIdx.x; i < n_valid; i += blockDim.x) {
+        const uint32_t v = e[i];
+        if (v != WV_NIL) e[i] = v < n_rows ? rowidx[v] : WV_NIL;
+    }
 }
 
 // exclusion bits of a compacted scan: rows >= n (the last tile's padding)
@@ -1248,9 +1259,11 @@ hipError_t wv_launch_h16_compact_aux(const float* xnorm, const uint32_t* rowidx,
     return hipGetLastError();
 }
 
-hipError_t wv_launch_remap_ids(uint32_t* ids, uint64_t n, const uint32_t* rowidx, hipStream_t s) {
-    if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(wv_remap_ids_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, ids, n, rowidx);
+hipError_t wv_launch_remap_ids(uint32_t* ids, int nq, int n_slots, int per_slot, int bq, uint64_t ntiles,
+                               uint64_t units_per_block, const uint32_t* rowidx, uint64_t n_rows, hipStream_t s) {
+    if (nq == 0) return hipSuccess;
+    hipLaunchKernelGGL(wv_remap_ids_kernel, dim3((unsigned)nq), dim3(64), 0, s, ids, nq, n_slots, per_slot, bq, ntiles,
+                       units_per_block, rowidx, n_rows);
     return hipGetLastError();
 }
 
