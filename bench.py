@@ -304,7 +304,10 @@ def exact_roofline(args, ix, kern_ms, stats, D, n_allowed, n_local, NQ):
     if os.environ.get("WV_BF_SPLIT") and not fp32:
         kind = "split" if 2 * n_allowed >= n_local else "fp32"
     elif not fp32:
-        kind = "h16" if 8 * n_allowed >= n_local else "fp32"
+        # round 3: a shared list under half the corpus runs the f16 pass over
+        # its gathered rows (WV_BF_H16_NO_GATHER=1: round 2's fp32 row-list
+        # pass below 1/8)
+        kind = "h16" if (8 * n_allowed >= n_local or not os.environ.get("WV_BF_H16_NO_GATHER")) else "fp32"
     else:
         kind = "fp32"
     # WV_H16_QUAD=1, D <= 128 with an even number of 16-k steps: the 16x16x32 kernel (wv_api.hip h16_quad)
@@ -869,6 +872,8 @@ def main():
     ap.add_argument("--seq-build", action="store_true",
                     help="hnsw at N=1: also build the restatement's insert-by-insert graph and report its recall "
                          "beside the GPU-built graph's (north_star's 0.5-pt criterion; ~40 s of CPU at 1M)")
+    ap.add_argument("--no-c5-line", action="store_true",
+                    help="skip the configs[4]-layout line (12.5M x 96 rows per GPU, sharded hnsw + merge)")
     ap.add_argument("--no-c3-line", action="store_true",
                     help="skip the configs[2] GloVe-shaped hnsw ef-sweep line reported beside the default value")
     ap.add_argument("--hnsw-build-threads", type=int, default=16)
@@ -985,6 +990,23 @@ def main():
             h = run_hnsw(a3, ctx, W, with_cpu)
             h.pop("metric", None)
             result["hnsw_c3"] = h
+        if not args.no_c5_line and args.rows == 1_000_000 and args.metric == "l2-squared":
+            # configs[4]'s layout at every N: a Deep/SIFT-shaped 96-d corpus of
+            # 12.5M rows per GPU (100M at N = 8), sharded by id range, each GPU
+            # building and searching the graph of its shard, per-shard top-k
+            # all-gathered over RCCL and merged (weak scaling per shard)
+            a5 = argparse.Namespace(**vars(args))
+            a5.rows, a5.dim, a5.metric, a5.hnsw_data = 12_500_000 * ws, 96, "l2-squared", "sift"
+            a5.ef, a5.ef_sweep, a5.concurrency, a5.split = 64, [128], [], "corpus"
+            a5.graph_build, a5.dump_ids, a5.seq_build = "gpu", "", False
+            try:
+                h = run_hnsw(a5, ctx, W, False)
+                h.pop("metric", None)
+                h["scaling"] = "weak (12.5M rows per GPU)"
+                h["value_units"] = f"queries/s over the whole {a5.rows:,}-row corpus (every rank searches the batch)"
+                result["hnsw_c5_sharded"] = h
+            except Exception as e:   # reported, not fatal to the headline line
+                result["hnsw_c5_sharded"] = {"error": f"{type(e).__name__}: {e}"}
     if ws > 1:
         ctx.barrier()
         ctx.dist.destroy_process_group()
