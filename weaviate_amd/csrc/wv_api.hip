@@ -52,8 +52,8 @@ hipError_t wv_launch_split_rows(const float* in, int ld_in, const uint64_t* ids,
 hipError_t wv_launch_h16_rows(const float* in, int ld_in, const uint64_t* ids, uint64_t n, int D, int ns, float sign,
                               float scale, const unsigned int* scale_from_max, void* out, uint64_t out_row0,
                               unsigned int* res_max_bits, float* res_out, int quad, hipStream_t s);
-hipError_t wv_launch_h16_rows_gather(const float* in, int ld_in, const uint32_t* gather, uint64_t n, int D, int ns,
-                                     float scale, void* out, hipStream_t s);
+hipError_t wv_launch_h16_rows_gather(const float* in, int ld_in, const uint32_t* gather, uint64_t n, uint64_t n_pad,
+                                     int D, int ns, float scale, void* out, hipStream_t s);
 hipError_t wv_launch_h16_compact_aux(const float* xnorm, const uint32_t* rowidx, uint64_t n, float* cxnorm,
                                      uint64_t* excl, uint64_t excl_words, hipStream_t s);
 hipError_t wv_launch_remap_ids(uint32_t* ids, int nq, int n_slots, int per_slot, int bq, uint64_t ntiles,
@@ -249,6 +249,10 @@ struct wv_index {
     float h16_sx = 0.f, h16_ex = 0.f;
     DevBuf ximg16, xns, qimg16, qres, qmax, qscale, tau, gtau, marg, allow_pad, ex_bits, gslot;
     DevBuf ximg16q;         // the corpus image in the 16x16x32 layout (h16_quad), beside ximg16
+    // the f16 pass's block order (block_order), cached for its schedule
+    DevBuf blk_order;
+    std::vector<int> blk_order_host;
+    uint64_t blk_key[3] = {0, 0, 0};
     DevBuf qmax_part;       // per-block max |q_i| of the query-norm pass
     float maxnorm_host = 0.f;   // max |x| (rounded up), cached after every row write
     DevBuf xnorm;           // [capacity]
@@ -268,6 +272,7 @@ struct wv_index {
     DevBuf tomb;            // tombstones (HNSW eligibility)
     DevBuf excl;            // tombstone | nil node | no vector (flatSearch skips)
     uint64_t bm_words = 0;
+    uint64_t clean_words = 0;   // leading exclusion words that are zero (refresh_bitmaps)
     bool bitmaps_dirty = true;
     // scratch
     DevBuf stage;           // contiguous host->device staging
@@ -369,6 +374,10 @@ int refresh_bitmaps(wv_index* ix) {
         }
     }
     ix->delta_count = dcount;
+    // the clean prefix: words (64-row tiles of the f16 pass) before the first
+    // excluded row, which the key pass need not test
+    ix->clean_words = 0;
+    while (ix->clean_words < words && ex[ix->clean_words] == 0) ix->clean_words++;
     if (dcount) {
         HIP_TRY(ix->delta.ensure(words * 8));
         HIP_TRY(hipMemcpyAsync(ix->delta.p, dl.data(), words * 8, hipMemcpyHostToDevice, ix->stream));
@@ -518,6 +527,34 @@ int run_pq_flat(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d
 // (compact_allowed) -- the pass then runs over an f16 image of just those N
 // rows (gathered here) and the candidate ids are mapped back to rows before
 // the finalize; d_allow is then already applied
+// Block order of an f16 pass: the blocks sorted by the corpus offset of their
+// first tile, read by the kernels at their XCD-contiguous position (locality
+// bit 1), so that each XCD runs the blocks of every query block over the same
+// part of the corpus at the same time -- a tile then comes into that XCD's L2
+// once per pass instead of once per query block.  nullptr: the identity
+// (WV_H16_BLOCK_ORDER=0, or a single query block).
+int block_order(wv_index* ix, uint64_t nqb, const wv::BfSchedule& sch, hipStream_t s, const int** out) {
+    *out = nullptr;
+    const char* e = std::getenv("WV_H16_BLOCK_ORDER");
+    if ((e && std::atoi(e) == 0) || nqb < 2 || sch.n_blocks < 16) return WV_OK;
+    const uint64_t key[3] = {nqb, sch.ntiles, sch.units_per_block};
+    if (!(ix->blk_key[0] == key[0] && ix->blk_key[1] == key[1] && ix->blk_key[2] == key[2])) {
+        const int nb = sch.n_blocks;
+        std::vector<int>& ord = ix->blk_order_host;
+        ord.resize(nb);
+        for (int i = 0; i < nb; ++i) ord[i] = i;
+        std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) {
+            return (uint64_t)a * sch.units_per_block % sch.ntiles < (uint64_t)b * sch.units_per_block % sch.ntiles;
+        });
+        HIP_TRY(ix->blk_order.ensure((size_t)nb * 4));
+        HIP_TRY(hipMemcpyAsync(ix->blk_order.p, ord.data(), (size_t)nb * 4, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipStreamSynchronize(s));   // (pageable source; a later schedule rewrites it)
+        std::copy(key, key + 3, ix->blk_key);
+    }
+    *out = ix->blk_order.as<int>();
+    return WV_OK;
+}
+
 int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_allow, uint64_t allow_nbits, uint64_t N,
             uint64_t* d_out_ids, float* d_out_d, int32_t* d_out_n, hipStream_t s, std::vector<int32_t>& fails,
             const uint32_t* rowidx = nullptr) {
@@ -581,9 +618,8 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
         HIP_TRY(ix->cimg16.ensure(ib));
         HIP_TRY(ix->cxnorm.ensure(rows * 4));
         HIP_TRY(ix->cexcl.ensure(ew * 8));
-        HIP_TRY(hipMemsetAsync(ix->cimg16.p, 0, ib, s));
         HIP_TRY(hipMemsetAsync(ix->cxnorm.p, 0, rows * 4, s));
-        HIP_TRY(wv_launch_h16_rows_gather(ix->vecs.as<float>(), ix->ldx, rowidx, N, ix->dim, ns, ix->h16_sx,
+        HIP_TRY(wv_launch_h16_rows_gather(ix->vecs.as<float>(), ix->ldx, rowidx, N, rows, ix->dim, ns, ix->h16_sx,
                                           ix->cimg16.p, s));
         HIP_TRY(wv_launch_h16_compact_aux(ix->xnorm.as<float>(), rowidx, N, ix->cxnorm.as<float>(),
                                           ix->cexcl.as<uint64_t>(), ew, s));
@@ -606,6 +642,9 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     hp.nq = nq;
     hp.metric = ix->metric;
     hp.n_qblocks = nqb;
+    // 64-row tiles the pass need not mask: every row present and eligible
+    // (no allow list; a compacted scan: the rows below N)
+    hp.clean_tiles = wd ? 0 : rowidx ? N / wv::H_BN : allow ? 0 : std::min<uint64_t>(ix->clean_words, N / wv::H_BN);
     hp.stagger = std::getenv("WV_H16_STAGGER") && std::atoi(std::getenv("WV_H16_STAGGER")) == 1;
     hp.locality = 1;
     if (const char* e = std::getenv("WV_BF_LOCALITY")) hp.locality = std::atoi(e);
@@ -702,7 +741,9 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     // (with the seed's threshold the running one only adds work: measured
     // 3.048 vs 3.092 ms per 1M x 10k key pass; without a seed -- corpora below
     // 64 * H_SAMPLE tiles -- it cuts the pass 4.13 -> 3.43 ms at 1M)
-    hp.kth = k <= prod * kp && (!seed || std::getenv("WV_H16_RUN_SEED")) && !wd && !std::getenv("WV_H16_NO_RUNNING")
+    // (the wide-D pass publishes from a lane pair's two lists: k <= 2 BF_KP)
+    hp.kth = k <= (wd ? 2 * kp : prod * kp) && (!seed || std::getenv("WV_H16_RUN_SEED")) &&
+                     !std::getenv("WV_H16_NO_RUNNING")
                  ? k
                  : 0;
     // cross-slot threshold (32x32x16 pass, <= 32 list heads per query; on
@@ -726,6 +767,7 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     }
     hp.out_d = ix->cand_d.as<float>();
     hp.out_id = ix->cand_id.as<uint32_t>();
+    if (int rc = block_order(ix, (uint64_t)nqb, sch, s, &hp.block_order)) return rc;
     TREC(0);
     HIP_TRY(wd ? wv_launch_bf_h16w(&hp, s)
                : solo ? wv_launch_bf_h16s(&hp, ns / 2, 0, s)

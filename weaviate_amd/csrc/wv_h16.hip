@@ -69,6 +69,7 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
         const int nwg = (int)gridDim.x, q8 = nwg / 8, r8 = nwg % 8, xcd = (int)blockIdx.x % 8;
         lb = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (int)blockIdx.x / 8;
     }
+    if (p.block_order) lb = p.block_order[lb];
     const uint64_t u_first = (uint64_t)lb * p.units_per_block;
     uint64_t u_last = u_first + p.units_per_block;
     if (u_last > (uint64_t)p.n_qblocks * p.ntiles) u_last = (uint64_t)p.n_qblocks * p.ntiles;
@@ -82,13 +83,16 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
     // this wave's LDS-DMA ops per tile (the counted waits below)
     const int n_ops = (wave < St::IMG_U4 / 64 ? (St::IMG_U4 / 64 - 1 - wave) / WAVES + 1 : 0) +
                       ((wave == 0 && L2) ? 1 : 0);
+    // the image words this wave moves per tile (its share, and the s|x|^2
+    // word on wave 0): a lane offset per share, computed once
+    const uint32_t voff = (uint32_t)(wave * 1024 + lane * 16);
     auto fill = [&](uint64_t t, int st) {
         const uint64_t tile = t * (uint64_t)p.tile_stride;
-        const uint32_t dst = lds0 + (uint32_t)(st * St::U4 * 16);
-        const uint4* src = X + tile * St::IMG_U4;
+        const uint32_t dst = lds0 + (uint32_t)(st * St::U4 * 16) + (uint32_t)(wave * 1024);
+        const uint4* src = uniform_ptr(X + tile * St::IMG_U4);
 #pragma unroll
-        for (int i = wave; i < St::IMG_U4 / 64; i += WAVES)
-            glds16s(src, (uint32_t)(i * 1024 + lane * 16), dst + i * 1024);
+        for (int i = 0; i < St::IMG_U4 / 64; i += WAVES)
+            if (wave + i < St::IMG_U4 / 64) glds16s(src, voff + (uint32_t)(i * 1024), dst + (uint32_t)(i * 1024));
         if (wave == 0 && L2) glds4(p.xns + tile * H_BN + lane, dst + St::IMG_U4 * 16);
     };
 
@@ -104,6 +108,8 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
         return n * n_ops;   // this wave's DMA ops for the group
     };
     auto tile_lds = [&](int t) { return lds + ((t / TPS) % NSTG * TPS + t % TPS) * St::U4; };
+    // (in the tile loop: the slot of tile t advances by one, wrapping at the ring)
+    auto next_slot = [](int sl) { return sl + 1 == NSTG * TPS ? 0 : sl + 1; };
 
     for (uint64_t u = u_first; u < u_last;) {
         const int qb = (int)(u / p.ntiles);
@@ -134,6 +140,10 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
             if (jq0 < p.nq) tau0 = fminf(FLT_MAX, p.tau[jq0] * s);
             if (jq1 < p.nq) tau1 = fminf(FLT_MAX, p.tau[jq1] * s);
         }
+        // the padding columns of a partial query block never extract (every
+        // later threshold update is a min): their tiles need no row mask
+        if (jq0 >= p.nq) tau0 = -__builtin_inff();
+        if (jq1 >= p.nq) tau1 = -__builtin_inff();
         // the running threshold's margin: 2 eps (scaled) + the rounding of the sum
         float marg0 = 0.f, marg1 = 0.f;
         if (!SEED && p.kth) {
@@ -221,8 +231,13 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
         // rows 4 khalf + ..., low word: rows 0-31, high word: rows 32-63)
         // (the lane-dependent shifts happen only when a tile needs the mask)
         auto tile_ok = [&](uint64_t t, uint64_t& okw) -> bool {
-            okw = tile_okw(p, t * (uint64_t)p.tile_stride, has_allow);
-            return okw != ~0ull || (qb + 1) * BQ > p.nq;
+            const uint64_t ct = t * (uint64_t)p.tile_stride;
+            if (ct < p.clean_tiles) {   // (the host's clean prefix: no word to read)
+                okw = ~0ull;
+                return false;
+            }
+            okw = tile_okw(p, ct, has_allow);
+            return okw != ~0ull;
         };
         auto lane_ok = [&](uint64_t okw, int jq) -> uint64_t { return (jq < p.nq ? okw : 0ull) >> (4 * khalf); };
         // mask a half's ineligible rows to +inf (rows (r & 3) + 8 (r >> 2) of its 32)
@@ -368,7 +383,17 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
             mfma_half(tile_lds(0), 0, acc00, acc01, [] {});
             need_mask = tile_ok(t_begin, okw);
         }
-        for (int t = 0; t < ntile; ++t) {
+        // a full group's DMA ops of this wave: a constant per wave class when
+        // the image shares divide evenly (the usual D = 64 / 128), so the
+        // per-group wait needs no runtime switch on the scalar unit
+        constexpr bool EVEN = (St::IMG_U4 / 64) % WAVES == 0;
+        constexpr int SHARE = (St::IMG_U4 / 64) / WAVES;
+        const bool xns_wave = wave == 0 && L2;
+        int slot_t = 0;   // LDS slot of tile t
+        uint32_t rb0 = (uint32_t)(t_begin * (uint64_t)p.tile_stride * H_BN) + 4 * khalf;
+        const uint32_t rb_step = (uint32_t)(p.tile_stride * H_BN);
+        int xs_next = XS && xs ? xs1 : -1;   // the next cross-slot exchange tile
+        for (int t = 0; t < ntile; ++t, rb0 += rb_step) {
             WV_DBG_COUNT(0)
             const int g = t / TPS;
 #ifndef WV_H16_ABLATE_NO_FILL
@@ -376,11 +401,23 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
             // group g - 1, before its closing barrier
             if (t % TPS == 0) ops_in_flight = g + 2 < ngroups ? fill_group(t_begin, g + 2, ntile) : 0;
 #endif
-            const uint4* img = tile_lds(t);
-            const uint32_t rb0 = (uint32_t)((t_begin + t) * (uint64_t)p.tile_stride * H_BN) + 4 * khalf;
+            const uint4* img = lds + slot_t * St::U4;
+            slot_t = next_slot(slot_t);
             const bool group_end = t % TPS == TPS - 1 || t == ntile - 1;
+            // group g + 1 landed: at most the newest group's ops outstanding
+            auto wait_group = [&] {
+                if (g + 1 >= ngroups) return;
+                if (EVEN && ops_in_flight == TPS * (SHARE + (xns_wave ? 1 : 0))) {
+                    if (xns_wave) vm_wait(TPS * (SHARE + 1));
+                    else vm_wait(TPS * SHARE);
+                } else if (EVEN) {
+                    vm_wait(0);   // (a partial group at the segment's end)
+                } else {
+                    vm_wait(ops_in_flight);
+                }
+            };
             if (lag && group_end) {   // (staggered waves: the group's barrier, half a tile early)
-                if (g + 1 < ngroups) vm_wait(ops_in_flight);
+                wait_group();
                 block_barrier();
             }
             // lanes l and l ^ 32 keep lists for the same query column (see the split pass)
@@ -418,13 +455,13 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
             // ---- C (last tile of a group): group g + 1 has landed (g + 2 may
             // stay in flight); every wave is done reading group g's stage ----
             if (!lag && group_end) {
-                if (g + 1 < ngroups) vm_wait(ops_in_flight);
+                wait_group();
                 block_barrier();
             }
             // ---- E: H0(t + 1) MFMAs, H1(t) minima ----
             if (mask_t) mask_half(acc10, acc11, (uint32_t)(mo0 >> 32), (uint32_t)(mo1 >> 32));
             if (t + 1 < ntile) {
-                mfma_half(tile_lds(t + 1), 0, acc00, acc01, [&] { m0 = min16(acc10); m1 = min16(acc11); });
+                mfma_half(lds + slot_t * St::U4, 0, acc00, acc01, [&] { m0 = min16(acc10); m1 = min16(acc11); });
                 need_mask = tile_ok(t_begin + t + 1, okw);
             } else {
                 m0 = min16(acc10);
@@ -455,8 +492,13 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
 #endif
                 if (running && (t & 15) == 15) publish();
                 else if (grew) refresh_pt();
-                if constexpr (XS)
-                    if (xs && (t == xs1 || t == xs2 || t == xs3 || t == xs4)) xslot_step(t != xs1, t != xs4);
+                if constexpr (XS) {
+                    if (t == xs_next) {
+                        xslot_step(t != xs1, t != xs4);
+                        // (equal points of a short segment collapse into one step)
+                        xs_next = t < xs2 && xs2 > t ? xs2 : t < xs3 && xs3 > t ? xs3 : t < xs4 && xs4 > t ? xs4 : -1;
+                    }
+                }
             }
         }
 
@@ -521,6 +563,7 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16q_kernel(H16Pa
         const int nwg = (int)gridDim.x, q8 = nwg / 8, r8 = nwg % 8, xcd = (int)blockIdx.x % 8;
         lb = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (int)blockIdx.x / 8;
     }
+    if (p.block_order) lb = p.block_order[lb];
     const uint64_t u_first = (uint64_t)lb * p.units_per_block;
     uint64_t u_last = u_first + p.units_per_block;
     if (u_last > (uint64_t)p.n_qblocks * p.ntiles) u_last = (uint64_t)p.n_qblocks * p.ntiles;
@@ -839,6 +882,7 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16w_kernel(H16Params p) {
         const int nwg = (int)gridDim.x, q8 = nwg / 8, r8 = nwg % 8, xcd = (int)blockIdx.x % 8;
         lb = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (int)blockIdx.x / 8;
     }
+    if (p.block_order) lb = p.block_order[lb];
     const uint64_t u_first = (uint64_t)lb * p.units_per_block;
     uint64_t u_last = u_first + p.units_per_block;
     if (u_last > (uint64_t)p.n_qblocks * p.ntiles) u_last = (uint64_t)p.n_qblocks * p.ntiles;
@@ -858,24 +902,49 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16w_kernel(H16Params p) {
         const int ntile = (int)(t_end - t_begin);
         const int nchunks = ntile * nch;
 
-        // chunk g = (tile t, chunk c) into stage g % 3; with c == 0 also the
-        // tile's extras into slot t & 1.  Returns this wave's DMA op count.
-        auto fill = [&](int g) -> int {
-            const int t = g / nch, c = g % nch;
-            const uint64_t tile = t_begin + t;
-            const uint32_t dst = lds0 + (uint32_t)((g % HW_STAGES) * St::U4 * 16);
+        // The chunks stream in order: chunk (t, c) into a stage of the 3-ring,
+        // with c == 0 also the tile's extras into slot t & 1.  This wave's
+        // share of a chunk is fixed: A blocks b = wave, wave + 8 (row groups
+        // wave / 4 + {0, 2}, step wave % 4) and B blocks b = 16 + wave + 8 j
+        // (query groups wave / 4 + 2 j), so their sources are one base each
+        // plus a chunk offset -- no per-block index arithmetic on the scalar
+        // unit (the round-2 loop spent 20 SALU per MFMA there, PMC).
+        const int wg4 = wave >> 2, ws4 = wave & 3;
+        const uint64_t gstride = 2ull * ns * 64;    // two row / query groups, in uint4
+        const uint4* b_src0 = Qg + (((uint64_t)qb * (HW_BQ / 32) + wg4) * ns + ws4) * 64;
+        // running sources of the next chunk to fill: +1 chunk (HW_KC KiB
+        // steps) per chunk; at a tile's end the corpus side moves on to the
+        // next tile's row groups (4 ns steps per tile: + 3 ns past the last
+        // chunk) and the query side starts over
+        const uint4* a_cur = X + (((uint64_t)t_begin * 4 + wg4) * ns + ws4) * 64;
+        const uint4* b_cur = b_src0;
+        int ft = 0, fc = 0;   // the next chunk to fill
+        auto fill_next = [&](int stage) -> int {
+            // (ft, fc are wave-uniform; the divergence analysis loses that
+            // through the lambda's captured state)
+            ft = __builtin_amdgcn_readfirstlane(ft);
+            fc = __builtin_amdgcn_readfirstlane(fc);
+            stage = __builtin_amdgcn_readfirstlane(stage);
+            const uint64_t tile = t_begin + ft;
+            const uint32_t dst = lds0 + (uint32_t)(stage * St::U4 * 16) + (uint32_t)(wave * 1024);
+            // (wave-uniform by construction; readfirstlane tells the compiler,
+            // which must keep the LDS-DMA bases in SGPRs)
+            const uint4* a = uniform_ptr(a_cur);
+            const uint4* b = uniform_ptr(b_cur);
             int n = 0;
-            for (int b = wave; b < (St::A_U4 + St::B_U4) / 64; b += H_WAVES) {
-                const int isb = b >= St::A_U4 / 64;
-                const int bb = isb ? b - St::A_U4 / 64 : b;      // (group, step) block
-                const int grp = bb / HW_KC, st = bb % HW_KC;
-                const uint64_t G = isb ? (uint64_t)qb * (HW_BQ / 32) + grp : tile * (HW_BN / 32) + grp;
-                const uint4* src = (isb ? Qg : X) + (G * ns + (uint64_t)c * HW_KC + st) * 64;
-                glds16s(src, (uint32_t)(lane * 16), dst + (uint32_t)(b * 1024));
-                ++n;
-            }
-            if (c == 0) {
-                const uint32_t xd = ex0 + (uint32_t)((t & 1) * St::EX_U4 * 16);
+#ifndef WV_H16W_ABLATE_NO_A
+            glds16s(a, (uint32_t)(lane * 16), dst);
+            glds16s(uniform_ptr(a + gstride), (uint32_t)(lane * 16), dst + 8 * 1024);
+            n += 2;
+#endif
+#ifndef WV_H16W_ABLATE_NO_B
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                glds16s(uniform_ptr(b + j * gstride), (uint32_t)(lane * 16), dst + (16 + 8 * j) * 1024);
+            n += 4;
+#endif
+            if (fc == 0) {
+                const uint32_t xd = ex0 + (uint32_t)((ft & 1) * St::EX_U4 * 16);
                 if (wave == 0 && L2) {
                     glds4(p.xns + tile * HW_BN + lane, xd);
                     glds4(p.xns + tile * HW_BN + 64 + lane, xd + 256);
@@ -888,6 +957,14 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16w_kernel(H16Params p) {
                     n += 1;
                 }
             }
+            a_cur = a + HW_KC * 64;
+            b_cur = b + HW_KC * 64;
+            if (++fc == nch) {
+                fc = 0;
+                ++ft;
+                a_cur += 3ull * ns * 64;
+                b_cur = b_src0;
+            }
             return n;
         };
 
@@ -898,8 +975,43 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16w_kernel(H16Params p) {
             l0d[i] = FLT_MAX; l1d[i] = FLT_MAX;
             l0i[i] = WV_NIL; l1i[i] = WV_NIL;
         }
-        floatx16 acc00, acc01, acc10, acc11;
         const float INF = __builtin_inff();
+        // extraction thresholds beside the list tails: the running per-query
+        // threshold every slot publishes (as wv_bf_h16_kernel's publish: k of
+        // the lane pair's 2 BF_KP entries bound the k-th key, + 2 eps), and
+        // -inf for the padding columns of a partial query block, which then
+        // never extract and need no row mask
+        float tau0 = jq0 < p.nq ? FLT_MAX : -INF, tau1 = jq1 < p.nq ? FLT_MAX : -INF;
+        const bool running = p.kth > 0 && p.gtau != nullptr;
+        float marg0 = 0.f, marg1 = 0.f;
+        if (running) {
+            if (jq0 < p.nq) marg0 = p.marg[jq0];
+            if (jq1 < p.nq) marg1 = p.marg[jq1];
+        }
+        const int ia = (p.kth + 1) >> 1, ib = p.kth >> 1;
+        auto publish = [&] {
+            int va = ia - 1, vb = ib - 1;
+            asm volatile("" : "+v"(va), "+v"(vb));   // (select chains over a VGPR index)
+            float a0 = -FLT_MAX, a1 = -FLT_MAX, b0 = -FLT_MAX, b1 = -FLT_MAX;
+#pragma unroll
+            for (int i = 0; i < BF_KP; ++i) {
+                a0 = va == i ? l0d[i] : a0;
+                a1 = va == i ? l1d[i] : a1;
+                b0 = vb == i ? l0d[i] : b0;
+                b1 = vb == i ? l1d[i] : b1;
+            }
+            b0 = __shfl_xor(b0, 32, 64);
+            b1 = __shfl_xor(b1, 32, 64);
+            const float k0 = fmaxf(a0, b0), k1 = fmaxf(a1, b1);
+            if (khalf == 0) {
+                const float u4 = 4.f * 5.9604645e-08f;
+                if (jq0 < p.nq && k0 < FLT_MAX) atomicMin(&p.gtau[jq0], h16_key_enc(k0 + marg0 + u4 * (fabsf(k0) + marg0)));
+                if (jq1 < p.nq && k1 < FLT_MAX) atomicMin(&p.gtau[jq1], h16_key_enc(k1 + marg1 + u4 * (fabsf(k1) + marg1)));
+            }
+            if (jq0 < p.nq) tau0 = fminf(tau0, h16_key_dec(__atomic_load_n(&p.gtau[jq0], __ATOMIC_RELAXED)));
+            if (jq1 < p.nq) tau1 = fminf(tau1, h16_key_dec(__atomic_load_n(&p.gtau[jq1], __ATOMIC_RELAXED)));
+        };
+        floatx16 acc00, acc01, acc10, acc11;
         auto min16 = [&](const floatx16& A) {
             float m0 = fminf(fminf(A[0], A[1]), A[2]), m1 = fminf(fminf(A[3], A[4]), A[5]);
             float m2 = fminf(fminf(A[6], A[7]), A[8]), m3 = fminf(fminf(A[9], A[10]), A[11]);
@@ -907,17 +1019,30 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16w_kernel(H16Params p) {
             m1 = fminf(fminf(m1, A[14]), A[15]);
             return fminf(fminf(m0, m1), fminf(m2, m3));
         };
-        int ops[HW_STAGES] = {0, 0, 0};
         // (the previous segment ended with every stage read and every DMA landed)
-        if (nchunks > 0) ops[0] = fill(0);
-        if (nchunks > 1) ops[1] = fill(1);
+        if (nchunks > 0) fill_next(0);
+        if (nchunks > 1) fill_next(1);
+        int t = 0, c = 0, stg = 0;   // the chunk computed: (tile, chunk), its stage
         for (int g = 0; g < nchunks; ++g) {
-            const int t = g / nch, c = g % nch;
-            // chunk g landed (g + 1 may stay in flight), for every wave
-            vm_wait(g + 1 < nchunks ? ops[(g + 1) % HW_STAGES] : 0);
+            // chunk g landed (g + 1 may stay in flight), for every wave: at
+            // most 6 of this wave's ops still outstanding -- chunk g + 1's
+            // blocks are its first 6 (its extras, issued after them, may then
+            // have to land as well: a chunk's compute later, long done)
+#if defined(WV_H16W_ABLATE_NO_A) && defined(WV_H16W_ABLATE_NO_B)
+            vm_wait(0);
+#elif defined(WV_H16W_ABLATE_NO_A)
+            if (g + 1 < nchunks) vm_wait(4);
+            else vm_wait(0);
+#elif defined(WV_H16W_ABLATE_NO_B)
+            if (g + 1 < nchunks) vm_wait(2);
+            else vm_wait(0);
+#else
+            if (g + 1 < nchunks) vm_wait(6);
+            else vm_wait(0);
+#endif
             block_barrier();
-            if (g + 2 < nchunks) ops[(g + 2) % HW_STAGES] = fill(g + 2);
-            const uint4* st = lds + (g % HW_STAGES) * St::U4;
+            if (g + 2 < nchunks) fill_next(stg == 0 ? 2 : stg - 1);
+            const uint4* st = lds + stg * St::U4;
             if (c == 0) {
                 // C-in: s|x|^2 of the wave's rows (L2) or zero
                 if (L2) {
@@ -947,16 +1072,20 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16w_kernel(H16Params p) {
                 acc10 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b0, acc10, 0, 0, 0);
                 acc11 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b1, acc11, 0, 0, 0);
             }
-            if (c != nch - 1) continue;
+            const int tc = t;   // (the chunk just computed)
+            stg = stg == 2 ? 0 : stg + 1;
+            if (++c != nch) continue;
+            c = 0;
+            ++t;
             // ---- tile epilogue ----
-            const uint64_t tile = t_begin + t;
-            const uint32_t* w = reinterpret_cast<const uint32_t*>(ex_lds + (t & 1) * St::EX_U4 + HW_BN / 4);
+            const uint64_t tile = t_begin + tc;
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(ex_lds + (tc & 1) * St::EX_U4 + HW_BN / 4);
             // the wave's 64 rows are the tile's word rh
             uint64_t okw = ~((uint64_t)w[2 * rh] | ((uint64_t)w[2 * rh + 1] << 32));
             if (has_allow) okw &= (uint64_t)w[4 + 2 * rh] | ((uint64_t)w[4 + 2 * rh + 1] << 32);
             const uint64_t row0 = tile * HW_BN + 64 * rh;
             if (row0 + 64 > p.N) okw &= p.N > row0 ? ((1ull << (p.N - row0)) - 1) : 0ull;
-            if (okw != ~0ull || (qb + 1) * HW_BQ > p.nq) {
+            if (okw != ~0ull) {
                 const uint64_t o0 = (jq0 < p.nq ? okw : 0ull) >> (4 * khalf);
                 const uint64_t o1 = (jq1 < p.nq ? okw : 0ull) >> (4 * khalf);
 #pragma unroll
@@ -969,13 +1098,19 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16w_kernel(H16Params p) {
                 }
             }
             const uint32_t rb0 = (uint32_t)row0 + 4 * khalf;
-            const float pt0 = __shfl_xor(l0d[BF_KP - 1], 32, 64);
-            const float pt1 = __shfl_xor(l1d[BF_KP - 1], 32, 64);
+            const float pt0 = fminf(__shfl_xor(l0d[BF_KP - 1], 32, 64), tau0);
+            const float pt1 = fminf(__shfl_xor(l1d[BF_KP - 1], 32, 64), tau1);
             float m;
+#ifdef WV_H16W_ABLATE_NO_EPI
+            if (acc00[0] == 1234.5f && acc01[0] == acc10[0] && acc11[0] == pt0 + pt1) l0d[0] = 0.f;
+            continue;
+#endif
             m = min16(acc00); if (m <= fminf(l0d[BF_KP - 1], pt0)) split_extract16(m, acc00, l0d, l0i, pt0, rb0);
             m = min16(acc10); if (m <= fminf(l0d[BF_KP - 1], pt0)) split_extract16(m, acc10, l0d, l0i, pt0, rb0 + 32);
             m = min16(acc01); if (m <= fminf(l1d[BF_KP - 1], pt1)) split_extract16(m, acc01, l1d, l1i, pt1, rb0);
             m = min16(acc11); if (m <= fminf(l1d[BF_KP - 1], pt1)) split_extract16(m, acc11, l1d, l1i, pt1, rb0 + 32);
+            // every tile while the lists fill, then every 4th
+            if (running && (tc < 8 || (tc & 3) == 3)) publish();
         }
         vm_wait(0);
         block_barrier();   // every stage read before the next segment's fills
@@ -1207,15 +1342,53 @@ hipError_t wv_launch_h16_rows(const float* in, int ld_in, const uint64_t* ids, u
     return hipGetLastError();
 }
 
-// the image of rows gather[0..n) (ascending row ids of a compacted allow
-// list) as image rows 0..n (h16_index layout)
-hipError_t wv_launch_h16_rows_gather(const float* in, int ld_in, const uint32_t* gather, uint64_t n, int D, int ns,
-                                     float scale, void* out, hipStream_t s) {
-    if (n == 0) return hipSuccess;
-    if (ns < 1 || ns > wv::HW_NS_MAX || D > ns * 16 || !gather) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(wv::wv_h16_rows_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, in, ld_in,
-                       (const uint64_t*)nullptr, gather, n, D, ns, 1.f, scale, (const unsigned int*)nullptr,
-                       static_cast<uint16_t*>(out), (uint64_t)0, (unsigned int*)nullptr, (float*)nullptr, 0);
+// The image of rows gather[0..n) (ascending row ids of a compacted allow
+// list) as image rows 0..n_pad (h16_index layout, rows past n zero): one
+// thread per 16-byte image word -- lane (h, r) of a (32-row group, 16-k step)
+// block, 8 halves of one row -- so the stores are whole contiguous 1 KiB
+// blocks (wv_h16_rows_kernel scatters 2-byte stores: 1.4 ms for 625k x 768
+// rows, measured) and the reads are 32-byte row pieces.
+__global__ void wv_h16_img_gather_kernel(const float* __restrict__ in, int ld_in, const uint32_t* __restrict__ gather,
+                                         uint64_t n, uint64_t n_pad, int D, int ns, float scale, uint4* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t total = n_pad / 32 * (uint64_t)ns * 64;
+    if (i >= total) return;
+    const uint64_t block = i >> 6;
+    const int lane = (int)(i & 63);
+    const uint64_t grp = block / (uint64_t)ns;
+    const int step = (int)(block - grp * ns);
+    const uint64_t r = grp * 32 + (lane & 31);
+    const int k0 = step * 16 + (lane >> 5) * 8;
+    uint32_t h[4] = {0u, 0u, 0u, 0u};
+    if (r < n) {
+        const float* src = in + (uint64_t)gather[r] * ld_in;
+        float x[8];
+        if (k0 + 8 <= D) {
+            const float4 a = *reinterpret_cast<const float4*>(src + k0);
+            const float4 b = *reinterpret_cast<const float4*>(src + k0 + 4);
+            x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w; x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) x[j] = k0 + j < D ? src[k0 + j] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const _Float16 lo = (_Float16)(scale * x[2 * j]), hi = (_Float16)(scale * x[2 * j + 1]);
+            h[j] = (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
+        }
+    }
+    out[i] = make_uint4(h[0], h[1], h[2], h[3]);
+}
+
+hipError_t wv_launch_h16_rows_gather(const float* in, int ld_in, const uint32_t* gather, uint64_t n, uint64_t n_pad,
+                                     int D, int ns, float scale, void* out, hipStream_t s) {
+    if (n_pad == 0) return hipSuccess;
+    // (ld_in a multiple of 4 floats: the corpus rows are 16-byte aligned)
+    if (ns < 1 || ns > wv::HW_NS_MAX || D > ns * 16 || !gather || n_pad % 32 || n > n_pad || ld_in % 4)
+        return hipErrorInvalidValue;
+    const uint64_t total = n_pad / 32 * (uint64_t)ns * 64;
+    hipLaunchKernelGGL(wv_h16_img_gather_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, in, ld_in,
+                       gather, n, n_pad, D, ns, scale, static_cast<uint4*>(out));
     return hipGetLastError();
 }
 

@@ -35,6 +35,13 @@ __device__ __forceinline__ void glds16s(const void* sbase, uint32_t voff, uint32
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds_wave_base) : "memory");
 }
+// a wave-uniform pointer the compiler cannot prove uniform, moved to SGPRs
+template <class T>
+__device__ __forceinline__ const T* uniform_ptr(const T* p) {
+    const uint64_t v = reinterpret_cast<uint64_t>(p);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return reinterpret_cast<const T*>(((uint64_t)hi << 32) | lo);
+}
 __device__ __forceinline__ void glds4(const void* src, uint32_t lds_wave_base) {
     uint32_t keep;
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"

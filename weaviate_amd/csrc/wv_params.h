@@ -150,7 +150,9 @@ struct H16Params {
     int n_qblocks, n_slots;
     uint64_t ntiles, units_per_block;   // ntiles: tiles scanned (the sample's when tile_stride > 1)
     int tile_stride;          // corpus tile = scanned tile * tile_stride (seed pre-pass)
+    uint64_t clean_tiles;     // corpus tiles [0, clean_tiles) have no excluded row (no allow list either): no mask
     int locality;             // bit 1: XCD-contiguous workgroup ids
+    const int* block_order;   // optional: XCD-contiguous position -> block (run_h16's block_order)
     float* out_d;             // [nq][n_slots][H_PROD][BF_KP] scaled keys
     uint32_t* out_id;
     // running per-query threshold shared by every slot (k <= 2 BF_KP): each
