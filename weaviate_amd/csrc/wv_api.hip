@@ -225,6 +225,10 @@ __global__ void popcount_rows_kernel(const uint64_t* bits, uint64_t words, uint6
 
 }  // namespace
 
+// rows of the corpus buffers: whole 128-row tiles of the brute-force passes
+// and whole 256-row tiles of the wide f16 pass (wv_bf_h16w_kernel<.., 128>)
+inline uint64_t align_rows(uint64_t n) { return (n + 255) / 256 * 256; }
+
 struct wv_index {
     int dim = 0, dpad = 0, metric = 0;
     int ldx = 0;            // corpus row stride: D rounded up to 32 floats (whole 128-B lines, whole MFMA k-chunks) when D >= 32
@@ -572,7 +576,10 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     // 4-wave 512-query workgroup per CU
     const int waves = solo ? 4 : std::getenv("WV_H16_WAVES") && std::atoi(std::getenv("WV_H16_WAVES")) == 4 ? 4 : 8;
     const int wg_per_cu = wd || solo ? 1 : 8 / waves;
-    const int tile_rows = wd ? wv::HW_BN : wv::H_BN, bq = wd ? wv::HW_BQ : solo ? wv::HS_BQ : waves * 64;
+    // (WV_H16W_ROWS=64: the wide pass's 128-row tiles, for comparison)
+    const char* wre = std::getenv("WV_H16W_ROWS");
+    const int wide_rows = wre && std::atoi(wre) == 64 ? 64 : 128;
+    const int tile_rows = wd ? 2 * wide_rows : wv::H_BN, bq = wd ? wv::HW_BQ : solo ? wv::HS_BQ : waves * 64;
     // seed minima per query and slot; lists per query and slot, entries per list
     const int seed_prod = wd ? wv::HW_PROD : (quad ? wv::HQ_PROD : wv::H_PROD);
     const int prod = quad ? 1 : seed_prod;
@@ -642,6 +649,7 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     hp.nq = nq;
     hp.metric = ix->metric;
     hp.n_qblocks = nqb;
+    hp.wide_rows = wide_rows;
     // 64-row tiles the pass need not mask: every row present and eligible
     // (no allow list; a compacted scan: the rows below N)
     hp.clean_tiles = wd ? 0 : rowidx ? N / wv::H_BN : allow ? 0 : std::min<uint64_t>(ix->clean_words, N / wv::H_BN);
@@ -1460,12 +1468,13 @@ int wv_index_create(int dim, int metric, const wv_config* cfg, uint64_t capacity
         ix->n_cus = cus;
     }
     ix->bm_words = (capacity + 63) / 64;
-    // whole brute-force tiles (wv_bf.hip layout contract): zero rows past capacity
-    const uint64_t cap_rows = (capacity + wv::BF_BN - 1) / wv::BF_BN * wv::BF_BN;
+    // whole brute-force tiles (wv_bf.hip layout contract) and whole 256-row
+    // tiles of the wide f16 pass: zero rows past capacity
+    const uint64_t cap_rows = align_rows(capacity);
     const size_t vbytes = cap_rows * (size_t)ix->ldx * 4;
     if (ix->vecs.ensure(vbytes) != hipSuccess || ix->xnorm.ensure(cap_rows * 4) != hipSuccess ||
         ix->maxnorm.ensure(4) != hipSuccess || ix->tomb.ensure(ix->bm_words * 8) != hipSuccess ||
-        ix->excl.ensure((ix->bm_words + 2) * 8) != hipSuccess) {   // + the word pair of a last 128-row tile
+        ix->excl.ensure((ix->bm_words + 4) * 8) != hipSuccess) {   // + the words of a last 256-row tile
         wv_index_destroy(ix);
         return fail(WV_EOOM, "wv_index_create: device allocation failed");
     }
@@ -1876,8 +1885,8 @@ int wv_index_reserve(wv_index* ix, uint64_t capacity) {
     HIP_TRY(hipSetDevice(ix->cfg.device));
     hipStream_t s = ix->stream;
     HIP_TRY(hipStreamSynchronize(s));
-    const uint64_t old_rows = (ix->capacity + wv::BF_BN - 1) / wv::BF_BN * wv::BF_BN;
-    const uint64_t cap_rows = (capacity + wv::BF_BN - 1) / wv::BF_BN * wv::BF_BN;
+    const uint64_t old_rows = align_rows(ix->capacity);
+    const uint64_t cap_rows = align_rows(capacity);
     const size_t ld4 = (size_t)ix->ldx * 4, img = (size_t)ix->h16_ns * 16 * 2;
     const uint64_t words = (capacity + 63) / 64;
     HIP_TRY(regrow(ix->vecs, old_rows * ld4, cap_rows * ld4, s));
@@ -1889,7 +1898,7 @@ int wv_index_reserve(wv_index* ix, uint64_t capacity) {
     HIP_TRY(regrow(ix->pq_codes, ix->capacity * ix->pq_stride, capacity * ix->pq_stride, s));
     // bitmaps are rewritten from the host copies by the next refresh
     HIP_TRY(ix->tomb.ensure(words * 8));
-    HIP_TRY(ix->excl.ensure((words + 2) * 8));
+    HIP_TRY(ix->excl.ensure((words + 4) * 8));
     ix->has_vec.resize(words, 0);
     ix->tomb_host.resize(words, 0);
     ix->pending_host.resize(words, 0);

@@ -844,36 +844,46 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16q_kernel(H16Pa
 
 // ---------------------------------------------------------------------------
 // f16 key pass for D > 128 (C4's 768-d dot product): both operands through
-// LDS.  Workgroup = 512 threads, one per CU; tile = 128 corpus rows x 256
-// queries; wave w computes rows 64 (w & 1) .. +64 x queries 64 (w >> 1) .. +64
-// (2 x 2 accumulators of 32 x 32).  The corpus and query images are h16_index
-// images with ns 16-k steps (ns a multiple of HW_KC, zero padded), so a chunk
-// (HW_KC steps) of a 32-row group is HW_KC contiguous 1 KiB operand blocks:
-// LDS-DMA'd as is, read back as one ds_read_b128 per operand.  Chunks go
-// through a 3-stage ring (wait for chunk g, barrier, issue chunk g + 2,
-// compute g); per tile a 2-slot ring holds s|x|^2 (the L2 C-in) and the tile's
-// exclusion / allow words.  The epilogue -- mask, minima, candidate
-// extraction into the same per-lane lists as the D <= 128 pass -- runs once
-// per tile, i.e. once per ns / HW_KC chunks.
+// LDS.  Workgroup = 512 threads, one per CU; tile = 2 WR corpus rows x 256
+// queries; wave w computes rows WR (w & 1) .. +WR x queries 64 (w >> 1) .. +64
+// (WR / 32 x 2 accumulators of 32 x 32).  WR = 128 (the default): 256 x 256
+// tiles, 2-step chunks -- per MFMA half the query-side bytes and LDS-DMA ops
+// of WR = 64 (128 x 256 tiles, 4-step chunks; 48 KiB per chunk and CU for 16
+// MFMAs a wave, which left the loop waiting on the DMA: ablation, DESIGN
+// §3.2).  The corpus and query images are h16_index images with ns 16-k steps
+// (ns a multiple of HW_KC, zero padded), so a chunk (KC steps) of a 32-row
+// group is KC contiguous 1 KiB operand blocks: LDS-DMA'd as is, read back as
+// one ds_read_b128 per operand.  Chunks go through a 3-stage ring (wait for
+// chunk g, barrier, issue chunk g + 2, compute g); per tile a 2-slot ring
+// holds s|x|^2 (the L2 C-in) and the tile's exclusion / allow words.  The
+// epilogue -- mask, minima, candidate extraction into the same per-lane lists
+// as the D <= 128 pass -- runs once per tile, i.e. once per ns / KC chunks.
+template <int WR>
 struct HWStage {
-    static constexpr int A_U4 = 4 * HW_KC * 64;    // 4 row groups x HW_KC steps x 64 lanes
-    static constexpr int B_U4 = 8 * HW_KC * 64;    // 8 query groups
+    static constexpr int RG = WR / 32;              // row groups per wave
+    static constexpr int BN = 2 * WR;               // corpus rows per tile
+    static constexpr int KC = WR == 64 ? HW_KC : HW_KC / 2;   // 16-k steps per chunk
+    static constexpr int A_U4 = 2 * RG * KC * 64;   // the tile's row groups x KC steps x 64 lanes (16 KiB)
+    static constexpr int B_U4 = 8 * KC * 64;        // 8 query groups
     static constexpr int U4 = A_U4 + B_U4;
-    static constexpr int EX_U4 = HW_BN / 4 + 2;    // s|x|^2 of the tile, then excl[2] and allow[2] words
+    static constexpr int WORDS = BN / 64;           // exclusion (and allow) words per tile
+    static constexpr int EX_U4 = BN / 4 + WORDS / 2 * 2;   // s|x|^2 of the tile, then excl and allow words
+    static constexpr int OPS = 2 + KC;              // a wave's LDS-DMA blocks per chunk (extras aside)
 };
 constexpr int HW_STAGES = 3;
 
-template <bool L2>
+template <bool L2, int WR>
 __global__ __launch_bounds__(512, 1) void wv_bf_h16w_kernel(H16Params p) {
     extern __shared__ uint4 lds[];
-    using St = HWStage;
+    using St = HWStage<WR>;
+    constexpr int RG = St::RG, KC = St::KC, BN = St::BN;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int khalf = lane >> 5;
     const int l31 = lane & 31;
     const int rh = wave & 1, qq = wave >> 1;
-    const int ns = p.ns, nch = ns / HW_KC;
+    const int ns = p.ns, nch = ns / KC;
     const uint4* __restrict__ X = reinterpret_cast<const uint4*>(p.X);
     const uint4* __restrict__ Qg = reinterpret_cast<const uint4*>(p.Q);
     const bool has_allow = p.allow != nullptr;
@@ -903,23 +913,24 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16w_kernel(H16Params p) {
         const int nchunks = ntile * nch;
 
         // The chunks stream in order: chunk (t, c) into a stage of the 3-ring,
-        // with c == 0 also the tile's extras into slot t & 1.  This wave's
-        // share of a chunk is fixed: A blocks b = wave, wave + 8 (row groups
-        // wave / 4 + {0, 2}, step wave % 4) and B blocks b = 16 + wave + 8 j
-        // (query groups wave / 4 + 2 j), so their sources are one base each
-        // plus a chunk offset -- no per-block index arithmetic on the scalar
-        // unit (the round-2 loop spent 20 SALU per MFMA there, PMC).
-        const int wg4 = wave >> 2, ws4 = wave & 3;
-        const uint64_t gstride = 2ull * ns * 64;    // two row / query groups, in uint4
-        const uint4* b_src0 = Qg + (((uint64_t)qb * (HW_BQ / 32) + wg4) * ns + ws4) * 64;
-        // running sources of the next chunk to fill: +1 chunk (HW_KC KiB
-        // steps) per chunk; at a tile's end the corpus side moves on to the
-        // next tile's row groups (4 ns steps per tile: + 3 ns past the last
-        // chunk) and the query side starts over
-        const uint4* a_cur = X + (((uint64_t)t_begin * 4 + wg4) * ns + ws4) * 64;
+        // with c == 0 also the tile's extras into slot t & 1.  A chunk is 16
+        // corpus blocks (block b = group * KC + step) and 8 KC query blocks;
+        // this wave's share is fixed: blocks b = wave + 8 j (group wave / KC +
+        // (8 / KC) j, step wave % KC) -- j < 2 on the corpus side, j < KC on
+        // the query side -- so their sources are one base each plus a chunk
+        // offset: no per-block index arithmetic on the scalar unit (the
+        // round-2 loop spent 20 SALU per MFMA there, PMC).
+        const int wg = wave / KC, wsk = wave % KC;
+        const uint64_t gstride = (uint64_t)(8 / KC) * ns * 64;   // 8 / KC groups, in uint4
+        const uint4* b_src0 = Qg + (((uint64_t)qb * (HW_BQ / 32) + wg) * ns + wsk) * 64;
+        // running sources of the next chunk to fill: +1 chunk (KC KiB steps)
+        // per chunk; at a tile's end the corpus side moves on to the next
+        // tile's row groups (2 RG ns steps per tile: + (2 RG - 1) ns past the
+        // last chunk) and the query side starts over
+        const uint4* a_cur = X + (((uint64_t)t_begin * 2 * RG + wg) * ns + wsk) * 64;
         const uint4* b_cur = b_src0;
         int ft = 0, fc = 0;   // the next chunk to fill
-        auto fill_next = [&](int stage) -> int {
+        auto fill_next = [&](int stage) {
             // (ft, fc are wave-uniform; the divergence analysis loses that
             // through the lambda's captured state)
             ft = __builtin_amdgcn_readfirstlane(ft);
@@ -931,41 +942,37 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16w_kernel(H16Params p) {
             // which must keep the LDS-DMA bases in SGPRs)
             const uint4* a = uniform_ptr(a_cur);
             const uint4* b = uniform_ptr(b_cur);
-            int n = 0;
 #ifndef WV_H16W_ABLATE_NO_A
             glds16s(a, (uint32_t)(lane * 16), dst);
             glds16s(uniform_ptr(a + gstride), (uint32_t)(lane * 16), dst + 8 * 1024);
-            n += 2;
 #endif
 #ifndef WV_H16W_ABLATE_NO_B
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-                glds16s(uniform_ptr(b + j * gstride), (uint32_t)(lane * 16), dst + (16 + 8 * j) * 1024);
-            n += 4;
+            for (int j = 0; j < KC; ++j)
+                glds16s(uniform_ptr(b + j * gstride), (uint32_t)(lane * 16), dst + (uint32_t)(St::A_U4 * 16 + 8 * j * 1024));
 #endif
             if (fc == 0) {
                 const uint32_t xd = ex0 + (uint32_t)((ft & 1) * St::EX_U4 * 16);
                 if (wave == 0 && L2) {
-                    glds4(p.xns + tile * HW_BN + lane, xd);
-                    glds4(p.xns + tile * HW_BN + 64 + lane, xd + 256);
-                    n += 2;
+#pragma unroll
+                    for (int j = 0; j < BN / 64; ++j) glds4(p.xns + tile * BN + 64 * j + lane, xd + 256 * j);
                 } else if (wave == 1) {
-                    // lanes 0-3: the tile's two exclusion words, 4-7: its two allow words
-                    const uint32_t* w = lane < 4 ? reinterpret_cast<const uint32_t*>(p.excl + 2 * tile) + lane
-                                                 : reinterpret_cast<const uint32_t*>(p.allow + 2 * tile) + (lane - 4);
-                    if (lane < 4 || (lane < 8 && has_allow)) glds4(w, xd + (HW_BN / 4) * 16);
-                    n += 1;
+                    // lanes 0 .. 2 WORDS - 1: the tile's exclusion words (as
+                    // u32 halves), then as many lanes for its allow words
+                    const uint32_t* w = lane < 2 * St::WORDS
+                                            ? reinterpret_cast<const uint32_t*>(p.excl + St::WORDS * tile) + lane
+                                            : reinterpret_cast<const uint32_t*>(p.allow + St::WORDS * tile) + (lane - 2 * St::WORDS);
+                    if (lane < 2 * St::WORDS || (lane < 4 * St::WORDS && has_allow)) glds4(w, xd + (BN / 4) * 16);
                 }
             }
-            a_cur = a + HW_KC * 64;
-            b_cur = b + HW_KC * 64;
+            a_cur = a + KC * 64;
+            b_cur = b + KC * 64;
             if (++fc == nch) {
                 fc = 0;
                 ++ft;
-                a_cur += 3ull * ns * 64;
+                a_cur += (uint64_t)(2 * RG - 1) * ns * 64;
                 b_cur = b_src0;
             }
-            return n;
         };
 
         float l0d[BF_KP], l1d[BF_KP];
@@ -1011,7 +1018,7 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16w_kernel(H16Params p) {
             if (jq0 < p.nq) tau0 = fminf(tau0, h16_key_dec(__atomic_load_n(&p.gtau[jq0], __ATOMIC_RELAXED)));
             if (jq1 < p.nq) tau1 = fminf(tau1, h16_key_dec(__atomic_load_n(&p.gtau[jq1], __ATOMIC_RELAXED)));
         };
-        floatx16 acc00, acc01, acc10, acc11;
+        floatx16 acc[RG][2];
         auto min16 = [&](const floatx16& A) {
             float m0 = fminf(fminf(A[0], A[1]), A[2]), m1 = fminf(fminf(A[3], A[4]), A[5]);
             float m2 = fminf(fminf(A[6], A[7]), A[8]), m3 = fminf(fminf(A[9], A[10]), A[11]);
@@ -1025,52 +1032,66 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16w_kernel(H16Params p) {
         int t = 0, c = 0, stg = 0;   // the chunk computed: (tile, chunk), its stage
         for (int g = 0; g < nchunks; ++g) {
             // chunk g landed (g + 1 may stay in flight), for every wave: at
-            // most 6 of this wave's ops still outstanding -- chunk g + 1's
-            // blocks are its first 6 (its extras, issued after them, may then
-            // have to land as well: a chunk's compute later, long done)
+            // most OPS of this wave's ops still outstanding -- chunk g + 1's
+            // blocks are its first OPS (its extras, issued after them, may
+            // then have to land as well: a chunk's compute later, long done)
 #if defined(WV_H16W_ABLATE_NO_A) && defined(WV_H16W_ABLATE_NO_B)
             vm_wait(0);
 #elif defined(WV_H16W_ABLATE_NO_A)
-            if (g + 1 < nchunks) vm_wait(4);
+            if (g + 1 < nchunks) vm_wait(KC);
             else vm_wait(0);
 #elif defined(WV_H16W_ABLATE_NO_B)
             if (g + 1 < nchunks) vm_wait(2);
             else vm_wait(0);
 #else
-            if (g + 1 < nchunks) vm_wait(6);
+            if (g + 1 < nchunks) vm_wait(St::OPS);
             else vm_wait(0);
 #endif
             block_barrier();
+#ifndef WV_H16W_FILL_MID
             if (g + 2 < nchunks) fill_next(stg == 0 ? 2 : stg - 1);
+#endif
             const uint4* st = lds + stg * St::U4;
             if (c == 0) {
                 // C-in: s|x|^2 of the wave's rows (L2) or zero
                 if (L2) {
-                    const float* xn = reinterpret_cast<const float*>(ex_lds + (t & 1) * St::EX_U4) + 64 * rh;
+                    const float* xn = reinterpret_cast<const float*>(ex_lds + (t & 1) * St::EX_U4) + WR * rh;
 #pragma unroll
-                    for (int g4 = 0; g4 < 4; ++g4) {
-                        const float4 v0 = *reinterpret_cast<const float4*>(xn + 4 * khalf + 8 * g4);
-                        const float4 v1 = *reinterpret_cast<const float4*>(xn + 32 + 4 * khalf + 8 * g4);
-                        acc00[4 * g4] = v0.x; acc00[4 * g4 + 1] = v0.y; acc00[4 * g4 + 2] = v0.z; acc00[4 * g4 + 3] = v0.w;
-                        acc10[4 * g4] = v1.x; acc10[4 * g4 + 1] = v1.y; acc10[4 * g4 + 2] = v1.z; acc10[4 * g4 + 3] = v1.w;
-                    }
-                    acc01 = acc00;
-                    acc11 = acc10;
+                    for (int i = 0; i < RG; ++i)
+#pragma unroll
+                        for (int g4 = 0; g4 < 4; ++g4) {
+                            const float4 v = *reinterpret_cast<const float4*>(xn + 32 * i + 4 * khalf + 8 * g4);
+                            acc[i][0][4 * g4] = v.x; acc[i][0][4 * g4 + 1] = v.y;
+                            acc[i][0][4 * g4 + 2] = v.z; acc[i][0][4 * g4 + 3] = v.w;
+                        }
+#pragma unroll
+                    for (int i = 0; i < RG; ++i) acc[i][1] = acc[i][0];
                 } else {
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) { acc00[r] = 0.f; acc01[r] = 0.f; acc10[r] = 0.f; acc11[r] = 0.f; }
+                    for (int i = 0; i < RG; ++i)
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) { acc[i][0][r] = 0.f; acc[i][1][r] = 0.f; }
                 }
             }
 #pragma unroll
-            for (int k = 0; k < HW_KC; ++k) {
-                const half8 a0 = __builtin_bit_cast(half8, st[((2 * rh) * HW_KC + k) * 64 + lane]);
-                const half8 a1 = __builtin_bit_cast(half8, st[((2 * rh + 1) * HW_KC + k) * 64 + lane]);
-                const half8 b0 = __builtin_bit_cast(half8, st[St::A_U4 + ((2 * qq) * HW_KC + k) * 64 + lane]);
-                const half8 b1 = __builtin_bit_cast(half8, st[St::A_U4 + ((2 * qq + 1) * HW_KC + k) * 64 + lane]);
-                acc00 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b0, acc00, 0, 0, 0);
-                acc01 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b1, acc01, 0, 0, 0);
-                acc10 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b0, acc10, 0, 0, 0);
-                acc11 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b1, acc11, 0, 0, 0);
+            for (int k = 0; k < KC; ++k) {
+                const half8 b0 = __builtin_bit_cast(half8, st[St::A_U4 + ((2 * qq) * KC + k) * 64 + lane]);
+                const half8 b1 = __builtin_bit_cast(half8, st[St::A_U4 + ((2 * qq + 1) * KC + k) * 64 + lane]);
+#pragma unroll
+                for (int i = 0; i < RG; ++i) {
+                    const half8 a = __builtin_bit_cast(half8, st[((RG * rh + i) * KC + k) * 64 + lane]);
+                    acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b0, acc[i][0], 0, 0, 0);
+                    acc[i][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b1, acc[i][1], 0, 0, 0);
+                }
+#ifdef WV_H16W_FILL_MID
+                // (the next fill between this chunk's MFMAs, not beside the
+                // partner wave's fill after the barrier)
+                if (k == KC / 2 - 1 || KC == 1) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (g + 2 < nchunks) fill_next(stg == 0 ? 2 : stg - 1);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+#endif
             }
             const int tc = t;   // (the chunk just computed)
             stg = stg == 2 ? 0 : stg + 1;
@@ -1079,36 +1100,45 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16w_kernel(H16Params p) {
             ++t;
             // ---- tile epilogue ----
             const uint64_t tile = t_begin + tc;
-            const uint32_t* w = reinterpret_cast<const uint32_t*>(ex_lds + (tc & 1) * St::EX_U4 + HW_BN / 4);
-            // the wave's 64 rows are the tile's word rh
-            uint64_t okw = ~((uint64_t)w[2 * rh] | ((uint64_t)w[2 * rh + 1] << 32));
-            if (has_allow) okw &= (uint64_t)w[4 + 2 * rh] | ((uint64_t)w[4 + 2 * rh + 1] << 32);
-            const uint64_t row0 = tile * HW_BN + 64 * rh;
-            if (row0 + 64 > p.N) okw &= p.N > row0 ? ((1ull << (p.N - row0)) - 1) : 0ull;
-            if (okw != ~0ull) {
-                const uint64_t o0 = (jq0 < p.nq ? okw : 0ull) >> (4 * khalf);
-                const uint64_t o1 = (jq1 < p.nq ? okw : 0ull) >> (4 * khalf);
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int bit = (r & 3) + 8 * (r >> 2);
-                    acc00[r] = (o0 >> bit) & 1u ? acc00[r] : INF;
-                    acc01[r] = (o1 >> bit) & 1u ? acc01[r] : INF;
-                    acc10[r] = (o0 >> (32 + bit)) & 1u ? acc10[r] : INF;
-                    acc11[r] = (o1 >> (32 + bit)) & 1u ? acc11[r] : INF;
-                }
-            }
-            const uint32_t rb0 = (uint32_t)row0 + 4 * khalf;
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(ex_lds + (tc & 1) * St::EX_U4 + BN / 4);
+            const uint64_t row0 = tile * BN + WR * rh;
             const float pt0 = fminf(__shfl_xor(l0d[BF_KP - 1], 32, 64), tau0);
             const float pt1 = fminf(__shfl_xor(l1d[BF_KP - 1], 32, 64), tau1);
-            float m;
 #ifdef WV_H16W_ABLATE_NO_EPI
-            if (acc00[0] == 1234.5f && acc01[0] == acc10[0] && acc11[0] == pt0 + pt1) l0d[0] = 0.f;
+            if (acc[0][0][0] == 1234.5f && acc[0][1][0] == pt0 + pt1) l0d[0] = 0.f;
             continue;
 #endif
-            m = min16(acc00); if (m <= fminf(l0d[BF_KP - 1], pt0)) split_extract16(m, acc00, l0d, l0i, pt0, rb0);
-            m = min16(acc10); if (m <= fminf(l0d[BF_KP - 1], pt0)) split_extract16(m, acc10, l0d, l0i, pt0, rb0 + 32);
-            m = min16(acc01); if (m <= fminf(l1d[BF_KP - 1], pt1)) split_extract16(m, acc01, l1d, l1i, pt1, rb0);
-            m = min16(acc11); if (m <= fminf(l1d[BF_KP - 1], pt1)) split_extract16(m, acc11, l1d, l1i, pt1, rb0 + 32);
+            // the wave's rows are the tile's words RG / 2 rh ..: 64 rows (two
+            // row groups) per word
+#pragma unroll
+            for (int h = 0; h < RG / 2; ++h) {
+                const int wi = RG / 2 * rh + h;
+                uint64_t okw = ~((uint64_t)w[2 * wi] | ((uint64_t)w[2 * wi + 1] << 32));
+                if (has_allow) okw &= (uint64_t)w[2 * St::WORDS + 2 * wi] | ((uint64_t)w[2 * St::WORDS + 2 * wi + 1] << 32);
+                const uint64_t r0 = row0 + 64 * h;
+                if (r0 + 64 > p.N) okw &= p.N > r0 ? ((1ull << (p.N - r0)) - 1) : 0ull;
+                floatx16& A0 = acc[2 * h][0];
+                floatx16& A1 = acc[2 * h][1];
+                floatx16& B0 = acc[2 * h + 1][0];
+                floatx16& B1 = acc[2 * h + 1][1];
+                if (okw != ~0ull) {
+                    const uint64_t o = okw >> (4 * khalf);
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int bit = (r & 3) + 8 * (r >> 2);
+                        A0[r] = (o >> bit) & 1u ? A0[r] : INF;
+                        A1[r] = (o >> bit) & 1u ? A1[r] : INF;
+                        B0[r] = (o >> (32 + bit)) & 1u ? B0[r] : INF;
+                        B1[r] = (o >> (32 + bit)) & 1u ? B1[r] : INF;
+                    }
+                }
+                const uint32_t rb = (uint32_t)r0 + 4 * khalf;
+                float m;
+                m = min16(A0); if (m <= fminf(l0d[BF_KP - 1], pt0)) split_extract16(m, A0, l0d, l0i, pt0, rb);
+                m = min16(B0); if (m <= fminf(l0d[BF_KP - 1], pt0)) split_extract16(m, B0, l0d, l0i, pt0, rb + 32);
+                m = min16(A1); if (m <= fminf(l1d[BF_KP - 1], pt1)) split_extract16(m, A1, l1d, l1i, pt1, rb);
+                m = min16(B1); if (m <= fminf(l1d[BF_KP - 1], pt1)) split_extract16(m, B1, l1d, l1i, pt1, rb + 32);
+            }
             // every tile while the lists fill, then every 4th
             if (running && (tc < 8 || (tc & 3) == 3)) publish();
         }
@@ -1561,9 +1591,18 @@ hipError_t wv_launch_bf_h16w(const wv::H16Params* p, hipStream_t s) {
         return hipErrorInvalidValue;
     const bool l2 = p->metric == WV_METRIC_L2;
     if (l2 && !p->xns) return hipErrorInvalidValue;
-    const size_t lds = ((size_t)wv::HW_STAGES * wv::HWStage::U4 + 2 * wv::HWStage::EX_U4) * 16;
-    if (l2) hipLaunchKernelGGL((wv::wv_bf_h16w_kernel<true>), dim3(nb), dim3(512), lds, s, *p);
-    else hipLaunchKernelGGL((wv::wv_bf_h16w_kernel<false>), dim3(nb), dim3(512), lds, s, *p);
+    if (p->wide_rows != 64 && p->wide_rows != 128) return hipErrorInvalidValue;
+    if (p->wide_rows == 64) {
+        using St = wv::HWStage<64>;
+        const size_t lds = ((size_t)wv::HW_STAGES * St::U4 + 2 * St::EX_U4) * 16;
+        if (l2) hipLaunchKernelGGL((wv::wv_bf_h16w_kernel<true, 64>), dim3(nb), dim3(512), lds, s, *p);
+        else hipLaunchKernelGGL((wv::wv_bf_h16w_kernel<false, 64>), dim3(nb), dim3(512), lds, s, *p);
+    } else {
+        using St = wv::HWStage<128>;
+        const size_t lds = ((size_t)wv::HW_STAGES * St::U4 + 2 * St::EX_U4) * 16;
+        if (l2) hipLaunchKernelGGL((wv::wv_bf_h16w_kernel<true, 128>), dim3(nb), dim3(512), lds, s, *p);
+        else hipLaunchKernelGGL((wv::wv_bf_h16w_kernel<false, 128>), dim3(nb), dim3(512), lds, s, *p);
+    }
     return hipGetLastError();
 }
 

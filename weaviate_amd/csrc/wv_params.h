@@ -169,13 +169,14 @@ struct H16Params {
     int xslot;                // 1: use gslot instead of the gtau publish
     int stagger;              // 32x32x16 8-wave pass: waves 4-7 half a tile behind (4-stage ring)
     int ns;                   // 16-k steps of the images (the wide-D kernel: a multiple of HW_KC)
+    int wide_rows;            // the wide-D kernel's rows per wave: 128 (256-row tiles) or 64 (128-row tiles)
 };
 
 // ---- f16 key pass for D > 128 (wv_bf_h16w_kernel, wv_h16.hip) --------------
 // Both operands stream through LDS in 64-k chunks (3 stages): 128 corpus rows
 // x 256 queries per 512-thread workgroup, 64 x 64 per wave; the tile epilogue
 // (mask, minima, extraction) runs once per D / 64 chunks.
-constexpr int HW_BN = 128;    // corpus rows per tile
+constexpr int HW_BN = 256;    // corpus rows per tile (wide_rows 128; 128 at wide_rows 64)
 constexpr int HW_BQ = 256;    // queries per block
 constexpr int HW_KC = 4;      // 16-k steps per chunk
 constexpr int HW_PROD = 4;    // lists per query per slot: 2 row halves x 2 lane halves
