@@ -702,6 +702,7 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
         const wv::BfSchedule ss = wv::bf_schedule(nq, nts * wv::H_BN, target(nts), bq, wv::H_BN);
         HIP_TRY(ix->cand_d.ensure((size_t)nq * ss.n_slots * seed_prod * 4));
         hp.ntiles = ss.ntiles;
+        hp.ntiles_real = ss.ntiles;
         hp.units_per_block = ss.units_per_block;
         hp.n_slots = ss.n_slots;
         hp.tile_stride = sample;
@@ -733,12 +734,21 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
         HIP_TRY(wv_launch_h16_seed(&sp, s));
         TREC(7);
     }
-    const wv::BfSchedule sch = wv::bf_schedule(nq, N, target(ntl), bq, tile_rows);
+    // the wide pass: query blocks cut at the same tile offsets where that
+    // costs no work (bf_schedule_aligned; WV_H16_ALIGNED=0: the flat schedule)
+    const char* ae = std::getenv("WV_H16_ALIGNED");
+    wv::BfSchedule sch{};
+    // (WV_H16_ALIGNED=2: also the 8-wave D <= 128 pass, at any cost -- for measurements)
+    const int aligned = ae ? std::atoi(ae) : 1;
+    if ((wd && !wide && aligned >= 1) || (aligned == 2 && !wd && !quad && !wide && seed))
+        sch = wv::bf_schedule_aligned(nq, N, target(ntl), bq, tile_rows, aligned == 2);
+    if (sch.n_blocks == 0) sch = wv::bf_schedule(nq, N, target(ntl), bq, tile_rows);
     if (wide && (uint64_t)sch.n_slots * prod * kp > (uint64_t)wv::FINW_NE)
         return fail(WV_ESTATE, "run_h16: too many lists for the wide finalize");
     HIP_TRY(ix->cand_d.ensure((size_t)nq * sch.n_slots * prod * kp * 4));
     HIP_TRY(ix->cand_id.ensure((size_t)nq * sch.n_slots * prod * kp * 4));
     hp.ntiles = sch.ntiles;
+    hp.ntiles_real = ntl;
     hp.units_per_block = sch.units_per_block;
     hp.n_slots = sch.n_slots;
     hp.tile_stride = 1;

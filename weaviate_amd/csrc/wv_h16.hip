@@ -120,7 +120,9 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
         const int slot = lb - bf_first_block(qb, p.ntiles, p.units_per_block);
         const int jq0 = qb * BQ + wave * 64 + l31;
         const int jq1 = jq0 + 32;
-        const int ntile = (int)(t_end - t_begin);
+        // (an aligned schedule's grid pads the corpus's tiles: no work past them)
+        const uint64_t t_stop = t_end < p.ntiles_real ? t_end : p.ntiles_real;
+        const int ntile = t_stop > t_begin ? (int)(t_stop - t_begin) : 0;
 
         // the wave's 64 queries as B operands, for the whole segment
         uint4 bq0[NS], bq1[NS];
@@ -909,7 +911,9 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16w_kernel(H16Params p) {
         const int slot = lb - bf_first_block(qb, p.ntiles, p.units_per_block);
         const int jq0 = qb * HW_BQ + qq * 64 + l31;
         const int jq1 = jq0 + 32;
-        const int ntile = (int)(t_end - t_begin);
+        // (an aligned schedule's grid pads the corpus's tiles: no work past them)
+        const uint64_t t_stop = t_end < p.ntiles_real ? t_end : p.ntiles_real;
+        const int ntile = t_stop > t_begin ? (int)(t_stop - t_begin) : 0;
         const int nchunks = ntile * nch;
 
         // The chunks stream in order: chunk (t, c) into a stage of the 3-ring,
@@ -996,6 +1000,12 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16w_kernel(H16Params p) {
             if (jq1 < p.nq) marg1 = p.marg[jq1];
         }
         const int ia = (p.kth + 1) >> 1, ib = p.kth >> 1;
+        // this wave's gtau return slot (64 words after the extras) and its
+        // source word (clamped for the padding columns, whose tau stays -inf)
+        const unsigned int* tau_lds = reinterpret_cast<const unsigned int*>(ex_lds + 2 * St::EX_U4) + 64 * wave;
+        const uint32_t tau_dst = ex0 + (uint32_t)(2 * St::EX_U4 * 16 + 256 * wave);
+        const int tau_src = min(jq0 - l31 + lane, p.nq - 1);
+        if (running) reinterpret_cast<unsigned int*>(lds + HW_STAGES * St::U4 + 2 * St::EX_U4)[64 * wave + lane] = 0xFFFFFFFFu;
         auto publish = [&] {
             int va = ia - 1, vb = ib - 1;
             asm volatile("" : "+v"(va), "+v"(vb));   // (select chains over a VGPR index)
@@ -1015,8 +1025,14 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16w_kernel(H16Params p) {
                 if (jq0 < p.nq && k0 < FLT_MAX) atomicMin(&p.gtau[jq0], h16_key_enc(k0 + marg0 + u4 * (fabsf(k0) + marg0)));
                 if (jq1 < p.nq && k1 < FLT_MAX) atomicMin(&p.gtau[jq1], h16_key_enc(k1 + marg1 + u4 * (fabsf(k1) + marg1)));
             }
-            if (jq0 < p.nq) tau0 = fminf(tau0, h16_key_dec(__atomic_load_n(&p.gtau[jq0], __ATOMIC_RELAXED)));
-            if (jq1 < p.nq) tau1 = fminf(tau1, h16_key_dec(__atomic_load_n(&p.gtau[jq1], __ATOMIC_RELAXED)));
+            // every slot's published thresholds come back by an LDS-DMA of the
+            // wave's 64 gtau words (lane l: query jq0 - l31 + l), read at the
+            // next publish: a plain load here would be waited for with
+            // vmcnt(0), i.e. behind the chunk DMAs in flight (the compiler does
+            // not see them) -- a drain of the operand stream per publish
+            tau0 = fminf(tau0, h16_key_dec(tau_lds[l31]));
+            tau1 = fminf(tau1, h16_key_dec(tau_lds[32 + l31]));
+            glds4_dev(p.gtau + tau_src, tau_dst);
         };
         floatx16 acc[RG][2];
         auto min16 = [&](const floatx16& A) {
@@ -1048,7 +1064,7 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16w_kernel(H16Params p) {
             else vm_wait(0);
 #endif
             block_barrier();
-#ifndef WV_H16W_FILL_MID
+#ifdef WV_H16W_FILL_EARLY
             if (g + 2 < nchunks) fill_next(stg == 0 ? 2 : stg - 1);
 #endif
             const uint4* st = lds + stg * St::U4;
@@ -1083,9 +1099,10 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16w_kernel(H16Params p) {
                     acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b0, acc[i][0], 0, 0, 0);
                     acc[i][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b1, acc[i][1], 0, 0, 0);
                 }
-#ifdef WV_H16W_FILL_MID
-                // (the next fill between this chunk's MFMAs, not beside the
-                // partner wave's fill after the barrier)
+#ifndef WV_H16W_FILL_EARLY
+                // the next fill between this chunk's MFMAs, not beside the
+                // partner wave's fill after the barrier (2.33 -> 2.23 ms per
+                // C4-shaped pass, profiles/r03_h16w_fill_schedule_ablation.log)
                 if (k == KC / 2 - 1 || KC == 1) {
                     __builtin_amdgcn_sched_barrier(0);
                     if (g + 2 < nchunks) fill_next(stg == 0 ? 2 : stg - 1);
@@ -1105,7 +1122,12 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16w_kernel(H16Params p) {
             const float pt0 = fminf(__shfl_xor(l0d[BF_KP - 1], 32, 64), tau0);
             const float pt1 = fminf(__shfl_xor(l1d[BF_KP - 1], 32, 64), tau1);
 #ifdef WV_H16W_ABLATE_NO_EPI
-            if (acc[0][0][0] == 1234.5f && acc[0][1][0] == pt0 + pt1) l0d[0] = 0.f;
+            {
+                float z = pt0 + pt1;
+#pragma unroll
+                for (int i = 0; i < RG; ++i) z += acc[i][0][0] + acc[i][1][0];
+                if (z == 1234.5f) l0d[0] = 0.f;
+            }
             continue;
 #endif
             // the wave's rows are the tile's words RG / 2 rh ..: 64 rows (two
@@ -1594,12 +1616,12 @@ hipError_t wv_launch_bf_h16w(const wv::H16Params* p, hipStream_t s) {
     if (p->wide_rows != 64 && p->wide_rows != 128) return hipErrorInvalidValue;
     if (p->wide_rows == 64) {
         using St = wv::HWStage<64>;
-        const size_t lds = ((size_t)wv::HW_STAGES * St::U4 + 2 * St::EX_U4) * 16;
+        const size_t lds = ((size_t)wv::HW_STAGES * St::U4 + 2 * St::EX_U4) * 16 + 8 * 256;   // + the gtau return slots
         if (l2) hipLaunchKernelGGL((wv::wv_bf_h16w_kernel<true, 64>), dim3(nb), dim3(512), lds, s, *p);
         else hipLaunchKernelGGL((wv::wv_bf_h16w_kernel<false, 64>), dim3(nb), dim3(512), lds, s, *p);
     } else {
         using St = wv::HWStage<128>;
-        const size_t lds = ((size_t)wv::HW_STAGES * St::U4 + 2 * St::EX_U4) * 16;
+        const size_t lds = ((size_t)wv::HW_STAGES * St::U4 + 2 * St::EX_U4) * 16 + 8 * 256;   // + the gtau return slots
         if (l2) hipLaunchKernelGGL((wv::wv_bf_h16w_kernel<true, 128>), dim3(nb), dim3(512), lds, s, *p);
         else hipLaunchKernelGGL((wv::wv_bf_h16w_kernel<false, 128>), dim3(nb), dim3(512), lds, s, *p);
     }

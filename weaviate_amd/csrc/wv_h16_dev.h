@@ -47,6 +47,13 @@ __device__ __forceinline__ void glds4(const void* src, uint32_t lds_wave_base) {
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep) : "v"(src), "s"(lds_wave_base) : "memory");
 }
+// the same at device scope (sc1: past the CU's L1, so a word other CUs
+// update with atomics is read from L2)
+__device__ __forceinline__ void glds4_dev(const void* src, uint32_t lds_wave_base) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off sc1\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(src), "s"(lds_wave_base) : "memory");
+}
 // wait until at most n of this wave's vector-memory ops are outstanding
 __device__ __forceinline__ void vm_wait(int n) {
     switch (n) {

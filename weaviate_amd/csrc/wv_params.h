@@ -79,6 +79,29 @@ inline BfSchedule bf_schedule(int nq, uint64_t N, int target_blocks, int bq = BF
     s.n_slots = (int)((s.ntiles + s.units_per_block - 1) / s.units_per_block) + 1;
     return s;
 }
+// The same schedule with every query block cut at the same tile offsets (S
+// slots of U tiles; the unit grid per query block is S U >= the corpus's tiles,
+// the padding units empty), so that the blocks of all query blocks that scan a
+// tile start and run together -- with the XCD block order (run_h16), in one
+// XCD's L2.  Used where it costs no work: S = target / nqb slots, U no larger
+// than the flat schedule's run (else n_blocks = 0: use bf_schedule).
+inline BfSchedule bf_schedule_aligned(int nq, uint64_t N, int target_blocks, int bq, int tile_rows,
+                                      bool any_cost = false) {
+    BfSchedule s{};
+    s.bq = bq;
+    const uint64_t nqb = (uint64_t)(nq + bq - 1) / bq;
+    const uint64_t nt = (N + tile_rows - 1) / tile_rows;
+    const uint64_t S = nqb ? (uint64_t)(target_blocks > 0 ? target_blocks : 1) / nqb : 0;
+    if (nqb < 2 || S < 1 || nt < S) return s;
+    const uint64_t U = (nt + S - 1) / S;
+    const uint64_t flat = (nqb * nt + (uint64_t)target_blocks - 1) / (uint64_t)target_blocks;
+    if (U > flat + flat / 64 && !any_cost) return s;
+    s.units_per_block = U;
+    s.ntiles = S * U;
+    s.n_blocks = (int)(nqb * S);
+    s.n_slots = (int)S + 1;
+    return s;
+}
 #if defined(__HIPCC__)
 __host__ __device__
 #endif
@@ -149,6 +172,7 @@ struct H16Params {
     int nq, metric;
     int n_qblocks, n_slots;
     uint64_t ntiles, units_per_block;   // ntiles: tiles scanned (the sample's when tile_stride > 1)
+    uint64_t ntiles_real;     // the wide-D pass: the corpus's tiles (ntiles, the unit grid per query block, may pad it)
     int tile_stride;          // corpus tile = scanned tile * tile_stride (seed pre-pass)
     uint64_t clean_tiles;     // corpus tiles [0, clean_tiles) have no excluded row (no allow list either): no mask
     int locality;             // bit 1: XCD-contiguous workgroup ids
