@@ -256,7 +256,7 @@ struct wv_index {
     // the f16 pass's block order (block_order), cached for its schedule
     DevBuf blk_order;
     std::vector<int> blk_order_host;
-    uint64_t blk_key[3] = {0, 0, 0};
+    uint64_t blk_key[4] = {0, 0, 0, 0};
     DevBuf qmax_part;       // per-block max |q_i| of the query-norm pass
     float maxnorm_host = 0.f;   // max |x| (rounded up), cached after every row write
     DevBuf xnorm;           // [capacity]
@@ -537,23 +537,30 @@ int run_pq_flat(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d
 // part of the corpus at the same time -- a tile then comes into that XCD's L2
 // once per pass instead of once per query block.  nullptr: the identity
 // (WV_H16_BLOCK_ORDER=0, or a single query block).
-int block_order(wv_index* ix, uint64_t nqb, const wv::BfSchedule& sch, hipStream_t s, const int** out) {
+// rotated: the tiles of query block qb are rotated by qb ntiles mod U (the
+// D <= 128 pass's locality bit 2), so a block's first tile is (slot U) mod ntiles.
+int block_order(wv_index* ix, uint64_t nqb, const wv::BfSchedule& sch, hipStream_t s, const int** out,
+                bool rotated = false) {
     *out = nullptr;
     const char* e = std::getenv("WV_H16_BLOCK_ORDER");
     if ((e && std::atoi(e) == 0) || nqb < 2 || sch.n_blocks < 16) return WV_OK;
-    const uint64_t key[3] = {nqb, sch.ntiles, sch.units_per_block};
-    if (!(ix->blk_key[0] == key[0] && ix->blk_key[1] == key[1] && ix->blk_key[2] == key[2])) {
+    const uint64_t key[4] = {nqb, sch.ntiles, sch.units_per_block, rotated ? 1u : 0u};
+    if (!std::equal(key, key + 4, ix->blk_key)) {
         const int nb = sch.n_blocks;
+        const uint64_t U = sch.units_per_block, nt = sch.ntiles;
+        auto first_tile = [&](int lb) -> uint64_t {
+            if (!rotated) return (uint64_t)lb * U % nt;
+            const uint64_t qb = (uint64_t)lb * U / nt;
+            return ((uint64_t)lb - (uint64_t)wv::bf_first_block(qb, nt, U)) * U % nt;
+        };
         std::vector<int>& ord = ix->blk_order_host;
         ord.resize(nb);
         for (int i = 0; i < nb; ++i) ord[i] = i;
-        std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) {
-            return (uint64_t)a * sch.units_per_block % sch.ntiles < (uint64_t)b * sch.units_per_block % sch.ntiles;
-        });
+        std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return first_tile(a) < first_tile(b); });
         HIP_TRY(ix->blk_order.ensure((size_t)nb * 4));
         HIP_TRY(hipMemcpyAsync(ix->blk_order.p, ord.data(), (size_t)nb * 4, hipMemcpyHostToDevice, s));
         HIP_TRY(hipStreamSynchronize(s));   // (pageable source; a later schedule rewrites it)
-        std::copy(key, key + 3, ix->blk_key);
+        std::copy(key, key + 4, ix->blk_key);
     }
     *out = ix->blk_order.as<int>();
     return WV_OK;
@@ -785,7 +792,12 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     }
     hp.out_d = ix->cand_d.as<float>();
     hp.out_id = ix->cand_id.as<uint32_t>();
-    if (int rc = block_order(ix, (uint64_t)nqb, sch, s, &hp.block_order)) return rc;
+    // the 8-wave D <= 128 pass on the flat schedule: tiles rotated per query
+    // block (locality bit 2; opt-in WV_H16_ROTATE=1)
+    const char* re = std::getenv("WV_H16_ROTATE");
+    const bool rotate = !wd && !quad && !solo && waves == 8 && nqb >= 2 && sch.ntiles == ntl && re && std::atoi(re) == 1;
+    if (rotate) hp.locality |= 2;
+    if (int rc = block_order(ix, (uint64_t)nqb, sch, s, &hp.block_order, rotate)) return rc;
     TREC(0);
     HIP_TRY(wd ? wv_launch_bf_h16w(&hp, s)
                : solo ? wv_launch_bf_h16s(&hp, ns / 2, 0, s)

@@ -97,13 +97,22 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
     };
 
     // the tiles of stage-group g (TPS consecutive tiles) into LDS stage g % 3
+    // (locality bit 2: a query block's tiles rotated by its first block's
+    // offset, so that every query block's slot boundaries fall on the same
+    // tiles -- the blocks scanning a tile together, in one XCD's L2 with the
+    // block order; shift 0 otherwise)
+    uint64_t shift = 0;
+    auto phys = [&](uint64_t t) {
+        const uint64_t v = t + shift;
+        return v >= p.ntiles ? v - p.ntiles : v;
+    };
     auto fill_group = [&](uint64_t t_begin, int g, int ntile) {
         const int st = g % NSTG;
         int n = 0;
 #pragma unroll
         for (int j = 0; j < TPS; ++j) {
             const int t = g * TPS + j;
-            if (t < ntile) { fill(t_begin + t, st * TPS + j); ++n; }
+            if (t < ntile) { fill(phys(t_begin + t), st * TPS + j); ++n; }
         }
         return n * n_ops;   // this wave's DMA ops for the group
     };
@@ -118,6 +127,7 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
         if (t_end > p.ntiles) t_end = p.ntiles;
         u += t_end - t_begin;
         const int slot = lb - bf_first_block(qb, p.ntiles, p.units_per_block);
+        shift = (p.locality & 2) ? (uint64_t)qb * p.ntiles % p.units_per_block % p.ntiles : 0;
         const int jq0 = qb * BQ + wave * 64 + l31;
         const int jq1 = jq0 + 32;
         // (an aligned schedule's grid pads the corpus's tiles: no work past them)
@@ -383,7 +393,7 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
         block_barrier();          // everyone's
         if (ntile > 0) {
             mfma_half(tile_lds(0), 0, acc00, acc01, [] {});
-            need_mask = tile_ok(t_begin, okw);
+            need_mask = tile_ok(phys(t_begin), okw);
         }
         // a full group's DMA ops of this wave: a constant per wave class when
         // the image shares divide evenly (the usual D = 64 / 128), so the
@@ -392,10 +402,14 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
         constexpr int SHARE = (St::IMG_U4 / 64) / WAVES;
         const bool xns_wave = wave == 0 && L2;
         int slot_t = 0;   // LDS slot of tile t
-        uint32_t rb0 = (uint32_t)(t_begin * (uint64_t)p.tile_stride * H_BN) + 4 * khalf;
-        const uint32_t rb_step = (uint32_t)(p.tile_stride * H_BN);
+        // row base of tile t (scalar; wraps with the rotation)
+        uint32_t rbase = (uint32_t)(phys(t_begin) * (uint64_t)p.tile_stride * H_BN);
+        const uint32_t rb_step = (uint32_t)(p.tile_stride * H_BN), rb_wrap = (uint32_t)(p.ntiles * p.tile_stride * H_BN);
         int xs_next = XS && xs ? xs1 : -1;   // the next cross-slot exchange tile
-        for (int t = 0; t < ntile; ++t, rb0 += rb_step) {
+        for (int t = 0; t < ntile; ++t) {
+            const uint32_t rb0 = rbase + 4 * khalf;
+            rbase += rb_step;
+            if (rbase >= rb_wrap) rbase -= rb_wrap;
             WV_DBG_COUNT(0)
             const int g = t / TPS;
 #ifndef WV_H16_ABLATE_NO_FILL
@@ -464,7 +478,7 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
             if (mask_t) mask_half(acc10, acc11, (uint32_t)(mo0 >> 32), (uint32_t)(mo1 >> 32));
             if (t + 1 < ntile) {
                 mfma_half(lds + slot_t * St::U4, 0, acc00, acc01, [&] { m0 = min16(acc10); m1 = min16(acc11); });
-                need_mask = tile_ok(t_begin + t + 1, okw);
+                need_mask = tile_ok(phys(t_begin + t + 1), okw);
             } else {
                 m0 = min16(acc10);
                 m1 = min16(acc11);
@@ -1155,11 +1169,16 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16w_kernel(H16Params p) {
                     }
                 }
                 const uint32_t rb = (uint32_t)r0 + 4 * khalf;
+                WV_DBG_COUNT(0)
+#ifdef WV_H16W_ABLATE_NO_EXTRACT
+                if (fminf(fminf(min16(A0), min16(B0)), fminf(min16(A1), min16(B1))) == 1234.5f) l0d[0] = pt0;
+#else
                 float m;
-                m = min16(A0); if (m <= fminf(l0d[BF_KP - 1], pt0)) split_extract16(m, A0, l0d, l0i, pt0, rb);
-                m = min16(B0); if (m <= fminf(l0d[BF_KP - 1], pt0)) split_extract16(m, B0, l0d, l0i, pt0, rb + 32);
-                m = min16(A1); if (m <= fminf(l1d[BF_KP - 1], pt1)) split_extract16(m, A1, l1d, l1i, pt1, rb);
-                m = min16(B1); if (m <= fminf(l1d[BF_KP - 1], pt1)) split_extract16(m, B1, l1d, l1i, pt1, rb + 32);
+                m = min16(A0); if (m <= fminf(l0d[BF_KP - 1], pt0)) { WV_DBG_COUNT(3) split_extract16(m, A0, l0d, l0i, pt0, rb); }
+                m = min16(B0); if (m <= fminf(l0d[BF_KP - 1], pt0)) { WV_DBG_COUNT(3) split_extract16(m, B0, l0d, l0i, pt0, rb + 32); }
+                m = min16(A1); if (m <= fminf(l1d[BF_KP - 1], pt1)) { WV_DBG_COUNT(3) split_extract16(m, A1, l1d, l1i, pt1, rb); }
+                m = min16(B1); if (m <= fminf(l1d[BF_KP - 1], pt1)) { WV_DBG_COUNT(3) split_extract16(m, B1, l1d, l1i, pt1, rb + 32); }
+#endif
             }
             // every tile while the lists fill, then every 4th
             if (running && (tc < 8 || (tc & 3) == 3)) publish();
