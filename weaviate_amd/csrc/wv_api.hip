@@ -252,6 +252,7 @@ struct wv_index {
     int h16_ns = 0;
     float h16_sx = 0.f, h16_ex = 0.f;
     DevBuf ximg16, xns, qimg16, qres, qmax, qscale, tau, gtau, marg, allow_pad, ex_bits, gslot;
+    DevBuf gbkt;            // the wide pass's bucket minima (H16Params::gbkt)
     DevBuf ximg16q;         // the corpus image in the 16x16x32 layout (h16_quad), beside ximg16
     // the f16 pass's block order (block_order), cached for its schedule
     DevBuf blk_order;
@@ -782,6 +783,14 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
         hp.gslot = ix->gslot.as<float>();
         hp.xslot = 1;
         hp.kth = k;
+    }
+    // the wide pass's bucket bound (opt-in WV_H16W_BUCKETS=1)
+    const char* be = std::getenv("WV_H16W_BUCKETS");
+    if (wd && hp.kth && hp.kth <= 16 && be && std::atoi(be) == 1) {
+        const size_t bb = (size_t)nqb * bq * 16 * 4;
+        HIP_TRY(ix->gbkt.ensure(bb));
+        HIP_TRY(hipMemsetAsync(ix->gbkt.p, 0xFF, bb, s));
+        hp.gbkt = ix->gbkt.as<unsigned int>();
     }
     if (hp.kth) {
         HIP_TRY(ix->marg.ensure((size_t)nq * 4));
@@ -1561,7 +1570,7 @@ int wv_index_destroy(wv_index* ix) {
                       &ix->out_ids, &ix->out_d, &ix->out_n, &ix->stage, &ix->fail_thr, &ix->fb_idx, &ix->fb_d, &ix->fb_i, &ix->fb_n, &ix->fb_of,
                       &ix->ac_cnt, &ix->ac_off, &ix->rowidx, &ix->pq_cent, &ix->pq_codes, &ix->pk_key,
                       &ix->pk_dist, &ix->pk_val, &ix->pk_skey, &ix->pk_sval, &ix->pk_off, &ix->ximg16, &ix->ximg16q, &ix->qmax_part, &ix->xns,
-                      &ix->qimg16, &ix->qres, &ix->qmax, &ix->qscale, &ix->tau, &ix->gtau, &ix->marg, &ix->allow_pad, &ix->ex_bits, &ix->gslot,
+                      &ix->qimg16, &ix->qres, &ix->qmax, &ix->qscale, &ix->tau, &ix->gtau, &ix->marg, &ix->allow_pad, &ix->ex_bits, &ix->gslot, &ix->gbkt, &ix->blk_order,
                       &ix->delta, &ix->dmask, &ix->dl_ids, &ix->dl_d, &ix->dl_n, &ix->dq_tmp, &ix->b_tgt, &ix->b_ci,
                       &ix->b_cd, &ix->b_cn, &ix->b_cnt0, &ix->b_cntu, &ix->b_rk, &ix->b_rn, &ix->b_rk2, &ix->b_rn2,
                       &ix->b_uk, &ix->b_ul, &ix->b_uo, &ix->b_nr, &ix->b_tmp, &ix->stat_acc, &ix->fbd_list,

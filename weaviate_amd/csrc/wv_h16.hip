@@ -1020,6 +1020,44 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16w_kernel(H16Params p) {
         const uint32_t tau_dst = ex0 + (uint32_t)(2 * St::EX_U4 * 16 + 256 * wave);
         const int tau_src = min(jq0 - l31 + lane, p.nq - 1);
         if (running) reinterpret_cast<unsigned int*>(lds + HW_STAGES * St::U4 + 2 * St::EX_U4)[64 * wave + lane] = 0xFFFFFFFFu;
+        // the bucket words of the wave's 64 queries come back the same way
+        // (1 024 words, 4 KiB per wave after the gtau slots)
+        const bool bkt = running && p.gbkt != nullptr;
+        const int bkt_id = (slot * 4 + rh * 2 + khalf) & 15;
+        unsigned int* bkt_lds = reinterpret_cast<unsigned int*>(lds + HW_STAGES * St::U4 + 2 * St::EX_U4 + 8 * 16) + 1024 * wave;
+        const uint32_t bkt_dst = ex0 + (uint32_t)(2 * St::EX_U4 * 16 + 8 * 256 + 4096 * wave);
+        const unsigned int* bkt_src = uniform_ptr(p.gbkt + (size_t)(jq0 - l31) * 16);
+        if (bkt) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) bkt_lds[64 * j + lane] = 0xFFFFFFFFu;
+        }
+        // k-th smallest of the 16 bucket minima of a query (ascending bitonic
+        // network; the index is a VGPR so the select chain stays in VALU)
+        auto bkt_kth = [&](const unsigned int* w) -> float {
+            float v[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) v[i] = h16_key_dec(w[i]);
+#pragma unroll
+            for (int size = 2; size <= 16; size <<= 1)
+#pragma unroll
+                for (int stride = size >> 1; stride > 0; stride >>= 1)
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        const int j = i ^ stride;
+                        if (j > i) {
+                            const float a = v[i], b = v[j];
+                            const bool up = (i & size) == 0;
+                            v[i] = up ? fminf(a, b) : fmaxf(a, b);
+                            v[j] = up ? fmaxf(a, b) : fminf(a, b);
+                        }
+                    }
+            int ve = p.kth - 1;
+            asm volatile("" : "+v"(ve));
+            float kv = FLT_MAX;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) kv = i == ve ? v[i] : kv;
+            return kv;
+        };
         auto publish = [&] {
             int va = ia - 1, vb = ib - 1;
             asm volatile("" : "+v"(va), "+v"(vb));   // (select chains over a VGPR index)
@@ -1047,6 +1085,32 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16w_kernel(H16Params p) {
             tau0 = fminf(tau0, h16_key_dec(tau_lds[l31]));
             tau1 = fminf(tau1, h16_key_dec(tau_lds[32 + l31]));
             glds4_dev(p.gtau + tau_src, tau_dst);
+            if (bkt) {
+                // this lane's list heads into its bucket; the previous
+                // publish's bucket words (landed long since) give the bound,
+                // which also goes to gtau (the finalize's tau_in must not
+                // exceed any threshold a key was dropped above)
+                if (jq0 < p.nq && l0d[0] < FLT_MAX) atomicMin(&p.gbkt[(size_t)jq0 * 16 + bkt_id], h16_key_enc(l0d[0]));
+                if (jq1 < p.nq && l1d[0] < FLT_MAX) atomicMin(&p.gbkt[(size_t)jq1 * 16 + bkt_id], h16_key_enc(l1d[0]));
+                // (lane half 0 selects for jq0, half 1 for jq1, then they swap)
+                const float u4 = 4.f * 5.9604645e-08f;
+                const float v = bkt_kth(bkt_lds + 16 * (32 * khalf + l31));
+                const float mg = khalf ? marg1 : marg0;
+                const float c = v < FLT_MAX ? v + mg + u4 * (fabsf(v) + mg) : FLT_MAX;
+                const float cx = __shfl_xor(c, 32, 64);
+                const float c0 = khalf ? cx : c, c1 = khalf ? c : cx;
+                if (khalf == 0) {
+                    if (jq0 < p.nq && c0 < tau0) atomicMin(&p.gtau[jq0], h16_key_enc(c0));
+                    if (jq1 < p.nq && c1 < tau1) atomicMin(&p.gtau[jq1], h16_key_enc(c1));
+                }
+                tau0 = fminf(tau0, c0);
+                tau1 = fminf(tau1, c1);
+                // (16 dwords per query: 64 lanes x 4 B per op from a scalar
+                // base -- no per-op address registers)
+                const uint32_t vo = (uint32_t)lane * 4;
+#pragma unroll
+                for (int j = 0; j < 16; ++j) glds4s_dev<0>(bkt_src + 64 * j, vo, bkt_dst + 256 * j);
+            }
         };
         floatx16 acc[RG][2];
         auto min16 = [&](const floatx16& A) {
@@ -1635,12 +1699,12 @@ hipError_t wv_launch_bf_h16w(const wv::H16Params* p, hipStream_t s) {
     if (p->wide_rows != 64 && p->wide_rows != 128) return hipErrorInvalidValue;
     if (p->wide_rows == 64) {
         using St = wv::HWStage<64>;
-        const size_t lds = ((size_t)wv::HW_STAGES * St::U4 + 2 * St::EX_U4) * 16 + 8 * 256;   // + the gtau return slots
+        const size_t lds = ((size_t)wv::HW_STAGES * St::U4 + 2 * St::EX_U4) * 16 + 8 * 256 + 8 * 4096;   // + the gtau and bucket return slots
         if (l2) hipLaunchKernelGGL((wv::wv_bf_h16w_kernel<true, 64>), dim3(nb), dim3(512), lds, s, *p);
         else hipLaunchKernelGGL((wv::wv_bf_h16w_kernel<false, 64>), dim3(nb), dim3(512), lds, s, *p);
     } else {
         using St = wv::HWStage<128>;
-        const size_t lds = ((size_t)wv::HW_STAGES * St::U4 + 2 * St::EX_U4) * 16 + 8 * 256;   // + the gtau return slots
+        const size_t lds = ((size_t)wv::HW_STAGES * St::U4 + 2 * St::EX_U4) * 16 + 8 * 256 + 8 * 4096;   // + the gtau and bucket return slots
         if (l2) hipLaunchKernelGGL((wv::wv_bf_h16w_kernel<true, 128>), dim3(nb), dim3(512), lds, s, *p);
         else hipLaunchKernelGGL((wv::wv_bf_h16w_kernel<false, 128>), dim3(nb), dim3(512), lds, s, *p);
     }

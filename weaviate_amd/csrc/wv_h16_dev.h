@@ -54,6 +54,14 @@ __device__ __forceinline__ void glds4_dev(const void* src, uint32_t lds_wave_bas
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off sc1\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep) : "v"(src), "s"(lds_wave_base) : "memory");
 }
+// the same from a wave-uniform base (SGPR pair) + a per-lane byte offset +
+// an immediate (a loop of them keeps no per-iteration address registers)
+template <int OFF>
+__device__ __forceinline__ void glds4s_dev(const void* sbase, uint32_t voff, uint32_t lds_wave_base) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dword %1, %2 offset:%4 sc1\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds_wave_base), "i"(OFF) : "memory");
+}
 // wait until at most n of this wave's vector-memory ops are outstanding
 __device__ __forceinline__ void vm_wait(int n) {
     switch (n) {

@@ -184,6 +184,12 @@ struct H16Params {
     // list entries) + 2 eps, atomicMin'ed into gtau (order-preserving keys of
     // scaled units, h16_key_enc); keys above it are dropped everywhere
     unsigned int* gtau;       // [nq] (nullable)
+    // the wide-D pass: 16 buckets of list heads per query (bucket = slot, row
+    // half, lane half mod 16: disjoint row sets), each the atomicMin of its
+    // lists' smallest keys -- the k-th smallest of 16 bucket minima is the key
+    // of one of k distinct rows, so it (+ 2 eps) bounds the k-th key with
+    // every slot's best rows, not one lane pair's 16 entries
+    unsigned int* gbkt;       // [n_qblocks * HW_BQ][16] (nullable)
     int kth;                  // k (0: no running threshold)
     const float* marg;        // [nq] 2 eps in scaled key units, rounded up (wv_h16_margin_kernel)
     // cross-slot threshold (xslot, 32x32x16 pass): each slot stores its lists'
