@@ -333,13 +333,24 @@ def exact_roofline(args, ix, kern_ms, stats, D, n_allowed, n_local, NQ):
 
 
 def attach_traffic(roof, n_local, NQ, D, data):
+    """roofline.traffic from a committed PMC summary -- only one collected from
+    this build of the key pass (tools/build_hash.py) on the same shape"""
     pmc = os.path.join(ROOT, "profiles", "pmc_%s.json" % roof["kernel"])
     if os.path.exists(pmc):
         with open(pmc) as f:
             p = json.load(f)
-        if (p.get("N"), p.get("nq"), p.get("dim"), p.get("data", "uniform")) == (n_local, NQ, D, data):
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        from build_hash import build_hash
+        same_shape = (p.get("N"), p.get("nq"), p.get("dim"), p.get("data", "uniform")) == (n_local, NQ, D, data)
+        if same_shape and p.get("build") == build_hash():
             roof["traffic"] = p.get("hbm_bytes_per_launch")
             roof["traffic_source"] = p.get("source", os.path.relpath(pmc, ROOT))
+            for key in ("per_mfma", "effective_clock_ghz", "mfma_busy_frac", "wait_inst_frac"):
+                if key in p:
+                    roof["pmc_" + key] = p[key]
+        elif same_shape:
+            roof["traffic_note"] = "profiles/%s is from another build (%s); not attached" % (
+                os.path.basename(pmc), p.get("build"))
 
 
 def run_exact(args, ctx, W):
@@ -495,6 +506,7 @@ def exact_cpu_baseline(args, st, O):
               "dists_bitwise_equal_frac": d_eq, "tie_aware_identical_frac": tie_ok, "id_match_frac": id_eq}
     n1, t1 = out[1][0], out[1][1]
     base_line = {"value": round(ns / cpu_t, 1), "unit": "queries/s", "cores": args.cpu_threads, "kind": "port",
+                 "host_cores": args.host_cores,
                  "value_t1": round(n1 / t1, 2), "cores_t1": 1,
                  "sample": f"{ns} (T={args.cpu_threads}) / {n1} (T=1) of the {args.nq} queries over the full "
                            f"{args.rows:,}-row corpus ({cpu_t:.2f} s / {t1:.2f} s); flatSearch restated in C "
@@ -707,6 +719,7 @@ def run_hnsw(args, ctx, W, with_cpu):
                                 "tie_aware_identical_frac": tie_ok, "recall@10_gpu": round(rec, 4),
                                 "recall@10_cpu_restatement": round(rec_cpu, 4)}
         res["cpu_baseline"] = {"value": round(NQ / cpu_t, 1), "unit": "queries/s", "cores": args.cpu_threads,
+                               "host_cores": args.host_cores,
                                "kind": "port", "value_t1": round(n1 / t1, 1), "cores_t1": 1,
                                "sample": f"all {NQ} queries x {reps} passes (T={args.cpu_threads}), {n1} queries "
                                          f"(T=1); knnSearchByVector restated in C on the same graph (oracle/)"}
@@ -863,7 +876,8 @@ def main():
                     help="exact mode: shared allow list, Bernoulli(p) over ids (seed 3, BASELINE configs[3])")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time (T=all)")
     ap.add_argument("--cpu-seconds-t1", type=float, default=5.0, help="target CPU-baseline sample time (T=1)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU-baseline threads (GOMAXPROCS-equivalent); 0 = every CPU this process may use")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-hnsw-line", action="store_true",
                     help="skip the configs[0] hnsw line that the exact workload reports beside its value")
@@ -893,6 +907,11 @@ def main():
     ap.add_argument("--group-leg", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--group-devices", default="0", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from build_hash import host_cores_info
+    args.host_cores = host_cores_info()
+    if args.cpu_threads <= 0:
+        args.cpu_threads = args.host_cores["cores"]
     args.ef_sweep = [int(x) for x in args.ef_sweep.split(",") if x]
     args.concurrency = [int(x) for x in args.concurrency.split(",") if x]
     GLOVE_NOISE = args.glove_noise

@@ -13,10 +13,15 @@
 // harness (tests/native/mirror_replay.cpp) tests exactly the calls below:
 //
 //	New              -> wv_mirror_create (dims learnt lazily, insert.go:43-65)
-//	PostStartup      -> cpu.PostStartup, then wv_mirror_post_startup: the
-//	                    shard's commit log <RootPath>/<ID>.hnsw.commitlog.d
-//	                    replayed as restoreFromDisk does (startup.go:56-152),
-//	                    rows pulled through VectorForIDThunk (shard.go:165)
+//	PostStartup      -> cpu.PostStartup, a log flush, then
+//	                    wv_mirror_post_startup_async: on the library's own
+//	                    thread the shard's commit log
+//	                    <RootPath>/<ID>.hnsw.commitlog.d is replayed as
+//	                    restoreFromDisk does (startup.go:56-152) and the rows
+//	                    are pulled through VectorForIDThunk (shard.go:165),
+//	                    while the CPU index serves (the reference prefills its
+//	                    cache in a goroutine, startup.go:174-203); writes that
+//	                    arrive meanwhile are replayed when it goes live
 //	Add(id, vec)     -> cpu.Add, then wv_mirror_add (the mirror grows like
 //	                    growIndexToAccomodateNode, maintainance.go:69-100)
 //	Delete(ids...)   -> cpu.Delete, then wv_mirror_delete (delete.go:29-84)
@@ -31,11 +36,14 @@
 // log -- the CPU index's own graph.
 //
 // A write the mirror cannot take marks it stale (the library refuses reads
-// with WV_ESTALE): searches are then answered by the CPU index until a later
-// PostStartup resyncs it, so a stale mirror never serves a deleted id or
-// misses an added one.  Writes hold mu shared across the CPU write and its
-// propagation; compaction holds it exclusively while it flushes the log, so
-// every node the flushed log holds has reached the mirror.
+// with WV_ESTALE): searches are then answered by the CPU index, so a stale
+// mirror never serves a deleted id or misses an added one, and the library
+// resyncs it in the background (wvgpuFlush flushes the CPU index's log first,
+// then the startup runs again; 1 s doubling to 60 s between failed tries).
+// Writes hold mu shared across the CPU write and its propagation; compaction
+// and the resync's flush hold it exclusively while they flush the log, so
+// every node the flushed log holds has reached the mirror.  PQ-compressed
+// classes (KMeans encoder) are served compressed from the log's quantizer.
 //
 // The Go toolchain is not part of the image this engine is developed in, so
 // this file has not been type-checked; tests/native/mirror_replay.cpp
@@ -48,10 +56,16 @@ package gpu
 #include <stdlib.h>
 #include "wvgpu.h"
 
-// the exported Go thunk (below), as a wv_vector_source
+// the exported Go thunks (below), as a wv_vector_source and a wv_flush_fn
 extern int wvgpuVectorForID(void *ctx, uint64_t id, float *out, int cap, int *len);
-static int wvgpu_post_startup(wv_mirror *m, void *ctx) {
-	return wv_mirror_post_startup(m, wvgpuVectorForID, ctx);
+extern int wvgpuFlush(void *ctx);
+static int wvgpu_post_startup_async(wv_mirror *m, void *ctx) {
+	return wv_mirror_post_startup_async(m, wvgpuVectorForID, ctx);
+}
+static void wvgpu_self_heal(wv_mirror_options *o, void *ctx) {
+	o->auto_resync = 1;
+	o->flush = wvgpuFlush;
+	o->flush_ctx = ctx;
 }
 */
 import "C"
@@ -108,9 +122,12 @@ type Index struct {
 	logDir     *C.char
 	vectorFor  VectorForID
 	device     int
-	mu         sync.RWMutex // calls shared; the log flush before a compaction, PostStartup and close exclusive
+	mu         sync.RWMutex // calls shared; the log flushes, PostStartup and close exclusive
 	compacting atomic.Bool
 	closed     atomic.Bool
+	handle     cgo.Handle      // this Index, for the library's callbacks (its threads call them)
+	ctx        *C.uintptr_t    // C memory holding handle: the callbacks' ctx, valid until close
+	metrics    *mirrorMetrics  // nil unless Options.Metrics
 }
 
 // Options: the shard's paths and the mirror's sizes.
@@ -123,6 +140,9 @@ type Options struct {
 	MaxWaitUsec  int         // batching window after the first waiting query (0: 200)
 	CompactRows  uint64      // delta rows that trigger a compaction (0: 8192)
 	InitialSize  uint64      // mirror capacity before growth (0: 25000)
+	Metrics      bool        // export the mirror's gauges (metrics.go; PROMETHEUS_MONITORING_ENABLED)
+	ClassName    string      // metric labels, as hnsw's Metrics (metrics.go:23-228)
+	ShardName    string
 }
 
 func lastErr(op string, rc C.int) error {
@@ -150,17 +170,44 @@ func New(cpu cpuIndex, metric int, uc ent.UserConfig, opt Options) (*Index, erro
 	cfg := configOf(uc, opt.Device)
 	g := &Index{cpuIndex: cpu, vectorFor: opt.VectorForID, device: opt.Device}
 	g.logDir = C.CString(opt.RootPath + "/" + opt.ID + ".hnsw.commitlog.d")
+	g.handle = cgo.NewHandle(g)
+	g.ctx = (*C.uintptr_t)(C.malloc(C.size_t(unsafe.Sizeof(C.uintptr_t(0)))))
+	*g.ctx = C.uintptr_t(g.handle)
 	var mo C.wv_mirror_options
 	mo.initial_capacity = C.uint64_t(opt.InitialSize)
 	mo.max_batch = C.int(opt.MaxBatch)
 	mo.max_wait_us = C.int(opt.MaxWaitUsec)
 	mo.compact_rows = C.uint64_t(opt.CompactRows)
 	mo.commitlog_dir = g.logDir
+	C.wvgpu_self_heal(&mo, unsafe.Pointer(g.ctx))
 	if rc := C.wv_mirror_create(C.int(metric), &cfg, &mo, &g.m); rc != 0 {
-		C.free(unsafe.Pointer(g.logDir))
+		g.freeHandles()
 		return nil, lastErr("create", rc)
 	}
+	if opt.Metrics {
+		g.metrics = newMirrorMetrics(g, opt.ClassName, opt.ShardName)
+	}
 	return g, nil
+}
+
+func (g *Index) freeHandles() {
+	C.free(unsafe.Pointer(g.logDir))
+	C.free(unsafe.Pointer(g.ctx))
+	g.handle.Delete()
+}
+
+//export wvgpuFlush
+func wvgpuFlush(ctx unsafe.Pointer) C.int {
+	g := cgo.Handle(*(*C.uintptr_t)(ctx)).Value().(*Index)
+	g.mu.Lock()
+	defer g.mu.Unlock()
+	if g.closed.Load() {
+		return C.WV_ESTATE
+	}
+	if err := g.cpuIndex.Flush(); err != nil {
+		return C.WV_ESTATE
+	}
+	return C.WV_OK
 }
 
 //export wvgpuVectorForID
@@ -182,21 +229,20 @@ func wvgpuVectorForID(ctx unsafe.Pointer, id C.uint64_t, out *C.float, capacity 
 	return C.WV_OK
 }
 
-// PostStartup: the CPU index's own routines, then the mirror is loaded from
-// the shard's commit log and object store (startup.go:169-205).
+// PostStartup: the CPU index's own routines, then the mirror loads from the
+// shard's commit log and object store on the library's thread
+// (startup.go:169-205); the CPU index serves until it is live.
 func (g *Index) PostStartup() {
 	g.cpuIndex.PostStartup()
-	g.mu.Lock() // no write slips between the log read and serving
+	g.mu.Lock() // every write before the flush is in the log, every later one is replayed
 	defer g.mu.Unlock()
-	if err := g.cpuIndex.Flush(); err != nil {
-		return // the mirror stays stale: the CPU index serves
+	if g.closed.Load() {
+		return
 	}
-	h := cgo.NewHandle(g)
-	defer h.Delete()
-	ctx := (*C.uintptr_t)(C.malloc(C.size_t(unsafe.Sizeof(C.uintptr_t(0)))))
-	defer C.free(unsafe.Pointer(ctx))
-	*ctx = C.uintptr_t(h)
-	C.wvgpu_post_startup(g.m, unsafe.Pointer(ctx)) // non-zero: stale, CPU serves
+	if err := g.cpuIndex.Flush(); err != nil {
+		return // the mirror stays idle: the CPU index serves
+	}
+	C.wvgpu_post_startup_async(g.m, unsafe.Pointer(g.ctx))
 }
 
 // Add mirrors hnsw.Add (insert.go:43-65).
@@ -206,11 +252,17 @@ func (g *Index) Add(id uint64, vector []float32) error {
 		g.mu.RUnlock()
 		return err
 	}
-	if len(vector) > 0 && !g.closed.Load() {
-		C.wv_mirror_add(g.m, C.uint64_t(id), (*C.float)(unsafe.Pointer(&vector[0])), C.int(len(vector)))
+	compact := false
+	if !g.closed.Load() {
+		if len(vector) > 0 {
+			C.wv_mirror_add(g.m, C.uint64_t(id), (*C.float)(unsafe.Pointer(&vector[0])), C.int(len(vector)))
+		}
+		compact = C.wv_mirror_needs_compaction(g.m) != 0 // (under mu: close cannot free the mirror meanwhile)
 	}
 	g.mu.RUnlock()
-	g.maybeCompact()
+	if compact {
+		g.startCompaction()
+	}
 	return nil
 }
 
@@ -228,15 +280,19 @@ func (g *Index) Delete(ids ...uint64) error {
 	return nil
 }
 
-// maybeCompact re-snapshots the mirror's graph from the flushed commit log
-// once the delta has grown past Options.CompactRows.
-func (g *Index) maybeCompact() {
-	if C.wv_mirror_needs_compaction(g.m) == 0 || !g.compacting.CompareAndSwap(false, true) {
+// startCompaction re-snapshots the mirror's graph from the flushed commit
+// log once the delta has grown past Options.CompactRows.
+func (g *Index) startCompaction() {
+	if !g.compacting.CompareAndSwap(false, true) {
 		return
 	}
 	go func() {
 		defer g.compacting.Store(false)
 		g.mu.Lock()
+		if g.closed.Load() {
+			g.mu.Unlock()
+			return
+		}
 		err := g.cpuIndex.Flush()
 		g.mu.Unlock()
 		g.mu.RLock() // (close waits for it)
@@ -335,9 +391,15 @@ func (g *Index) close() {
 		g.mu.Unlock()
 		return
 	}
-	defer g.mu.Unlock()
-	C.wv_mirror_destroy(g.m) // waits for a running compaction, drains waiting searches
-	C.free(unsafe.Pointer(g.logDir))
+	// every call that holds mu shared has returned, and every later one sees
+	// closed; mu is released before the destroy, which joins the library's
+	// thread (a resync's wvgpuFlush takes mu, then finds closed set)
+	g.mu.Unlock()
+	if g.metrics != nil {
+		g.metrics.stop()
+	}
+	C.wv_mirror_destroy(g.m) // joins startups / resyncs, waits for a compaction, drains searches
+	g.freeHandles()
 }
 
 func (g *Index) Shutdown(ctx context.Context) error {

@@ -254,7 +254,7 @@ typedef struct {
     int max_level;           /* SetEntryPointMaxLevel's level */
     int max_node_level;      /* highest level field of a live node */
     int max_deg0, max_degU;  /* longest layer-0 / upper neighbour list */
-    int compressed;          /* an AddPQ record was seen: PQ is not served by the GPU */
+    int compressed;          /* an AddPQ record was seen (wv_graph_get_pq: its quantizer) */
     int truncated;           /* a file ended inside a record */
 } wv_graph_info;
 /* one log held in memory */
@@ -275,6 +275,17 @@ int wv_graph_node(const wv_graph *g, uint64_t id, int level, int *node_level, ui
  * tomb_bits[(n+63)/64] (nullable).  deg0 >= info.max_deg0, degU >= info.max_degU. */
 int wv_graph_export_csr(wv_graph *g, int deg0, int degU, int8_t *levels, uint32_t *layer0, uint32_t *upper_row,
                         uint32_t *upper, uint64_t *tomb_bits);
+/* The last AddPQ record's quantizer (deserializer.go ReadPQ :510-563): the
+ * header, and for the KMeans encoder (encoder 1) the centroid table
+ * [segments][centroids][dims/segments] of ReadKMeansEncoder :487-508 --
+ * wv_index_set_pq's layout; copied when table_cap >= table_floats.  The tile
+ * encoder (encoder 0) holds distribution parameters, not centres
+ * (table_floats 0).  present = 0: the log is not compressed. */
+typedef struct {
+    int present, dims, segments, centroids, encoder, distribution, use_bits_encoding;
+    uint64_t table_floats;
+} wv_graph_pq;
+int wv_graph_get_pq(const wv_graph *g, wv_graph_pq *pq, float *centroid_table, uint64_t table_cap);
 int wv_graph_destroy(wv_graph *g);
 
 /* Micro-batcher (SURVEY 8b "Threading"): SearchByVector is called once per
@@ -337,13 +348,21 @@ int wv_batcher_create_group(wv_group *g, int dim, int max_batch, int max_wait_us
 /* GPU mirror of one shard's hnsw index -- the whole lifecycle the cgo
  * decorator (go/vector/gpu/gpu.go) drives, kept native so that the replay
  * harness (tests/native/mirror_replay.cpp) tests the code Go calls:
- *   startup   wv_mirror_post_startup: the shard's commit log
+ *   startup   wv_mirror_post_startup{,_async}: the shard's commit log
  *             (<RootPath>/<ID>.hnsw.commitlog.d, replayed as restoreFromDisk,
  *             startup.go:56-152) becomes the mirror's graph, its rows come
  *             from the shard's VectorForIDThunk (shard.go:165,
  *             shard_read.go:145-161) as PostStartup's cache prefill does
  *             (startup.go:169-205); a node whose object is gone is skipped
- *             as search.go's handleDeletedNode path skips it (a nil node);
+ *             as search.go's handleDeletedNode path skips it (a nil node).
+ *             The async form returns at once and builds on a background
+ *             thread while the CPU index serves (the reference prefills its
+ *             cache in a goroutine the same way, startup.go:174-203); writes
+ *             that arrive meanwhile are kept and replayed when the new index
+ *             is installed.  A PQ-compressed log (AddPQ record, KMeans
+ *             encoder) is served compressed: the quantizer comes from the log,
+ *             the codes are encoded on the device (compress.go:39-99,
+ *             kmeans.go:78-110); a tile-encoded one stays on the CPU index;
  *   writes    wv_mirror_add (hnsw.Add, insert.go:43-65: the dimension is
  *             learnt from the first vector, capacity grows as
  *             growIndexToAccomodateNode does, maintainance.go:22-24,69-100),
@@ -358,12 +377,18 @@ int wv_batcher_create_group(wv_group *g, int dim, int max_batch, int max_wait_us
  *             index's own graph -- or, without a log directory, builds it on
  *             the device (wv_index_build_graph).
  * Any failed write marks the mirror stale: every read then returns
- * WV_ESTALE (the decorator answers from the CPU index) until
- * wv_mirror_post_startup runs again.  Reads and writes may run concurrently
- * from many threads; growth, compaction and startup are exclusive. */
+ * WV_ESTALE (the decorator answers from the CPU index).  With
+ * opt.auto_resync the mirror heals itself: a background thread flushes the
+ * CPU index's log through opt.flush and rebuilds as an async startup does,
+ * backing off (1 s doubling to 60 s) while it keeps failing.  Reads and
+ * writes may run concurrently from many threads; growth, compaction and
+ * install are exclusive. */
 typedef struct wv_mirror wv_mirror;
 enum { WV_ESTALE = 6,      /* mirror not serving: answer from the CPU index */
        WV_ENOTFOUND = 7 }; /* vector source: no object for this doc id */
+enum { WV_MIRROR_IDLE = 0, WV_MIRROR_STARTING = 1, WV_MIRROR_LIVE = 2, WV_MIRROR_STALE = 3 };
+/* the CPU index's Flush (commit log to disk) before a resync reads the log */
+typedef int (*wv_flush_fn)(void *ctx);
 typedef struct {
     int dim;                   /* 0: learnt from the first vector */
     uint64_t initial_capacity; /* 0: 25000 (maintainance.go:22 initialSize) */
@@ -373,20 +398,34 @@ typedef struct {
     int ef_construction;       /* device-build compaction (0: 128) */
     uint64_t build_seed;       /* device-build level draw */
     const char *commitlog_dir; /* NULL: no commit log, compaction builds on the device */
+    int auto_resync;           /* 1: a stale mirror rebuilds itself in the background */
+    wv_flush_fn flush;         /* nullable: called before a resync reads the log */
+    void *flush_ctx;
+    int resync_backoff_ms;     /* first delay before a resync (0: 1000) */
 } wv_mirror_options;
 /* VectorForIDThunk for one doc id: WV_OK with *len = the vector's length
  * (copied to out when *len <= cap), WV_ENOTFOUND for a deleted object, any
- * other status is an error. */
+ * other status is an error.  The async startup and resyncs call it from the
+ * mirror's own thread: ctx must stay valid until wv_mirror_destroy. */
 typedef int (*wv_vector_source)(void *ctx, uint64_t id, float *out, int cap, int *len);
 typedef struct {
-    int live;                  /* serving (not stale) */
+    int live;                  /* serving (state == WV_MIRROR_LIVE) */
     int dim;
     uint64_t capacity, n_rows, delta_rows, graph_nodes;
     uint64_t growths, compactions, startup_rows, startup_missing;
     uint64_t batcher_requests, batcher_batches;
+    int state;                 /* WV_MIRROR_* */
+    int pq;                    /* serving PQ-compressed (KMeans codes on the device) */
+    uint64_t startups, resyncs, failed_startups, replayed_writes;
 } wv_mirror_stats;
 int wv_mirror_create(int metric, const wv_config *cfg, const wv_mirror_options *opt, wv_mirror **out);
 int wv_mirror_post_startup(wv_mirror *m, wv_vector_source src, void *ctx);
+int wv_mirror_post_startup_async(wv_mirror *m, wv_vector_source src, void *ctx);
+/* WV_OK once live; WV_ESTALE if not live after timeout_ms (< 0: wait for the
+ * running startup / resync to end) */
+int wv_mirror_wait_live(wv_mirror *m, int timeout_ms);
+/* the caller knows the mirror missed a write: stale now (resync if enabled) */
+int wv_mirror_mark_stale(wv_mirror *m);
 int wv_mirror_add(wv_mirror *m, uint64_t id, const float *vector, int len);
 int wv_mirror_delete(wv_mirror *m, const uint64_t *ids, uint64_t n);
 /* filtered != 0: allow_ids[n_allow] ascending doc ids (may be empty: nothing

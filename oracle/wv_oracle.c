@@ -1339,6 +1339,14 @@ int wvo_add(wvo_index *h, uint64_t id, const float *vec) {
     if (id >= h->cap) return -1;
     if (h->level[id] >= 0) return -3;
     wvo_set_vector(h, id, vec); /* Add normalizes for cosine (insert.go:56-60) */
+    if (h->compressed) {
+        /* insert.go:91-95: a compressed index stores the new node's code
+         * (pq.Encode of the stored vector; KMeans encoders: the nearest centre
+         * per segment, kmeans.go:78-110) */
+        wvo_pq_encode_kmeans(vec_of(h, id), 1, h->dim, h->pq_m, h->pq_ks, h->pq_cent, h->pq_use_bits,
+                             h->pq_codes + id * h->pq_code_len);
+        h->pq_has[id] = 1;
+    }
     ctx_t c;
     ctx_init(&c, h->cap);
     int lvl = h->next_level;

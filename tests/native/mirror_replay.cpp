@@ -22,6 +22,22 @@
 //              the delta set.  Check 2: the delta stays bounded.
 //   quiescent  final flush + compaction; check 3: searches equal the
 //              restatement's again, and the delta is empty.
+// Modes (argv[3]):
+//   sync   (default) the above, PostStartup on the caller's thread;
+//   async  wv_mirror_post_startup_async: writers and searchers start at once
+//          while the mirror builds on its own thread (the vector source is
+//          slowed so that writes do arrive meanwhile); searchers answered
+//          WV_ESTALE until it is live (the CPU index serves); every write
+//          made during the build must be replayed (stats) and then found;
+//   heal   auto_resync with the log flush as the flush callback: a third of
+//          the way through, one add reaches the CPU index but not the mirror
+//          and the mirror is marked stale (a failed write); it must resync by
+//          itself (stats.resyncs), find that row afterwards, and end equal to
+//          the restatement;
+//   pq     the CPU index is compressed before startup (KMeans quantizer,
+//          compress.go:39-99; the AddPQ record appended to its log): the
+//          mirror must load the quantizer from the log, serve compressed
+//          (stats.pq), and equal the restatement's PQ searches; async start.
 // Exit 0 with one JSON line, or 1 with the first violation.
 #include <algorithm>
 #include <atomic>
@@ -44,12 +60,20 @@
 namespace {
 
 constexpr int DIM = 32;
+#ifdef WV_REPLAY_TSAN   // (ThreadSanitizer build over the CPU stand-in: the same scenario, smaller)
+constexpr uint64_t N0 = 4000;
+constexpr uint64_t N_ADD = 4000;
+constexpr uint64_t INIT_CAP = 5000;
+constexpr uint64_t COMPACT_ROWS = 1024;
+#else
 constexpr uint64_t N0 = 20000;
 constexpr uint64_t N_ADD = 20000;
+constexpr uint64_t INIT_CAP = 25000;   // (the mirror's default, maintainance.go:22)
+constexpr uint64_t COMPACT_ROWS = 4096;
+#endif
 constexpr uint64_t CAP = N0 + N_ADD;
 constexpr int M = 16, EFC = 64, EF = 64, K = 10;
 constexpr int64_t CUTOFF = 5000;
-constexpr uint64_t COMPACT_ROWS = 4096;
 constexpr int SEARCHERS = 8;
 constexpr int NQ_CHECK = 400;
 
@@ -72,7 +96,9 @@ void row(uint64_t id, float* out) { for (int j = 0; j < DIM; ++j) out[j] = urand
 std::vector<float> store(CAP * DIM);
 std::vector<uint8_t> in_store(CAP, 0);
 
+std::atomic<int> source_delay_us{0};
 int vector_for_id(void*, uint64_t id, float* out, int cap, int* len) {
+    if (const int d = source_delay_us.load()) std::this_thread::sleep_for(std::chrono::microseconds(d));
     if (id >= CAP || !in_store[id]) return WV_ENOTFOUND;
     *len = DIM;
     if (cap >= DIM) std::memcpy(out, &store[id * DIM], DIM * sizeof(float));
@@ -112,9 +138,61 @@ std::vector<uint64_t> to_bits(const std::vector<uint64_t>& ids, uint64_t range) 
     return b;
 }
 
+// KMeans quantizer for the pq mode: PQ_M segments of DIM / PQ_M dims, PQ_KS
+// centres each taken from spread-out rows (a fitted table stands in for
+// KMeans.Fit, which is not restated); the AddPQ record in logger.go:77-96's
+// layout (KMeans data: kmeans.go:61-69)
+constexpr int PQ_M = 8, PQ_KS = 256;
+std::vector<float> pq_table() {
+    const int ds = DIM / PQ_M;
+    std::vector<float> t((size_t)PQ_M * PQ_KS * ds);
+    for (int i = 0; i < PQ_M; ++i)
+        for (int c = 0; c < PQ_KS; ++c)
+            for (int j = 0; j < ds; ++j) t[((size_t)i * PQ_KS + c) * ds + j] = store[(uint64_t)(c * 73 + i) % N0 * DIM + i * ds + j];
+    return t;
+}
+std::vector<uint8_t> add_pq_record(const std::vector<float>& t) {
+    std::vector<uint8_t> r = {11};   // AddPQ
+    auto u16 = [&](uint16_t v) { r.push_back(v & 0xFF); r.push_back(v >> 8); };
+    u16(DIM);
+    r.push_back(1);   // UseKMeansEncoder
+    u16(PQ_KS);
+    u16(PQ_M);
+    r.push_back(0);   // distribution (tile encoder only)
+    r.push_back(0);   // useBitsEncoding
+    for (float f : t) {
+        uint32_t u;
+        std::memcpy(&u, &f, 4);
+        for (int b = 0; b < 4; ++b) r.push_back((u >> (8 * b)) & 0xFF);
+    }
+    return r;
+}
+
+// heal mode: the decorator's flush callback (wvgpuFlush: hnsw.Flush under
+// the write lock); every row added before it is then in the log's graph
+std::atomic<uint64_t>* g_n_added = nullptr;
+std::mutex* g_in_graph_mu = nullptr;
+std::vector<uint8_t>* g_compacted = nullptr;
+std::atomic<int> flushes{0};
+int flush_cb(void*) {
+    std::lock_guard<std::mutex> l(cpu_mu);
+    flush_log();
+    const uint64_t na = g_n_added ? g_n_added->load() : 0;
+    if (g_compacted) {
+        std::lock_guard<std::mutex> gl(*g_in_graph_mu);
+        for (uint64_t a = 0; a < na; ++a) (*g_compacted)[N0 + a] = 1;
+    }
+    flushes++;
+    return 0;
+}
+
 // mirror vs restatement on NQ_CHECK queries (a third unfiltered, a third with
 // a small allow list -> flatSearch, a third with a large one -> filtered HNSW)
 int compare(wv_mirror* m, uint64_t range, int seed, const char* phase) {
+#ifdef WV_REPLAY_TSAN
+    (void)m; (void)range; (void)seed; (void)phase;
+    return 0;   // the CPU stand-in (tsan/cpu_index.cpp) searches exactly: no HNSW parity to check
+#endif
     std::mt19937_64 g(seed);
     std::vector<float> q(DIM);
     uint64_t oi[K], mi[K];
@@ -163,9 +241,12 @@ int compare(wv_mirror* m, uint64_t range, int seed, const char* phase) {
 }  // namespace
 
 int main(int argc, char** argv) {
-    if (argc < 2) { std::fprintf(stderr, "usage: mirror_replay <dir> [device]\n"); return 2; }
+    if (argc < 2) { std::fprintf(stderr, "usage: mirror_replay <dir> [device] [sync|async|heal|pq]\n"); return 2; }
     const std::string root = argv[1];
     const int device = argc > 2 ? std::atoi(argv[2]) : 0;
+    const std::string mode = argc > 3 ? argv[3] : "sync";
+    const bool async_start = mode == "async" || mode == "pq", heal = mode == "heal", pqm = mode == "pq";
+    if (mode != "sync" && !async_start && !heal) { std::fprintf(stderr, "unknown mode %s\n", mode.c_str()); return 2; }
     const std::string log_dir = root + "/main.hnsw.commitlog.d";
     mkdir(root.c_str(), 0755);
     mkdir(log_dir.c_str(), 0755);
@@ -201,6 +282,20 @@ int main(int argc, char** argv) {
         ++gone;
     }
     flush_log();
+    if (pqm) {   // Compress (compress.go:39-89): codes of every stored row, then the AddPQ record
+        const std::vector<float> t = pq_table();
+        std::vector<uint8_t> codes((size_t)N0 * PQ_M), has(N0, 0);
+        for (uint64_t id = 0; id < N0; ++id) has[id] = in_store[id];
+        wvo_pq_encode_kmeans(store.data(), N0, DIM, PQ_M, PQ_KS, t.data(), 0, codes.data());
+        if (wvo_compress(cpu, PQ_M, PQ_KS, 0, t.data(), codes.data(), has.data(), N0)) {
+            std::fprintf(stderr, "restatement compress failed\n");
+            return 1;
+        }
+        const std::vector<uint8_t> rec = add_pq_record(t);
+        FILE* f = std::fopen(log_file.c_str(), "ab");
+        std::fwrite(rec.data(), 1, rec.size(), f);
+        std::fclose(f);
+    }
 
     wv_config cfg;
     wv_config_default(&cfg);
@@ -210,8 +305,14 @@ int main(int argc, char** argv) {
     cfg.flat_search_cutoff = CUTOFF;
     wv_mirror_options opt{};
     opt.compact_rows = COMPACT_ROWS;
+    if (INIT_CAP != 25000) opt.initial_capacity = INIT_CAP;
     opt.max_batch = 256;
     opt.commitlog_dir = log_dir.c_str();
+    if (heal) {
+        opt.auto_resync = 1;
+        opt.flush = flush_cb;
+        opt.resync_backoff_ms = 50;
+    }
     wv_mirror* m = nullptr;
     if (wv_mirror_create(WV_L2_SQUARED, &cfg, &opt, &m)) { std::fprintf(stderr, "create: %s\n", wv_last_error()); return 1; }
     {
@@ -221,20 +322,35 @@ int main(int argc, char** argv) {
             violation("a mirror serves before PostStartup");
     }
     const auto t_start = std::chrono::steady_clock::now();
-    if (wv_mirror_post_startup(m, vector_for_id, nullptr)) {
-        std::fprintf(stderr, "post_startup: %s\n", wv_last_error());
-        return 1;
+    wv_mirror_stats st0{};
+    int diffs_startup = -1;
+    if (!async_start) {
+        if (wv_mirror_post_startup(m, vector_for_id, nullptr)) {
+            std::fprintf(stderr, "post_startup: %s\n", wv_last_error());
+            return 1;
+        }
+        wv_mirror_get_stats(m, &st0);
+        if (!st0.live || st0.dim != DIM || st0.startup_missing != gone || st0.startup_rows != N0 - gone ||
+            st0.graph_nodes != N0 || st0.delta_rows != 0 || st0.capacity != INIT_CAP)
+            violation("startup stats: live " + std::to_string(st0.live) + " dim " + std::to_string(st0.dim) + " rows " +
+                      std::to_string(st0.startup_rows) + " missing " + std::to_string(st0.startup_missing) + " nodes " +
+                      std::to_string(st0.graph_nodes) + " delta " + std::to_string(st0.delta_rows) + " capacity " +
+                      std::to_string(st0.capacity));
+        diffs_startup = failed ? -1 : compare(m, N0, 11, "startup");
+    } else {
+        // PostStartup returns at once; the build runs on the mirror's thread
+        // while the writer and the searchers below already run
+        source_delay_us = 40;   // ~0.8 s of vector source: writes land during the build
+        if (wv_mirror_post_startup_async(m, vector_for_id, nullptr)) {
+            std::fprintf(stderr, "post_startup_async: %s\n", wv_last_error());
+            return 1;
+        }
+        wv_mirror_stats s;
+        wv_mirror_get_stats(m, &s);
+        if (s.state != WV_MIRROR_STARTING) violation("async startup: the mirror is not starting after the call");
+        diffs_startup = 0;   // (no quiescent point: the final comparison covers it)
     }
-    const double startup_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
-    wv_mirror_stats st0;
-    wv_mirror_get_stats(m, &st0);
-    if (!st0.live || st0.dim != DIM || st0.startup_missing != gone || st0.startup_rows != N0 - gone ||
-        st0.graph_nodes != N0 || st0.delta_rows != 0 || st0.capacity != 25000)
-        violation("startup stats: live " + std::to_string(st0.live) + " dim " + std::to_string(st0.dim) + " rows " +
-                  std::to_string(st0.startup_rows) + " missing " + std::to_string(st0.startup_missing) + " nodes " +
-                  std::to_string(st0.graph_nodes) + " delta " + std::to_string(st0.delta_rows) + " capacity " +
-                  std::to_string(st0.capacity));
-    const int diffs_startup = failed ? -1 : compare(m, N0, 11, "startup");
+    const double startup_call_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
 
     // ---- serving: adds, deletes, compactions and searches at once ----
     std::atomic<int> n_deleted{(int)deleted.size()};
@@ -244,6 +360,12 @@ int main(int argc, char** argv) {
     std::atomic<uint64_t> max_delta{0}, n_compact{0}, n_search{0}, n_added_checks{0}, n_filtered{0};
     std::mutex in_graph_mu;
     std::vector<uint8_t> compacted(CAP, 0);   // added rows that a compaction moved into the graph
+    g_n_added = &n_added;
+    g_in_graph_mu = &in_graph_mu;
+    g_compacted = &compacted;
+    std::atomic<uint64_t> stale_answers{0};   // searches the CPU index answered (mirror not live)
+    std::atomic<uint64_t> missed_id{UINT64_MAX};
+    std::atomic<bool> live_seen{!async_start};
 
     auto writer = std::thread([&] {
         std::mt19937_64 g(21);
@@ -255,8 +377,15 @@ int main(int argc, char** argv) {
                 std::lock_guard<std::mutex> l(cpu_mu);
                 wvo_add(cpu, id, &store[id * DIM]);
             }
-            const int rc = wv_mirror_add(m, id, &store[id * DIM], DIM);
-            if (rc) violation(std::string("add: ") + wv_last_error());
+            if (heal && a == N_ADD / 3) {
+                // a write the mirror never saw (the decorator's propagation
+                // failed): stale now, the mirror must heal itself
+                missed_id = id;
+                wv_mirror_mark_stale(m);
+            } else {
+                const int rc = wv_mirror_add(m, id, &store[id * DIM], DIM);
+                if (rc && !(heal && rc == WV_ESTALE)) violation(std::string("add: ") + wv_last_error());
+            }
             n_added.store(a + 1, std::memory_order_release);
             if (a % 3 == 0) {
                 const uint64_t del = a % 9 == 0 && a > 16 ? N0 + a - 16 : g() % N0;
@@ -284,7 +413,9 @@ int main(int argc, char** argv) {
                     std::lock_guard<std::mutex> l(cpu_mu);
                     flush_log();
                 }
-                if (wv_mirror_compact(m)) violation(std::string("compact: ") + wv_last_error());
+                const int crc = wv_mirror_compact(m);
+                if (crc && !(crc == WV_ESTALE && (heal || async_start)))
+                    violation(std::string("compact: ") + wv_last_error());
                 {
                     std::lock_guard<std::mutex> l(in_graph_mu);
                     for (uint64_t a = 0; a < na; ++a) compacted[N0 + a] = 1;
@@ -330,7 +461,12 @@ int main(int argc, char** argv) {
             }
             int32_t n = 0;
             const int rc = wv_mirror_search(m, q.data(), DIM, K, filtered, al.data(), al.size(), ids, ds, &n);
+            if (rc == WV_ESTALE && (async_start || heal)) {   // starting / resyncing: the CPU index answers
+                stale_answers++;
+                continue;
+            }
             if (rc) { violation(std::string("search: ") + wv_last_error()); return; }
+            live_seen = true;
             n_search++;
             for (int i = 0; i < n; ++i) {
                 if (ids[i] >= CAP) violation("id out of range");
@@ -357,7 +493,24 @@ int main(int argc, char** argv) {
     maint.join();
     const double serve_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 
-    // ---- quiescent: final flush + compaction, then the restatement again ----
+    // ---- quiescent: live again, final flush + compaction, then the restatement ----
+    if (!failed && wv_mirror_wait_live(m, 120000)) violation("the mirror did not become live");
+    if (async_start) {
+        wv_mirror_stats s;
+        wv_mirror_get_stats(m, &s);
+        st0 = s;
+        if (s.replayed_writes == 0) violation("async startup: no write arrived during the build (test too fast)");
+        if (pqm && !s.pq) violation("pq: the mirror does not serve compressed");
+    }
+    if (heal && !failed) {
+        // the missed row: found first by an exact (filtered) search
+        const uint64_t id = missed_id.load();
+        uint64_t ids[K];
+        float ds[K];
+        int32_t n = 0;
+        const int rc = wv_mirror_search(m, &store[id * DIM], DIM, K, 1, &id, 1, ids, ds, &n);
+        if (rc || n != 1 || ids[0] != id || ds[0] != 0.f) violation("heal: the missed row is not served after the resync");
+    }
     {
         std::lock_guard<std::mutex> l(cpu_mu);
         flush_log();
@@ -365,11 +518,13 @@ int main(int argc, char** argv) {
     if (!failed && wv_mirror_compact(m)) violation(std::string("final compact: ") + wv_last_error());
     wv_mirror_stats st;
     wv_mirror_get_stats(m, &st);
+    if (heal && !failed && (st.resyncs < 1 || flushes < 1)) violation("heal: the mirror did not resync by itself");
     const int diffs_final = failed ? -1 : compare(m, CAP, 12, "final");
     if (!failed && st.delta_rows != 0) violation("delta not empty after the final compaction");
     if (!failed && max_delta > 2 * COMPACT_ROWS) violation("delta grew to " + std::to_string(max_delta.load()));
     if (!failed && st.growths < 1) violation("the mirror never grew past its initial capacity");
-    if (!failed && n_compact < 2) violation("fewer than two compactions while serving");
+    // (async / heal: the mirror serves only part of the writer's run)
+    if (!failed && n_compact < (async_start || heal ? 1u : 2u)) violation("too few compactions while serving");
     if (!failed && (diffs_startup != 0 || diffs_final != 0))
         violation("searches differ from the restatement: startup " + std::to_string(diffs_startup) + ", final " +
                   std::to_string(diffs_final) + " of " + std::to_string(NQ_CHECK));
@@ -379,12 +534,15 @@ int main(int argc, char** argv) {
         std::fprintf(stderr, "VIOLATION: %s\n", first_err.c_str());
         return 1;
     }
-    std::printf("{\"ok\": true, \"startup_rows\": %llu, \"startup_missing\": %llu, \"startup_s\": %.2f, "
+    std::printf("{\"ok\": true, \"mode\": \"%s\", \"resyncs\": %llu, \"replayed_writes\": %llu, \"pq\": %d, "
+                "\"stale_answers\": %llu, \"startup_call_s\": %.3f, \"startup_rows\": %llu, \"startup_missing\": %llu, "
                 "\"diffs_startup\": %d, \"diffs_final\": %d, \"exact_fallbacks\": %d, \"checked\": %d, \"adds\": %llu, \"deletes\": %d, "
                 "\"compactions\": %llu, \"max_delta\": %llu, \"capacity\": %llu, \"growths\": %llu, "
                 "\"searches\": %llu, \"added_checks\": %llu, \"filtered\": %llu, \"batcher_requests\": %llu, "
                 "\"batcher_batches\": %llu, \"serve_s\": %.2f}\n",
-                (unsigned long long)st0.startup_rows, (unsigned long long)st0.startup_missing, startup_s,
+                mode.c_str(), (unsigned long long)st.resyncs, (unsigned long long)st.replayed_writes, st.pq,
+                (unsigned long long)stale_answers.load(), startup_call_s,
+                (unsigned long long)st0.startup_rows, (unsigned long long)st0.startup_missing,
                 diffs_startup, diffs_final, exact_fallbacks, NQ_CHECK, (unsigned long long)n_added.load(), n_deleted.load(),
                 (unsigned long long)st.compactions, (unsigned long long)max_delta.load(),
                 (unsigned long long)st.capacity, (unsigned long long)st.growths, (unsigned long long)n_search.load(),

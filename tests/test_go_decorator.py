@@ -35,16 +35,26 @@ def test_go_decorator_binds_only_header_symbols():
                          ("SearchByVector", "wv_mirror_search"),
                          ("SearchByVectorDistance", "wv_mirror_search_by_distance"),
                          ("UpdateUserConfig", "wv_mirror_update_config"),
-                         ("PostStartup", "wvgpu_post_startup")):
+                         ("PostStartup", "wvgpu_post_startup_async")):
         body = re.search(r"func \(g \*Index\) %s\(.*?\n}\n" % method, src, re.S)
         assert body, method
         assert f"C.{call}(" in body.group(0), f"{method} does not call {call}"
-    # PostStartup goes live from the shard's commit log and VectorForIDThunk
-    assert "wv_mirror_post_startup(m, wvgpuVectorForID, ctx)" in src
+    # PostStartup goes live from the shard's commit log and VectorForIDThunk,
+    # on the library's thread (startup.go:174-203 prefills in a goroutine)
+    assert "wv_mirror_post_startup_async(m, wvgpuVectorForID, ctx)" in src
     assert '".hnsw.commitlog.d"' in src and "//export wvgpuVectorForID" in src
-    # compaction flushes the CPU index's log first
-    body = re.search(r"func \(g \*Index\) maybeCompact\(.*?\n}\n", src, re.S).group(0)
-    assert body.index("cpuIndex.Flush()") < body.index("C.wv_mirror_compact(")
+    # self-healing: the resync flushes the CPU index's log through wvgpuFlush
+    assert "//export wvgpuFlush" in src and "o->auto_resync = 1;" in src and "o->flush = wvgpuFlush;" in src
+    # compaction flushes the CPU index's log first, and never after close
+    body = re.search(r"func \(g \*Index\) startCompaction\(.*?\n}\n", src, re.S).group(0)
+    assert body.index("g.closed.Load()") < body.index("cpuIndex.Flush()") < body.index("C.wv_mirror_compact(")
+    # (advisor, round 3) the compaction check runs under mu and only while open
+    add = re.search(r"func \(g \*Index\) Add\(.*?\n}\n", src, re.S).group(0)
+    assert add.index("C.wv_mirror_needs_compaction(") < add.rindex("g.mu.RUnlock()") < add.index("g.startCompaction()")
+    assert "!g.closed.Load()" in add
+    # close releases mu before joining the library's thread (a resync's flush takes mu)
+    cl = re.search(r"func \(g \*Index\) close\(.*?\n}\n", src, re.S).group(0)
+    assert cl.index("g.mu.Unlock()") < cl.index("C.wv_mirror_destroy(") < cl.index("g.freeHandles()")
 
 
 def test_replay_harness_binds_only_header_symbols():
@@ -73,6 +83,32 @@ def test_mirror_lifecycle_from_commit_log(tmp_path):
     assert r["compactions"] >= 3 and r["max_delta"] <= 2 * 4096
     assert r["added_checks"] > 100 and r["filtered"] > 50
     assert r["batcher_batches"] < r["batcher_requests"]
+    print(r)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["async", "heal", "pq"])
+def test_mirror_lifecycle_modes(tmp_path, mode):
+    """async: PostStartup returns at once and the mirror builds on its own
+    thread while writers and searchers run (the CPU index answers until it is
+    live; writes made meanwhile are replayed); heal: a write the mirror never
+    saw marks it stale and it resyncs by itself (flush callback, then a
+    rebuild), serving the missed row afterwards; pq: a KMeans-compressed
+    index (AddPQ record in the log) is served compressed, equal to the
+    restatement's PQ searches (compress.go:39-99, search.go:172-197)."""
+    binp = os.path.join(ROOT, "tests", "native", "mirror_replay")
+    assert os.path.exists(binp), "build tests/native first (__graft_entry__.build())"
+    p = subprocess.run([binp, str(tmp_path), "0", mode], capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:] + p.stdout[-2000:]
+    r = json.loads(p.stdout.strip().splitlines()[-1])
+    assert r["ok"] and r["mode"] == mode and r["diffs_final"] == 0
+    assert r["adds"] == 20000 and r["max_delta"] <= 2 * 4096
+    if mode in ("async", "pq"):
+        assert r["replayed_writes"] > 0 and r["stale_answers"] > 0 and r["startup_call_s"] < 0.5
+    if mode == "heal":
+        assert r["resyncs"] >= 1 and r["stale_answers"] > 0
+    if mode == "pq":
+        assert r["pq"] == 1
     print(r)
 
 

@@ -5,6 +5,7 @@
 set -e
 O=gpurun_out/pmc_h16; mkdir -p $O
 export TMPDIR=/tmp
+export WV_BUILD_HASH=${WV_BUILD_HASH:-$(python3 tools/build_hash.py)}
 B=${B:-build/h16/abl_base}
 ARGS="${N:-1000000} ${NQ:-10000} ${D:-128} pmc"
 timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- $B $ARGS > $O/trace.log 2>&1
@@ -17,12 +18,12 @@ for set in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE
   timeout -s KILL 60 rocprofv3 --pmc $set --output-format csv -d $O/p$i -o run -- $B $ARGS > $O/p$i.log 2>&1 || echo "pass $i failed rc=$?"
 done
 python3 - <<'PY'
-import csv, glob, statistics, json
+import csv, glob, statistics, json, os
 out = {}
 for f in sorted(glob.glob("gpurun_out/pmc_h16/p*/run_counter_collection.csv")):
     vals = {}
     for r in csv.DictReader(open(f)):
-        if "h16_kernel<8, true, false, 8, 2" in r["Kernel_Name"]:
+        if os.environ.get("KSUB", "h16p_kernel<8, true, false, true") in r["Kernel_Name"]:
             vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
     for k, v in vals.items():
         out[k] = statistics.mean(v)
@@ -37,7 +38,7 @@ import os
 avg_ns = None
 for f in glob.glob("gpurun_out/pmc_h16/trace/run_kernel_stats.csv"):
     for r in csv.DictReader(open(f)):
-        if "h16_kernel<8, true, false, 8, 2" in r["Name"]:
+        if os.environ.get("KSUB", "h16p_kernel<8, true, false, true") in r["Name"]:
             avg_ns = float(r["AverageNs"])
 if "FETCH_SIZE" in out:
     rd = 2.0 * out["FETCH_SIZE"] * 1024
@@ -50,5 +51,19 @@ if "FETCH_SIZE" in out:
                   "tools/h16_ablate.cpp harness (same shape as bench.py's configs[1]); write traffic is the "
                   "candidate lists only (not collected)",
           "source": "profiles/pmc_wv_bf_h16_kernel.json (tools/pmc_h16.sh)"}
+    sq = js["sq"]
+    mf = sq.get("SQ_INSTS_MFMA") or 0
+    if mf:
+        js["per_mfma"] = {"valu": sq.get("SQ_INSTS_VALU", 0) / mf, "salu": sq.get("SQ_INSTS_SALU", 0) / mf,
+                          "lds": sq.get("SQ_INSTS_LDS", 0) / mf}
+    if sq.get("SQ_WAVE_CYCLES"):
+        js["wait_inst_frac"] = sq.get("SQ_WAIT_INST_ANY", 0) / sq["SQ_WAVE_CYCLES"]
+        js["wait_any_frac"] = sq.get("SQ_WAIT_ANY", 0) / sq["SQ_WAVE_CYCLES"]
+    if sq.get("GRBM_GUI_ACTIVE") and avg_ns:
+        js["effective_clock_ghz"] = sq["GRBM_GUI_ACTIVE"] / 8.0 / avg_ns
+    if mf and sq.get("SQ_VALU_MFMA_BUSY_CYCLES") is not None and sq.get("GRBM_GUI_ACTIVE"):
+        # MFMA pipe busy share: busy cycles summed over SIMDs / (SIMDs x cycles)
+        js["mfma_busy_frac"] = sq["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024.0 * sq["GRBM_GUI_ACTIVE"] / 8.0)
+    js["build"] = os.environ.get("WV_BUILD_HASH")
     json.dump(js, open("gpurun_out/pmc_h16/pmc_wv_bf_h16_kernel.json", "w"), indent=1)
 PY

@@ -35,6 +35,17 @@
 
 extern "C" void wv_internal_set_error(const char* msg);
 
+// condition-variable deadlines on steady_clock (pthread_cond_clockwait); the
+// ThreadSanitizer build (tests/native/Makefile mirror_replay_tsan) uses
+// system_clock, whose pthread_cond_timedwait GCC 11's libtsan intercepts --
+// it has no pthread_cond_clockwait interceptor, so every steady wait would
+// look like a lock never released
+#ifdef WV_TSAN_BUILD
+using wait_clock = std::chrono::system_clock;
+#else
+using wait_clock = std::chrono::steady_clock;
+#endif
+
 namespace {
 
 struct Request {
@@ -141,7 +152,7 @@ struct wv_batcher {
             cv_work.wait(l, [&] { return stop || !queue.empty(); });
             if (queue.empty() && stop) return;
             // the window opens with the first waiting request
-            const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(max_wait_us);
+            const auto deadline = wait_clock::now() + std::chrono::microseconds(max_wait_us);
             cv_work.wait_until(l, deadline, [&] { return stop || (int)queue.size() >= max_batch; });
             std::vector<Request*> take;
             while (!queue.empty() && (int)take.size() < max_batch) {

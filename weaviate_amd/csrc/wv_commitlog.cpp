@@ -81,6 +81,12 @@ struct wv_graph {
     uint64_t entrypoint = 0;
     uint16_t level = 0;
     bool compressed = false;
+    // the last AddPQ record's quantizer (ReadPQ :510-563): header and, for the
+    // KMeans encoder, every segment's Ks x dims/M centres (ReadKMeansEncoder
+    // :487-508, little-endian float32, ExposeDataForRestore's order)
+    uint16_t pq_dims = 0, pq_ks = 0, pq_m = 0;
+    uint8_t pq_enc = 0, pq_dist = 0, pq_bits = 0;
+    std::vector<float> pq_centers;
     bool truncated = false;       // a file ended inside a record
     uint64_t valid_bytes = 0;     // bytes of complete records, all files
     uint64_t dropped_links = 0;   // export: links to ids past the last node
@@ -201,18 +207,36 @@ struct wv_graph {
                 level = 0;
                 clear_nodes();
                 break;
-            case AddPQ: {   // ReadPQ :510-563: parsed to stay aligned; PQ is not served by the GPU
+            case AddPQ: {   // ReadPQ :510-563
                 uint16_t dims = 0, ks = 0, m = 0;
                 uint8_t enc = 0, dist = 0, bits = 0;
                 ok = r.u16(dims) && r.u8(enc) && r.u16(ks) && r.u16(m) && r.u8(dist) && r.u8(bits);
+                std::vector<float> centers;
                 for (uint16_t i = 0; ok && i < m; ++i) {
                     // ssdhelpers: UseTileEncoder = 0 (51 bytes, tile_encoder.go:138-149),
                     // UseKMeansEncoder = 1 (Ks x dims/M float32 centres, kmeans.go:61-69)
-                    if (enc == 0) ok = r.skip(6 * 8 + 2 + 1);
-                    else if (enc == 1) ok = r.skip((size_t)ks * (dims / (m ? m : 1)) * 4);
-                    else return fail(WV_EINVAL, "commit log: unsupported PQ encoder type");
+                    if (enc == 0) {
+                        ok = r.skip(6 * 8 + 2 + 1);
+                    } else if (enc == 1) {
+                        const size_t nf = (size_t)ks * (dims / (m ? m : 1));
+                        const size_t at = centers.size();
+                        centers.resize(at + nf);
+                        for (size_t j = 0; ok && j < nf; ++j) {
+                            uint8_t b[4];
+                            ok = r.get(b, 4);
+                            const uint32_t u = (uint32_t)b[0] | (uint32_t)b[1] << 8 | (uint32_t)b[2] << 16 |
+                                               (uint32_t)b[3] << 24;
+                            std::memcpy(&centers[at + j], &u, 4);
+                        }
+                    } else {
+                        return fail(WV_EINVAL, "commit log: unsupported PQ encoder type");
+                    }
                 }
-                if (ok) compressed = true;
+                if (ok) {
+                    compressed = true;
+                    pq_dims = dims; pq_ks = ks; pq_m = m; pq_enc = enc; pq_dist = dist; pq_bits = bits;
+                    pq_centers.swap(centers);
+                }
                 break;
             }
             default:
@@ -397,6 +421,23 @@ int wv_graph_export_csr(wv_graph* g, int deg0, int degU, int8_t* levels, uint32_
         for (uint64_t t : g->tombstones)
             if (t < n) tomb_bits[t >> 6] |= 1ull << (t & 63);
     }
+    return WV_OK;
+}
+
+int wv_graph_get_pq(const wv_graph* g, wv_graph_pq* pq, float* centroid_table, uint64_t table_cap) {
+    if (!g || !pq) return fail(WV_EINVAL, "wv_graph_get_pq: bad argument");
+    std::memset(pq, 0, sizeof(*pq));
+    if (!g->compressed) return WV_OK;
+    pq->present = 1;
+    pq->dims = g->pq_dims;
+    pq->segments = g->pq_m;
+    pq->centroids = g->pq_ks;
+    pq->encoder = g->pq_enc;
+    pq->distribution = g->pq_dist;
+    pq->use_bits_encoding = g->pq_bits;
+    pq->table_floats = g->pq_centers.size();
+    if (centroid_table && table_cap >= g->pq_centers.size())
+        std::memcpy(centroid_table, g->pq_centers.data(), g->pq_centers.size() * sizeof(float));
     return WV_OK;
 }
 

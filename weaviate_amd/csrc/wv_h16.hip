@@ -174,11 +174,6 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
             l0d[i] = FLT_MAX; l1d[i] = FLT_MAX;
             l0i[i] = WV_NIL; l1i[i] = WV_NIL;
         }
-        // extraction of a half tile's keys into list c (0 / 1)
-        auto extract = [&](float& m, floatx16& acc, int c, float pt, uint32_t rb) {
-            if (c == 0) split_extract16(m, acc, l0d, l0i, pt, rb);
-            else split_extract16(m, acc, l1d, l1i, pt, rb);
-        };
         // Two-phase software pipeline over half tiles (rows 0-31: H0 =
         // acc00/acc01, rows 32-63: H1 = acc10/acc11).  Iteration t:
         //   A  MFMAs of H1(t)       beside the tile minima of H0(t)
@@ -463,8 +458,10 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
                 grew = __any(x0 || x1);
                 if (__builtin_expect(grew, 0)) {
                     WV_DBG_COUNT(3)
-                    if (x0) extract(m0, acc00, 0, pt0, rb0);
-                    if (x1) extract(m1, acc01, 1, pt1, rb0);
+                    // (round 4: insertion by key position, wv_topk.h ballot_extract:
+                    // 2.67-2.68 -> 2.65-2.67 ms per 1M x 10k pass)
+                    if (__any(x0)) ballot_extract(acc00, x0 ? fminf(l0d[BF_KP - 1], pt0) : -INF, l0d, l0i, rb0);
+                    if (__any(x1)) ballot_extract(acc01, x1 ? fminf(l1d[BF_KP - 1], pt1) : -INF, l1d, l1i, rb0);
                 }
 #endif
             }
@@ -501,8 +498,8 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
                 const bool any1 = __any(x0 || x1);
                 if (__builtin_expect(any1, 0)) {
                     WV_DBG_COUNT(3)
-                    if (x0) extract(m0, acc10, 0, pt0, rb0 + 32);
-                    if (x1) extract(m1, acc11, 1, pt1, rb0 + 32);
+                    if (__any(x0)) ballot_extract(acc10, x0 ? fminf(l0d[BF_KP - 1], pt0) : -INF, l0d, l0i, rb0 + 32);
+                    if (__any(x1)) ballot_extract(acc11, x1 ? fminf(l1d[BF_KP - 1], pt1) : -INF, l1d, l1i, rb0 + 32);
                 }
                 grew = any1 || grew;
 #endif
@@ -1237,11 +1234,19 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16w_kernel(H16Params p) {
 #ifdef WV_H16W_ABLATE_NO_EXTRACT
                 if (fminf(fminf(min16(A0), min16(B0)), fminf(min16(A1), min16(B1))) == 1234.5f) l0d[0] = pt0;
 #else
-                float m;
-                m = min16(A0); if (m <= fminf(l0d[BF_KP - 1], pt0)) { WV_DBG_COUNT(3) split_extract16(m, A0, l0d, l0i, pt0, rb); }
-                m = min16(B0); if (m <= fminf(l0d[BF_KP - 1], pt0)) { WV_DBG_COUNT(3) split_extract16(m, B0, l0d, l0i, pt0, rb + 32); }
-                m = min16(A1); if (m <= fminf(l1d[BF_KP - 1], pt1)) { WV_DBG_COUNT(3) split_extract16(m, A1, l1d, l1i, pt1, rb); }
-                m = min16(B1); if (m <= fminf(l1d[BF_KP - 1], pt1)) { WV_DBG_COUNT(3) split_extract16(m, B1, l1d, l1i, pt1, rb + 32); }
+                // insertion by key position (wv_topk.h ballot_extract), wave-uniform
+                auto xt = [&](const floatx16& A, float (&ld)[BF_KP], uint32_t (&li)[BF_KP], float pt, uint32_t rr) {
+                    const float th = fminf(ld[BF_KP - 1], pt);
+                    const bool x = min16(A) <= th;
+                    if (__any(x)) {
+                        WV_DBG_COUNT(3)
+                        ballot_extract(A, x ? th : -__builtin_inff(), ld, li, rr);
+                    }
+                };
+                xt(A0, l0d, l0i, pt0, rb);
+                xt(B0, l0d, l0i, pt0, rb + 32);
+                xt(A1, l1d, l1i, pt1, rb);
+                xt(B1, l1d, l1i, pt1, rb + 32);
 #endif
             }
             // every tile while the lists fill, then every 4th

@@ -25,7 +25,7 @@ __device__ unsigned long long wv_dbg_counts[4];
             if ((i) == 1) atomicAdd(&wv_dbg_counts[2], (unsigned long long)__popcll(dbg_b));   \
         }                                                                                      \
     }
-extern "C" void wv_dbg_read(unsigned long long* out) { hipMemcpyFromSymbol(out, HIP_SYMBOL(wv_dbg_counts), 32); }
+extern "C" __attribute__((weak)) void wv_dbg_read(unsigned long long* out) { hipMemcpyFromSymbol(out, HIP_SYMBOL(wv_dbg_counts), 32); }
 #else
 #define WV_DBG_COUNT(i)
 #endif
@@ -120,6 +120,42 @@ __device__ __forceinline__ void split_extract16(float& M, floatx16& A, float (&l
         m0 = fminf(fminf(m0, A[12]), A[13]);
         m1 = fminf(fminf(m1, A[14]), A[15]);
         M = fminf(fminf(m0, m1), fminf(m2, m3));
+    }
+}
+
+// Candidate insertion by key position (the f16 passes' rare path, round 4):
+// for each of the lane's NK keys (rows rb + (r & 3) + 8 (r >> 2), + 32 for
+// the second accumulator) the wave tests key <= thr by ballot; only positions
+// where some lane hits run the insertion, for every hitting lane at once.  So
+// an event costs NK compares + one insertion per hit position, instead of a
+// wave-serial round (scan for the minimum's position, mask it, insert,
+// re-reduce) per key that serves ~1 lane.  thr is the lane's threshold at the
+// event's start; a key that no longer beats the list's tail when its turn
+// comes is dropped by the insertion itself (key-only compares: a key equal to
+// the tail does not enter -- the certificate covers it, see split_extract).
+__device__ __forceinline__ void list_insert(float d, uint32_t id, float (&ld)[BF_KP], uint32_t (&li)[BF_KP]) {
+#pragma unroll
+    for (int i = 0; i < BF_KP; ++i) {
+        const bool lt = d < ld[i];
+        const float td = ld[i];
+        const uint32_t ti = li[i];
+        ld[i] = lt ? d : td;
+        li[i] = lt ? id : ti;
+        d = lt ? td : d;
+        id = lt ? ti : id;
+    }
+}
+__device__ __forceinline__ void ballot_extract(const floatx16& A, float thr, float (&ld)[BF_KP], uint32_t (&li)[BF_KP],
+                                               uint32_t rb) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const bool c = A[r] <= thr;
+        if (__any(c)) {
+            WV_DBG_COUNT(1)
+            uint32_t id = rb;   // opaque: the row ids stay in this rare path
+            asm volatile("" : "+v"(id));
+            if (c) list_insert(A[r], id + (uint32_t)((r & 3) + 8 * (r >> 2)), ld, li);
+        }
     }
 }
 
