@@ -305,17 +305,12 @@ def exact_roofline(args, ix, kern_ms, stats, D, n_allowed, n_local, NQ):
         kind = "split" if 2 * n_allowed >= n_local else "fp32"
     elif not fp32:
         # round 3: a shared list under half the corpus runs the f16 pass over
-        # its gathered rows (WV_BF_H16_NO_GATHER=1: round 2's fp32 row-list
-        # pass below 1/8)
-        kind = "h16" if (8 * n_allowed >= n_local or not os.environ.get("WV_BF_H16_NO_GATHER")) else "fp32"
+        # its gathered rows
+        kind = "h16"
     else:
         kind = "fp32"
-    # WV_H16_QUAD=1, D <= 128 with an even number of 16-k steps: the 16x16x32 kernel (wv_api.hip h16_quad)
-    # (k <= 32; wider k runs the 32x32x16 kernel)
-    quad = D <= 128 and ((D + 15) // 16) % 2 == 0 and os.environ.get("WV_H16_QUAD", "0") == "1" and args.k <= 32
-    peak, kname, kp = {"h16": (F16_MFMA_PEAK_TF,
-                               "wv_bf_h16w_kernel" if D > 128 else ("wv_bf_h16q_kernel" if quad else "wv_bf_h16_kernel"),
-                               "f16 MFMA keys (%s; peak = f16 dense)" % ("16x16x32" if quad else "32x32x16")),
+    peak, kname, kp = {"h16": (F16_MFMA_PEAK_TF, "wv_bf_h16w_kernel" if D > 128 else "wv_bf_h16_kernel",
+                               "f16 MFMA keys (32x32x16; peak = f16 dense)"),
                        "split": (BF16_MFMA_PEAK_TF / 3, "wv_bf_split_kernel", "bf16x3 (peak = bf16 dense / 3)"),
                        "fp32": (FP32_MFMA_PEAK_TF, "wv_bf_mfma_kernel", "fp32 MFMA")}[kind]
     roof = {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 2), "peak": round(peak, 1),
@@ -324,9 +319,8 @@ def exact_roofline(args, ix, kern_ms, stats, D, n_allowed, n_local, NQ):
             "finalize_ms": round(float(np.mean([k["bf_finalize_ms"] for k in kern_ms])), 3),
             "fallback_queries": stats["fallbacks"]}
     if kind == "h16":
-        shape = "16x16x32" if kname == "wv_bf_h16q_kernel" else "32x32x16"
-        roof["frac_of_bare_mfma_loop"] = round(achieved / F16_MFMA_BARE_LOOP_TF[shape], 4)
-        roof["bare_mfma_loop_tf"] = F16_MFMA_BARE_LOOP_TF[shape]
+        roof["frac_of_bare_mfma_loop"] = round(achieved / F16_MFMA_BARE_LOOP_TF["32x32x16"], 4)
+        roof["bare_mfma_loop_tf"] = F16_MFMA_BARE_LOOP_TF["32x32x16"]
         roof["seed_pass_ms"] = round(seed_ms, 3)
         roof["achieved_incl_seed_pass"] = round(flops / ((mfma_ms + seed_ms) * 1e-3) / 1e12, 2)
     return roof, kind

@@ -771,8 +771,8 @@ def test_split_key_pass_equals_fp32_key_pass(metric):
 @pytest.mark.parametrize("dim", [32, 96, 128])
 @pytest.mark.parametrize("metric", [O.L2, O.DOT, O.COSINE])
 def test_split_pass_query_blocks_multi_segment(dim, metric):
-    """The split key pass in 256-query blocks (one 512-thread workgroup per CU,
-    default), 128- and 192-query blocks (WV_BF_BQ) over several query blocks
+    """The split key pass (WV_BF_SPLIT=1: 256-query blocks, one 512-thread
+    workgroup per CU) over several query blocks
     (nq = 700: a partial last block), a ragged corpus (last tile partial),
     tombstones and a shared allow list that keeps over half the rows (masked
     in the epilogue, not compacted); D = 32 / 96 / 128 = 1 / 3 / 4 k-chunks
@@ -792,11 +792,8 @@ def test_split_pass_query_blocks_multi_segment(dim, metric):
     oi, od, on = O.flat_scan(metric, b, q, 10, allow_bits=al.words, tomb_bits=tb)
     ui, ud, un = O.flat_scan(metric, b, q, 10, tomb_bits=tb)
     runs = []
-    # default (the f16 key pass), and the bf16x3 split pass: 256-query blocks
-    # (two waves per SIMD), 128-query blocks, the three-waves-per-SIMD kernel
-    # (192-query blocks) and the one-wave-per-SIMD kernel (4 k-chunks only)
-    for env in ({}, {"WV_BF_SPLIT": "1"}, {"WV_BF_SPLIT": "1", "WV_BF_BQ": "128"},
-                {"WV_BF_SPLIT": "1", "WV_BF_BQ": "192"}, {"WV_BF_SPLIT": "1", "WV_BF_SPLIT_1W": "1"}):
+    # default (the f16 key pass), and the bf16x3 split pass
+    for env in ({}, {"WV_BF_SPLIT": "1"}):
         os.environ.update(env)
         try:
             ix = W.GPUVectorIndex(dim, METRIC_NAMES[metric], capacity=n)
@@ -819,9 +816,9 @@ def test_split_pass_query_blocks_multi_segment(dim, metric):
 @pytest.mark.parametrize("metric", [O.L2, O.DOT, O.COSINE])
 def test_h16_key_pass_seeded_equals_unseeded_and_fp32(dim, metric):
     """The f16 key pass at a corpus size that runs the seed pre-pass (>= 64k
-    rows): seeded (default), unseeded (WV_H16_NO_SEED), without the XCD remap
-    (WV_BF_LOCALITY=0), the 16x16x32 kernel seeded and unseeded (WV_H16_QUAD)
-    and the fp32 pass return the same ids and distances,
+    rows): seeded (default), unseeded (WV_H16_NO_SEED), with the seed sampling
+    every 8th / 32nd tile (WV_H16_SAMPLE), without the running threshold
+    (WV_H16_NO_RUNNING) and the fp32 pass return the same ids and distances,
     with tombstones, a shared allow list kept in the epilogue and a partial
     last query block -- and equal the restatement up to tie order.  D=100 is
     GloVe-shaped (7 k-steps of 16: 112, not 128)."""
@@ -833,10 +830,8 @@ def test_h16_key_pass_seeded_equals_unseeded_and_fp32(dim, metric):
     allow_ids = np.nonzero(rng.random(n) < 0.6)[0]
     al = W.AllowList.from_ids(allow_ids, n)
     runs = []
-    # WV_H16_QUAD: the 16x16x32 kernel (shared column lists) where D allows
-    # it (128: 4 32-k steps; at 100 the 32x32x16 kernel runs regardless)
-    for env in ({}, {"WV_H16_NO_SEED": "1"}, {"WV_BF_LOCALITY": "0"}, {"WV_BF_FP32": "1"}, {"WV_H16_QUAD": "1"},
-                {"WV_H16_QUAD": "1", "WV_H16_NO_SEED": "1"}):
+    for env in ({}, {"WV_H16_NO_SEED": "1"}, {"WV_H16_SAMPLE": "8"}, {"WV_H16_SAMPLE": "32"},
+                {"WV_H16_NO_SEED": "1", "WV_H16_NO_RUNNING": "1"}, {"WV_BF_FP32": "1"}):
         os.environ.update(env)
         try:
             ix = W.GPUVectorIndex(dim, METRIC_NAMES[metric], capacity=n)
@@ -891,9 +886,7 @@ def test_h16_cross_slot_threshold_equals_default():
     base, qs = _data(n, d, nq, seed=91)
     tomb_ids = np.nonzero(np.random.default_rng(92).random(n) < 0.01)[0]
     runs = []
-    # (third run: the staggered 8-wave pass, WV_H16_STAGGER=1 -- same lists,
-    # another schedule)
-    for env in ({}, {"WV_H16_XSLOT": "0"}, {"WV_H16_STAGGER": "1"}):
+    for env in ({}, {"WV_H16_XSLOT": "0"}):
         os.environ.update(env)
         try:
             ix = W.GPUVectorIndex(d, "l2-squared", capacity=n)
@@ -904,7 +897,7 @@ def test_h16_cross_slot_threshold_equals_default():
         finally:
             for key in env:
                 os.environ.pop(key, None)
-    for other in (runs[1], runs[2]):
+    for other in runs[1:]:
         for (ai, ad, an), (bi, bd, bn) in zip(runs[0], other):
             assert an.tolist() == bn.tolist()
             _same(ai, ad, bi, bd)

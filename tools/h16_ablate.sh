@@ -10,17 +10,17 @@ VARIANTS=${VARIANTS:-"base= noext=-DWV_H16_ABLATE_NO_EXTRACT pure=-DWV_H16_ABLAT
 if [ "$1" == "build" ]; then
   make -s -C $C ARCH=gfx950
   /opt/rocm/bin/hipcc $HF -x hip -c tools/h16_ablate.cpp -o $B/main.o
+  # (the API with the ablation-only fallback skip: WV_ABLATE_NO_FALLBACK)
+  /opt/rocm/bin/hipcc $HF -DWV_ABLATION_BUILD -c $C/wv_api.hip -o $B/api.o
   rm -f $B/abl_*
   for v in $VARIANTS; do
     name=${v%%=*}; defs=${v#*=}; defs=${defs//:/ }
     (
-    # the variant's defines apply to the one-wave-per-SIMD pass (wv_h16s.hip,
-    # WV_H16_SOLO=1 at run time) unless SOLO_ONLY=0 also builds wv_h16.hip with them
-    if [ "${SOLO_ONLY:-1}" == "1" ]; then cp $C/wv_h16.o $B/h16_$name.o; else
+    # the variant's defines apply to wv_h16.hip (the library's object without any)
+    if [ -z "$defs" ]; then cp $C/wv_h16.o $B/h16_$name.o; else
       /opt/rocm/bin/hipcc $HF -fno-honor-nans $defs -c $C/wv_h16.hip -o $B/h16_$name.o; fi
-    /opt/rocm/bin/hipcc $HF -fno-honor-nans -mllvm -amdgpu-mfma-vgpr-form $defs -c $C/wv_h16s.hip -o $B/h16s_$name.o
-    /opt/rocm/bin/hipcc --offload-arch=gfx950 -pthread $B/main.o $B/h16_$name.o $B/h16s_$name.o $C/wv_bf.o $C/wv_hnsw.o $C/wv_pq.o \
-        $C/wv_api.o $C/wv_batcher.o $C/wv_commitlog.o $C/wv_group.o -L/opt/rocm/lib -lrccl -o $B/abl_$name
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -pthread $B/main.o $B/h16_$name.o $C/wv_bf.o $C/wv_hnsw.o $C/wv_pq.o \
+        $B/api.o $C/wv_batcher.o $C/wv_commitlog.o $C/wv_group.o $C/wv_mirror.o -L/opt/rocm/lib -lrccl -o $B/abl_$name
     ) &
   done
   wait

@@ -62,9 +62,7 @@ hipError_t wv_launch_absmax(const float* in, int ld, uint64_t n, int D, unsigned
 hipError_t wv_launch_h16_qscale(const float* part, int nparts, unsigned int* max_bits, float bsign, float* qscale,
                                 hipStream_t s);
 hipError_t wv_launch_h16_xns(const float* xnorm, uint64_t n, float sx, const float* qscale, float* xns, hipStream_t s);
-hipError_t wv_launch_bf_h16(const wv::H16Params* p, int ns, int seed, int waves, hipStream_t s);
-hipError_t wv_launch_bf_h16q(const wv::H16Params* p, int ns32, int seed, int waves, hipStream_t s);
-hipError_t wv_launch_bf_h16s(const wv::H16Params* p, int ns32, int seed, hipStream_t s);
+hipError_t wv_launch_bf_h16(const wv::H16Params* p, int ns, int seed, hipStream_t s);
 hipError_t wv_launch_bf_h16w(const wv::H16Params* p, hipStream_t s);
 hipError_t wv_launch_h16_seed(const wv::H16SeedParams* p, hipStream_t s);
 hipError_t wv_launch_h16_margin(int metric, int D, const float* qnorm, const float* qres, float xnorm_max,
@@ -247,13 +245,9 @@ struct wv_index {
     // norm |x - f16(s_x x) / s_x| over the rows (rounded up), both host-cached
     bool use_h16 = false;
     bool h16_wide = false;  // D > 128: wv_bf_h16w_kernel (both operands through LDS, 128-row tiles)
-    bool h16_quad = false;  // D <= 128, even 16-k steps: wv_bf_h16q_kernel (16x16x32 MFMA, h16q_index images)
-    bool h16_solo = false;  // D <= 128, even 16-k steps: wv_bf_h16s_kernel (one wave per SIMD, h16q_index images)
     int h16_ns = 0;
     float h16_sx = 0.f, h16_ex = 0.f;
     DevBuf ximg16, xns, qimg16, qres, qmax, qscale, tau, gtau, marg, allow_pad, ex_bits, gslot;
-    DevBuf gbkt;            // the wide pass's bucket minima (H16Params::gbkt)
-    DevBuf ximg16q;         // the corpus image in the 16x16x32 layout (h16_quad), beside ximg16
     // the f16 pass's block order (block_order), cached for its schedule
     DevBuf blk_order;
     std::vector<int> blk_order_host;
@@ -537,14 +531,13 @@ int run_pq_flat(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d
 // bit 1), so that each XCD runs the blocks of every query block over the same
 // part of the corpus at the same time -- a tile then comes into that XCD's L2
 // once per pass instead of once per query block.  nullptr: the identity
-// (WV_H16_BLOCK_ORDER=0, or a single query block).
+// (a single query block).
 // rotated: the tiles of query block qb are rotated by qb ntiles mod U (the
 // D <= 128 pass's locality bit 2), so a block's first tile is (slot U) mod ntiles.
 int block_order(wv_index* ix, uint64_t nqb, const wv::BfSchedule& sch, hipStream_t s, const int** out,
                 bool rotated = false) {
     *out = nullptr;
-    const char* e = std::getenv("WV_H16_BLOCK_ORDER");
-    if ((e && std::atoi(e) == 0) || nqb < 2 || sch.n_blocks < 16) return WV_OK;
+    if (nqb < 2 || sch.n_blocks < 16) return WV_OK;
     const uint64_t key[4] = {nqb, sch.ntiles, sch.units_per_block, rotated ? 1u : 0u};
     if (!std::equal(key, key + 4, ix->blk_key)) {
         const int nb = sch.n_blocks;
@@ -572,26 +565,14 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
             const uint32_t* rowidx = nullptr) {
     const int ns = ix->h16_ns;
     const bool wd = ix->h16_wide;   // D > 128: the wide-D kernel
-    // the 16x16x32 kernel (one 16-entry list per column and slot) for k <=
-    // FIN_KF; wider k on the 32x32x16 kernel
-    // k <= FIN_KF: the one-wave-per-SIMD 16x16x32 kernel (h16_solo) or the
-    // opt-in two-waves-per-SIMD one (h16_quad) -- one 16-entry list per
-    // column and slot; wider k on the 32x32x16 kernel
-    const bool solo = ix->h16_solo && k <= wv::FIN_KF && !rowidx;
-    const bool quad = (ix->h16_quad || solo) && k <= wv::FIN_KF && !rowidx;   // (a gathered image: h16_index)
-    // D <= 128: 8-wave (512-query) workgroups, one per CU; WV_H16_WAVES=4:
-    // 4-wave (256-query) workgroups, two independent ones per CU; solo: one
-    // 4-wave 512-query workgroup per CU
-    const int waves = solo ? 4 : std::getenv("WV_H16_WAVES") && std::atoi(std::getenv("WV_H16_WAVES")) == 4 ? 4 : 8;
-    const int wg_per_cu = wd || solo ? 1 : 8 / waves;
-    // (WV_H16W_ROWS=64: the wide pass's 128-row tiles, for comparison)
-    const char* wre = std::getenv("WV_H16W_ROWS");
-    const int wide_rows = wre && std::atoi(wre) == 64 ? 64 : 128;
-    const int tile_rows = wd ? 2 * wide_rows : wv::H_BN, bq = wd ? wv::HW_BQ : solo ? wv::HS_BQ : waves * 64;
+    // D <= 128: 8-wave (512-query) workgroups, one per CU; D > 128: 256-row
+    // tiles x 256-query blocks, one workgroup per CU
+    const int wg_per_cu = 1;
+    const int tile_rows = wd ? wv::HW_BN : wv::H_BN, bq = wd ? wv::HW_BQ : 512;
     // seed minima per query and slot; lists per query and slot, entries per list
-    const int seed_prod = wd ? wv::HW_PROD : (quad ? wv::HQ_PROD : wv::H_PROD);
-    const int prod = quad ? 1 : seed_prod;
-    const int kp = quad ? wv::HQ_PROD * wv::HQ_KP : wv::BF_KP;
+    const int seed_prod = wd ? wv::HW_PROD : wv::H_PROD;
+    const int prod = seed_prod;
+    const int kp = wv::BF_KP;
     const uint64_t ntl = (N + tile_rows - 1) / tile_rows;
     const uint64_t words = ntl * (uint64_t)(tile_rows / 64);   // allow words the kernel reads
     const uint64_t* allow = d_allow;
@@ -621,8 +602,8 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     HIP_TRY(wv_launch_h16_qscale(ix->qmax_part.as<float>(), (nq + 3) / 4, ix->qmax.as<unsigned int>(), bsign,
                                  ix->qscale.as<float>(), s));
     HIP_TRY(wv_launch_h16_rows(d_q, ix->dpad, nullptr, nq, ix->dim, ns, bsign, 1.f, ix->qmax.as<unsigned int>(),
-                               ix->qimg16.p, 0, nullptr, ix->qres.as<float>(), quad, s));
-    const void* ximg = quad ? ix->ximg16q.p : ix->ximg16.p;
+                               ix->qimg16.p, 0, nullptr, ix->qres.as<float>(), 0, s));
+    const void* ximg = ix->ximg16.p;
     const float* xnorm = ix->xnorm.as<float>();
     const uint64_t* excl = ix->excl.as<uint64_t>();
     if (rowidx) {
@@ -657,13 +638,11 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     hp.nq = nq;
     hp.metric = ix->metric;
     hp.n_qblocks = nqb;
-    hp.wide_rows = wide_rows;
+    hp.wide_rows = 128;
     // 64-row tiles the pass need not mask: every row present and eligible
     // (no allow list; a compacted scan: the rows below N)
     hp.clean_tiles = wd ? 0 : rowidx ? N / wv::H_BN : allow ? 0 : std::min<uint64_t>(ix->clean_words, N / wv::H_BN);
-    hp.stagger = std::getenv("WV_H16_STAGGER") && std::atoi(std::getenv("WV_H16_STAGGER")) == 1;
-    hp.locality = 1;
-    if (const char* e = std::getenv("WV_BF_LOCALITY")) hp.locality = std::atoi(e);
+    hp.locality = 1;   // XCD-contiguous workgroup ids
     wv::BfFinParams fp{};
     fp.X = ix->vecs.as<float>();
     fp.Q = d_q;
@@ -718,8 +697,7 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
         hp.out_d = ix->cand_d.as<float>();
         hp.out_id = nullptr;
         TREC(6);
-        HIP_TRY(solo ? wv_launch_bf_h16s(&hp, ns / 2, 1, s)
-                     : quad ? wv_launch_bf_h16q(&hp, ns / 2, 1, waves, s) : wv_launch_bf_h16(&hp, ns, 1, waves, s));
+        HIP_TRY(wv_launch_bf_h16(&hp, ns, 1, s));
         wv::H16SeedParams sp{};
         sp.minima = ix->cand_d.as<float>();
         sp.n_slots = ss.n_slots;
@@ -743,13 +721,9 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
         TREC(7);
     }
     // the wide pass: query blocks cut at the same tile offsets where that
-    // costs no work (bf_schedule_aligned; WV_H16_ALIGNED=0: the flat schedule)
-    const char* ae = std::getenv("WV_H16_ALIGNED");
+    // costs no work (bf_schedule_aligned)
     wv::BfSchedule sch{};
-    // (WV_H16_ALIGNED=2: also the 8-wave D <= 128 pass, at any cost -- for measurements)
-    const int aligned = ae ? std::atoi(ae) : 1;
-    if ((wd && !wide && aligned >= 1) || (aligned == 2 && !wd && !quad && !wide && seed))
-        sch = wv::bf_schedule_aligned(nq, N, target(ntl), bq, tile_rows, aligned == 2);
+    if (wd && !wide) sch = wv::bf_schedule_aligned(nq, N, target(ntl), bq, tile_rows, false);
     if (sch.n_blocks == 0) sch = wv::bf_schedule(nq, N, target(ntl), bq, tile_rows);
     if (wide && (uint64_t)sch.n_slots * prod * kp > (uint64_t)wv::FINW_NE)
         return fail(WV_ESTATE, "run_h16: too many lists for the wide finalize");
@@ -768,29 +742,20 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     // 3.048 vs 3.092 ms per 1M x 10k key pass; without a seed -- corpora below
     // 64 * H_SAMPLE tiles -- it cuts the pass 4.13 -> 3.43 ms at 1M)
     // (the wide-D pass publishes from a lane pair's two lists: k <= 2 BF_KP)
-    hp.kth = k <= (wd ? 2 * kp : prod * kp) && (!seed || std::getenv("WV_H16_RUN_SEED")) &&
-                     !std::getenv("WV_H16_NO_RUNNING")
+    hp.kth = k <= (wd ? 2 * kp : prod * kp) && !seed && !std::getenv("WV_H16_NO_RUNNING")
                  ? k
                  : 0;
     // cross-slot threshold (32x32x16 pass, <= 32 list heads per query; on
     // unless WV_H16_XSLOT=0): 2.87-2.91 vs 2.98-3.00 ms per 1M x 10k key pass
     const char* xe = std::getenv("WV_H16_XSLOT");
     const bool xs_on = !xe || std::atoi(xe) != 0;
-    if (xs_on && (!quad || solo) && !wd && 2 * sch.n_slots <= 32 && k <= 2 * sch.n_slots) {
+    if (xs_on && !wd && 2 * sch.n_slots <= 32 && k <= 2 * sch.n_slots) {
         const size_t gb = (size_t)nq * 2 * sch.n_slots * 4;
         HIP_TRY(ix->gslot.ensure(gb));
         HIP_TRY(hipMemsetAsync(ix->gslot.p, 0x7F, gb, s));   // 3.4e38: no head yet
         hp.gslot = ix->gslot.as<float>();
         hp.xslot = 1;
         hp.kth = k;
-    }
-    // the wide pass's bucket bound (opt-in WV_H16W_BUCKETS=1)
-    const char* be = std::getenv("WV_H16W_BUCKETS");
-    if (wd && hp.kth && hp.kth <= 16 && be && std::atoi(be) == 1) {
-        const size_t bb = (size_t)nqb * bq * 16 * 4;
-        HIP_TRY(ix->gbkt.ensure(bb));
-        HIP_TRY(hipMemsetAsync(ix->gbkt.p, 0xFF, bb, s));
-        hp.gbkt = ix->gbkt.as<unsigned int>();
     }
     if (hp.kth) {
         HIP_TRY(ix->marg.ensure((size_t)nq * 4));
@@ -802,16 +767,13 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     hp.out_d = ix->cand_d.as<float>();
     hp.out_id = ix->cand_id.as<uint32_t>();
     // the 8-wave D <= 128 pass on the flat schedule: tiles rotated per query
-    // block (locality bit 2; WV_H16_ROTATE=0: off): 2.73-2.75 -> 2.66-2.68 ms
-    // per 1M x 10k pass, L2-miss bytes 5.23 -> 0.66 GB
-    const char* re = std::getenv("WV_H16_ROTATE");
-    const bool rotate = !wd && !quad && !solo && waves == 8 && nqb >= 2 && sch.ntiles == ntl && !(re && std::atoi(re) == 0);
+    // block (locality bit 2): 2.73-2.75 -> 2.66-2.68 ms per 1M x 10k pass,
+    // L2-miss bytes 5.23 -> 0.66 GB
+    const bool rotate = !wd && nqb >= 2 && sch.ntiles == ntl;
     if (rotate) hp.locality |= 2;
     if (int rc = block_order(ix, (uint64_t)nqb, sch, s, &hp.block_order, rotate)) return rc;
     TREC(0);
-    HIP_TRY(wd ? wv_launch_bf_h16w(&hp, s)
-               : solo ? wv_launch_bf_h16s(&hp, ns / 2, 0, s)
-               : (quad ? wv_launch_bf_h16q(&hp, ns / 2, 0, waves, s) : wv_launch_bf_h16(&hp, ns, 0, waves, s)));
+    HIP_TRY(wd ? wv_launch_bf_h16w(&hp, s) : wv_launch_bf_h16(&hp, ns, 0, s));
     TREC(1);
     if (rowidx)
         HIP_TRY(wv_launch_remap_ids(ix->cand_id.as<uint32_t>(), nq, sch.n_slots, prod * kp, bq, sch.ntiles,
@@ -873,7 +835,9 @@ int queue_fbd(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
     bp.scratch = ix->fbd_scr.as<float>();
     bp.n_scr = wv::FBD_SCR;
     bp.fb_total = ix->stat_acc.as<unsigned long long>() + 2;
-    if (std::getenv("WV_ABLATE_NO_FALLBACK")) return WV_OK;   // kernel ablations only
+#ifdef WV_ABLATION_BUILD
+    if (std::getenv("WV_ABLATE_NO_FALLBACK")) return WV_OK;   // kernel ablations only (tools/h16_ablate.sh)
+#endif
     HIP_TRY(wv_launch_fbd(ix->fail.as<int32_t>(), nq, &bp, s));
     return WV_OK;
 }
@@ -916,15 +880,15 @@ int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
             // rows -- on the f16 pass over their gathered image (h16_ok), else
             // on the fp32 pass over the row list
             const bool compact = (2 * n_ok < N && !std::getenv("WV_BF_NO_COMPACT")) || d_rowmask;
-            if (compact && h16_ok && !std::getenv("WV_BF_H16_NO_GATHER")) {
+            if (compact && h16_ok) {
                 std::vector<int32_t> none;
                 int rc2 = run_h16(ix, d_q, nq, k, nullptr, 0, n_ok, d_out_ids, d_out_d, d_out_n, s, none,
                                   ix->rowidx.as<uint32_t>());
                 if (rc2) return rc2;
                 return queue_fbd(ix, d_q, nq, k, d_allow, allow_nbits, allow_stride, d_out_ids, d_out_d, d_out_n, s);
             }
-            // (WV_BF_H16_NO_GATHER: round 2's rule -- the f16 pass masks the
-            // whole corpus unless the list keeps under 1/8 of it)
+            // (no gathered f16 pass: the f16 pass masks the whole corpus
+            // unless the list keeps under 1/8 of it)
             const uint64_t frac = ix->use_h16 && !allow_stride ? 8 : 2;
             if (((frac * n_ok < N && !std::getenv("WV_BF_NO_COMPACT")) || d_rowmask) && k <= wv::BF_FAST_KMAX) {
                 n_scan = n_ok;
@@ -938,18 +902,11 @@ int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
             return queue_fbd(ix, d_q, nq, k, d_allow, allow_nbits, allow_stride, d_out_ids, d_out_d, d_out_n, s);
         }
         // bf16x3 key pass on native images (whole-corpus or shared allow list
-        // scans): 256-query blocks, one 512-thread workgroup per CU, two waves
-        // per SIMD (wv_bf_split_kernel, the fastest measured); WV_BF_BQ=128
-        // runs 128-query blocks (two 256-thread workgroups per CU) and
-        // WV_BF_BQ=192 the three-waves-per-SIMD kernel (wv_bf_split3_kernel)
+        // scans, opt-in WV_BF_SPLIT=1): 256-query blocks, one 512-thread
+        // workgroup per CU, two waves per SIMD (wv_bf_split_kernel)
         const bool split = ix->use_split && !d_rowidx && !allow_stride;
-        int bq = wv::BF_BQ;
-        if (split) {
-            const char* e = std::getenv("WV_BF_BQ");
-            const int v = e ? std::atoi(e) : 0;
-            bq = v == wv::BF_BQ ? wv::BF_BQ : v == wv::BF_BQ3 ? wv::BF_BQ3 : 2 * wv::BF_BQ;
-        }
-        const int prod = bq == wv::BF_BQ3 ? wv::BF_PROD3 : wv::BF_PROD;
+        const int bq = split ? 2 * wv::BF_BQ : wv::BF_BQ;
+        const int prod = wv::BF_PROD;
         const int n_qblocks = (nq + bq - 1) / bq;
         const wv::BfSchedule sch =
             wv::bf_schedule(nq, n_scan, bq == wv::BF_BQ ? ix->bf_blocks : ix->bf_blocks / 2, bq);
@@ -977,10 +934,7 @@ int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
         bp.split = split ? 1 : 0;
         bp.bq = bq;
         bp.prod = prod;
-        {
-            const char* e = std::getenv("WV_BF_LOCALITY");   // ablation: 0..3, default 3
-            bp.locality = e ? std::atoi(e) : 3;
-        }
+        bp.locality = 3;   // XCD-contiguous workgroups, aligned tile rotation
         bp.X = split ? ix->xsplit.as<float>() : ix->vecs.as<float>();
         bp.Q = ix->q_scaled.as<float>();
         bp.xnorm = ix->xnorm.as<float>();
@@ -1042,7 +996,9 @@ int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
         for (int i = 0; i < nq; ++i) fails.push_back(i);
     }
     ix->last_fallbacks += fails.size();
+#ifdef WV_ABLATION_BUILD
     if (!fails.empty() && std::getenv("WV_ABLATE_NO_FALLBACK")) fails.clear();   // kernel ablations only
+#endif
     if (!fails.empty() && keyed) {
         // batched threshold filter over the corpus for every failed query
         std::vector<int32_t> rest;
@@ -1494,9 +1450,7 @@ int wv_index_create(int dim, int metric, const wv_config* cfg, uint64_t capacity
         int cus = 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ix->cfg.device) != hipSuccess || cus <= 0)
             cus = 256;
-        int rounds = 1;
-        if (const char* r = std::getenv("WV_BF_ROUNDS")) rounds = std::max(1, std::atoi(r));
-        ix->bf_blocks = cus * 2 * rounds;
+        ix->bf_blocks = cus * 2;
         ix->n_cus = cus;
     }
     ix->bm_words = (capacity + 63) / 64;
@@ -1515,31 +1469,19 @@ int wv_index_create(int dim, int metric, const wv_config* cfg, uint64_t capacity
     // fp32 MFMA pass for every scan
     // f16 key pass (wv_bf_h16_kernel) for D <= 128 unless an ablation switch
     // asks for the bf16x3 (WV_BF_SPLIT=1) or the fp32 (WV_BF_FP32=1) pass
-    ix->use_h16 = dim <= 16 * wv::HW_NS_MAX && !std::getenv("WV_BF_FP32") && !std::getenv("WV_BF_SPLIT") &&
-                  (dim <= 16 * wv::H_NS_MAX || !std::getenv("WV_BF_NO_H16W"));
+    ix->use_h16 = dim <= 16 * wv::HW_NS_MAX && !std::getenv("WV_BF_FP32") && !std::getenv("WV_BF_SPLIT");
     if (ix->use_h16) {
         // D > 128: the wide-D kernel, whose chunks are HW_KC 16-k steps
         ix->h16_wide = dim > 16 * wv::H_NS_MAX;
         ix->h16_ns = ix->h16_wide ? (dim + 16 * wv::HW_KC - 1) / (16 * wv::HW_KC) * wv::HW_KC : (dim + 15) / 16;
-        // opt-in 16x16x32 pass (WV_H16_QUAD=1) when D fills whole 32-k steps:
-        // 4.3 % faster key pass, but its 4-entry lists fail the certificate
-        // for ~0.3 % of the queries (31 of 10k at 1M x 128), whose device
-        // fallback costs more than the pass gains
-        const char* eq = std::getenv("WV_H16_QUAD");
-        ix->h16_quad = !ix->h16_wide && ix->h16_ns % 2 == 0 && eq && std::atoi(eq) == 1;
-        // the one-wave-per-SIMD 16x16x32 kernel (WV_H16_SOLO=1)
-        const char* es = std::getenv("WV_H16_SOLO");
-        ix->h16_solo = !ix->h16_wide && ix->h16_ns % 2 == 0 && es && std::atoi(es) == 1;
         const size_t ibytes = cap_rows * (size_t)ix->h16_ns * 16 * 2;
         if (ix->ximg16.ensure(ibytes) != hipSuccess || ix->xns.ensure(cap_rows * 4) != hipSuccess ||
-            ((ix->h16_quad || ix->h16_solo) && ix->ximg16q.ensure(ibytes) != hipSuccess) ||
             ix->ex_bits.ensure(4) != hipSuccess || ix->qmax.ensure(4) != hipSuccess ||
             ix->qscale.ensure(4) != hipSuccess) {
             wv_index_destroy(ix);
             return fail(WV_EOOM, "wv_index_create: device allocation failed");
         }
         (void)hipMemsetAsync(ix->ximg16.p, 0, ibytes, ix->stream);
-        if (ix->h16_quad || ix->h16_solo) (void)hipMemsetAsync(ix->ximg16q.p, 0, ibytes, ix->stream);
         (void)hipMemsetAsync(ix->xns.p, 0, cap_rows * 4, ix->stream);
         (void)hipMemsetAsync(ix->ex_bits.p, 0, 4, ix->stream);
     }
@@ -1569,8 +1511,8 @@ int wv_index_destroy(wv_index* ix) {
                       &ix->sort_tmp, &ix->g_idx, &ix->g_q, &ix->g_allow, &ix->g_ids, &ix->g_d, &ix->g_n, &ix->g_cnt,
                       &ix->out_ids, &ix->out_d, &ix->out_n, &ix->stage, &ix->fail_thr, &ix->fb_idx, &ix->fb_d, &ix->fb_i, &ix->fb_n, &ix->fb_of,
                       &ix->ac_cnt, &ix->ac_off, &ix->rowidx, &ix->pq_cent, &ix->pq_codes, &ix->pk_key,
-                      &ix->pk_dist, &ix->pk_val, &ix->pk_skey, &ix->pk_sval, &ix->pk_off, &ix->ximg16, &ix->ximg16q, &ix->qmax_part, &ix->xns,
-                      &ix->qimg16, &ix->qres, &ix->qmax, &ix->qscale, &ix->tau, &ix->gtau, &ix->marg, &ix->allow_pad, &ix->ex_bits, &ix->gslot, &ix->gbkt, &ix->blk_order,
+                      &ix->pk_dist, &ix->pk_val, &ix->pk_skey, &ix->pk_sval, &ix->pk_off, &ix->ximg16, &ix->qmax_part, &ix->xns,
+                      &ix->qimg16, &ix->qres, &ix->qmax, &ix->qscale, &ix->tau, &ix->gtau, &ix->marg, &ix->allow_pad, &ix->ex_bits, &ix->gslot, &ix->blk_order,
                       &ix->delta, &ix->dmask, &ix->dl_ids, &ix->dl_d, &ix->dl_n, &ix->dq_tmp, &ix->b_tgt, &ix->b_ci,
                       &ix->b_cd, &ix->b_cn, &ix->b_cnt0, &ix->b_cntu, &ix->b_rk, &ix->b_rn, &ix->b_rk2, &ix->b_rn2,
                       &ix->b_uk, &ix->b_ul, &ix->b_uo, &ix->b_nr, &ix->b_tmp, &ix->stat_acc, &ix->fbd_list,
@@ -1623,9 +1565,9 @@ static int rows_written(wv_index* ix, const uint64_t* d_ids, uint64_t n, uint64_
     if (ix->h16_sx == 0.f || rebuild) ix->h16_sx = sx;
     unsigned int* exb = ix->ex_bits.as<unsigned int>();
     if (rebuild) HIP_TRY(hipMemsetAsync(exb, 0, 4, ix->stream));
-    // both layouts: 32x32x16 (ximg16) and, with h16_quad, 16x16x32 (ximg16q)
-    for (int quad = 0; quad <= (ix->h16_quad || ix->h16_solo ? 1 : 0); ++quad) {
-        void* img = quad ? ix->ximg16q.p : ix->ximg16.p;
+    {
+        void* img = ix->ximg16.p;
+        const int quad = 0;
         if (rebuild) {
             HIP_TRY(wv_launch_h16_rows(ix->vecs.as<float>(), ix->ldx, nullptr, ix->n_rows, ix->dim, ix->h16_ns, 1.f,
                                        ix->h16_sx, nullptr, img, 0, exb, nullptr, quad, ix->stream));
@@ -1926,7 +1868,6 @@ int wv_index_reserve(wv_index* ix, uint64_t capacity) {
     HIP_TRY(regrow(ix->xnorm, old_rows * 4, cap_rows * 4, s));
     HIP_TRY(regrow(ix->xns, old_rows * 4, cap_rows * 4, s));
     HIP_TRY(regrow(ix->ximg16, old_rows * img, cap_rows * img, s));
-    HIP_TRY(regrow(ix->ximg16q, old_rows * img, cap_rows * img, s));
     HIP_TRY(regrow(ix->pq_codes, ix->capacity * ix->pq_stride, capacity * ix->pq_stride, s));
     // bitmaps are rewritten from the host copies by the next refresh
     HIP_TRY(ix->tomb.ensure(words * 8));

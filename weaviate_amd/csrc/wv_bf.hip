@@ -627,445 +627,6 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void wv_bf_split_kernel(BfParams 
 }
 
 // ---------------------------------------------------------------------------
-// Split key pass, one wave per SIMD (D in (96, 128]: NK = 4 chunks).
-//
-// The two-waves-per-SIMD kernel above leaves the MFMA pipe idle half the time
-// (ablation: its MFMA + LDS floor is 4.5 ms per 1M x 10k batch, the kernel
-// 8.1 ms): each wave keeps one chunk of corpus operands in flight, and its
-// epilogue and operand waits are not covered by the partner wave.  Here one
-// 256-thread workgroup per CU runs 4 waves (one per SIMD, 512 registers
-// each), wave (wm, wn) owning base rows 64 wm .. +63 and queries
-// 128 wn .. +127 of the 128 x 256 tile (8 accumulators of 32 x 32, 192 MFMAs
-// per tile), and a 4-slot operand ring indexed by the chunk keeps 3 chunks
-// (~4.6k cycles) of corpus operands in flight.  Same images, lists (4 query
-// columns per lane), producers and finalize as wv_bf_split_kernel.
-// Measured SLOWER (11.5 vs 8.1 ms, parity green): with no partner wave the
-// B-operand LDS reads at each k-step and the epilogue (acc reads from AGPRs,
-// 4 columns) are exposed; kept opt-in (WV_BF_SPLIT_1W=1) as the base for a
-// B-prefetching variant.
-template <bool L2>
-__global__ __launch_bounds__(256, 1) void wv_bf_split1_kernel(BfParams p) {
-    extern __shared__ uint4 qimg[];            // [8 query groups][NK][2 s][2 part][64 lanes]
-    constexpr int NK = 4;
-    constexpr int GRP = NK * 4 * 64;
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave >> 1, wn = wave & 1;
-    const int khalf = lane >> 5;
-    const int l31 = lane & 31;
-    const uint64_t tomb_words = (p.tomb_nbits + 63) / 64;
-    const uint64_t allow_words = (p.allow_nbits + 63) / 64;
-    const uint64_t* __restrict__ tomb = p.tomb;
-    const uint64_t* __restrict__ allow = p.allow;
-    const uint4* __restrict__ X = reinterpret_cast<const uint4*>(p.X);
-    const uint4* __restrict__ Qg = reinterpret_cast<const uint4*>(p.Q);
-    int lb = (int)blockIdx.x;
-    if ((p.locality & 1) && gridDim.x % 8 == 0) lb = (int)(blockIdx.x % 8) * (int)(gridDim.x / 8) + (int)(blockIdx.x / 8);
-    const uint64_t u_first = (uint64_t)lb * p.units_per_block;
-    uint64_t u_last = u_first + p.units_per_block;
-    if (u_last > (uint64_t)p.n_qblocks * p.ntiles) u_last = (uint64_t)p.n_qblocks * p.ntiles;
-    float* __restrict__ xnl = reinterpret_cast<float*>(qimg + 8 * GRP) + wave * 64;
-
-    for (uint64_t u = u_first; u < u_last;) {
-        const int qb = (int)(u / p.ntiles);
-        const uint64_t t_begin = u % p.ntiles;
-        uint64_t t_end = t_begin + (u_last - u);
-        if (t_end > p.ntiles) t_end = p.ntiles;
-        u += t_end - t_begin;
-        const int slot = lb - bf_first_block(qb, p.ntiles, p.units_per_block);
-        uint64_t rt_begin = t_begin;
-        if (p.locality & 2) {
-            const uint64_t rot = ((p.units_per_block - (uint64_t)qb * p.ntiles % p.units_per_block) %
-                                  p.units_per_block) % p.ntiles;
-            rt_begin = t_begin >= rot ? t_begin - rot : t_begin + p.ntiles - rot;
-        }
-        const int jq_base = qb * 256 + wn * 128 + l31;   // columns jq_base + 32 j, j = 0..3
-
-        __syncthreads();   // the previous segment's reads of qimg are done
-        {
-            const uint4* __restrict__ src = Qg + (uint64_t)qb * 8 * GRP;
-#pragma unroll
-            for (int i = 0; i < 8 * GRP / 256; ++i) qimg[tid + 256 * i] = src[tid + 256 * i];
-        }
-        __syncthreads();
-
-        float ld[4][BF_KP];
-        uint32_t li[4][BF_KP];
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int i = 0; i < BF_KP; ++i) { ld[j][i] = FLT_MAX; li[j][i] = WV_NIL; }
-        const uint4* __restrict__ qw = qimg + 4 * wn * GRP + lane;   // query groups 4 wn .. 4 wn + 3
-        auto xsrc = [&](uint64_t tile, int c) { return X + (tile * 4 + 2 * wm) * GRP + c * 256 + lane; };
-        uint4 xb[2][8];   // operand ping-pong: slot = chunk & 1
-        auto load_x = [&](uint4 (&dst)[8], const uint4* src) {
-#pragma unroll
-            for (int h = 0; h < 2; ++h)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) dst[4 * h + j] = src[h * GRP + 64 * j];
-        };
-        float xv = 0.f;
-        const int ntile = (int)(t_end - t_begin);
-        if (ntile > 0) {
-            load_x(xb[0], xsrc(rt_begin, 0));
-            if (L2) xnl[lane] = p.xnorm[rt_begin * BF_BN + wm * 64 + lane];
-        }
-        uint64_t tw_next = 0, aw_next = ~0ull;
-        auto load_words = [&](uint64_t tile) {
-            const uint64_t w = (tile * BF_BN + wm * 64) >> 6;
-            tw_next = tomb && w < tomb_words ? tomb[w] : 0ull;
-            if (allow) aw_next = w < allow_words ? allow[w] : 0ull;
-        };
-        if (ntile > 0) load_words(rt_begin);
-        // B operands (queries, from LDS) double-buffered by k-step parity: the
-        // next step's 8 reads are issued before this step's 24 MFMAs; the
-        // step after the tile's last is step 0 again (same query block)
-        bf16x8 bh[2][4], bl[2][4];
-        auto load_b = [&](int buf, int c, int s2) {
-            const int qo = c * 256 + s2 * 128;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                bh[buf][j] = __builtin_bit_cast(bf16x8, qw[j * GRP + qo]);
-                bl[buf][j] = __builtin_bit_cast(bf16x8, qw[j * GRP + qo + 64]);
-            }
-        };
-        load_b(0, 0, 0);
-        for (int t = 0; t < ntile; ++t) {
-            uint64_t tile = rt_begin + (uint64_t)t;
-            if (tile >= p.ntiles) tile -= p.ntiles;
-            uint64_t ntl = tile + 1;
-            if (ntl >= p.ntiles) ntl -= p.ntiles;
-            const uint64_t row0 = tile * BF_BN + wm * 64;
-            const uint64_t tw = tw_next, aw = aw_next;
-
-            floatx16 acc[2][4];
-            floatx16 xc0, xc1;
-            if (L2) {
-#pragma unroll
-                for (int g4 = 0; g4 < 4; ++g4) {
-                    const float4 a = *reinterpret_cast<const float4*>(xnl + 4 * khalf + 8 * g4);
-                    const float4 b = *reinterpret_cast<const float4*>(xnl + 32 + 4 * khalf + 8 * g4);
-                    xc0[4 * g4] = a.x; xc0[4 * g4 + 1] = a.y; xc0[4 * g4 + 2] = a.z; xc0[4 * g4 + 3] = a.w;
-                    xc1[4 * g4] = b.x; xc1[4 * g4 + 1] = b.y; xc1[4 * g4 + 2] = b.z; xc1[4 * g4 + 3] = b.w;
-                }
-            } else {
-#pragma unroll
-                for (int r = 0; r < 16; ++r) { xc0[r] = 0.f; xc1[r] = 0.f; }
-            }
-#pragma unroll
-            for (int c = 0; c < NK; ++c) {
-                if (c + 1 < NK) load_x(xb[(c + 1) & 1], xsrc(tile, c + 1));
-                else if (t + 1 < ntile) load_x(xb[0], xsrc(ntl, 0));
-                if (L2 && c == 0 && t + 1 < ntile) xv = p.xnorm[ntl * BF_BN + wm * 64 + lane];
-                __builtin_amdgcn_sched_group_barrier(0x020, 9, 0);
-                const uint4* cur = xb[c & 1];
-#pragma unroll
-                for (int s2 = 0; s2 < 2; ++s2) {
-                    if (s2 == 0) load_b(1, c, 1);
-                    else load_b(0, (c + 1) % NK, 0);
-                    const bf16x8* bhc = bh[s2];
-                    const bf16x8* blc = bl[s2];
-                    const bf16x8 ah0 = __builtin_bit_cast(bf16x8, cur[2 * s2]);
-                    const bf16x8 al0 = __builtin_bit_cast(bf16x8, cur[2 * s2 + 1]);
-                    const bf16x8 ah1 = __builtin_bit_cast(bf16x8, cur[4 + 2 * s2]);
-                    const bf16x8 al1 = __builtin_bit_cast(bf16x8, cur[4 + 2 * s2 + 1]);
-                    const bool first = c == 0 && s2 == 0;
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        acc[0][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al0, bhc[j], first ? xc0 : acc[0][j], 0, 0, 0);
-                        acc[1][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al1, bhc[j], first ? xc1 : acc[1][j], 0, 0, 0);
-                    }
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        acc[0][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah0, blc[j], acc[0][j], 0, 0, 0);
-                        acc[1][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah1, blc[j], acc[1][j], 0, 0, 0);
-                    }
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        acc[0][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah0, bhc[j], acc[0][j], 0, 0, 0);
-                        acc[1][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah1, bhc[j], acc[1][j], 0, 0, 0);
-                    }
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            if (L2 && t + 1 < ntile) xnl[lane] = xv;
-            if (t + 1 < ntile) load_words(ntl);
-            auto uni64 = [](uint64_t v) {
-                return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
-                       ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32);
-            };
-            uint64_t okw = ~uni64(tw) & uni64(aw);
-            if (row0 + 64 > p.N) okw &= p.N > row0 ? ((1ull << (p.N - row0)) - 1) : 0ull;
-            const uint32_t rb0 = (uint32_t)row0 + 4 * khalf;
-            const float INF = __builtin_inff();
-            if (okw != ~0ull || (qb + 1) * 256 > p.nq) {
-                const uint64_t okl = okw >> (4 * khalf);
-                constexpr uint32_t LANE_ROWS = 0x0F0F0F0Fu;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const uint64_t o = jq_base + 32 * j < p.nq ? okl : 0ull;
-                    const uint32_t olo = (uint32_t)o, ohi = (uint32_t)(o >> 32);
-                    if (!__all((olo & ohi & LANE_ROWS) == LANE_ROWS)) {
-#pragma unroll
-                        for (int r = 0; r < 16; ++r) {
-                            const int bit = (r & 3) + 8 * (r >> 2);
-                            acc[0][j][r] = (olo >> bit) & 1u ? acc[0][j][r] : INF;
-                            acc[1][j][r] = (ohi >> bit) & 1u ? acc[1][j][r] : INF;
-                        }
-                    }
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                float m = INF;
-#pragma unroll
-                for (int r = 0; r < 16; ++r) m = min3_raw(m, acc[0][j][r], acc[1][j][r]);
-                while (m <= ld[j][BF_KP - 1]) {
-                    uint32_t rb = rb0;   // opaque: the row ids stay in this rare loop
-                    asm volatile("" : "+v"(rb));
-                    uint32_t idm = WV_NIL;
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const bool hit = idm == WV_NIL && acc[0][j][r] == m;
-                        idm = hit ? rb + (r & 3) + 8 * (r >> 2) : idm;
-                        acc[0][j][r] = hit ? INF : acc[0][j][r];
-                    }
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const bool hit = idm == WV_NIL && acc[1][j][r] == m;
-                        idm = hit ? rb + 32 + (r & 3) + 8 * (r >> 2) : idm;
-                        acc[1][j][r] = hit ? INF : acc[1][j][r];
-                    }
-                    if (!key_less(m, idm, ld[j][BF_KP - 1], li[j][BF_KP - 1])) break;
-                    list_insert(ld[j], li[j], m, idm);
-                    m = INF;
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) m = min3_raw(m, acc[0][j][r], acc[1][j][r]);
-                }
-            }
-        }
-
-        const int prod = wm * 2 + khalf;
-        const size_t per_q = (size_t)p.n_slots * BF_PROD * BF_KP;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int jq = jq_base + 32 * j;
-            if (jq < p.nq) {
-                const size_t base = (size_t)jq * per_q + ((size_t)slot * BF_PROD + prod) * BF_KP;
-#pragma unroll
-                for (int i = 0; i < BF_KP; ++i) { p.out_d[base + i] = ld[j][i]; p.out_id[base + i] = li[j][i]; }
-            }
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Split key pass, three waves per SIMD (opt-in: WV_BF_BQ=192).
-//
-// Measured 8.6 ms vs 8.1 ms for wv_bf_split_kernel on 1M x 128 x 10k (parity
-// green): the smaller per-wave tile doubles the query-operand LDS reads and
-// the corpus loads per MFMA, which costs more than the third wave recovers.
-//
-// Ablation of wv_bf_split_kernel (two waves per SIMD, 64 x 64 per wave): the
-// MFMA + LDS floor is 4.5 ms per 1M x 10k batch but the kernel takes 8.1 ms,
-// because one wave's epilogue and operand waits are not covered by its single
-// partner.  Here each wave owns 32 base rows x 64 queries (2 accumulators,
-// 48 MFMAs per tile), which fits 168 VGPRs: a 768-thread workgroup of 12 waves
-// (4 row waves x 3 query waves) per CU runs 3 waves per SIMD over a
-// 128-row x 192-query tile; the 192-query block image (96 KiB at D = 128)
-// stays in LDS.  Eight producers per query (4 row waves x 2 lane halves).
-template <int NK, bool L2>
-__global__ __launch_bounds__(768, 1) void wv_bf_split3_kernel(BfParams p) {
-    extern __shared__ uint4 qimg[];            // [6 query groups][NK][2 s][2 part][64 lanes]
-    constexpr int GRP = NK * 4 * 64;
-    constexpr int QW = 3;                      // query waves (64 queries each)
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave / QW, wn = wave % QW;   // rows 32 wm .. +31, queries 64 wn .. +63
-    const int khalf = lane >> 5;
-    const int l31 = lane & 31;
-    const uint64_t tomb_words = (p.tomb_nbits + 63) / 64;
-    const uint64_t allow_words = (p.allow_nbits + 63) / 64;
-    const uint64_t* __restrict__ tomb = p.tomb;
-    const uint64_t* __restrict__ allow = p.allow;
-    const uint4* __restrict__ X = reinterpret_cast<const uint4*>(p.X);
-    const uint4* __restrict__ Qg = reinterpret_cast<const uint4*>(p.Q);
-    int lb = (int)blockIdx.x;
-    if ((p.locality & 1) && gridDim.x % 8 == 0) lb = (int)(blockIdx.x % 8) * (int)(gridDim.x / 8) + (int)(blockIdx.x / 8);
-    const uint64_t u_first = (uint64_t)lb * p.units_per_block;
-    uint64_t u_last = u_first + p.units_per_block;
-    if (u_last > (uint64_t)p.n_qblocks * p.ntiles) u_last = (uint64_t)p.n_qblocks * p.ntiles;
-    float* __restrict__ xnl = reinterpret_cast<float*>(qimg + 2 * QW * GRP) + wave * 32;
-
-    for (uint64_t u = u_first; u < u_last;) {
-        const int qb = (int)(u / p.ntiles);
-        const uint64_t t_begin = u % p.ntiles;
-        uint64_t t_end = t_begin + (u_last - u);
-        if (t_end > p.ntiles) t_end = p.ntiles;
-        u += t_end - t_begin;
-        const int slot = lb - bf_first_block(qb, p.ntiles, p.units_per_block);
-        uint64_t rt_begin = t_begin;
-        if (p.locality & 2) {
-            const uint64_t rot = ((p.units_per_block - (uint64_t)qb * p.ntiles % p.units_per_block) %
-                                  p.units_per_block) % p.ntiles;
-            rt_begin = t_begin >= rot ? t_begin - rot : t_begin + p.ntiles - rot;
-        }
-        const int jq0 = qb * 64 * QW + wn * 64 + l31;
-        const int jq1 = jq0 + 32;
-
-        __syncthreads();   // the previous segment's reads of qimg are done
-        {
-            const uint4* __restrict__ src = Qg + (uint64_t)qb * 2 * QW * GRP;
-#pragma unroll
-            for (int i = 0; i < 2 * QW * GRP / 768; ++i) qimg[tid + 768 * i] = src[tid + 768 * i];
-        }
-        __syncthreads();
-
-        float l0d[BF_KP], l1d[BF_KP];
-        uint32_t l0i[BF_KP], l1i[BF_KP];
-#pragma unroll
-        for (int i = 0; i < BF_KP; ++i) {
-            l0d[i] = FLT_MAX; l1d[i] = FLT_MAX;
-            l0i[i] = WV_NIL; l1i[i] = WV_NIL;
-        }
-        const uint4* __restrict__ qw = qimg + 2 * wn * GRP + lane;   // query groups 2 wn, 2 wn + 1
-        auto xsrc = [&](uint64_t tile, int c) { return X + (tile * 4 + wm) * GRP + c * 256 + lane; };
-        uint4 xb[2][4];   // ping-pong by chunk parity: [s][part]
-        auto load_x = [&](uint4 (&dst)[4], const uint4* src) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) dst[j] = src[64 * j];
-        };
-        float xv = 0.f;
-        const int ntile = (int)(t_end - t_begin);
-        if (ntile > 0) {
-            load_x(xb[0], xsrc(rt_begin, 0));
-            if (L2 && lane < 32) xnl[lane] = p.xnorm[rt_begin * BF_BN + wm * 32 + lane];
-        }
-        uint64_t tw_next = 0, aw_next = ~0ull;
-        auto load_words = [&](uint64_t tile) {
-            const uint64_t w = (tile * BF_BN + wm * 32) >> 6;
-            tw_next = tomb && w < tomb_words ? tomb[w] : 0ull;
-            if (allow) aw_next = w < allow_words ? allow[w] : 0ull;
-        };
-        if (ntile > 0) load_words(rt_begin);
-        for (int t = 0; t < ntile; ++t) {
-            uint64_t tile = rt_begin + (uint64_t)t;
-            if (tile >= p.ntiles) tile -= p.ntiles;
-            uint64_t ntl = tile + 1;
-            if (ntl >= p.ntiles) ntl -= p.ntiles;
-            const uint64_t row0 = tile * BF_BN + wm * 32;
-            const uint64_t tw = tw_next, aw = aw_next;
-
-            floatx16 acc0, acc1, xc;
-            if (L2) {
-#pragma unroll
-                for (int g4 = 0; g4 < 4; ++g4) {
-                    const float4 a = *reinterpret_cast<const float4*>(xnl + 4 * khalf + 8 * g4);
-                    xc[4 * g4] = a.x; xc[4 * g4 + 1] = a.y; xc[4 * g4 + 2] = a.z; xc[4 * g4 + 3] = a.w;
-                }
-            } else {
-#pragma unroll
-                for (int r = 0; r < 16; ++r) xc[r] = 0.f;
-            }
-#pragma unroll
-            for (int c = 0; c < NK; ++c) {
-                if (c + 1 < NK) load_x(xb[(c + 1) & 1], xsrc(tile, c + 1));
-                else if (t + 1 < ntile) load_x(xb[NK & 1], xsrc(ntl, 0));
-                if (L2 && c == 0 && t + 1 < ntile && lane < 32) xv = p.xnorm[ntl * BF_BN + wm * 32 + lane];
-                __builtin_amdgcn_sched_group_barrier(0x020, 5, 0);
-                const uint4* cur = xb[c & 1];
-#pragma unroll
-                for (int s2 = 0; s2 < 2; ++s2) {
-                    const int qo = c * 256 + s2 * 128;
-                    const bf16x8 bh0 = __builtin_bit_cast(bf16x8, qw[qo]);
-                    const bf16x8 bl0 = __builtin_bit_cast(bf16x8, qw[qo + 64]);
-                    const bf16x8 bh1 = __builtin_bit_cast(bf16x8, qw[GRP + qo]);
-                    const bf16x8 bl1 = __builtin_bit_cast(bf16x8, qw[GRP + qo + 64]);
-                    const bf16x8 ah = __builtin_bit_cast(bf16x8, cur[2 * s2]);
-                    const bf16x8 al = __builtin_bit_cast(bf16x8, cur[2 * s2 + 1]);
-                    const bool first = c == 0 && s2 == 0;
-                    acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh0, first ? xc : acc0, 0, 0, 0);
-                    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh1, first ? xc : acc1, 0, 0, 0);
-                    acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl0, acc0, 0, 0, 0);
-                    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl1, acc1, 0, 0, 0);
-                    acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh0, acc0, 0, 0, 0);
-                    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh1, acc1, 0, 0, 0);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            if constexpr (NK & 1) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) xb[0][j] = xb[1][j];
-            }
-            if (L2 && t + 1 < ntile && lane < 32) xnl[lane] = xv;
-            if (t + 1 < ntile) load_words(ntl);
-            auto uni64 = [](uint64_t v) {
-                return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
-                       ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32);
-            };
-            // eligibility of the wave's 32 rows (bit i = row row0 + i)
-            uint64_t okw = (~uni64(tw) & uni64(aw)) >> (row0 & 63);
-            if (row0 + 32 > p.N) okw &= p.N > row0 ? ((1ull << (p.N - row0)) - 1) : 0ull;
-            const uint32_t ok32 = (uint32_t)okw;
-            const uint32_t rb0 = (uint32_t)row0 + 4 * khalf;
-            const float INF = __builtin_inff();
-            if (ok32 != 0xFFFFFFFFu || (qb + 1) * 64 * QW > p.nq) {
-                const uint32_t o0 = (jq0 < p.nq ? ok32 : 0u) >> (4 * khalf);
-                const uint32_t o1 = (jq1 < p.nq ? ok32 : 0u) >> (4 * khalf);
-                constexpr uint32_t LANE_ROWS = 0x0F0F0F0Fu;
-                if (!__all((o0 & o1 & LANE_ROWS) == LANE_ROWS)) {
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const int bit = (r & 3) + 8 * (r >> 2);
-                        acc0[r] = (o0 >> bit) & 1u ? acc0[r] : INF;
-                        acc1[r] = (o1 >> bit) & 1u ? acc1[r] : INF;
-                    }
-                }
-            }
-            float m0 = INF, m1 = INF;
-#pragma unroll
-            for (int r = 0; r < 16; r += 2) {
-                m0 = min3_raw(m0, acc0[r], acc0[r + 1]);
-                m1 = min3_raw(m1, acc1[r], acc1[r + 1]);
-            }
-#define WV_EXTRACT3(M, A, LD, LI)                                                                \
-            while (M <= LD[BF_KP - 1]) {                                                        \
-                uint32_t rb = rb0;  /* opaque: the row ids stay in this rare loop */             \
-                asm volatile("" : "+v"(rb));                                                    \
-                uint32_t idm = WV_NIL;                                                          \
-                _Pragma("unroll") for (int r = 0; r < 16; ++r) {                                \
-                    const bool hit = idm == WV_NIL && A[r] == M;                                \
-                    idm = hit ? rb + (r & 3) + 8 * (r >> 2) : idm;                              \
-                    A[r] = hit ? INF : A[r];                                                    \
-                }                                                                               \
-                if (!key_less(M, idm, LD[BF_KP - 1], LI[BF_KP - 1])) break;                     \
-                list_insert(LD, LI, M, idm);                                                    \
-                M = INF;                                                                        \
-                _Pragma("unroll") for (int r = 0; r < 16; r += 2) M = min3_raw(M, A[r], A[r + 1]); \
-            }
-            WV_EXTRACT3(m0, acc0, l0d, l0i)
-            WV_EXTRACT3(m1, acc1, l1d, l1i)
-#undef WV_EXTRACT3
-        }
-
-        const int prod = wm * 2 + khalf;
-        const size_t per_q = (size_t)p.n_slots * BF_PROD3 * BF_KP;
-        if (jq0 < p.nq) {
-            const size_t base = (size_t)jq0 * per_q + ((size_t)slot * BF_PROD3 + prod) * BF_KP;
-#pragma unroll
-            for (int i = 0; i < BF_KP; ++i) { p.out_d[base + i] = l0d[i]; p.out_id[base + i] = l0i[i]; }
-        }
-        if (jq1 < p.nq) {
-            const size_t base = (size_t)jq1 * per_q + ((size_t)slot * BF_PROD3 + prod) * BF_KP;
-#pragma unroll
-            for (int i = 0; i < BF_KP; ++i) { p.out_d[base + i] = l1d[i]; p.out_id[base + i] = l1i[i]; }
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
 // Finalize: one wave per query.
 
 // FAST: every query has <= 256 list entries (n_slots * prod * kp): the
@@ -1973,20 +1534,6 @@ hipError_t wv_launch_bf_mfma(const wv::BfParams* p, hipStream_t s) {
         if (p->ldx % wv::BF_BK || p->ldq != p->ldx || nk < 1 || nk > 4 || p->rowidx || p->allow_stride)
             return hipErrorInvalidValue;
         const bool l2 = p->metric == WV_METRIC_L2;
-        if (p->bq == wv::BF_BQ3) {   // three waves per SIMD (opt-in)
-            const size_t lds3 = (size_t)nk * 6 * 4096 + 12 * 128;
-#define WV_SPLIT3_LAUNCH(NK)                                                                                   \
-            if (l2) hipLaunchKernelGGL((wv::wv_bf_split3_kernel<NK, true>), dim3(nb), dim3(768), lds3, s, *p);   \
-            else hipLaunchKernelGGL((wv::wv_bf_split3_kernel<NK, false>), dim3(nb), dim3(768), lds3, s, *p);
-            switch (nk) {
-                case 1: WV_SPLIT3_LAUNCH(1) break;
-                case 2: WV_SPLIT3_LAUNCH(2) break;
-                case 3: WV_SPLIT3_LAUNCH(3) break;
-                default: WV_SPLIT3_LAUNCH(4) break;
-            }
-#undef WV_SPLIT3_LAUNCH
-            return hipGetLastError();
-        }
         const bool wide = p->bq == 2 * wv::BF_BQ;
         if (!wide && p->bq != wv::BF_BQ) return hipErrorInvalidValue;
         const size_t lds = (size_t)nk * (wide ? 32768 : 16384) + (wide ? 8 : 4) * 256;   // + per-wave norm slots
@@ -1997,15 +1544,6 @@ hipError_t wv_launch_bf_mfma(const wv::BfParams* p, hipStream_t s) {
         } else {                                                                                              \
             if (l2) hipLaunchKernelGGL((wv::wv_bf_split_kernel<NK, true, 2>), dim3(nb), dim3(256), lds, s, *p);  \
             else hipLaunchKernelGGL((wv::wv_bf_split_kernel<NK, false, 2>), dim3(nb), dim3(256), lds, s, *p);    \
-        }
-        // one wave per SIMD (wv_bf_split1_kernel, 4 k-chunks, 256-query blocks):
-        // opt-in with WV_BF_SPLIT_1W=1 -- measured 11.5 ms vs 8.1 ms for the
-        // two-waves-per-SIMD kernel on 1M x 128 x 10k
-        if (nk == 4 && wide && std::getenv("WV_BF_SPLIT_1W")) {
-            const size_t lds1 = (size_t)8 * 16384 + 4 * 256;
-            if (l2) hipLaunchKernelGGL((wv::wv_bf_split1_kernel<true>), dim3(nb), dim3(256), lds1, s, *p);
-            else hipLaunchKernelGGL((wv::wv_bf_split1_kernel<false>), dim3(nb), dim3(256), lds1, s, *p);
-            return hipGetLastError();
         }
         switch (nk) {
             case 1: WV_SPLIT_LAUNCH(1) break;

@@ -37,21 +37,21 @@ namespace wv {
 // SEED: the pre-pass over every H_SAMPLE-th tile keeps only each lane's
 // running minimum per query column (distinct rows per (slot, lane half)),
 // written as one key per list; wv_h16_seed_kernel turns them into thresholds.
-// WAVES = 8: one 512-query workgroup per CU (two waves per SIMD, kept in
-// phase by the stage barrier); WAVES = 4: two independent 256-query
-// workgroups per CU (one wave per SIMD each), TPS tiles per LDS stage.
-// STG: stagger (8 waves only) -- waves 4-7 (the second wave of every SIMD)
-// run half a tile behind waves 0-3, so that one wave's half-tile boundary
-// (accumulator restart, fragment reads) falls inside its partner's MFMA run
-// instead of beside the partner's own boundary (MI355X_MICROARCH 'Two waves
-// per SIMD' item 9).  The lagging waves meet each group's barrier half a tile
-// earlier in their stream (before the group's last A phase), which a 4-stage
-// ring allows: a fill overwrites the stage of group g - 2, never one a
-// lagging wave still reads.
-template <int NS, bool L2, bool SEED, int WAVES, int TPS, bool XS = false, bool STG = false>
-__global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Params p) {
+// One 512-query workgroup per CU (two waves per SIMD), H_TPS8 tiles per LDS
+// stage, one barrier per stage.
+//
+// Operand stream (round 4): a half tile's 16 MFMAs read their A fragments two
+// k-steps ahead (3 in registers instead of all 8), and the next half's C-in
+// and first two fragments are read during the current half's last MFMAs, so
+// no half starts by waiting on an LDS round trip (ablation before: the A
+// fragments' LDS reads cost 0.35 ms of a 2.66 ms 1M x 10k pass).  The stage
+// barrier sits before the first half (A) of a group's last tile: the next
+// group's first tile is then landed when A prefetches it.
+template <int NS, bool L2, bool SEED, bool XS = false>
+__global__ __launch_bounds__(512, 1) void wv_bf_h16_kernel(H16Params p) {
+    constexpr int WAVES = 8, TPS = H_TPS8;
     constexpr int BQ = WAVES * 64;
-    constexpr int NSTG = STG ? 4 : H_STAGES;
+    constexpr int NSTG = H_STAGES;
     extern __shared__ uint4 lds[];
     using St = H16Stage<NS>;
     const int tid = threadIdx.x;
@@ -116,7 +116,6 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
         }
         return n * n_ops;   // this wave's DMA ops for the group
     };
-    auto tile_lds = [&](int t) { return lds + ((t / TPS) % NSTG * TPS + t % TPS) * St::U4; };
     // (in the tile loop: the slot of tile t advances by one, wrapping at the ring)
     auto next_slot = [](int sl) { return sl + 1 == NSTG * TPS ? 0 : sl + 1; };
 
@@ -176,63 +175,84 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
         }
         // Two-phase software pipeline over half tiles (rows 0-31: H0 =
         // acc00/acc01, rows 32-63: H1 = acc10/acc11).  Iteration t:
-        //   A  MFMAs of H1(t)       beside the tile minima of H0(t)
+        //   (group's last tile: group g + 1 landed, barrier)
+        //   A  MFMAs of H1(t)       beside the tile minima of H0(t); at its
+        //      end the C-in and first fragments of H0(t + 1) are read
         //   B  extraction of H0(t)  (rare)
-        //   C  tile t + 1 landed, barrier
-        //   E  MFMAs of H0(t + 1)   beside the tile minima of H1(t)
+        //   E  MFMAs of H0(t + 1)   beside the tile minima of H1(t); at its
+        //      end the head of H1(t + 1) is read
         //   F  extraction of H1(t)
-        // so each wave's epilogue VALU issues between its own MFMAs instead of
-        // after them (the per-tile barrier keeps the two waves of a SIMD in
-        // phase, so they cannot cover each other).
         const float INF = __builtin_inff();
         floatx16 acc00, acc01, acc10, acc11;
-        // one half tile's MFMAs (all operands read from LDS up front: 8 A
-        // fragments + the C-in), with VALU work of the other half placed
-        // between them by the `between` callback and sched_group_barrier
-        auto mfma_half = [&](const uint4* img, int rb, floatx16& accA, floatx16& accB, auto&& between) {
-            // the C-in first, then the A fragments in k order: the LDS returns
-            // in issue order, so each MFMA waits (counted lgkmcnt) only for
-            // its own fragment, not for the whole half's reads
-            floatx16 xc;
+        // the head of the next half: its C-in and k-step 0 / 1 A fragments
+        floatx16 xcn;
+        uint4 an0, an1;
+        auto head = [&](const uint4* img, int rb) {
             if (L2) {
                 const float* xn = reinterpret_cast<const float*>(img + St::IMG_U4) + 32 * rb;
 #pragma unroll
                 for (int g4 = 0; g4 < 4; ++g4) {
                     const float4 v = *reinterpret_cast<const float4*>(xn + 4 * khalf + 8 * g4);
-                    xc[4 * g4] = v.x; xc[4 * g4 + 1] = v.y; xc[4 * g4 + 2] = v.z; xc[4 * g4 + 3] = v.w;
+                    xcn[4 * g4] = v.x; xcn[4 * g4 + 1] = v.y; xcn[4 * g4 + 2] = v.z; xcn[4 * g4 + 3] = v.w;
                 }
-            } else {
+            }
+            an0 = img[(rb * NS) * 64 + lane];
+            if (NS > 1) an1 = img[(rb * NS + 1) * 64 + lane];
+        };
+        // one half tile's 16 MFMAs (k-interleaved over the two accumulators),
+        // its fragments read two k-steps ahead, the VALU work of the other
+        // half (`between(k)`, a share per k-step) beside them, and the next
+        // half's head read during the last k-steps (after the last tile: a
+        // harmless re-read of img).  The order is pinned with scheduling
+        // fences: the compiler's own schedule hoisted every read to the
+        // front and drained them all before the first MFMA.
+        auto mfma_half = [&](const uint4* img, int rb, floatx16& accA, floatx16& accB, auto&& between,
+                             const uint4* nimg, int nrb) {
+            floatx16 xc;
+            if (L2) xc = xcn;
+            else {
 #pragma unroll
                 for (int r = 0; r < 16; ++r) xc[r] = 0.f;
             }
-            __builtin_amdgcn_sched_barrier(0);   // the C-in reads issue first
-            uint4 a[NS];
-#ifdef WV_H16_ABLATE_NO_LDS
-#pragma unroll
-            for (int k = 0; k < NS; ++k) { a[k] = bq1[k]; a[k].x ^= (uint32_t)rb; }
-#else
-#pragma unroll
-            for (int k = 0; k < NS; ++k) a[k] = img[(rb * NS + k) * 64 + lane];
-#endif
-            between();
+            uint4 a[3];
+            a[0] = an0;
+            a[1] = an1;
 #pragma unroll
             for (int k = 0; k < NS; ++k) {
-                const half8 ak = __builtin_bit_cast(half8, a[k]);
+                __builtin_amdgcn_sched_barrier(0);
+#ifdef WV_H16_ABLATE_NO_LDS
+                if (k + 2 < NS) { a[(k + 2) % 3] = bq1[k + 2]; a[(k + 2) % 3].x ^= (uint32_t)rb; }
+#else
+                if (k + 2 < NS) a[(k + 2) % 3] = img[(rb * NS + k + 2) * 64 + lane];
+#endif
+                if (k == NS - 2) head(nimg, nrb);   // (unconditional: a branch here would make every
+                                                    // later wait drain these reads too)
+                const half8 ak = __builtin_bit_cast(half8, a[k % 3]);
                 accA = __builtin_amdgcn_mfma_f32_32x32x16_f16(ak, __builtin_bit_cast(half8, bq0[k]), k == 0 ? xc : accA,
                                                               0, 0, 0);
                 accB = __builtin_amdgcn_mfma_f32_32x32x16_f16(ak, __builtin_bit_cast(half8, bq1[k]), k == 0 ? xc : accB,
                                                               0, 0, 0);
+                between(k);
             }
-            // LDS reads first (in source order), a few VALU while they land,
-            // then the MFMAs (k-interleaved over the two accumulators) each
-            // followed by one VALU op
-            __builtin_amdgcn_sched_group_barrier(0x100, NS, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        // the minima of a half's two accumulators as `between` work: four
+        // v_min3 chains per accumulator, two ops per k-step
+        auto min_steps = [&](const floatx16& A, const floatx16& B, float& mA, float& mB) {
+            return [&](int k) {
+                // chain c of A covers keys 4c .. 4c + 3; B likewise
+                if (k == 0) { mA = fminf(fminf(A[0], A[1]), A[2]); mB = fminf(fminf(B[0], B[1]), B[2]); }
+                else if (k == 1) { mA = fminf(fminf(mA, A[3]), A[4]); mB = fminf(fminf(mB, B[3]), B[4]); }
+                else if (k == 2) { mA = fminf(fminf(mA, A[5]), A[6]); mB = fminf(fminf(mB, B[5]), B[6]); }
+                else if (k == 3) { mA = fminf(fminf(mA, A[7]), A[8]); mB = fminf(fminf(mB, B[7]), B[8]); }
+                else if (k == 4) { mA = fminf(fminf(mA, A[9]), A[10]); mB = fminf(fminf(mB, B[9]), B[10]); }
+                else if (k == 5) { mA = fminf(fminf(mA, A[11]), A[12]); mB = fminf(fminf(mB, B[11]), B[12]); }
+                else if (k == 6) { mA = fminf(fminf(mA, A[13]), A[14]); mB = fminf(fminf(mB, B[13]), B[14]); }
+                if (k == NS - 1) {   // (the remaining keys at the last k-step)
 #pragma unroll
-            for (int i = 0; i < 2 * NS; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
-            }
+                    for (int r = 2 * NS + 1; r < 16; ++r) { mA = fminf(mA, A[r]); mB = fminf(mB, B[r]); }
+                }
+            };
         };
         // eligibility of a tile's 64 rows for this lane's two columns (bits of
         // rows 4 khalf + ..., low word: rows 0-31, high word: rows 32-63)
@@ -377,9 +397,24 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
                     __hip_atomic_store(p.gslot + (size_t)jq1 * nv + s2, l1d[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         };
+        // a half's candidates: the column minima against the thresholds, and
+        // (rare, wave-uniform) insertion by key position (wv_topk.h)
+        auto extract_half = [&](float m0, float m1, floatx16& A, floatx16& B, uint32_t rb) -> bool {
+#ifdef WV_H16_ABLATE_NO_EXTRACT
+            if (m0 == 1234.5f) l0d[0] = m1 + pt0 + pt1;
+            return false;
+#endif
+            const bool x0 = m0 <= fminf(l0d[BF_KP - 1], pt0), x1 = m1 <= fminf(l1d[BF_KP - 1], pt1);
+            const bool any = __any(x0 || x1);
+            if (__builtin_expect(any, 0)) {
+                WV_DBG_COUNT(3)
+                if (__any(x0)) ballot_extract(A, x0 ? fminf(l0d[BF_KP - 1], pt0) : -INF, l0d, l0i, rb);
+                if (__any(x1)) ballot_extract(B, x1 ? fminf(l1d[BF_KP - 1], pt1) : -INF, l1d, l1i, rb);
+            }
+            return any;
+        };
         const int xs1 = ntile / 8, xs2 = ntile / 4, xs3 = ntile / 2, xs4 = (3 * ntile) / 4;
         const int ngroups = (ntile + TPS - 1) / TPS;
-        const bool lag = STG && wave >= 4;
         // (the previous segment ended with every stage read and every DMA landed)
         int ops_in_flight = 0;   // this wave's DMA ops of the newest group issued
         if (ngroups > 0) fill_group(t_begin, 0, ntile);
@@ -387,7 +422,8 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
         vm_wait(ops_in_flight);   // this wave's part of group 0
         block_barrier();          // everyone's
         if (ntile > 0) {
-            mfma_half(tile_lds(0), 0, acc00, acc01, [] {});
+            head(lds, 0);
+            mfma_half(lds, 0, acc00, acc01, [](int) {}, lds, 1);   // H0(0), then the head of H1(0)
             need_mask = tile_ok(phys(t_begin), okw);
         }
         // a full group's DMA ops of this wave: a constant per wave class when
@@ -408,16 +444,17 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
             WV_DBG_COUNT(0)
             const int g = t / TPS;
 #ifndef WV_H16_ABLATE_NO_FILL
-            // group g + 2 goes to stage (g + 2) % 3 = (g - 1) % 3, last read in
-            // group g - 1, before its closing barrier
+            // group g + 2 goes to stage (g + 2) % 3 = (g - 1) % 3, last read
+            // in group g - 1, before the barrier of group g's last tile
             if (t % TPS == 0) ops_in_flight = g + 2 < ngroups ? fill_group(t_begin, g + 2, ntile) : 0;
 #endif
             const uint4* img = lds + slot_t * St::U4;
             slot_t = next_slot(slot_t);
-            const bool group_end = t % TPS == TPS - 1 || t == ntile - 1;
-            // group g + 1 landed: at most the newest group's ops outstanding
-            auto wait_group = [&] {
-                if (g + 1 >= ngroups) return;
+            const bool more = t + 1 < ntile;
+            // the group's last tile: group g + 1 landed (at most the newest
+            // group's ops outstanding) and everyone is past its reads of
+            // group g - 1's stage, before A prefetches tile t + 1
+            if (t % TPS == TPS - 1 && g + 1 < ngroups) {
                 if (EVEN && ops_in_flight == TPS * (SHARE + (xns_wave ? 1 : 0))) {
                     if (xns_wave) vm_wait(TPS * (SHARE + 1));
                     else vm_wait(TPS * SHARE);
@@ -426,55 +463,38 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
                 } else {
                     vm_wait(ops_in_flight);
                 }
-            };
-            if (lag && group_end) {   // (staggered waves: the group's barrier, half a tile early)
-                wait_group();
                 block_barrier();
             }
             // lanes l and l ^ 32 keep lists for the same query column (see the split pass)
             const bool mask_t = need_mask;
             const uint64_t mo0 = mask_t ? lane_ok(okw, jq0) : 0ull, mo1 = mask_t ? lane_ok(okw, jq1) : 0ull;
-            bool grew = false;   // a list of this wave changed: thresholds to refresh
-            // ---- A: H1(t) MFMAs, H0(t) minima ----
+            const uint4* nimg = more ? lds + slot_t * St::U4 : img;
+            // ---- A: H1(t) MFMAs, H0(t) minima, head of H0(t + 1) ----
             if (mask_t) mask_half(acc00, acc01, (uint32_t)mo0, (uint32_t)mo1);
             float m0, m1;
-            mfma_half(img, 1, acc10, acc11, [&] { m0 = min16(acc00); m1 = min16(acc01); });
+#ifdef WV_H16_ABLATE_NO_MIN
+            m0 = acc00[0]; m1 = acc01[0];
+            mfma_half(img, 1, acc10, acc11, [](int) {}, nimg, 0);
+#else
+            mfma_half(img, 1, acc10, acc11, min_steps(acc00, acc01, m0, m1), nimg, 0);
+#endif
             // ---- B ----
+            bool grew = false;   // a list of this wave changed: thresholds to refresh
             if constexpr (SEED) {
                 l0d[0] = fminf(l0d[0], m0);
                 l1d[0] = fminf(l1d[0], m1);
             } else {
-#ifdef WV_H16_ABLATE_NO_EXTRACT
-                if (m0 == 1234.5f) l0d[0] = m1 + pt0 + pt1;
-#else
-#ifdef WV_H16_ABLATE_EXT_NEVER
-                float never = -INF;
-                asm volatile("" : "+v"(never));
-                const bool x0 = m0 <= never, x1 = m1 <= never;
-#else
-                const bool x0 = m0 <= fminf(l0d[BF_KP - 1], pt0), x1 = m1 <= fminf(l1d[BF_KP - 1], pt1);
-#endif
-                // one wave-uniform (rarely taken) branch around the extraction
-                grew = __any(x0 || x1);
-                if (__builtin_expect(grew, 0)) {
-                    WV_DBG_COUNT(3)
-                    // (round 4: insertion by key position, wv_topk.h ballot_extract:
-                    // 2.67-2.68 -> 2.65-2.67 ms per 1M x 10k pass)
-                    if (__any(x0)) ballot_extract(acc00, x0 ? fminf(l0d[BF_KP - 1], pt0) : -INF, l0d, l0i, rb0);
-                    if (__any(x1)) ballot_extract(acc01, x1 ? fminf(l1d[BF_KP - 1], pt1) : -INF, l1d, l1i, rb0);
-                }
-#endif
+                grew = extract_half(m0, m1, acc00, acc01, rb0);
             }
-            // ---- C (last tile of a group): group g + 1 has landed (g + 2 may
-            // stay in flight); every wave is done reading group g's stage ----
-            if (!lag && group_end) {
-                wait_group();
-                block_barrier();
-            }
-            // ---- E: H0(t + 1) MFMAs, H1(t) minima ----
+            // ---- E: H0(t + 1) MFMAs, H1(t) minima, head of H1(t + 1) ----
             if (mask_t) mask_half(acc10, acc11, (uint32_t)(mo0 >> 32), (uint32_t)(mo1 >> 32));
-            if (t + 1 < ntile) {
-                mfma_half(lds + slot_t * St::U4, 0, acc00, acc01, [&] { m0 = min16(acc10); m1 = min16(acc11); });
+            if (more) {
+#ifdef WV_H16_ABLATE_NO_MIN
+                m0 = acc10[0]; m1 = acc11[0];
+                mfma_half(nimg, 0, acc00, acc01, [](int) {}, nimg, 1);
+#else
+                mfma_half(nimg, 0, acc00, acc01, min_steps(acc10, acc11, m0, m1), nimg, 1);
+#endif
                 need_mask = tile_ok(phys(t_begin + t + 1), okw);
             } else {
                 m0 = min16(acc10);
@@ -485,24 +505,7 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
                 l0d[0] = fminf(l0d[0], m0);
                 l1d[0] = fminf(l1d[0], m1);
             } else {
-#ifdef WV_H16_ABLATE_NO_EXTRACT
-                if (m0 == 1234.5f) l0d[0] = m1 + pt0 + pt1;
-#else
-#ifdef WV_H16_ABLATE_EXT_NEVER
-                float never = -INF;
-                asm volatile("" : "+v"(never));
-                const bool x0 = m0 <= never, x1 = m1 <= never;
-#else
-                const bool x0 = m0 <= fminf(l0d[BF_KP - 1], pt0), x1 = m1 <= fminf(l1d[BF_KP - 1], pt1);
-#endif
-                const bool any1 = __any(x0 || x1);
-                if (__builtin_expect(any1, 0)) {
-                    WV_DBG_COUNT(3)
-                    if (__any(x0)) ballot_extract(acc10, x0 ? fminf(l0d[BF_KP - 1], pt0) : -INF, l0d, l0i, rb0 + 32);
-                    if (__any(x1)) ballot_extract(acc11, x1 ? fminf(l1d[BF_KP - 1], pt1) : -INF, l1d, l1i, rb0 + 32);
-                }
-                grew = any1 || grew;
-#endif
+                grew = extract_half(m0, m1, acc10, acc11, rb0 + 32) || grew;
                 if (running && (t & 15) == 15) publish();
                 else if (grew) refresh_pt();
                 if constexpr (XS) {
@@ -514,10 +517,10 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
                 }
             }
         }
+        // every stage read and every DMA landed before the next segment's fills
+        vm_wait(0);
+        block_barrier();
 
-        // (staggered: everyone past the segment's last reads before the next
-        // segment's fills)
-        if constexpr (STG) block_barrier();
         if constexpr (SEED) {
             if (jq0 < p.nq) p.out_d[((size_t)jq0 * p.n_slots + slot) * H_PROD + khalf] = l0d[0];
             if (jq1 < p.nq) p.out_d[((size_t)jq1 * p.n_slots + slot) * H_PROD + khalf] = l1d[0];
@@ -533,324 +536,6 @@ __global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16_kernel(H16Par
             const size_t base = (size_t)jq1 * per_q + ((size_t)slot * H_PROD + khalf) * BF_KP;
 #pragma unroll
             for (int i = 0; i < BF_KP; ++i) { p.out_d[base + i] = l1d[i]; p.out_id[base + i] = l1i[i]; }
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
-// The same key pass on v_mfma_f32_16x16x32_f16 (NS32 32-k steps, D <= 128 with
-// an even number of 16-k steps).  The chip holds a higher clock on this shape
-// under an MFMA-dense load: a bare loop at the same 64 x 64 tile per wave and
-// two waves per SIMD ran 1.92 PF/s vs 1.67 PF/s for 32x32x16
-// (tools/mfma_shape_bench.cpp, MI355X_MICROARCH.md 'DVFS give-back' item 7).
-// Structure as wv_bf_h16_kernel (LDS-DMA'd 64-row tiles, 3 stages of 2 tiles,
-// the wave's 64 queries as B operands in registers, a half-tile software
-// pipeline); per wave and tile 4 row groups x 4 query groups of 16 x 16
-// accumulators.  Keys: acc[rg][qg][r] is row 16 rg + 4 (lane / 16) + r x query
-// 16 qg + lane % 16, so a lane owns 4 query columns with 8 keys per half tile
-// each; the 4 lanes of a column (lane % 16 equal) share the column's sorted
-// list of HQ_PROD * HQ_KP = 16 entries, lane quarter q holding entries
-// 4 q .. 4 q + 3 (a 16-entry list per column and slot, so the certificate's
-// list tails lie well beyond the top k).
-//
-// WAVES = 8: one 512-query workgroup per CU, 2 tiles per LDS stage; WAVES = 4:
-// two independent 256-query workgroups per CU (their own barriers), 1 tile
-// per stage.
-template <int NS32, bool L2, bool SEED, int WAVES>
-__global__ __launch_bounds__(WAVES * 64, 8 / WAVES) void wv_bf_h16q_kernel(H16Params p) {
-    constexpr int BQ = WAVES * 64;
-    constexpr int TPS = WAVES == 8 ? 2 : 1;
-    extern __shared__ uint4 lds[];
-    using St = H16Stage<2 * NS32>;   // same stage bytes: 4 row groups x NS32 32-k steps
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int lq = lane >> 4;        // lane quarter: rows 4 lq .. 4 lq + 3 of each 16-row group
-    const int l15 = lane & 15;
-    const uint4* __restrict__ X = reinterpret_cast<const uint4*>(p.X);
-    const uint4* __restrict__ Qg = reinterpret_cast<const uint4*>(p.Q);
-    const bool has_allow = p.allow != nullptr;
-    const float s = p.sx * p.qscale[0];
-    int lb = (int)blockIdx.x;
-    if ((p.locality & 1) && gridDim.x >= 8) {   // bijective XCD remap (blocks b, b + 8, ... share an XCD)
-        const int nwg = (int)gridDim.x, q8 = nwg / 8, r8 = nwg % 8, xcd = (int)blockIdx.x % 8;
-        lb = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (int)blockIdx.x / 8;
-    }
-    if (p.block_order) lb = p.block_order[lb];
-    const uint64_t u_first = (uint64_t)lb * p.units_per_block;
-    uint64_t u_last = u_first + p.units_per_block;
-    if (u_last > (uint64_t)p.n_qblocks * p.ntiles) u_last = (uint64_t)p.n_qblocks * p.ntiles;
-    const uint32_t lds0 = lds_addr(lds);
-    const int n_ops = (wave < St::IMG_U4 / 64 ? (St::IMG_U4 / 64 - 1 - wave) / WAVES + 1 : 0) +
-                      ((wave == 0 && L2) ? 1 : 0);
-    auto fill = [&](uint64_t t, int st) {
-        const uint64_t tile = t * (uint64_t)p.tile_stride;
-        const uint32_t dst = lds0 + (uint32_t)(st * St::U4 * 16);
-        const uint4* src = X + tile * St::IMG_U4;
-#pragma unroll
-        for (int i = wave; i < St::IMG_U4 / 64; i += WAVES) glds16s(src, (uint32_t)(i * 1024 + lane * 16), dst + i * 1024);
-        if (wave == 0 && L2) glds4(p.xns + tile * H_BN + lane, dst + St::IMG_U4 * 16);
-    };
-    auto fill_group = [&](uint64_t t_begin, int g, int ntile) {
-        const int st = g % H_STAGES;
-        int n = 0;
-#pragma unroll
-        for (int j = 0; j < TPS; ++j) {
-            const int t = g * TPS + j;
-            if (t < ntile) { fill(t_begin + t, st * TPS + j); ++n; }
-        }
-        return n * n_ops;
-    };
-    auto tile_lds = [&](int t) { return lds + ((t / TPS) % H_STAGES * TPS + t % TPS) * St::U4; };
-
-    for (uint64_t u = u_first; u < u_last;) {
-        const int qb = (int)(u / p.ntiles);
-        const uint64_t t_begin = u % p.ntiles;
-        uint64_t t_end = t_begin + (u_last - u);
-        if (t_end > p.ntiles) t_end = p.ntiles;
-        u += t_end - t_begin;
-        const int slot = lb - bf_first_block(qb, p.ntiles, p.units_per_block);
-        const int ntile = (int)(t_end - t_begin);
-        int jq[4];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) jq[g] = qb * BQ + wave * 64 + 16 * g + l15;
-
-        // the wave's 64 queries (4 groups of 16) as B operands
-        uint4 bq[4][NS32];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const uint64_t G = (uint64_t)qb * (BQ / 16) + 4 * wave + g;
-#pragma unroll
-            for (int kk = 0; kk < NS32; ++kk) bq[g][kk] = Qg[(G * NS32 + kk) * 64 + lane];
-        }
-        float tau[4], marg[4];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            tau[g] = FLT_MAX;
-            marg[g] = 0.f;
-            if (jq[g] < p.nq) {
-                if (!SEED && p.gtau) tau[g] = fminf(FLT_MAX, h16_key_dec(p.gtau[jq[g]]));
-                else if (p.tau) tau[g] = fminf(FLT_MAX, p.tau[jq[g]] * s);
-                if (!SEED && p.kth) marg[g] = p.marg[jq[g]];
-            }
-        }
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-#pragma unroll
-            for (int kk = 0; kk < NS32; ++kk) asm volatile("" ::"v"(bq[g][kk].x));
-#pragma unroll
-        for (int g = 0; g < 4; ++g) asm volatile("" ::"v"(tau[g]), "v"(marg[g]));
-        float ld[4][HQ_KP];
-        uint32_t li[4][HQ_KP];
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-#pragma unroll
-            for (int i = 0; i < HQ_KP; ++i) { ld[g][i] = FLT_MAX; li[g][i] = WV_NIL; }
-
-        const float INF = __builtin_inff();
-        floatx4 acc[4][4];   // [row group][query group]
-        // one half tile's MFMAs (row groups 2 h, 2 h + 1), the C-in and A
-        // fragments read from LDS first, `between` VALU interleaved
-        auto mfma_half = [&](const uint4* img, int h, auto&& between) {
-            floatx4 xc[2];
-#pragma unroll
-            for (int r = 0; r < 2; ++r) {
-                if (L2) {
-                    const float* xn = reinterpret_cast<const float*>(img + St::IMG_U4) + 16 * (2 * h + r) + 4 * lq;
-                    const float4 v = *reinterpret_cast<const float4*>(xn);
-                    xc[r] = floatx4{v.x, v.y, v.z, v.w};
-                } else {
-                    xc[r] = floatx4{0.f, 0.f, 0.f, 0.f};
-                }
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            uint4 a[2][NS32];
-#pragma unroll
-            for (int kk = 0; kk < NS32; ++kk)
-#pragma unroll
-                for (int r = 0; r < 2; ++r) a[r][kk] = img[((2 * h + r) * NS32 + kk) * 64 + lane];
-            between();
-#pragma unroll
-            for (int kk = 0; kk < NS32; ++kk)
-#pragma unroll
-                for (int r = 0; r < 2; ++r)
-#pragma unroll
-                    for (int g = 0; g < 4; ++g)
-                        acc[2 * h + r][g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
-                            __builtin_bit_cast(half8, a[r][kk]), __builtin_bit_cast(half8, bq[g][kk]),
-                            kk == 0 ? xc[r] : acc[2 * h + r][g], 0, 0, 0);
-            __builtin_amdgcn_sched_group_barrier(0x100, 2 * NS32, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
-#pragma unroll
-            for (int i = 0; i < 8 * NS32; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
-            }
-        };
-        auto tile_ok = [&](uint64_t t, uint64_t& okw) -> bool {
-            okw = tile_okw(p, t * (uint64_t)p.tile_stride, has_allow);
-            return okw != ~0ull || (qb + 1) * BQ > p.nq;
-        };
-        // ineligible keys of half h to +inf (row 16 rg + 4 lq + r of the tile)
-        auto mask_half = [&](int h, uint64_t okw) {
-            uint32_t ow[4];
-#pragma unroll
-            for (int g = 0; g < 4; ++g) ow[g] = (uint32_t)((jq[g] < p.nq ? okw : 0ull) >> (32 * h + 4 * lq));
-            constexpr uint32_t LANE_ROWS = 0x000F000Fu;   // bits r and 16 + r, r < 4
-            bool all = true;
-#pragma unroll
-            for (int g = 0; g < 4; ++g) all = all && (ow[g] & LANE_ROWS) == LANE_ROWS;
-            if (__all(all)) return;
-#pragma unroll
-            for (int g = 0; g < 4; ++g)
-#pragma unroll
-                for (int r = 0; r < 2; ++r)
-#pragma unroll
-                    for (int e = 0; e < 4; ++e)
-                        acc[2 * h + r][g][e] = (ow[g] >> (16 * r + e)) & 1u ? acc[2 * h + r][g][e] : INF;
-        };
-        auto min8 = [&](int h, int g) {
-            const floatx4& A = acc[2 * h][g];
-            const floatx4& B = acc[2 * h + 1][g];
-#ifdef WV_H16_ABLATE_NO_MIN
-            return fminf(A[0], B[0]);   // (both accumulators stay live)
-#endif
-            // 4 VALU: two independent v_min3, one v_min, a final v_min3
-            return min3_raw(min3_raw(A[0], A[1], A[2]), min3_raw(A[3], B[0], B[1]), fminf(B[2], B[3]));
-        };
-        // extraction thresholds: min(the column list's tail, tau)
-        float pt[4];
-        auto refresh_pt = [&] {
-#pragma unroll
-            for (int g = 0; g < 4; ++g) pt[g] = fminf(__shfl(ld[g][HQ_KP - 1], l15 + 48, 64), tau[g]);
-        };
-        refresh_pt();
-        // running threshold: entry k - 1 of the column list (k distinct rows
-        // with keys <= it), held by lane quarter (k - 1) / 4
-        const int ke = p.kth > 0 ? p.kth - 1 : 0;
-        const int ksrc = l15 + 16 * (ke >> 2);
-        auto publish = [&] {
-            int ve = ke & 3;
-            asm volatile("" : "+v"(ve));
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                float v = FLT_MAX;
-#pragma unroll
-                for (int i = 0; i < HQ_KP; ++i) v = ve == i ? ld[g][i] : v;
-                v = __shfl(v, ksrc, 64);
-                if (lq == 0 && jq[g] < p.nq && v < FLT_MAX) {
-                    const float u4 = 4.f * 5.9604645e-08f;
-                    atomicMin(&p.gtau[jq[g]], h16_key_enc(v + marg[g] + u4 * (fabsf(v) + marg[g])));
-                }
-            }
-#pragma unroll
-            for (int g = 0; g < 4; ++g)
-                if (jq[g] < p.nq) tau[g] = fminf(tau[g], h16_key_dec(__atomic_load_n(&p.gtau[jq[g]], __ATOMIC_RELAXED)));
-            refresh_pt();
-        };
-        const bool running = !SEED && p.kth > 0 && p.gtau != nullptr;
-        // the epilogue of half h of tile t: minima (already in m[]), extraction
-        auto epilogue = [&](int h, const float (&m)[4], uint32_t rb) -> bool {
-            if constexpr (SEED) {
-#pragma unroll
-                for (int g = 0; g < 4; ++g) ld[g][0] = fminf(ld[g][0], m[g]);
-                return false;
-            } else {
-#ifdef WV_H16_ABLATE_NO_EXTRACT
-                if (m[0] == 1234.5f) ld[0][0] = m[1] + m[2] + m[3] + pt[0];
-                return false;
-#endif
-                bool x[4], anyx = false;
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    x[g] = m[g] <= pt[g];
-                    anyx = anyx || x[g];
-                }
-                if (__builtin_expect(__any(anyx), 0)) {
-                    WV_DBG_COUNT(3)
-#pragma unroll
-                    for (int g = 0; g < 4; ++g)
-                        if (__any(x[g]))
-                            qcol_extract(m[g], acc[2 * h][g], acc[2 * h + 1][g], ld[g], li[g], pt[g], tau[g], rb, lane);
-                }
-                return false;   // (the thresholds are current)
-            }
-        };
-
-        uint64_t okw = 0;
-        bool need_mask = false;
-        const int ngroups = (ntile + TPS - 1) / TPS;
-        int ops_in_flight = 0;
-        if (ngroups > 0) fill_group(t_begin, 0, ntile);
-        if (ngroups > 1) ops_in_flight = fill_group(t_begin, 1, ntile);
-        vm_wait(ops_in_flight);
-        block_barrier();
-        if (ntile > 0) {
-            mfma_half(tile_lds(0), 0, [] {});
-            need_mask = tile_ok(t_begin, okw);
-        }
-        for (int t = 0; t < ntile; ++t) {
-            WV_DBG_COUNT(0)
-            const int g = t / TPS;
-#ifndef WV_H16_ABLATE_NO_FILL
-            if (t % TPS == 0) ops_in_flight = g + 2 < ngroups ? fill_group(t_begin, g + 2, ntile) : 0;
-#endif
-            const uint4* img = tile_lds(t);
-            const uint32_t rb0 = (uint32_t)((t_begin + t) * (uint64_t)p.tile_stride * H_BN) + 4 * lq;
-            const bool mask_t = need_mask;
-            const uint64_t mo = okw;
-            // ---- A: H1(t) MFMAs, H0(t) minima ----
-            if (mask_t) mask_half(0, mo);
-            float m[4];
-            mfma_half(img, 1, [&] {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) m[q] = min8(0, q);
-            });
-            // ---- B ----
-            bool grew = epilogue(0, m, rb0);
-            // ---- C: group g + 1 landed; every wave done with group g's stage ----
-            if (t % TPS == TPS - 1 || t == ntile - 1) {
-#ifndef WV_H16_ABLATE_NO_VMWAIT
-                if (g + 1 < ngroups) vm_wait(ops_in_flight);
-#endif
-                block_barrier();
-            }
-            // ---- E: H0(t + 1) MFMAs, H1(t) minima ----
-            if (mask_t) mask_half(1, mo);
-            if (t + 1 < ntile) {
-                mfma_half(tile_lds(t + 1), 0, [&] {
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) m[q] = min8(1, q);
-                });
-#ifndef WV_H16_ABLATE_NO_TILEOK
-                need_mask = tile_ok(t_begin + t + 1, okw);
-#endif
-            } else {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) m[q] = min8(1, q);
-            }
-            // ---- F ----
-            grew = epilogue(1, m, rb0 + 32) || grew;
-            if constexpr (!SEED) {
-                if (running && (t & 15) == 15) publish();
-                else if (grew) refresh_pt();
-            }
-        }
-
-        if constexpr (SEED) {
-#pragma unroll
-            for (int g = 0; g < 4; ++g)
-                if (jq[g] < p.nq) p.out_d[((size_t)jq[g] * p.n_slots + slot) * HQ_PROD + lq] = ld[g][0];
-            continue;
-        }
-        // one 16-entry list per query and slot, lane quarter lq's entries at 4 lq
-        const size_t per_q = (size_t)p.n_slots * HQ_PROD * HQ_KP;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            if (jq[g] >= p.nq) continue;
-            const size_t base = (size_t)jq[g] * per_q + (size_t)slot * HQ_PROD * HQ_KP + lq * HQ_KP;
-#pragma unroll
-            for (int i = 0; i < HQ_KP; ++i) { p.out_d[base + i] = ld[g][i]; p.out_id[base + i] = li[g][i]; }
         }
     }
 }
@@ -1017,44 +702,6 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16w_kernel(H16Params p) {
         const uint32_t tau_dst = ex0 + (uint32_t)(2 * St::EX_U4 * 16 + 256 * wave);
         const int tau_src = min(jq0 - l31 + lane, p.nq - 1);
         if (running) reinterpret_cast<unsigned int*>(lds + HW_STAGES * St::U4 + 2 * St::EX_U4)[64 * wave + lane] = 0xFFFFFFFFu;
-        // the bucket words of the wave's 64 queries come back the same way
-        // (1 024 words, 4 KiB per wave after the gtau slots)
-        const bool bkt = running && p.gbkt != nullptr;
-        const int bkt_id = (slot * 4 + rh * 2 + khalf) & 15;
-        unsigned int* bkt_lds = reinterpret_cast<unsigned int*>(lds + HW_STAGES * St::U4 + 2 * St::EX_U4 + 8 * 16) + 1024 * wave;
-        const uint32_t bkt_dst = ex0 + (uint32_t)(2 * St::EX_U4 * 16 + 8 * 256 + 4096 * wave);
-        const unsigned int* bkt_src = uniform_ptr(p.gbkt + (size_t)(jq0 - l31) * 16);
-        if (bkt) {
-#pragma unroll
-            for (int j = 0; j < 16; ++j) bkt_lds[64 * j + lane] = 0xFFFFFFFFu;
-        }
-        // k-th smallest of the 16 bucket minima of a query (ascending bitonic
-        // network; the index is a VGPR so the select chain stays in VALU)
-        auto bkt_kth = [&](const unsigned int* w) -> float {
-            float v[16];
-#pragma unroll
-            for (int i = 0; i < 16; ++i) v[i] = h16_key_dec(w[i]);
-#pragma unroll
-            for (int size = 2; size <= 16; size <<= 1)
-#pragma unroll
-                for (int stride = size >> 1; stride > 0; stride >>= 1)
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) {
-                        const int j = i ^ stride;
-                        if (j > i) {
-                            const float a = v[i], b = v[j];
-                            const bool up = (i & size) == 0;
-                            v[i] = up ? fminf(a, b) : fmaxf(a, b);
-                            v[j] = up ? fmaxf(a, b) : fminf(a, b);
-                        }
-                    }
-            int ve = p.kth - 1;
-            asm volatile("" : "+v"(ve));
-            float kv = FLT_MAX;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) kv = i == ve ? v[i] : kv;
-            return kv;
-        };
         auto publish = [&] {
             int va = ia - 1, vb = ib - 1;
             asm volatile("" : "+v"(va), "+v"(vb));   // (select chains over a VGPR index)
@@ -1082,32 +729,6 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16w_kernel(H16Params p) {
             tau0 = fminf(tau0, h16_key_dec(tau_lds[l31]));
             tau1 = fminf(tau1, h16_key_dec(tau_lds[32 + l31]));
             glds4_dev(p.gtau + tau_src, tau_dst);
-            if (bkt) {
-                // this lane's list heads into its bucket; the previous
-                // publish's bucket words (landed long since) give the bound,
-                // which also goes to gtau (the finalize's tau_in must not
-                // exceed any threshold a key was dropped above)
-                if (jq0 < p.nq && l0d[0] < FLT_MAX) atomicMin(&p.gbkt[(size_t)jq0 * 16 + bkt_id], h16_key_enc(l0d[0]));
-                if (jq1 < p.nq && l1d[0] < FLT_MAX) atomicMin(&p.gbkt[(size_t)jq1 * 16 + bkt_id], h16_key_enc(l1d[0]));
-                // (lane half 0 selects for jq0, half 1 for jq1, then they swap)
-                const float u4 = 4.f * 5.9604645e-08f;
-                const float v = bkt_kth(bkt_lds + 16 * (32 * khalf + l31));
-                const float mg = khalf ? marg1 : marg0;
-                const float c = v < FLT_MAX ? v + mg + u4 * (fabsf(v) + mg) : FLT_MAX;
-                const float cx = __shfl_xor(c, 32, 64);
-                const float c0 = khalf ? cx : c, c1 = khalf ? c : cx;
-                if (khalf == 0) {
-                    if (jq0 < p.nq && c0 < tau0) atomicMin(&p.gtau[jq0], h16_key_enc(c0));
-                    if (jq1 < p.nq && c1 < tau1) atomicMin(&p.gtau[jq1], h16_key_enc(c1));
-                }
-                tau0 = fminf(tau0, c0);
-                tau1 = fminf(tau1, c1);
-                // (16 dwords per query: 64 lanes x 4 B per op from a scalar
-                // base -- no per-op address registers)
-                const uint32_t vo = (uint32_t)lane * 4;
-#pragma unroll
-                for (int j = 0; j < 16; ++j) glds4s_dev<0>(bkt_src + 64 * j, vo, bkt_dst + 256 * j);
-            }
         };
         floatx16 acc[RG][2];
         auto min16 = [&](const floatx16& A) {
@@ -1409,7 +1030,7 @@ __global__ void wv_h16_rows_kernel(const float* in, int ld_in, const uint64_t* i
         const float back = (float)h / scale;
         const float e = x - back;           // exact (Sterbenz) unless h overflowed
         acc = __builtin_fmaf(e, e, acc);
-        out[quad ? h16q_index(out_row0 + row, k, ns >> 1) : h16_index(out_row0 + row, k, ns)] =
+        out[h16_index(out_row0 + row, k, ns)] =
             __builtin_bit_cast(uint16_t, h);
     }
     for (int m = 32; m >= 1; m >>= 1) acc += __shfl_xor(acc, m, 64);
@@ -1474,7 +1095,7 @@ hipError_t wv_launch_h16_rows(const float* in, int ld_in, const uint64_t* ids, u
                               float scale, const unsigned int* scale_from_max, void* out, uint64_t out_row0,
                               unsigned int* res_max_bits, float* res_out, int quad, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    // quad: 0 = h16_index, 1 = h16q_index (ns even)
+    // (quad: unused, always 0 -- the 16x16x32 layout was retired in round 4)
     if (ns < 1 || ns > wv::HW_NS_MAX || D > ns * 16 || (quad && ns % 2)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(wv::wv_h16_rows_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, in, ld_in, ids,
                        (const uint32_t*)nullptr, n, D, ns, sign, scale, scale_from_max, static_cast<uint16_t*>(out),
@@ -1601,27 +1222,19 @@ hipError_t wv_launch_h16_xns(const float* xnorm, uint64_t n, float sx, const flo
     return hipGetLastError();
 }
 
-hipError_t wv_launch_bf_h16(const wv::H16Params* p, int ns, int seed, int waves, hipStream_t s) {
+hipError_t wv_launch_bf_h16(const wv::H16Params* p, int ns, int seed, hipStream_t s) {
     const uint64_t total = (uint64_t)p->n_qblocks * p->ntiles;
     const unsigned nb = (unsigned)((total + p->units_per_block - 1) / p->units_per_block);
     if (nb == 0) return hipSuccess;
-    if (ns < 1 || ns > wv::H_NS_MAX || !p->X || !p->Q || !p->excl || !p->qscale || p->tile_stride < 1 ||
-        (waves != 8 && waves != 4))
+    if (ns < 1 || ns > wv::H_NS_MAX || !p->X || !p->Q || !p->excl || !p->qscale || p->tile_stride < 1)
         return hipErrorInvalidValue;
     const bool l2 = p->metric == WV_METRIC_L2;
     if (l2 && !p->xns) return hipErrorInvalidValue;
-    const int tps = waves == 8 ? wv::H_TPS8 : 1;
-    const bool stg = waves == 8 && p->stagger;
-    const size_t lds = (size_t)(stg ? 4 : wv::H_STAGES) * tps * (2 * ns * 64 + 17) * 16;
+    const size_t lds = (size_t)wv::H_STAGES * wv::H_TPS8 * (2 * ns * 64 + 17) * 16;
 #define WV_H16_GO(NS, L, S)                                                                                    \
-    if (stg && !S && p->xslot)                                                                                 \
-        hipLaunchKernelGGL((wv::wv_bf_h16_kernel<NS, L, false, 8, wv::H_TPS8, true, true>), dim3(nb), dim3(512), lds, s, *p); \
-    else if (stg)                                                                                              \
-        hipLaunchKernelGGL((wv::wv_bf_h16_kernel<NS, L, S, 8, wv::H_TPS8, false, true>), dim3(nb), dim3(512), lds, s, *p); \
-    else if (waves == 8 && !S && p->xslot)                                                                     \
-        hipLaunchKernelGGL((wv::wv_bf_h16_kernel<NS, L, false, 8, wv::H_TPS8, true>), dim3(nb), dim3(512), lds, s, *p); \
-    else if (waves == 8) hipLaunchKernelGGL((wv::wv_bf_h16_kernel<NS, L, S, 8, wv::H_TPS8>), dim3(nb), dim3(512), lds, s, *p); \
-    else hipLaunchKernelGGL((wv::wv_bf_h16_kernel<NS, L, S, 4, 1>), dim3(nb), dim3(256), lds, s, *p);
+    if (!S && p->xslot)                                                                                        \
+        hipLaunchKernelGGL((wv::wv_bf_h16_kernel<NS, L, false, true>), dim3(nb), dim3(512), lds, s, *p);       \
+    else hipLaunchKernelGGL((wv::wv_bf_h16_kernel<NS, L, S>), dim3(nb), dim3(512), lds, s, *p);
 #define WV_H16_LAUNCH(NS)                     \
     if (seed) {                               \
         if (l2) { WV_H16_GO(NS, true, true) } \
@@ -1642,38 +1255,6 @@ hipError_t wv_launch_bf_h16(const wv::H16Params* p, int ns, int seed, int waves,
     }
 #undef WV_H16_LAUNCH
 #undef WV_H16_GO
-    return hipGetLastError();
-}
-
-hipError_t wv_launch_bf_h16q(const wv::H16Params* p, int ns32, int seed, int waves, hipStream_t s) {
-    const uint64_t total = (uint64_t)p->n_qblocks * p->ntiles;
-    const unsigned nb = (unsigned)((total + p->units_per_block - 1) / p->units_per_block);
-    if (nb == 0) return hipSuccess;
-    if (ns32 < 1 || ns32 > wv::H_NS_MAX / 2 || !p->X || !p->Q || !p->excl || !p->qscale || p->tile_stride < 1)
-        return hipErrorInvalidValue;
-    const bool l2 = p->metric == WV_METRIC_L2;
-    if (l2 && !p->xns) return hipErrorInvalidValue;
-    if (waves != 8 && waves != 4) return hipErrorInvalidValue;
-    const size_t lds = (size_t)wv::H_STAGES * (waves == 8 ? 2 : 1) * (4 * ns32 * 64 + 17) * 16;
-#define WV_H16Q_GO(NS, L, S)                                                                                  \
-    if (waves == 8) hipLaunchKernelGGL((wv::wv_bf_h16q_kernel<NS, L, S, 8>), dim3(nb), dim3(512), lds, s, *p); \
-    else hipLaunchKernelGGL((wv::wv_bf_h16q_kernel<NS, L, S, 4>), dim3(nb), dim3(256), lds, s, *p);
-#define WV_H16Q_LAUNCH(NS)                     \
-    if (seed) {                                \
-        if (l2) { WV_H16Q_GO(NS, true, true) } \
-        else { WV_H16Q_GO(NS, false, true) }   \
-    } else {                                   \
-        if (l2) { WV_H16Q_GO(NS, true, false) } \
-        else { WV_H16Q_GO(NS, false, false) }  \
-    }
-    switch (ns32) {
-        case 1: WV_H16Q_LAUNCH(1) break;
-        case 2: WV_H16Q_LAUNCH(2) break;
-        case 3: WV_H16Q_LAUNCH(3) break;
-        default: WV_H16Q_LAUNCH(4) break;
-    }
-#undef WV_H16Q_LAUNCH
-#undef WV_H16Q_GO
     return hipGetLastError();
 }
 
@@ -1701,18 +1282,11 @@ hipError_t wv_launch_bf_h16w(const wv::H16Params* p, hipStream_t s) {
         return hipErrorInvalidValue;
     const bool l2 = p->metric == WV_METRIC_L2;
     if (l2 && !p->xns) return hipErrorInvalidValue;
-    if (p->wide_rows != 64 && p->wide_rows != 128) return hipErrorInvalidValue;
-    if (p->wide_rows == 64) {
-        using St = wv::HWStage<64>;
-        const size_t lds = ((size_t)wv::HW_STAGES * St::U4 + 2 * St::EX_U4) * 16 + 8 * 256 + 8 * 4096;   // + the gtau and bucket return slots
-        if (l2) hipLaunchKernelGGL((wv::wv_bf_h16w_kernel<true, 64>), dim3(nb), dim3(512), lds, s, *p);
-        else hipLaunchKernelGGL((wv::wv_bf_h16w_kernel<false, 64>), dim3(nb), dim3(512), lds, s, *p);
-    } else {
-        using St = wv::HWStage<128>;
-        const size_t lds = ((size_t)wv::HW_STAGES * St::U4 + 2 * St::EX_U4) * 16 + 8 * 256 + 8 * 4096;   // + the gtau and bucket return slots
-        if (l2) hipLaunchKernelGGL((wv::wv_bf_h16w_kernel<true, 128>), dim3(nb), dim3(512), lds, s, *p);
-        else hipLaunchKernelGGL((wv::wv_bf_h16w_kernel<false, 128>), dim3(nb), dim3(512), lds, s, *p);
-    }
+    if (p->wide_rows != 128) return hipErrorInvalidValue;
+    using St = wv::HWStage<128>;
+    const size_t lds = ((size_t)wv::HW_STAGES * St::U4 + 2 * St::EX_U4) * 16 + 8 * 256;   // + the gtau return slots
+    if (l2) hipLaunchKernelGGL((wv::wv_bf_h16w_kernel<true, 128>), dim3(nb), dim3(512), lds, s, *p);
+    else hipLaunchKernelGGL((wv::wv_bf_h16w_kernel<false, 128>), dim3(nb), dim3(512), lds, s, *p);
     return hipGetLastError();
 }
 

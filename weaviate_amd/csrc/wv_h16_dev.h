@@ -1,7 +1,6 @@
-// wv_h16_dev.h -- device helpers shared by the f16 key passes (wv_h16.hip,
-// wv_h16s.hip): LDS-DMA as inline asm with counted waits, the tile
-// eligibility words, the LDS stage layout, and the column-list extraction of
-// the 16x16x32 passes.
+// wv_h16_dev.h -- device helpers of the f16 key passes (wv_h16.hip): LDS-DMA
+// as inline asm with counted waits, the tile eligibility words, the LDS stage
+// layout.
 #pragma once
 #include "wv_device.h"
 #include "wv_params.h"
@@ -108,110 +107,9 @@ struct H16Stage {
     static constexpr int U4 = IMG_U4 + 16 + 1;
 };
 #ifndef WV_H16_TPS
-#define WV_H16_TPS 2
+#define WV_H16_TPS 3   // (round 4: 3 tiles per stage, 2.66 -> 2.60 ms per 1M x 10k pass; 3 stages of 3 = 150 KiB at D = 128)
 #endif
 constexpr int H_TPS8 = WV_H16_TPS;   // tiles per LDS stage (8-wave kernel): one barrier per H_TPS8 tiles
 constexpr int H_STAGES = 3;   // a stage holds H_TPS tiles; stage p % 3 computes while p + 1, p + 2 land
-
-// Extraction of one query group's keys of a half tile (a lane's 8 values v:
-// rows rb + 16 (v / 4) + v % 4) into the column lists, in wave-uniform rounds:
-// every lane whose smallest remaining key is <= its column's threshold (the
-// list's tail, the seed / running threshold) takes it out; the candidates of
-// each lane quarter in turn are broadcast to the column's four lanes, which
-// merge them into their entries (entry j becomes med3(e[j - 1], d, e[j]),
-// e[-1] the previous quarter's last entry).  Keys equal to the tail are taken
-// out without entering.
-__device__ __forceinline__ void qcol_extract(float M, floatx4& A, floatx4& B, float (&ld)[HQ_KP],
-                                             uint32_t (&li)[HQ_KP], float& thr, float tau, uint32_t rb, int lane) {
-    const float INF = __builtin_inff();
-    const int l15 = lane & 15;
-    const int prev = (lane + 48) & 63;   // the same column's previous lane quarter
-    for (;;) {
-        const bool has = M <= thr;
-        const uint64_t hb = __ballot(has);
-        if (!hb) break;
-        WV_DBG_COUNT(1)
-        // position of M: a descending scan, so among equal keys the lowest row wins
-        uint32_t sel = 0;
-#pragma unroll
-        for (int r = 3; r >= 0; --r) sel = B[r] == M ? 4u + r : sel;
-#pragma unroll
-        for (int r = 3; r >= 0; --r) sel = A[r] == M ? (uint32_t)r : sel;
-        sel = has ? sel : 8u;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            A[r] = sel == (uint32_t)r ? INF : A[r];
-            B[r] = sel == 4u + r ? INF : B[r];
-        }
-        uint32_t rbo = rb;   // opaque: the row ids stay in this rare loop
-        asm volatile("" : "+v"(rbo));
-        const uint32_t id = rbo + (sel & 3u) + 16u * ((sel >> 2) & 1u);
-        const float d = has ? M : INF;
-#pragma unroll
-        for (int q = 0; q < HQ_PROD; ++q) {
-            if (!((hb >> (16 * q)) & 0xFFFFull)) continue;   // (wave-uniform)
-            const float cd = __shfl(d, l15 + 16 * q, 64);
-            const uint32_t cid = __shfl(id, l15 + 16 * q, 64);
-            float pk = __shfl(ld[HQ_KP - 1], prev, 64);
-            const uint32_t pi = __shfl(li[HQ_KP - 1], prev, 64);
-            pk = lane < 16 ? -INF : pk;
-#pragma unroll
-            for (int i = HQ_KP - 1; i >= 0; --i) {
-                const float lo = i ? ld[i - 1] : pk;
-                const uint32_t loi = i ? li[i - 1] : pi;
-                const bool a = cd < lo, b = cd < ld[i];
-                li[i] = a ? loi : (b ? cid : li[i]);
-                ld[i] = __builtin_amdgcn_fmed3f(lo, cd, ld[i]);
-            }
-        }
-        thr = fminf(__shfl(ld[HQ_KP - 1], l15 + 48, 64), tau);
-        M = fminf(fminf(fminf(A[0], A[1]), fminf(A[2], A[3])), fminf(fminf(B[0], B[1]), fminf(B[2], B[3])));
-    }
-}
-
-// qcol_extract over one 16 x 16 accumulator's 4 keys of a lane (rows rb + e,
-// e < 4; wv_bf_h16s_kernel's row-group steps), on a copy: the accumulators
-// stay read-only
-__device__ __forceinline__ void qcol_extract4(float M, floatx4 A, float (&ld)[HQ_KP], uint32_t (&li)[HQ_KP],
-                                              float& thr, float tau, uint32_t rb, int lane) {
-    const float INF = __builtin_inff();
-    const int l15 = lane & 15;
-    const int prev = (lane + 48) & 63;   // the same column's previous lane quarter
-    for (;;) {
-        const bool has = M <= thr;
-        const uint64_t hb = __ballot(has);
-        if (!hb) break;
-        WV_DBG_COUNT(1)
-        uint32_t sel = 0;   // position of M: a descending scan, so among equal keys the lowest row wins
-#pragma unroll
-        for (int r = 3; r >= 0; --r) sel = A[r] == M ? (uint32_t)r : sel;
-        sel = has ? sel : 4u;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) A[r] = sel == (uint32_t)r ? INF : A[r];
-        uint32_t rbo = rb;   // opaque: the row ids stay in this rare loop
-        asm volatile("" : "+v"(rbo));
-        const uint32_t id = rbo + (sel & 3u);
-        const float d = has ? M : INF;
-#pragma unroll
-        for (int q = 0; q < HQ_PROD; ++q) {
-            if (!((hb >> (16 * q)) & 0xFFFFull)) continue;   // (wave-uniform)
-            const float cd = __shfl(d, l15 + 16 * q, 64);
-            const uint32_t cid = __shfl(id, l15 + 16 * q, 64);
-            float pk = __shfl(ld[HQ_KP - 1], prev, 64);
-            const uint32_t pi = __shfl(li[HQ_KP - 1], prev, 64);
-            pk = lane < 16 ? -INF : pk;
-#pragma unroll
-            for (int i = HQ_KP - 1; i >= 0; --i) {
-                const float lo = i ? ld[i - 1] : pk;
-                const uint32_t loi = i ? li[i - 1] : pi;
-                const bool a = cd < lo, b = cd < ld[i];
-                li[i] = a ? loi : (b ? cid : li[i]);
-                ld[i] = __builtin_amdgcn_fmed3f(lo, cd, ld[i]);
-            }
-        }
-        thr = fminf(__shfl(ld[HQ_KP - 1], l15 + 48, 64), tau);
-        M = fminf(fminf(A[0], A[1]), fminf(A[2], A[3]));
-    }
-}
 
 }  // namespace wv

@@ -10,8 +10,6 @@ constexpr int BF_BK = 32;    // k-chunk staged through LDS
 constexpr int BF_LDT = 36;   // LDS row: 32 k + 4 pad floats (odd 16-byte stride: conflict-free b128)
 constexpr int BF_KP = 8;     // candidates kept per producer lane (register list)
 constexpr int BF_PROD = 4;   // producers per query: 2 base-row waves x 2 lane halves
-constexpr int BF_PROD3 = 8;  // wv_bf_split3_kernel: 4 base-row waves x 2 lane halves
-constexpr int BF_BQ3 = 192;  // wv_bf_split3_kernel: queries per block (3 query waves x 64)
 constexpr int FIN_KF = 32;   // candidates re-ranked exactly per query
 constexpr int BF_FAST_KMAX = 32;   // k served by the MFMA + finalize pipeline
 // larger k (searches with limit > 32, SearchByVectorDistance's deepening): the
@@ -38,8 +36,8 @@ struct BfParams {
     float* out_d;           // [nq][n_slots][BF_PROD*BF_KP]
     uint32_t* out_id;
     int split;              // X and Q are split images (split_hi_index): wv_bf_split_kernel
-    int bq;                 // queries per block (BF_BQ; the split kernels also run 2 * BF_BQ and BF_BQ3)
-    int prod;               // producers (lists) per query per slot: BF_PROD, or BF_PROD3 at bq = BF_BQ3
+    int bq;                 // queries per block (BF_BQ; the split kernel runs 2 * BF_BQ)
+    int prod;               // producers (lists) per query per slot: BF_PROD
     int locality;           // bit 1: XCD-contiguous block ids; bit 2: aligned tile rotation
 };
 
@@ -134,31 +132,6 @@ inline uint64_t h16_index(uint64_t row, int k, int ns) {
     return (block * 64 + lane) * 8 + (uint64_t)(k & 7);
 }
 
-// ---- f16 key pass on v_mfma_f32_16x16x32_f16 (wv_bf_h16q_kernel) ------------
-// The same 64-row tiles and 512-query blocks as wv_bf_h16_kernel, in the
-// 16x16x32 operand layout (h16q_index: per 16-row group and 32-k step a 1 KiB
-// block, lane (h, r) holding k 8h .. 8h + 7 of row r).  A lane's keys cover 4
-// query columns (16 q + lane % 16) and rows 4 (lane / 16) ...; the four lanes
-// of a column share one sorted list of HQ_PROD * HQ_KP entries per slot, lane
-// quarter q holding entries HQ_KP q ...; the seed pass keeps one minimum per
-// lane quarter (HQ_PROD per query and slot).
-constexpr int HQ_PROD = 4;    // lane quarters per column
-constexpr int HQ_KP = 4;      // list entries per lane quarter
-// one-wave-per-SIMD variant (wv_bf_h16s_kernel): 4-wave workgroups, one per
-// CU, 8 query groups of 16 per wave; h16q images and lists
-constexpr int HS_QG = 8;      // query groups per wave
-constexpr int HS_BQ = 512;    // queries per block: 4 waves x 8 groups x 16
-constexpr int HS_TPS = 2;     // tiles per LDS stage
-
-#if defined(__HIPCC__)
-__host__ __device__
-#endif
-inline uint64_t h16q_index(uint64_t row, int k, int ns32) {
-    const uint64_t block = (row >> 4) * (uint64_t)ns32 + (uint64_t)(k >> 5);   // (16-row group, 32-k step)
-    const uint64_t lane = (uint64_t)(((k >> 3) & 3) * 16) + (row & 15);
-    return (block * 64 + lane) * 8 + (uint64_t)(k & 7);
-}
-
 struct H16Params {
     const void* X;            // corpus image (h16_index), rows padded to whole tiles (zeros)
     const void* Q;            // query image (h16_index over query rows), padded to whole H_BQ blocks
@@ -184,12 +157,6 @@ struct H16Params {
     // list entries) + 2 eps, atomicMin'ed into gtau (order-preserving keys of
     // scaled units, h16_key_enc); keys above it are dropped everywhere
     unsigned int* gtau;       // [nq] (nullable)
-    // the wide-D pass: 16 buckets of list heads per query (bucket = slot, row
-    // half, lane half mod 16: disjoint row sets), each the atomicMin of its
-    // lists' smallest keys -- the k-th smallest of 16 bucket minima is the key
-    // of one of k distinct rows, so it (+ 2 eps) bounds the k-th key with
-    // every slot's best rows, not one lane pair's 16 entries
-    unsigned int* gbkt;       // [n_qblocks * HW_BQ][16] (nullable)
     int kth;                  // k (0: no running threshold)
     const float* marg;        // [nq] 2 eps in scaled key units, rounded up (wv_h16_margin_kernel)
     // cross-slot threshold (xslot, 32x32x16 pass): each slot stores its lists'
@@ -197,7 +164,6 @@ struct H16Params {
     // reads the others', whose k-th smallest + 2 eps bounds the k-th key
     float* gslot;             // [nq][2 n_slots] (xslot)
     int xslot;                // 1: use gslot instead of the gtau publish
-    int stagger;              // 32x32x16 8-wave pass: waves 4-7 half a tile behind (4-stage ring)
     int ns;                   // 16-k steps of the images (the wide-D kernel: a multiple of HW_KC)
     int wide_rows;            // the wide-D kernel's rows per wave: 128 (256-row tiles) or 64 (128-row tiles)
 };
@@ -267,7 +233,7 @@ struct BfFinParams {
     int split;              // approximate keys came from the bf16x3 pass (wider eps)
     int bq;                 // queries per block of the key pass (BfParams.bq)
     int prod;               // producers per query per slot (BfParams.prod)
-    int kp;                 // entries per list (0: BF_KP; the 16x16x32 f16 pass: HQ_PROD * HQ_KP)
+    int kp;                 // entries per list (0: BF_KP)
     int finw_ne;            // wide finalize: LDS entry capacity (a power of two >= FINW_KF; 0: FINW_NE)
     // f16 key pass (h16 = 1): keys are scaled by s = sx * qscale[0]; eps adds
     // ex_max * |B| + xnorm_max * qres[q] (the f16 rounding of corpus and query)
