@@ -137,7 +137,7 @@ type Options struct {
 	ID           string      // hnsw.Config.ID: the log is RootPath/ID.hnsw.commitlog.d
 	VectorForID  VectorForID // hnsw.Config.VectorForIDThunk
 	MaxBatch     int         // queries per coalesced launch (0: 1024)
-	MaxWaitUsec  int         // batching window after the first waiting query (0: 200)
+	MaxWaitUsec  int         // micro-batcher linger at an idle device (0: none, launch at once)
 	CompactRows  uint64      // delta rows that trigger a compaction (0: 8192)
 	InitialSize  uint64      // mirror capacity before growth (0: 25000)
 	Metrics      bool        // export the mirror's gauges (metrics.go; PROMETHEUS_MONITORING_ENABLED)

@@ -291,12 +291,15 @@ int wv_graph_destroy(wv_graph *g);
 /* Micro-batcher (SURVEY 8b "Threading"): SearchByVector is called once per
  * request from many threads (adapters/repos/db/index.go:988-1028 ->
  * shard_read.go:246-252).  wv_batcher_search blocks its caller while a
- * dispatcher thread coalesces up to max_batch waiting requests (or those that
- * arrived within max_wait_us of the first) into one wv_search_batch with
- * per-query allow lists, then returns this caller's row: the same result as
- * wv_search_by_vector(ix, vector, k, allow_bits, allow_nbits, ...).  Two
- * workers alternate, so one batch is coalesced and queued while the previous
- * one runs.  Destroy the batcher before the index. */
+ * dispatcher thread coalesces up to max_batch waiting requests into one
+ * wv_search_batch with per-query allow lists, then returns this caller's row:
+ * the same result as wv_search_by_vector(ix, vector, k, allow_bits,
+ * allow_nbits, ...).  Latency-first: one batch runs on the device at a time and
+ * takes every request queued while the previous one ran, so a lone request
+ * launches at once; max_wait_us > 0 lets the oldest request at an idle device
+ * linger that long for company.  Two workers: one wakes a finished batch's
+ * callers (each alone) while the other launches the next.  Destroy the
+ * batcher before the index. */
 typedef struct wv_batcher wv_batcher;
 int wv_batcher_create(wv_index *ix, int dim, int max_batch, int max_wait_us, wv_batcher **out);
 int wv_batcher_search(wv_batcher *b, const float *vector, int k, const uint64_t *allow_bits, uint64_t allow_nbits,
@@ -393,7 +396,7 @@ typedef struct {
     int dim;                   /* 0: learnt from the first vector */
     uint64_t initial_capacity; /* 0: 25000 (maintainance.go:22 initialSize) */
     int max_batch;             /* micro-batcher: queries per launch (0: 1024) */
-    int max_wait_us;           /* micro-batcher window (0: 200) */
+    int max_wait_us;           /* micro-batcher linger at an idle device (0: none) */
     uint64_t compact_rows;     /* delta rows that ask for a compaction (0: 8192) */
     int ef_construction;       /* device-build compaction (0: 128) */
     uint64_t build_seed;       /* device-build level draw */

@@ -478,7 +478,9 @@ int main(int argc, char** argv) {
                 if (filtered && !std::binary_search(al.begin(), al.end(), ids[i]))
                     violation("filtered search returned a disallowed id");
             }
-            if (target != UINT64_MAX && !del_now[target] && (filtered || !target_in_graph)) {
+            // (pq: a compressed index ranks by the PQ distance, under which a
+            // row's own vector need not come first -- no such check there)
+            if (!pqm && target != UINT64_MAX && !del_now[target] && (filtered || !target_in_graph)) {
                 n_added_checks++;
                 bool deleted_since = false;
                 const int nd2 = n_deleted.load(std::memory_order_acquire);

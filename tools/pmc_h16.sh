@@ -23,7 +23,7 @@ out = {}
 for f in sorted(glob.glob("gpurun_out/pmc_h16/p*/run_counter_collection.csv")):
     vals = {}
     for r in csv.DictReader(open(f)):
-        if os.environ.get("KSUB", "h16p_kernel<8, true, false, true") in r["Kernel_Name"]:
+        if os.environ.get("KSUB", "wv_bf_h16_kernel<8, true, false, true>") in r["Kernel_Name"]:
             vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
     for k, v in vals.items():
         out[k] = statistics.mean(v)
@@ -38,7 +38,7 @@ import os
 avg_ns = None
 for f in glob.glob("gpurun_out/pmc_h16/trace/run_kernel_stats.csv"):
     for r in csv.DictReader(open(f)):
-        if os.environ.get("KSUB", "h16p_kernel<8, true, false, true") in r["Name"]:
+        if os.environ.get("KSUB", "wv_bf_h16_kernel<8, true, false, true>") in r["Name"]:
             avg_ns = float(r["AverageNs"])
 if "FETCH_SIZE" in out:
     rd = 2.0 * out["FETCH_SIZE"] * 1024

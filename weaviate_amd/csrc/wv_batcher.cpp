@@ -5,9 +5,8 @@
 // of Index.objectVectorSearch (adapters/repos/db/index.go:988-1028) reach
 // Shard.objectVectorSearch -> SearchByVector (shard_read.go:246-252).  One
 // query is far too little work for a GPU launch, so callers hand their query to
-// a dispatcher thread that coalesces up to max_batch waiting requests (or what
-// arrived within max_wait_us of the first) into one wv_search_batch call and
-// fans the rows back out.  Each caller blocks until its own row is written;
+// a dispatcher thread that coalesces up to max_batch waiting requests into one
+// wv_search_batch call and fans the rows back out.  Each caller blocks until its own row is written;
 // no caller pointer is kept after its call returns (cgo pointer rules).
 //
 // Requests are grouped by (k, filtered): searchTimeEF depends on k
@@ -18,9 +17,17 @@
 // helpers/allow_list.go:19-118), written straight into the batch's row; a
 // group whose requests all carry the same list sends it once (shared).
 //
-// Two workers take batches off the queue: while one batch runs on the GPU
-// (wv_search_batch releases the index before it waits), the other coalesces
-// and queues the next, so the device does not idle between batches.
+// Dispatch is latency-first ("natural batching"): one batch runs on the device
+// at a time, and a free worker takes EVERY request queued meanwhile the moment
+// the device is free -- a lone request on an idle device launches at once, and
+// under load the batch size follows the arrival rate times one batch's device
+// time.  max_wait_us is an optional linger for an idle device (the oldest
+// request waits at most that long for company; 0 = none).  Two workers: while
+// one fans a finished batch's rows back out, the other is already launching
+// the next.  Each caller sleeps on its own condition variable and is woken
+// alone when its row is written (no broadcast to every waiting caller); the
+// workers' staging buffers live as long as the batcher (no per-batch heap
+// allocation once they have grown to max_batch).
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
@@ -61,7 +68,21 @@ struct Request {
     int32_t* out_n;
     int rc = WV_OK;
     std::string err;
+    wait_clock::time_point arrived;
+    // the caller's own wakeup: set and notified under m by the worker, which
+    // touches nothing of the request after releasing m
+    std::mutex m;
+    std::condition_variable cv;
     bool done = false;
+};
+
+// one worker's staging, reused batch after batch
+struct Staging {
+    std::vector<Request*> take, g;
+    std::vector<char> used;
+    std::vector<float> q, ds;
+    std::vector<uint64_t> bits, ids;
+    std::vector<int32_t> cnt;
 };
 
 }  // namespace
@@ -71,12 +92,14 @@ struct wv_batcher {
     wv_group* grp = nullptr;   // a multi-GPU group instead of one index
     int dim = 0;
     int max_batch = 256;
-    int max_wait_us = 200;
+    int max_wait_us = 0;
     std::mutex mu;
-    std::condition_variable cv_work, cv_done;
+    std::condition_variable cv_work;
     std::deque<Request*> queue;
     bool stop = false;
+    bool device_busy = false;      // a worker holds the device (one batch at a time)
     std::vector<std::thread> th;   // the workers
+    Staging st[2];
     uint64_t n_requests = 0, n_batches = 0, n_launch_rows = 0;
 
     static uint64_t nbits_of(const Request* r) {
@@ -101,77 +124,98 @@ struct wv_batcher {
         }
     }
 
-    void run_group(std::vector<Request*>& g) {
-        const int n = (int)g.size();
-        const int k = g[0]->k;
-        const bool filtered = g[0]->filtered;
-        std::vector<float> q((size_t)n * dim);
-        for (int i = 0; i < n; ++i) std::memcpy(q.data() + (size_t)i * dim, g[i]->q, sizeof(float) * dim);
-        std::vector<uint64_t> bits;
+    // one (k, filtered) group on the device; returns the call's status
+    int run_group(Staging& s) {
+        const int n = (int)s.g.size();
+        const int k = s.g[0]->k;
+        const bool filtered = s.g[0]->filtered;
+        s.q.resize((size_t)n * dim);
+        for (int i = 0; i < n; ++i) std::memcpy(s.q.data() + (size_t)i * dim, s.g[i]->q, sizeof(float) * dim);
         uint64_t nbits = 0, stride = 0;
         if (filtered) {
             bool shared = true;
-            for (int i = 1; i < n && shared; ++i) shared = same_list(g[0], g[i]);
-            for (Request* r : g) nbits = std::max(nbits, nbits_of(r));
+            for (int i = 1; i < n && shared; ++i) shared = same_list(s.g[0], s.g[i]);
+            for (Request* r : s.g) nbits = std::max(nbits, nbits_of(r));
             nbits = std::max<uint64_t>(nbits, 1);   // (an empty list allows nothing)
             const uint64_t words = (nbits + 63) / 64;
             stride = shared ? 0 : words;
-            bits.assign((size_t)(shared ? 1 : n) * words, 0);
-            for (int i = 0; i < (shared ? 1 : n); ++i) write_row(g[i], bits.data() + (size_t)i * words);
+            s.bits.assign((size_t)(shared ? 1 : n) * words, 0);
+            for (int i = 0; i < (shared ? 1 : n); ++i) write_row(s.g[i], s.bits.data() + (size_t)i * words);
         }
-        std::vector<uint64_t> ids((size_t)n * k);
-        std::vector<float> ds((size_t)n * k);
-        std::vector<int32_t> cnt(n);
-        const int rc = grp ? wv_group_search_batch(grp, q.data(), n, k, 0, filtered ? bits.data() : nullptr, nbits,
-                                                   stride, WV_MODE_AUTO, ids.data(), ds.data(), cnt.data())
-                           : wv_search_batch(ix, q.data(), n, k, 0, filtered ? bits.data() : nullptr, nbits, stride,
-                                             WV_MODE_AUTO, ids.data(), ds.data(), cnt.data());
-        const std::string msg = rc ? wv_last_error() : "";
-        std::lock_guard<std::mutex> l(mu);
-        for (int i = 0; i < n; ++i) {
-            Request* r = g[i];
+        s.ids.resize((size_t)n * k);
+        s.ds.resize((size_t)n * k);
+        s.cnt.resize(n);
+        const uint64_t* bits = filtered ? s.bits.data() : nullptr;
+        return grp ? wv_group_search_batch(grp, s.q.data(), n, k, 0, bits, nbits, stride, WV_MODE_AUTO, s.ids.data(),
+                                           s.ds.data(), s.cnt.data())
+                   : wv_search_batch(ix, s.q.data(), n, k, 0, bits, nbits, stride, WV_MODE_AUTO, s.ids.data(),
+                                     s.ds.data(), s.cnt.data());
+    }
+
+    // each caller's row, then its own wakeup
+    static void fan_out(Staging& s, int rc, const std::string& msg) {
+        const int k = s.g[0]->k;
+        for (size_t i = 0; i < s.g.size(); ++i) {
+            Request* r = s.g[i];
             r->rc = rc;
             if (rc) {
                 r->err = msg;
             } else {
-                const int m = cnt[i];
-                std::memcpy(r->out_ids, ids.data() + (size_t)i * k, sizeof(uint64_t) * m);
-                std::memcpy(r->out_d, ds.data() + (size_t)i * k, sizeof(float) * m);
+                const int m = s.cnt[i];
+                std::memcpy(r->out_ids, s.ids.data() + i * k, sizeof(uint64_t) * m);
+                std::memcpy(r->out_d, s.ds.data() + i * k, sizeof(float) * m);
                 *r->out_n = m;
             }
+            std::lock_guard<std::mutex> g(r->m);
             r->done = true;
+            r->cv.notify_one();
         }
-        n_batches++;
-        n_launch_rows += n;
-        cv_done.notify_all();
     }
 
-    void loop() {
+    void loop(Staging& s) {
         std::unique_lock<std::mutex> l(mu);
         for (;;) {
-            cv_work.wait(l, [&] { return stop || !queue.empty(); });
-            if (queue.empty() && stop) return;
-            // the window opens with the first waiting request
-            const auto deadline = wait_clock::now() + std::chrono::microseconds(max_wait_us);
-            cv_work.wait_until(l, deadline, [&] { return stop || (int)queue.size() >= max_batch; });
-            std::vector<Request*> take;
-            while (!queue.empty() && (int)take.size() < max_batch) {
-                take.push_back(queue.front());
+            cv_work.wait(l, [&] { return (!queue.empty() && !device_busy) || (stop && queue.empty()); });
+            if (queue.empty()) return;   // (stop)
+            if (max_wait_us > 0 && (int)queue.size() < max_batch && !stop) {
+                // linger at an idle device: until max_batch or the oldest request's deadline
+                const auto deadline = queue.front()->arrived + std::chrono::microseconds(max_wait_us);
+                cv_work.wait_until(l, deadline, [&] { return stop || (int)queue.size() >= max_batch; });
+                if (device_busy || queue.empty()) continue;   // (the other worker took them)
+            }
+            device_busy = true;
+            s.take.clear();
+            while (!queue.empty() && (int)s.take.size() < max_batch) {
+                s.take.push_back(queue.front());
                 queue.pop_front();
             }
             l.unlock();
             // group by (k, filtered), keeping arrival order inside a group
-            std::vector<bool> used(take.size(), false);
-            for (size_t i = 0; i < take.size(); ++i) {
-                if (used[i]) continue;
-                std::vector<Request*> g;
-                for (size_t j = i; j < take.size(); ++j) {
-                    if (used[j] || take[j]->k != take[i]->k || take[j]->filtered != take[i]->filtered)
+            s.used.assign(s.take.size(), 0);
+            size_t left = s.take.size();
+            for (size_t i = 0; i < s.take.size(); ++i) {
+                if (s.used[i]) continue;
+                s.g.clear();
+                for (size_t j = i; j < s.take.size(); ++j) {
+                    if (s.used[j] || s.take[j]->k != s.take[i]->k || s.take[j]->filtered != s.take[i]->filtered)
                         continue;
-                    used[j] = true;
-                    g.push_back(take[j]);
+                    s.used[j] = 1;
+                    s.g.push_back(s.take[j]);
                 }
-                run_group(g);
+                left -= s.g.size();
+                const int rc = run_group(s);
+                const std::string msg = rc ? wv_last_error() : std::string();
+                if (left == 0) {
+                    // the device is free: the other worker launches the next
+                    // batch while this one wakes its callers
+                    l.lock();
+                    device_busy = false;
+                    n_batches++;
+                    n_launch_rows += s.take.size();
+                    l.unlock();
+                    cv_work.notify_all();
+                }
+                fan_out(s, rc, msg);
             }
             l.lock();
         }
@@ -191,7 +235,7 @@ static int create_batcher(wv_index* ix, wv_group* grp, int dim, int max_batch, i
     b->dim = dim;
     b->max_batch = max_batch;
     b->max_wait_us = max_wait_us;
-    for (int w = 0; w < 2; ++w) b->th.emplace_back([b] { b->loop(); });
+    for (int w = 0; w < 2; ++w) b->th.emplace_back([b, w] { b->loop(b->st[w]); });
     *out = b;
     return WV_OK;
 }
@@ -205,21 +249,24 @@ int wv_batcher_create_group(wv_group* g, int dim, int max_batch, int max_wait_us
 }
 
 static int submit(wv_batcher* b, Request& r) {
+    r.arrived = wait_clock::now();
     {
-        std::unique_lock<std::mutex> l(b->mu);
+        std::lock_guard<std::mutex> l(b->mu);
         if (b->stop) {
             wv_internal_set_error("wv_batcher_search: batcher is shut down");
             return WV_ESTATE;
         }
         b->queue.push_back(&r);
         b->n_requests++;
-        b->cv_work.notify_one();
-        b->cv_done.wait(l, [&] { return r.done; });
+    }
+    b->cv_work.notify_one();
+    {
+        std::unique_lock<std::mutex> l(r.m);
+        r.cv.wait(l, [&] { return r.done; });
     }
     if (r.rc) wv_internal_set_error(r.err.c_str());
     return r.rc;
 }
-
 int wv_batcher_search(wv_batcher* b, const float* vector, int k, const uint64_t* allow_bits, uint64_t allow_nbits,
                       uint64_t* out_ids, float* out_dists, int32_t* out_n) {
     if (!b || !vector || k <= 0 || !out_ids || !out_dists || !out_n) {

@@ -84,31 +84,31 @@ __device__ __forceinline__ float exact_dist_group8(const float* __restrict__ q,
     return 1.0f - r;
 }
 
-// Exact reference-order distances of up to 32 rows at once (4 per 8-lane
+// Exact reference-order distances of up to 8*RPG rows at once (RPG per 8-lane
 // group), all row loads of a 4-block (128-float) slab issued before any FMA so
-// one memory round trip serves 32 rows.  ids/out live in LDS; rows >= n are
+// one memory round trip serves 8*RPG rows.  ids/out live in LDS; rows >= n are
 // skipped.  Same arithmetic, in the same order, as exact_dist_group8.
-template <int METRIC>
-__device__ __forceinline__ void exact_dist_rows32(const float* __restrict__ q, const float* __restrict__ X,
-                                                  int ldx, int D, const uint32_t* ids, int n, float* out,
-                                                  int lane) {
+template <int METRIC, int RPG = 4>
+__device__ __forceinline__ void exact_dist_rows(const float* __restrict__ q, const float* __restrict__ X,
+                                                int ldx, int D, const uint32_t* ids, int n, float* out,
+                                                int lane) {
     const int g = lane & 7, grp = lane >> 3;
     const int nb = D >> 5;
-    const float* row[4];
-    bool ok[4];
+    const float* row[RPG];
+    bool ok[RPG];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < RPG; ++j) {
         const int c = grp + 8 * j;
         ok[j] = c < n;
         row[j] = X + (uint64_t)(ok[j] ? ids[c] : ids[0]) * ldx;
     }
-    float a[4][4];
+    float a[RPG][4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) a[j][0] = a[j][1] = a[j][2] = a[j][3] = 0.f;
+    for (int j = 0; j < RPG; ++j) a[j][0] = a[j][1] = a[j][2] = a[j][3] = 0.f;
     for (int b0 = 0; b0 < nb; b0 += 4) {
-        float4 y[4][4];
+        float4 y[RPG][4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < RPG; ++j)
 #pragma unroll
             for (int bb = 0; bb < 4; ++bb)
                 if (ok[j] && b0 + bb < nb) y[j][bb] = ld4(row[j] + 32 * (b0 + bb) + 4 * g);
@@ -117,7 +117,7 @@ __device__ __forceinline__ void exact_dist_rows32(const float* __restrict__ q, c
             if (b0 + bb >= nb) break;
             const float4 x = ld4(q + 32 * (b0 + bb) + 4 * g);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
+            for (int j = 0; j < RPG; ++j) {
                 if (!ok[j]) continue;
                 const float4 yy = y[j][bb];
                 if (METRIC == WV_METRIC_L2) {
@@ -136,7 +136,7 @@ __device__ __forceinline__ void exact_dist_rows32(const float* __restrict__ q, c
         }
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < RPG; ++j) {
         float t = 0.f;
         if (ok[j]) {
             for (int i = nb * 32; i < D; i += 4) {

@@ -47,8 +47,22 @@ namespace wv {
 // fragments' LDS reads cost 0.35 ms of a 2.66 ms 1M x 10k pass).  The stage
 // barrier sits before the first half (A) of a group's last tile: the next
 // group's first tile is then landed when A prefetches it.
+// the keys min_steps (below) folds at k-steps 0 .. ns - 1: 0-2 at k = 0, 2k+1
+// and 2k+2 at k = 1 .. 6, the rest at k = ns - 1
+constexpr bool min_steps_cover(int ns) {
+    unsigned m = 0;
+    for (int k = 0; k < ns; ++k) {
+        if (k == 0) m |= 7u;
+        else if (k <= 6) m |= 3u << (2 * k + 1);
+        if (k == ns - 1)
+            for (int r = ns <= 7 ? 2 * ns + 1 : 15; r < 16; ++r) m |= 1u << r;
+    }
+    return m == 0xFFFFu;
+}
+
 template <int NS, bool L2, bool SEED, bool XS = false>
 __global__ __launch_bounds__(512, 1) void wv_bf_h16_kernel(H16Params p) {
+    static_assert(min_steps_cover(NS), "the spread tile minima must cover all 16 keys of a half");
     constexpr int WAVES = 8, TPS = H_TPS8;
     constexpr int BQ = WAVES * 64;
     constexpr int NSTG = H_STAGES;
@@ -225,8 +239,10 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16_kernel(H16Params p) {
 #else
                 if (k + 2 < NS) a[(k + 2) % 3] = img[(rb * NS + k + 2) * 64 + lane];
 #endif
-                if (k == NS - 2) head(nimg, nrb);   // (unconditional: a branch here would make every
-                                                    // later wait drain these reads too)
+                // (unconditional: a branch here would make every later wait
+                // drain these reads too; with one k-step at k = 0, after the
+                // copies above)
+                if (k == (NS >= 2 ? NS - 2 : 0)) head(nimg, nrb);
                 const half8 ak = __builtin_bit_cast(half8, a[k % 3]);
                 accA = __builtin_amdgcn_mfma_f32_32x32x16_f16(ak, __builtin_bit_cast(half8, bq0[k]), k == 0 ? xc : accA,
                                                               0, 0, 0);
@@ -248,9 +264,11 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16_kernel(H16Params p) {
                 else if (k == 4) { mA = fminf(fminf(mA, A[9]), A[10]); mB = fminf(fminf(mB, B[9]), B[10]); }
                 else if (k == 5) { mA = fminf(fminf(mA, A[11]), A[12]); mB = fminf(fminf(mB, B[11]), B[12]); }
                 else if (k == 6) { mA = fminf(fminf(mA, A[13]), A[14]); mB = fminf(fminf(mB, B[13]), B[14]); }
-                if (k == NS - 1) {   // (the remaining keys at the last k-step)
+                if (k == NS - 1) {   // (the remaining keys at the last k-step: those after
+                                     // key 2 NS when the steps above ran to k = NS - 1, key 15 when
+                                     // they stopped at k = 6)
 #pragma unroll
-                    for (int r = 2 * NS + 1; r < 16; ++r) { mA = fminf(mA, A[r]); mB = fminf(mB, B[r]); }
+                    for (int r = NS <= 7 ? 2 * NS + 1 : 15; r < 16; ++r) { mA = fminf(mA, A[r]); mB = fminf(mB, B[r]); }
                 }
             };
         };

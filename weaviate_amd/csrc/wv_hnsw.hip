@@ -37,6 +37,40 @@ namespace wv {
 
 constexpr int BATCH = 128;
 constexpr int MAX_LOCAL_TOMB = 4;
+// rows per 8-lane group in one distance round trip (exact_dist_rows)
+#ifndef WV_HNSW_RPG
+#define WV_HNSW_RPG 4
+#endif
+
+// Diagnostic build only (-DWV_HNSW_STAMPS, tools/hnsw_latency.sh): per-phase
+// shader-clock cycles of the expansion loop, summed over the queries of a
+// launch -- pop, neighbour-id/level load, visited filter, distances, merge --
+// plus the whole query's cycles and wall ticks (100 MHz).  Empty otherwise.
+struct Stamps {
+#ifdef WV_HNSW_STAMPS
+    uint64_t acc[5] = {0, 0, 0, 0, 0};
+    uint64_t t = 0;
+    __device__ __forceinline__ void start() { t = __builtin_amdgcn_s_memtime(); }
+    __device__ __forceinline__ void lap(int i) {
+        const uint64_t n = __builtin_amdgcn_s_memtime();
+        acc[i] += n - t;
+        t = n;
+    }
+#else
+    __device__ __forceinline__ void start() {}
+    __device__ __forceinline__ void lap(int) {}
+#endif
+};
+#ifdef WV_HNSW_STAMPS
+__device__ unsigned long long wv_hnsw_stamps[16];
+extern "C" void wv_hnsw_stamps_read(unsigned long long* out, int reset) {
+    (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(wv_hnsw_stamps), sizeof(wv_hnsw_stamps));
+    if (reset) {
+        unsigned long long z[16] = {};
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(wv_hnsw_stamps), z, sizeof(z));
+    }
+}
+#endif
 
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -77,7 +111,7 @@ __device__ __forceinline__ int lower_bound(const float* ad, const uint32_t* ai, 
 template <int METRIC, bool PQ = false>
 __device__ __forceinline__ void search_layer(const HnswParams& p, WaveState& w_io, int level, int ef, uint32_t ep,
                              float epd, const uint64_t* allow, int& Rl_out, int& Sh_out, int& Sl_out, int& status,
-                             int nlt, uint32_t& n_dist, uint32_t& n_exp) {
+                             int nlt, uint32_t& n_dist, uint32_t& n_exp, Stamps& ts) {
     // the state lives in registers for the whole layer (LDS pointers and the
     // R / S lengths are wave-uniform); written back once at the end
     WaveState w = w_io;
@@ -112,6 +146,7 @@ __device__ __forceinline__ void search_layer(const HnswParams& p, WaveState& w_i
 
     const uint32_t* nbr_base;
     int deg;
+    ts.start();
     for (;;) {
         // A full side set or expanded-set table makes the state inexact (an
         // expanded side candidate that X cannot record would be re-inserted
@@ -152,6 +187,7 @@ __device__ __forceinline__ void search_layer(const HnswParams& p, WaveState& w_i
             status = __shfl(status, 0, 64);
         }
         wave_sync();
+        ts.lap(0);
         // :217-234 nil node / level check.  Every layer-0 row exists (nil
         // nodes hold pads), so there the first neighbour ids are fetched in
         // the same memory round trip as the level.
@@ -169,6 +205,7 @@ __device__ __forceinline__ void search_layer(const HnswParams& p, WaveState& w_i
             deg = p.degU;
         }
         n_exp++;
+        ts.lap(1);
 
         for (int c0 = 0; c0 < deg; c0 += BATCH) {
             // ---- neighbour ids, visited-cache filter, compaction ----
@@ -195,6 +232,7 @@ __device__ __forceinline__ void search_layer(const HnswParams& p, WaveState& w_i
             if (v0) w.Bi[mbcnt64(m0)] = id0;
             if (v1) w.Bi[n0 + mbcnt64(m1)] = id1;
             wave_sync();
+            ts.lap(2);
             if (nb == 0) continue;
 
             // ---- exact distances, 8 lanes per row (search.go:265-271); on a
@@ -203,11 +241,13 @@ __device__ __forceinline__ void search_layer(const HnswParams& p, WaveState& w_i
                 for (int base = 0; base < nb; base += 64)
                     if (base + lane < nb) w.Bd[base + lane] = pq_dist_row<METRIC>(w.qv, p.pq, w.Bi[base + lane]);
             } else {
-                for (int base = 0; base < nb; base += 32)
-                    exact_dist_rows32<METRIC>(w.qv, p.X, p.ldx, p.D, w.Bi + base, nb - base, w.Bd + base, lane);
+                for (int base = 0; base < nb; base += 8 * WV_HNSW_RPG)
+                    exact_dist_rows<METRIC, WV_HNSW_RPG>(w.qv, p.X, p.ldx, p.D, w.Bi + base, nb - base, w.Bd + base,
+                                                         lane);
             }
             n_dist += nb;
             wave_sync();
+            ts.lap(3);
 
             // ---- keep test + dedupe (lanes hold batch slots lane, lane+64) ----
             // Only a neighbour the reference pushes into the candidate heap
@@ -252,6 +292,7 @@ __device__ __forceinline__ void search_layer(const HnswParams& p, WaveState& w_i
             const int ns = __popcll(ms0) + __popcll(ms1);
             if (ne + ns == 0) {
                 wave_sync();
+                ts.lap(4);
                 continue;
             }
             // compact the kept keys into the (consumed) raw batch: eligible
@@ -332,12 +373,194 @@ __device__ __forceinline__ void search_layer(const HnswParams& p, WaveState& w_i
                 Sl = newSl;
             }
             wave_sync();
+            ts.lap(4);
         }
     }
     Rl_out = Rl;
     Sh_out = Sh;
     Sl_out = Sl;
     w_io = w;
+}
+
+
+// wave-wide shift by one lane toward higher lanes (lane 0 keeps its value)
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x138, 0xF, 0xF, false);
+}
+__device__ __forceinline__ float wave_shr1(float v) { return __uint_as_float(wave_shr1(__float_as_uint(v))); }
+
+// The unfiltered search with ef <= 64 (no allow list, tombstones or nil nodes:
+// every node is eligible, so S stays empty): the results R live in registers,
+// entry i in lane i (distance rd, id ri, WV_FLAG once expanded).  The pop is a
+// ballot; a neighbour that passes the keep test (d < worst || |R| < ef,
+// search.go:282) is inserted by one ballot (its rank), a duplicate check on
+// the entry at that rank and a one-lane DPP shift of the tail.  Inserting the
+// kept neighbours one by one ends in the same R as the LDS path's sorted batch
+// merge (the ef smallest keys of R and the kept neighbours, duplicates once),
+// so the expansion order and the results are the same, bit for bit.
+template <int METRIC, bool PQ>
+__device__ __forceinline__ void search_layer_reg(const HnswParams& p, WaveState& w, int level, int ef, uint32_t ep,
+                                                 float epd, float& rd, uint32_t& ri, int& Rl, uint32_t& n_dist,
+                                                 uint32_t& n_exp, Stamps& ts) {
+    const int lane = threadIdx.x & 63;
+    const int VC = 1 << p.vc_log2;
+    for (int i = lane; i < VC; i += 64) w.vc[i] = WV_NIL;
+    wave_sync();
+    if (lane == 0) w.vc[hash32(ep) >> (32 - p.vc_log2)] = ep;
+    rd = lane == 0 ? epd : FLT_MAX;
+    ri = lane == 0 ? ep : WV_NIL;
+    Rl = 1;
+    float worst = epd;
+    wave_sync();
+    const uint32_t* nbr_base;
+    int deg;
+    ts.start();
+    for (;;) {
+        // ---- pop the best unexpanded result ----
+        const uint64_t um = __ballot(lane < Rl && !(ri & WV_FLAG));
+        if (!um) break;
+        const int ridx = __builtin_ctzll(um);
+        const float cd = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(rd), ridx));
+        const uint32_t cid = (uint32_t)__builtin_amdgcn_readlane(ri, ridx) & WV_IDMASK;
+        if (cd > worst) break;   // :213-215
+        if (lane == ridx) ri |= WV_FLAG;
+        ts.lap(0);
+        uint32_t pre0 = WV_NIL, pre1 = WV_NIL;
+        if (level == 0) {
+            nbr_base = p.layer0 + (uint64_t)cid * p.deg0;
+            deg = p.deg0;
+            if (lane < deg) pre0 = nbr_base[lane];
+            if (64 + lane < deg) pre1 = nbr_base[64 + lane];
+            if (p.levels[cid] < 0) continue;
+        } else {
+            if (p.levels[cid] < level) continue;
+            const uint32_t row = p.upper_row[cid];
+            nbr_base = p.upper + ((uint64_t)row * p.upper_levels + (level - 1)) * p.degU;
+            deg = p.degU;
+        }
+        n_exp++;
+        ts.lap(1);
+        for (int c0 = 0; c0 < deg; c0 += BATCH) {
+            uint32_t id0 = WV_NIL, id1 = WV_NIL;
+            if (level == 0 && c0 == 0) {
+                id0 = pre0;
+                id1 = pre1;
+            } else {
+                if (c0 + lane < deg) id0 = nbr_base[c0 + lane];
+                if (c0 + 64 + lane < deg) id1 = nbr_base[c0 + 64 + lane];
+            }
+            bool v0 = id0 != WV_NIL && id0 < p.N;
+            bool v1 = id1 != WV_NIL && id1 < p.N;
+            const uint32_t h0 = v0 ? hash32(id0) >> (32 - p.vc_log2) : 0;
+            const uint32_t h1 = v1 ? hash32(id1) >> (32 - p.vc_log2) : 0;
+            if (v0 && w.vc[h0] == id0) v0 = false;
+            if (v1 && w.vc[h1] == id1) v1 = false;
+            wave_sync();
+            if (v0) w.vc[h0] = id0;
+            if (v1) w.vc[h1] = id1;
+            const uint64_t m0 = __ballot(v0), m1 = __ballot(v1);
+            const int n0 = __popcll(m0);
+            const int nb = n0 + __popcll(m1);
+            if (v0) w.Bi[mbcnt64(m0)] = id0;
+            if (v1) w.Bi[n0 + mbcnt64(m1)] = id1;
+            wave_sync();
+            ts.lap(2);
+            if (nb == 0) continue;
+            if (PQ) {
+                for (int base = 0; base < nb; base += 64)
+                    if (base + lane < nb) w.Bd[base + lane] = pq_dist_row<METRIC>(w.qv, p.pq, w.Bi[base + lane]);
+            } else {
+                for (int base = 0; base < nb; base += 8 * WV_HNSW_RPG)
+                    exact_dist_rows<METRIC, WV_HNSW_RPG>(w.qv, p.X, p.ldx, p.D, w.Bi + base, nb - base, w.Bd + base,
+                                                         lane);
+            }
+            n_dist += nb;
+            wave_sync();
+            ts.lap(3);
+            // ---- keep test against the batch's starting R (as the LDS path's
+            // merge), then one insertion per kept neighbour, in batch order; a
+            // kept key ranked past ef falls out like the merge's tail ----
+            float bd[2];
+            uint32_t bi[2];
+            uint64_t kmask[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int e = lane + 64 * h;
+                bd[h] = e < nb ? w.Bd[e] : FLT_MAX;
+                bi[h] = e < nb ? w.Bi[e] : WV_NIL;
+                kmask[h] = __ballot(e < nb && (bd[h] < worst || Rl < ef));
+            }
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                uint64_t km = kmask[h];
+                while (km) {
+                    const int src = __builtin_ctzll(km);
+                    km &= km - 1;
+                    const float d = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(bd[h]), src));
+                    const uint32_t id = (uint32_t)__builtin_amdgcn_readlane(bi[h], src);
+                    const int pos = __popcll(__ballot(lane < Rl && key_less(rd, ri & WV_IDMASK, d, id)));
+                    if (pos >= ef) continue;
+                    if (pos < Rl && __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(rd), pos)) == d &&
+                        ((uint32_t)__builtin_amdgcn_readlane(ri, pos) & WV_IDMASK) == id)
+                        continue;   // already a result (a neighbour the visited cache forgot)
+                    const float sd = wave_shr1(rd);
+                    const uint32_t si = wave_shr1(ri);
+                    if (lane > pos) { rd = sd; ri = si; }
+                    if (lane == pos) { rd = d; ri = id; }
+                    Rl = min(Rl + 1, ef);
+                    worst = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(rd), Rl - 1));
+                }
+            }
+            ts.lap(4);
+        }
+    }
+}
+
+template <int METRIC, bool PQ>
+__device__ __forceinline__ void knn_one_reg(const HnswParams& p, WaveState& w, int q) {
+    const int lane = threadIdx.x & 63;
+    const int g = lane & 7;
+    for (int i = lane; i < p.dpad; i += 64) w.qv[i] = i < p.D ? p.Q[(uint64_t)q * p.ldq + i] : 0.f;
+    wave_sync();
+    uint32_t n_dist = 0, n_exp = 0;
+    Stamps ts;
+#ifdef WV_HNSW_STAMPS
+    const uint64_t c0 = __builtin_amdgcn_s_memtime(), w0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    uint32_t ep = p.entrypoint;
+    float epd = PQ ? pq_dist_row<METRIC>(w.qv, p.pq, ep)
+                   : exact_dist_group8<METRIC>(w.qv, p.X + (uint64_t)ep * p.ldx, p.D, g);
+    epd = __shfl(epd, 0, 64);
+    n_dist++;
+    float rd;
+    uint32_t ri;
+    int Rl;
+    for (int level = p.max_level; level >= 1; --level) {
+        search_layer_reg<METRIC, PQ>(p, w, level, 1, ep, epd, rd, ri, Rl, n_dist, n_exp, ts);
+        // (no nil nodes on this path: the closest result is the next entry)
+        ep = (uint32_t)__builtin_amdgcn_readlane(ri, 0) & WV_IDMASK;
+        epd = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(rd), 0));
+    }
+    search_layer_reg<METRIC, PQ>(p, w, 0, p.ef, ep, epd, rd, ri, Rl, n_dist, n_exp, ts);
+    const int n = min(Rl, p.k);
+    if (lane < n) {
+        p.out_ids[(uint64_t)q * p.k + lane] = p.id_base + (ri & WV_IDMASK);
+        p.out_d[(uint64_t)q * p.k + lane] = rd;
+    }
+    if (lane == 0) {
+        p.out_n[q] = n;
+        p.status[q] = 0;
+        if (p.counters) { p.counters[2 * q] = n_dist; p.counters[2 * q + 1] = n_exp; }
+#ifdef WV_HNSW_STAMPS
+        const uint64_t c1 = __builtin_amdgcn_s_memtime(), w1 = __builtin_amdgcn_s_memrealtime();
+        for (int i = 0; i < 5; ++i) atomicAdd(&wv_hnsw_stamps[i], (unsigned long long)ts.acc[i]);
+        atomicAdd(&wv_hnsw_stamps[5], (unsigned long long)(c1 - c0));
+        atomicAdd(&wv_hnsw_stamps[6], (unsigned long long)(w1 - w0));
+        atomicAdd(&wv_hnsw_stamps[7], (unsigned long long)n_exp);
+        atomicAdd(&wv_hnsw_stamps[8], 1ull);
+        atomicAdd(&wv_hnsw_stamps[9], (unsigned long long)n_dist);
+#endif
+    }
 }
 
 template <int METRIC, bool PQ>
@@ -351,6 +574,10 @@ __device__ __forceinline__ void knn_one(const HnswParams& p, WaveState& w, int q
     int status = 0;
     uint32_t n_dist = 0, n_exp = 0;
     int nlt = 0;
+    Stamps ts;
+#ifdef WV_HNSW_STAMPS
+    const uint64_t c0 = __builtin_amdgcn_s_memtime(), w0 = __builtin_amdgcn_s_memrealtime();
+#endif
 
     // entry point distance (search.go:467-476)
     uint32_t ep = p.entrypoint;
@@ -361,7 +588,7 @@ __device__ __forceinline__ void knn_one(const HnswParams& p, WaveState& w, int q
     int Rl, Sh, Sl;
     // greedy descent, levels max..1 with ef = 1 (:479-521)
     for (int level = p.max_level; level >= 1; --level) {
-        search_layer<METRIC, PQ>(p, w, level, 1, ep, epd, nullptr, Rl, Sh, Sl, status, nlt, n_dist, n_exp);
+        search_layer<METRIC, PQ>(p, w, level, 1, ep, epd, nullptr, Rl, Sh, Sl, status, nlt, n_dist, n_exp, ts);
         if (Rl > 0) {
             const uint32_t cid = w.Ri[0] & WV_IDMASK;
             if (p.levels[cid] < 0) {
@@ -378,7 +605,7 @@ __device__ __forceinline__ void knn_one(const HnswParams& p, WaveState& w, int q
         }
     }
     // layer 0 with ef and the allow list (:523-528)
-    search_layer<METRIC, PQ>(p, w, 0, p.ef, ep, epd, allow, Rl, Sh, Sl, status, nlt, n_dist, n_exp);
+    search_layer<METRIC, PQ>(p, w, 0, p.ef, ep, epd, allow, Rl, Sh, Sl, status, nlt, n_dist, n_exp, ts);
     const int n = min(Rl, p.k);
     for (int i = lane; i < n; i += 64) {
         p.out_ids[(uint64_t)q * p.k + i] = p.id_base + (w.Ri[i] & WV_IDMASK);
@@ -388,13 +615,22 @@ __device__ __forceinline__ void knn_one(const HnswParams& p, WaveState& w, int q
         p.out_n[q] = n;
         p.status[q] = status;
         if (p.counters) { p.counters[2 * q] = n_dist; p.counters[2 * q + 1] = n_exp; }
+#ifdef WV_HNSW_STAMPS
+        const uint64_t c1 = __builtin_amdgcn_s_memtime(), w1 = __builtin_amdgcn_s_memrealtime();
+        for (int i = 0; i < 5; ++i) atomicAdd(&wv_hnsw_stamps[i], (unsigned long long)ts.acc[i]);
+        atomicAdd(&wv_hnsw_stamps[5], (unsigned long long)(c1 - c0));
+        atomicAdd(&wv_hnsw_stamps[6], (unsigned long long)(w1 - w0));
+        atomicAdd(&wv_hnsw_stamps[7], (unsigned long long)n_exp);
+        atomicAdd(&wv_hnsw_stamps[8], 1ull);
+        atomicAdd(&wv_hnsw_stamps[9], (unsigned long long)n_dist);
+#endif
     }
 }
 
-// One instantiation per (metric, raw / PQ): each gets its own register
-// allocation (one kernel holding all six inlined searches spilled 431 SGPRs
-// into VGPR lanes); the host launches the matching one.
-template <int METRIC, bool PQ>
+// One instantiation per (metric, raw / PQ, register / LDS results): each gets
+// its own register allocation (one kernel holding all six inlined searches
+// spilled 431 SGPRs into VGPR lanes); the host launches the matching one.
+template <int METRIC, bool PQ, bool REG>
 __global__ __launch_bounds__(256) void wv_hnsw_kernel(HnswParams p) {
     extern __shared__ float lds[];
     const int wave = threadIdx.x >> 6;
@@ -413,7 +649,8 @@ __global__ __launch_bounds__(256) void wv_hnsw_kernel(HnswParams p) {
     w.vc = reinterpret_cast<uint32_t*>(cur); cur += (1 << p.vc_log2);
     w.xs = reinterpret_cast<uint32_t*>(cur); cur += (1 << p.xs_log2);
     w.ltomb = reinterpret_cast<uint32_t*>(cur); cur += MAX_LOCAL_TOMB;
-    knn_one<METRIC, PQ>(p, w, q);
+    if constexpr (REG) knn_one_reg<METRIC, PQ>(p, w, q);
+    else knn_one<METRIC, PQ>(p, w, q);
 }
 
 // ===========================================================================
@@ -438,6 +675,7 @@ __global__ __launch_bounds__(256) void wv_hnsw_kernel(HnswParams p) {
 
 template <int METRIC>
 __device__ void build_search_one(const BuildParams& b, WaveState& w, int slot) {
+    Stamps ts;   // (not sampled in the build)
     const HnswParams& p = b.h;
     const int lane = threadIdx.x & 63;
     const int g = lane & 7;
@@ -451,11 +689,11 @@ __device__ void build_search_one(const BuildParams& b, WaveState& w, int slot) {
     float epd = __shfl(exact_dist_group8<METRIC>(w.qv, p.X + (uint64_t)ep * p.ldx, p.D, g), 0, 64);
     int Rl, Sh, Sl;
     for (int level = p.max_level; level > target; --level) {
-        search_layer<METRIC>(p, w, level, 1, ep, epd, nullptr, Rl, Sh, Sl, status, nlt, n_dist, n_exp);
+        search_layer<METRIC>(p, w, level, 1, ep, epd, nullptr, Rl, Sh, Sl, status, nlt, n_dist, n_exp, ts);
         if (Rl > 0) { ep = w.Ri[0] & WV_IDMASK; epd = w.Rd[0]; }
     }
     for (int level = min(target, p.max_level); level >= 0; --level) {
-        search_layer<METRIC>(p, w, level, p.ef, ep, epd, nullptr, Rl, Sh, Sl, status, nlt, n_dist, n_exp);
+        search_layer<METRIC>(p, w, level, p.ef, ep, epd, nullptr, Rl, Sh, Sl, status, nlt, n_dist, n_exp, ts);
         const uint64_t o = ((uint64_t)slot * b.lb + level) * p.ef;
         for (int i = lane; i < Rl; i += 64) {
             b.cand_i[o + i] = w.Ri[i] & WV_IDMASK;
@@ -687,8 +925,15 @@ hipError_t wv_launch_hnsw(const wv::HnswParams* p, int waves_per_block, hipStrea
     const size_t lds = (size_t)waves_per_block * p->per_wave_words * sizeof(float);
     const unsigned blocks = (unsigned)((p->nq + waves_per_block - 1) / waves_per_block);
     if (blocks == 0) return hipSuccess;
-#define WV_HNSW_LAUNCH(M, PQ) \
-    hipLaunchKernelGGL((wv::wv_hnsw_kernel<M, PQ>), dim3(blocks), dim3(64 * waves_per_block), lds, s, *p)
+    // results in registers: unfiltered (no side set) with ef <= 64
+    const bool reg = p->sc == 0 && p->efc == 64 && !p->allow;
+#define WV_HNSW_LAUNCH(M, PQ)                                                                                     \
+    do {                                                                                                          \
+        if (reg) hipLaunchKernelGGL((wv::wv_hnsw_kernel<M, PQ, true>), dim3(blocks), dim3(64 * waves_per_block), \
+                                    lds, s, *p);                                                                  \
+        else hipLaunchKernelGGL((wv::wv_hnsw_kernel<M, PQ, false>), dim3(blocks), dim3(64 * waves_per_block),    \
+                                lds, s, *p);                                                                      \
+    } while (0)
     // a compressed index (PQ codes) is its own instantiation: the raw-vector
     // kernel keeps its registers and schedule
     if (p->pq.codes) {

@@ -535,7 +535,7 @@ int wv_mirror_create(int metric, const wv_config* cfg, const wv_mirror_options* 
     if (opt) m->opt = *opt;
     if (m->opt.initial_capacity == 0) m->opt.initial_capacity = kInitialSize;
     if (m->opt.max_batch <= 0) m->opt.max_batch = 1024;
-    if (m->opt.max_wait_us <= 0) m->opt.max_wait_us = 200;
+    if (m->opt.max_wait_us < 0) m->opt.max_wait_us = 0;
     if (m->opt.compact_rows == 0) m->opt.compact_rows = 8192;
     if (m->opt.ef_construction <= 0) m->opt.ef_construction = 128;
     if (m->opt.resync_backoff_ms <= 0) m->opt.resync_backoff_ms = 1000;
