@@ -21,12 +21,18 @@
 // at a time, and a free worker takes EVERY request queued meanwhile the moment
 // the device is free -- a lone request on an idle device launches at once, and
 // under load the batch size follows the arrival rate times one batch's device
-// time.  max_wait_us is an optional linger for an idle device (the oldest
-// request waits at most that long for company; 0 = none).  Two workers: while
-// one fans a finished batch's rows back out, the other is already launching
-// the next.  Each caller sleeps on its own condition variable and is woken
-// alone when its row is written (no broadcast to every waiting caller); the
-// workers' staging buffers live as long as the batcher (no per-batch heap
+// time.  Right after a batch of n finished, its callers resubmit as they wake:
+// the next batch waits for n queued requests, or refill_us(n) past the
+// batch's end, whichever comes first -- otherwise the first caller to return would be
+// launched alone and the rest would queue behind it, two half batches taking
+// turns (each caller then waits two device times).  max_wait_us is an
+// optional linger for an idle device (the oldest request waits at most that
+// long for company; 0 = none).  Two workers: while one fans a finished batch's
+// rows back out, the other is already launching the next.  Each caller sleeps
+// on its own condition variable and is woken alone when its row is written;
+// the wakeups run as 8 chains (the worker wakes the heads, every woken caller
+// the next of its chain), so a batch of n pays n/8 sequential wakeups, not n.
+// The workers' staging buffers live as long as the batcher (no per-batch heap
 // allocation once they have grown to max_batch).
 #include <algorithm>
 #include <chrono>
@@ -69,12 +75,25 @@ struct Request {
     int rc = WV_OK;
     std::string err;
     wait_clock::time_point arrived;
-    // the caller's own wakeup: set and notified under m by the worker, which
-    // touches nothing of the request after releasing m
+    // the caller's own wakeup: set and notified under m by its waker (the
+    // worker, or the previous caller of its chain), which touches nothing of
+    // the request after releasing m
     std::mutex m;
     std::condition_variable cv;
     bool done = false;
+    Request* chain_next = nullptr;   // the caller this one wakes once it is woken
 };
+
+void wake(Request* r) {
+    std::lock_guard<std::mutex> g(r->m);
+    r->done = true;
+    r->cv.notify_one();
+}
+
+constexpr int WAKE_CHAINS = 8;
+// how long the next batch waits for the last one's callers: a base plus a
+// share per caller (the wakeup chains' hops), capped
+int refill_us(int n) { return std::min(300, 50 + n); }
 
 // one worker's staging, reused batch after batch
 struct Staging {
@@ -98,6 +117,11 @@ struct wv_batcher {
     std::deque<Request*> queue;
     bool stop = false;
     bool device_busy = false;      // a worker holds the device (one batch at a time)
+    wait_clock::time_point idle_since{};   // when the last batch finished
+    int expect = 0;                        // its size: the callers about to resubmit
+    // a worker waiting for company (refill or linger) wants this many queued:
+    // submitters wake it only then (0: any submit at an idle device wakes)
+    int wake_at = 0;
     std::vector<std::thread> th;   // the workers
     Staging st[2];
     uint64_t n_requests = 0, n_batches = 0, n_launch_rows = 0;
@@ -152,10 +176,11 @@ struct wv_batcher {
                                      s.ds.data(), s.cnt.data());
     }
 
-    // each caller's row, then its own wakeup
+    // every caller's row, then the heads of the wakeup chains
     static void fan_out(Staging& s, int rc, const std::string& msg) {
         const int k = s.g[0]->k;
-        for (size_t i = 0; i < s.g.size(); ++i) {
+        const size_t n = s.g.size();
+        for (size_t i = 0; i < n; ++i) {
             Request* r = s.g[i];
             r->rc = rc;
             if (rc) {
@@ -166,10 +191,9 @@ struct wv_batcher {
                 std::memcpy(r->out_d, s.ds.data() + i * k, sizeof(float) * m);
                 *r->out_n = m;
             }
-            std::lock_guard<std::mutex> g(r->m);
-            r->done = true;
-            r->cv.notify_one();
+            r->chain_next = i + WAKE_CHAINS < n ? s.g[i + WAKE_CHAINS] : nullptr;
         }
+        for (size_t i = 0; i < n && i < (size_t)WAKE_CHAINS; ++i) wake(s.g[i]);
     }
 
     void loop(Staging& s) {
@@ -177,10 +201,24 @@ struct wv_batcher {
         for (;;) {
             cv_work.wait(l, [&] { return (!queue.empty() && !device_busy) || (stop && queue.empty()); });
             if (queue.empty()) return;   // (stop)
+            const int want = std::min(expect, max_batch);
+            if (!stop && (int)queue.size() < want) {
+                // the finished batch's callers are still resubmitting
+                const auto deadline = idle_since + std::chrono::microseconds(refill_us(want));
+                if (wait_clock::now() < deadline) {
+                    wake_at = want;
+                    cv_work.wait_until(l, deadline,
+                                       [&] { return stop || device_busy || (int)queue.size() >= want; });
+                    wake_at = 0;
+                }
+                if (device_busy || queue.empty()) continue;   // (the other worker took them)
+            }
             if (max_wait_us > 0 && (int)queue.size() < max_batch && !stop) {
                 // linger at an idle device: until max_batch or the oldest request's deadline
                 const auto deadline = queue.front()->arrived + std::chrono::microseconds(max_wait_us);
+                wake_at = max_batch;
                 cv_work.wait_until(l, deadline, [&] { return stop || (int)queue.size() >= max_batch; });
+                wake_at = 0;
                 if (device_busy || queue.empty()) continue;   // (the other worker took them)
             }
             device_busy = true;
@@ -210,6 +248,8 @@ struct wv_batcher {
                     // batch while this one wakes its callers
                     l.lock();
                     device_busy = false;
+                    idle_since = wait_clock::now();
+                    expect = (int)s.take.size();
                     n_batches++;
                     n_launch_rows += s.take.size();
                     l.unlock();
@@ -250,6 +290,7 @@ int wv_batcher_create_group(wv_group* g, int dim, int max_batch, int max_wait_us
 
 static int submit(wv_batcher* b, Request& r) {
     r.arrived = wait_clock::now();
+    bool notify = false;
     {
         std::lock_guard<std::mutex> l(b->mu);
         if (b->stop) {
@@ -258,12 +299,16 @@ static int submit(wv_batcher* b, Request& r) {
         }
         b->queue.push_back(&r);
         b->n_requests++;
+        // a busy device: the worker that frees it takes the queue; a worker
+        // waiting for company: only once the count it waits for is there
+        notify = !b->device_busy && (b->wake_at == 0 || (int)b->queue.size() >= b->wake_at);
     }
-    b->cv_work.notify_one();
+    if (notify) b->cv_work.notify_all();   // (two workers: whichever is free)
     {
         std::unique_lock<std::mutex> l(r.m);
         r.cv.wait(l, [&] { return r.done; });
     }
+    if (r.chain_next) wake(r.chain_next);
     if (r.rc) wv_internal_set_error(r.err.c_str());
     return r.rc;
 }

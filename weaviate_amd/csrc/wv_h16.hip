@@ -416,18 +416,27 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16_kernel(H16Params p) {
             }
         };
         // a half's candidates: the column minima against the thresholds, and
-        // (rare, wave-uniform) insertion by key position (wv_topk.h)
+        // (rare) insertion of the column minimum (wv_topk.h min_extract)
         auto extract_half = [&](float m0, float m1, floatx16& A, floatx16& B, uint32_t rb) -> bool {
 #ifdef WV_H16_ABLATE_NO_EXTRACT
             if (m0 == 1234.5f) l0d[0] = m1 + pt0 + pt1;
             return false;
 #endif
+#ifdef WV_H16_ABLATE_NO_EVENTS
+            // (ablation: the extraction code stays, no event ever fires)
+            float nev = -INF;
+            asm volatile("" : "+v"(nev));
+            const bool x0 = m0 <= fminf(fminf(l0d[BF_KP - 1], pt0), nev), x1 = m1 <= fminf(fminf(l1d[BF_KP - 1], pt1), nev);
+#else
             const bool x0 = m0 <= fminf(l0d[BF_KP - 1], pt0), x1 = m1 <= fminf(l1d[BF_KP - 1], pt1);
+#endif
             const bool any = __any(x0 || x1);
             if (__builtin_expect(any, 0)) {
                 WV_DBG_COUNT(3)
-                if (__any(x0)) ballot_extract(A, x0 ? fminf(l0d[BF_KP - 1], pt0) : -INF, l0d, l0i, rb);
-                if (__any(x1)) ballot_extract(B, x1 ? fminf(l1d[BF_KP - 1], pt1) : -INF, l1d, l1i, rb);
+                // (the smallest key by its position; the per-key scan only
+                // for a second key under the threshold: 2.645 -> 2.622 ms)
+                if (__any(x0)) min_extract(m0, x0, A, pt0, l0d, l0i, rb);
+                if (__any(x1)) min_extract(m1, x1, B, pt1, l1d, l1i, rb);
             }
             return any;
         };

@@ -159,6 +159,31 @@ __device__ __forceinline__ void ballot_extract(const floatx16& A, float thr, flo
     }
 }
 
+// A column whose smallest key m is under its threshold (x, per lane): m goes
+// in straight from its position (a select chain, no per-key branch); the
+// column's other keys are scanned only when one of them is also under the
+// lane's threshold after the insertion (rare).  The list ends as after
+// ballot_extract(A, thr): a key between the new and the old tail falls off
+// the list either way.  A's entry at m's position is cleared to +inf.
+__device__ __forceinline__ void min_extract(float m, bool x, floatx16& A, float pt, float (&ld)[BF_KP],
+                                            uint32_t (&li)[BF_KP], uint32_t rb) {
+    int pos = 15;
+#pragma unroll
+    for (int r = 14; r >= 0; --r) pos = A[r] == m ? r : pos;
+    uint32_t id = rb;   // opaque: the row ids stay in this rare path
+    asm volatile("" : "+v"(id));
+    if (x) list_insert(m, id + (uint32_t)((pos & 3) + 8 * (pos >> 2)), ld, li);
+    const float thr2 = x ? fminf(ld[BF_KP - 1], pt) : -__builtin_inff();
+    float m2 = __builtin_inff();
+#pragma unroll
+    for (int r = 0; r < 16; r += 2) {
+        A[r] = r == pos ? __builtin_inff() : A[r];
+        A[r + 1] = r + 1 == pos ? __builtin_inff() : A[r + 1];
+        m2 = fminf(fminf(m2, A[r]), A[r + 1]);
+    }
+    if (__builtin_expect(__any(m2 <= thr2), 0)) ballot_extract(A, thr2, ld, li, rb);
+}
+
 // Certificate eps of the f16 key pass (true units): |key + offset - reference
 // distance| <= eps for every row, offset = |q|^2 (L2), 0 (dot), 1 (cosine).
 // Accumulation and reference-order terms 6 (D + 4) 2^-24 (|q| + max|x|)^2
