@@ -329,20 +329,26 @@ def exact_roofline(args, ix, kern_ms, stats, D, n_allowed, n_local, NQ):
 def attach_traffic(roof, n_local, NQ, D, data):
     """roofline.traffic from a committed PMC summary -- only one collected from
     this build of the key pass (tools/build_hash.py) on the same shape"""
-    pmc = os.path.join(ROOT, "profiles", "pmc_%s.json" % roof["kernel"])
-    if os.path.exists(pmc):
+    import glob
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from build_hash import build_hash
+    want = build_hash(roof["kernel"])
+    # profiles/pmc_<kernel>.json and pmc_<kernel>_<shape>.json: the one of this shape
+    for pmc in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_%s*.json" % roof["kernel"]))):
         with open(pmc) as f:
             p = json.load(f)
-        sys.path.insert(0, os.path.join(ROOT, "tools"))
-        from build_hash import build_hash
+        if p.get("kernel") != roof["kernel"]:
+            continue
         same_shape = (p.get("N"), p.get("nq"), p.get("dim"), p.get("data", "uniform")) == (n_local, NQ, D, data)
-        if same_shape and p.get("build") == build_hash():
+        if same_shape and p.get("build") == want:
             roof["traffic"] = p.get("hbm_bytes_per_launch")
             roof["traffic_source"] = p.get("source", os.path.relpath(pmc, ROOT))
             for key in ("per_mfma", "effective_clock_ghz", "mfma_busy_frac", "wait_inst_frac"):
                 if key in p:
                     roof["pmc_" + key] = p[key]
-        elif same_shape:
+            roof.pop("traffic_note", None)
+            return
+        if same_shape:
             roof["traffic_note"] = "profiles/%s is from another build (%s); not attached" % (
                 os.path.basename(pmc), p.get("build"))
 
@@ -677,6 +683,23 @@ def run_hnsw(args, ctx, W, with_cpu):
         res["ef_sweep"] = sweep
     if args.concurrency and ws == 1:
         res["concurrent_callers"] = concurrent_callers(args, ix, queries)
+    if not with_cpu and getattr(args, "counts_sample", 0) > 0:
+        # SURVEY 8d's byte basis from the restatement's own evaluation counts
+        # on a query sample of this shard's graph (no CPU timing): the GPU's
+        # visited-cache re-evaluations are not counted as useful bytes
+        O = _oracle()
+        ref = O.Index(D, args.metric, args.M, args.efc, capacity=n_local, seed=1)
+        ref.import_graph(base, ix.download_graph())
+        ns_ = min(NQ, args.counts_sample)
+        ost = ref.search_batch(queries[:ns_], K, args.ef, threads=args.cpu_threads)[3]
+        e_q, x_q = ost["dist_evals"] / ns_, ost["expansions"] / ns_
+        by = (4.0 * D * e_q + 4.0 * 2 * args.M * x_q) * NQ
+        achieved = by / (hnsw_ms * 1e-3) / 1e9
+        res["roofline"].update({"achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4),
+                                "counts_from": f"CPU restatement (oracle/) on the same graph, {ns_}-query sample",
+                                "dist_evals_per_query": round(e_q, 1), "expansions_per_query": round(x_q, 1),
+                                "gpu_dist_evals_per_query": round(stats[-1]["dist_evals"] / NQ, 1)})
+        del ref
     if with_cpu:
         ref = O.Index(D, args.metric, args.M, args.efc, capacity=N, seed=1)
         ref.import_graph(base, ix.download_graph())   # the restatement searches the very same graph
@@ -1015,6 +1038,7 @@ def main():
             a5.rows, a5.dim, a5.metric, a5.hnsw_data = c5_rows, 96, "l2-squared", "sift"
             a5.ef, a5.ef_sweep, a5.concurrency, a5.split = 64, [128], [], "corpus"
             a5.graph_build, a5.dump_ids, a5.seq_build = "gpu", "", False
+            a5.counts_sample = 1000 if rank == 0 else 0
             try:
                 h = run_hnsw(a5, ctx, W, False)
                 h.pop("metric", None)

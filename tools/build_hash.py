@@ -7,11 +7,13 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SOURCES = ("wv_h16.hip", "wv_h16_dev.h", "wv_topk.h", "wv_api.hip", "wv_params.h", "wv_device.h")
+# the HNSW search kernel and its launch
+SOURCES_HNSW = ("wv_hnsw.hip", "wv_api.hip", "wv_params.h", "wv_device.h")
 
 
-def build_hash() -> str:
+def build_hash(kernel: str = "wv_bf_h16_kernel") -> str:
     h = hashlib.sha1()
-    for name in SOURCES:
+    for name in (SOURCES_HNSW if "hnsw" in kernel else SOURCES):
         with open(os.path.join(ROOT, "weaviate_amd", "csrc", name), "rb") as f:
             h.update(name.encode() + b"\0" + f.read())
     return h.hexdigest()[:16]
