@@ -903,8 +903,11 @@ def main():
     ap.add_argument("--seq-build", action="store_true",
                     help="hnsw at N=1: also build the restatement's insert-by-insert graph and report its recall "
                          "beside the GPU-built graph's (north_star's 0.5-pt criterion; ~40 s of CPU at 1M)")
+    ap.add_argument("--c5-fixed-corpus", action="store_true",
+                    help="N > 1: the configs[4] line shards a fixed 100M corpus (100M / N rows per GPU) instead of "
+                         "12.5M rows per GPU")
     ap.add_argument("--no-c5-line", action="store_true",
-                    help="skip the configs[4] line (100M x 96 sharded over N GPUs; one 12.5M shard at N = 1)")
+                    help="skip the configs[4] line (12.5M x 96 rows per GPU, sharded hnsw + RCCL merge)")
     ap.add_argument("--no-c3-line", action="store_true",
                     help="skip the configs[2] GloVe-shaped hnsw ef-sweep line reported beside the default value")
     ap.add_argument("--hnsw-build-threads", type=int, default=16)
@@ -1027,27 +1030,32 @@ def main():
             h.pop("metric", None)
             result["hnsw_c3"] = h
         if not args.no_c5_line and args.rows == 1_000_000 and args.metric == "l2-squared":
-            # configs[4] as configured: a fixed Deep/SIFT-shaped 100M x 96 corpus
-            # sharded by id range over the N GPUs (100M / N rows each), every
-            # GPU building and searching the graph of its shard, per-shard top-k
-            # all-gathered over RCCL and merged on the device (index.go:967-1044).
-            # At N = 1 the line is ONE shard of the 8-way layout (12.5M rows):
-            # the whole 100M corpus and its graph build exceed the bench's time.
+            # configs[4]'s layout: a Deep/SIFT-shaped 96-d corpus sharded by id
+            # range over the N GPUs, every GPU building and searching the graph
+            # of its shard, per-shard top-k all-gathered over RCCL and merged on
+            # the device (index.go:967-1044).  Default: 12.5M rows per GPU (the
+            # 100M corpus at N = 8, weak scaling below).  --c5-fixed-corpus
+            # shards a fixed 100M corpus (100M / N rows per GPU, strong
+            # scaling): the 50M-row shard graph of N = 2 takes > 185 s to build
+            # on one MI355X (12.5M: 17 s), too long for the default run.
             a5 = argparse.Namespace(**vars(args))
-            c5_rows = 100_000_000 if ws > 1 else 12_500_000
+            c5_fixed = args.c5_fixed_corpus and ws > 1
+            c5_rows = 100_000_000 if c5_fixed else 12_500_000 * ws
             a5.rows, a5.dim, a5.metric, a5.hnsw_data = c5_rows, 96, "l2-squared", "sift"
             a5.ef, a5.ef_sweep, a5.concurrency, a5.split = 64, [128], [], "corpus"
             a5.graph_build, a5.dump_ids, a5.seq_build = "gpu", "", False
-            a5.counts_sample = 1000 if rank == 0 else 0
+            a5.counts_sample = 1000 if ws == 1 else 0   # (N > 1: the 100M / N shards are large to restate)
             try:
                 h = run_hnsw(a5, ctx, W, False)
                 h.pop("metric", None)
-                if ws > 1:
+                if c5_fixed:
                     h["scaling"] = f"strong (fixed 100M-row corpus, {c5_rows // ws:,} rows per GPU)"
-                    h["value_units"] = f"queries/s over the whole {a5.rows:,}-row corpus (every rank searches the batch)"
+                elif ws > 1:
+                    h["scaling"] = "weak (12.5M rows per GPU; the 100M corpus at N = 8)"
                 else:
                     h["scaling"] = "one shard: 12.5M rows = the per-GPU share of 100M over 8 GPUs"
-                    h["value_units"] = "queries/s over one 12,500,000-row shard (not the 100M corpus)"
+                h["value_units"] = (f"queries/s over the whole {a5.rows:,}-row corpus (every rank searches the batch)"
+                                    if ws > 1 else "queries/s over one 12,500,000-row shard (not the 100M corpus)")
                 result["hnsw_c5_sharded"] = h
             except Exception as e:   # reported, not fatal to the headline line
                 result["hnsw_c5_sharded"] = {"error": f"{type(e).__name__}: {e}"}
