@@ -25,7 +25,7 @@ import pytest
 
 import pyoracle as O
 import weaviate_amd as W
-from bench import counter_gauss, counter_sift, counter_uniform
+from bench import counter_gauss, counter_glove, counter_sift, counter_uniform
 from helpers import merge_lists, recall, same, same_tie_aware, tie_aware_equal
 
 pytestmark = pytest.mark.gpu
@@ -98,13 +98,16 @@ def test_configs0_sift_hnsw_m64_efc128_ef64():
     ix.close()
 
 
-@pytest.mark.parametrize("ef", [128, 256])
+@pytest.mark.parametrize("ef", [64, 128, 256])
 def test_configs2_glove_cosine_d100_large_ef(ef):
     """configs[2]: 100-d cosine (stored rows normalized on upload, queries
-    per search), ef at the top of the sweep."""
+    per search) on the bench's GloVe-shaped generator (bench.py
+    counter_glove: Zipf-sized clusters in a 24-d latent family, full-rank
+    residual, log-normal norms), ef across the sweep: ids and distances as
+    the restatement's, and the recall operating point the bench reports."""
     n, d, nq, k = 20000, 100, 300, 10
-    base = counter_gauss(1, 0, n, d)
-    qs = counter_gauss(2, 0, nq, d)
+    base = counter_glove(1, 0, n, d)
+    qs = counter_glove(2, 0, nq, d)
     ref = O.Index(d, "cosine-dot", 32, 128, capacity=n, seed=2)
     ref.add_batch(base, threads=THREADS)
     ix = W.GPUVectorIndex(d, "cosine-dot", capacity=n, max_connections=32)
@@ -116,7 +119,9 @@ def test_configs2_glove_cosine_d100_large_ef(ef):
     assert not _unexplained(ref, qs, k, ef, gi, gd, oi, od)
     assert ix.last_batch_stats()["fallbacks"] == 0
     truth, _, _ = O.flat_scan(O.COSINE, O.normalize_rows(base), O.normalize_rows(qs), k, threads=THREADS)
-    assert abs(recall(gi, truth) - recall(oi, truth)) <= 0.005
+    r_gpu = recall(gi, truth)
+    assert abs(r_gpu - recall(oi, truth)) <= 0.005
+    assert r_gpu >= 0.9, r_gpu   # (an operating point: i.i.d. Gaussians had none)
     ix.close()
 
 
