@@ -902,7 +902,9 @@ def main():
                     help="N>1 exact: skip the corpus-sharded (RCCL merge) leg reported beside the query split")
     ap.add_argument("--seq-build", action="store_true",
                     help="hnsw at N=1: also build the restatement's insert-by-insert graph and report its recall "
-                         "beside the GPU-built graph's (north_star's 0.5-pt criterion; ~40 s of CPU at 1M)")
+                         "beside the GPU-built graph's (north_star's 0.5-pt criterion; ~40 s of CPU at 1M; on by "
+                         "default for the C1 line beside the exact value)")
+    ap.add_argument("--no-seq-build", action="store_true", help="skip the C1 line's sequential-build recall check")
     ap.add_argument("--c5-fixed-corpus", action="store_true",
                     help="N > 1: the configs[4] line shards a fixed 100M corpus (100M / N rows per GPU) instead of "
                          "12.5M rows per GPU")
@@ -1017,7 +1019,11 @@ def main():
         else:
             st["ix"].close()
         if not args.no_hnsw_line and args.metric == "l2-squared":
-            h = run_hnsw(args, ctx, W, with_cpu)
+            # (the C1 line at N = 1 also reports north_star's criterion: recall
+            # within 0.5 pt of the insert-by-insert graph; --no-seq-build skips it)
+            a1 = argparse.Namespace(**vars(args))
+            a1.seq_build = (args.seq_build or (not args.no_seq_build and args.rows == 1_000_000)) and ws == 1
+            h = run_hnsw(a1, ctx, W, with_cpu)
             h.pop("metric", None)
             result["hnsw_c1"] = h
         if not args.no_c3_line and ws == 1 and (args.rows, args.dim, args.metric) == (1_000_000, 128, "l2-squared"):
