@@ -86,9 +86,11 @@ __device__ __forceinline__ float exact_dist_group8(const float* __restrict__ q,
 
 // Exact reference-order distances of up to 8*RPG rows at once (RPG per 8-lane
 // group), all row loads of a 4-block (128-float) slab issued before any FMA so
-// one memory round trip serves 8*RPG rows.  ids/out live in LDS; rows >= n are
-// skipped.  Same arithmetic, in the same order, as exact_dist_group8.
-template <int METRIC, int RPG = 4>
+// one memory round trip serves 8*RPG rows; a tail of one float4 (D = 32 m + 4,
+// e.g. GloVe's 100) is loaded with the first slab instead of after it (it was
+// a second dependent round trip per call; HOIST_TAIL, 16 more VGPRs).  ids/out live in LDS; rows >= n
+// are skipped.  Same arithmetic, in the same order, as exact_dist_group8.
+template <int METRIC, int RPG = 4, bool HOIST_TAIL = false>
 __device__ __forceinline__ void exact_dist_rows(const float* __restrict__ q, const float* __restrict__ X,
                                                 int ldx, int D, const uint32_t* ids, int n, float* out,
                                                 int lane) {
@@ -105,6 +107,13 @@ __device__ __forceinline__ void exact_dist_rows(const float* __restrict__ q, con
     float a[RPG][4];
 #pragma unroll
     for (int j = 0; j < RPG; ++j) a[j][0] = a[j][1] = a[j][2] = a[j][3] = 0.f;
+    const bool tail1 = HOIST_TAIL && D - nb * 32 > 0 && D - nb * 32 <= 4;
+    float4 yt[RPG];
+    if (tail1) {
+#pragma unroll
+        for (int j = 0; j < RPG; ++j)
+            if (ok[j]) yt[j] = ld4(row[j] + nb * 32);
+    }
     for (int b0 = 0; b0 < nb; b0 += 4) {
         float4 y[RPG][4];
 #pragma unroll
@@ -141,7 +150,7 @@ __device__ __forceinline__ void exact_dist_rows(const float* __restrict__ q, con
         if (ok[j]) {
             for (int i = nb * 32; i < D; i += 4) {
                 const float4 x = ld4(q + i);
-                const float4 yy = ld4(row[j] + i);
+                const float4 yy = tail1 ? yt[j] : ld4(row[j] + i);
                 if (METRIC == WV_METRIC_L2) {
                     float d = x.x - yy.x; t = __builtin_fmaf(d, d, t);
                     d = x.y - yy.y;       t = __builtin_fmaf(d, d, t);

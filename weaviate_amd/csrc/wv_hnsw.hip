@@ -471,7 +471,7 @@ __device__ __forceinline__ void search_layer_reg(const HnswParams& p, WaveState&
                     if (base + lane < nb) w.Bd[base + lane] = pq_dist_row<METRIC>(w.qv, p.pq, w.Bi[base + lane]);
             } else {
                 for (int base = 0; base < nb; base += 8 * WV_HNSW_RPG)
-                    exact_dist_rows<METRIC, WV_HNSW_RPG>(w.qv, p.X, p.ldx, p.D, w.Bi + base, nb - base, w.Bd + base,
+                    exact_dist_rows<METRIC, WV_HNSW_RPG, true>(w.qv, p.X, p.ldx, p.D, w.Bi + base, nb - base, w.Bd + base,
                                                          lane);
             }
             n_dist += nb;
