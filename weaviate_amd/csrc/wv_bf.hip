@@ -633,7 +633,7 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void wv_bf_split_kernel(BfParams 
 // bitonic selection; otherwise per-lane top-KF runs and a KF-round merge
 // (separate instantiations: one kernel holding both needs 210 VGPRs)
 template <int METRIC, bool FAST>
-__device__ void finalize_one(const BfFinParams& p, int q, float* sd, uint32_t* si, float* qv) {
+__device__ __forceinline__ void finalize_one(const BfFinParams& p, int q, float* sd, uint32_t* si, float* qv) {
     const int lane = threadIdx.x & 63;
     const int n_lists = bf_slots_of((uint64_t)(q / p.bq), p.ntiles, p.units_per_block) * p.prod;
     const int kp = p.kp ? p.kp : BF_KP;   // entries per list
@@ -677,11 +677,11 @@ __device__ void finalize_one(const BfFinParams& p, int q, float* sd, uint32_t* s
 #pragma unroll
             for (int jj = k >> 1; jj > 0; jj >>= 1) {
                 if (jj >= 64) {
-                    const int m = jj >> 6;
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const int pj = j ^ m;
-                        if (pj <= j) continue;
+                    // (register pairs named by literal indices: a runtime
+                    // j ^ (jj / 64) made the arrays dynamically indexed, i.e.
+                    // 208 bytes of scratch per lane)
+                    auto cas = [&](auto jc, auto pc) {
+                        constexpr int j = decltype(jc)::value, pj = decltype(pc)::value;
                         const bool up = ((64 * j + lane) & k) == 0;   // element j is the lower index
                         const bool sw = up ? key_less(kd[pj], ki[pj], kd[j], ki[j]) : key_less(kd[j], ki[j], kd[pj], ki[pj]);
                         const float td = kd[j];
@@ -690,7 +690,13 @@ __device__ void finalize_one(const BfFinParams& p, int q, float* sd, uint32_t* s
                         ki[j] = sw ? ki[pj] : ki[j];
                         kd[pj] = sw ? td : kd[pj];
                         ki[pj] = sw ? ti : ki[pj];
-                    }
+                    };
+                    using I0 = std::integral_constant<int, 0>;
+                    using I1 = std::integral_constant<int, 1>;
+                    using I2 = std::integral_constant<int, 2>;
+                    using I3 = std::integral_constant<int, 3>;
+                    if (jj == 64) { cas(I0{}, I1{}); cas(I2{}, I3{}); }
+                    else { cas(I0{}, I2{}); cas(I1{}, I3{}); }
                 } else {
                     const bool lower = (lane & jj) == 0;
 #pragma unroll

@@ -674,7 +674,7 @@ __global__ __launch_bounds__(256) void wv_hnsw_kernel(HnswParams p) {
 // one before the batch); batches grow with the graph (a fixed fraction).
 
 template <int METRIC>
-__device__ void build_search_one(const BuildParams& b, WaveState& w, int slot) {
+__device__ __forceinline__ void build_search_one(const BuildParams& b, WaveState& w, int slot) {
     Stamps ts;   // (not sampled in the build)
     const HnswParams& p = b.h;
     const int lane = threadIdx.x & 63;
