@@ -783,7 +783,7 @@ __device__ __forceinline__ void finalize_one(const BfFinParams& p, int q, float*
         const int c = pass * 8 + grp;
         const uint32_t id = si[c];
         float d = FLT_MAX;
-        if (id != WV_NIL) d = exact_dist_group8<METRIC>(qv, p.X + (size_t)id * p.ldx, p.D, g);
+        if (id != WV_NIL) d = exact_dist_group8<METRIC, 8>(qv, p.X + (size_t)id * p.ldx, p.D, g);
         ex[pass] = d;
     }
     __builtin_amdgcn_wave_barrier();
@@ -994,7 +994,7 @@ __device__ void finalize_wide(const BfFinParams& p, int q, float* qv, float* sd,
         uint32_t id = WV_NIL;
         if (c < kf) {
             id = si[c];
-            d = exact_dist_group8<METRIC>(qv, p.X + (size_t)id * p.ldx, p.D, g);
+            d = exact_dist_group8<METRIC, 8>(qv, p.X + (size_t)id * p.ldx, p.D, g);
         }
         __syncthreads();
         if (c < kf && g == 0) sd[c] = d;
