@@ -389,26 +389,43 @@ __device__ __forceinline__ uint32_t wave_shr1(uint32_t v) {
 }
 __device__ __forceinline__ float wave_shr1(float v) { return __uint_as_float(wave_shr1(__float_as_uint(v))); }
 
-// The unfiltered search with ef <= 64 (no allow list, tombstones or nil nodes:
-// every node is eligible, so S stays empty): the results R live in registers,
-// entry i in lane i (distance rd, id ri, WV_FLAG once expanded).  The pop is a
-// ballot; a neighbour that passes the keep test (d < worst || |R| < ef,
-// search.go:282) is inserted by one ballot (its rank), a duplicate check on
-// the entry at that rank and a one-lane DPP shift of the tail.  Inserting the
+// The unfiltered search with ef <= 64 NR (no allow list, tombstones or nil
+// nodes: every node is eligible, so S stays empty): the results R live in
+// registers, entry i in lane i % 64 of register i / 64 (distance rd, id ri,
+// WV_FLAG once expanded).  The pop is a ballot; a neighbour that passes the
+// keep test (d < worst || |R| < ef, search.go:282) is inserted by one ballot
+// per register (its rank), a duplicate check on the entry at that rank and a
+// one-lane DPP shift of the tail (lane 63 of a register carried into lane 0
+// of the next).  Inserting the
 // kept neighbours one by one ends in the same R as the LDS path's sorted batch
 // merge (the ef smallest keys of R and the kept neighbours, duplicates once),
 // so the expansion order and the results are the same, bit for bit.
-template <int METRIC, bool PQ>
+template <int NR>
+__device__ __forceinline__ float reg_entry_d(const float (&rd)[NR], int e) {
+    if (NR == 1 || e < 64) return __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(rd[0]), e));
+    return __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(rd[NR - 1]), e - 64));
+}
+template <int NR>
+__device__ __forceinline__ uint32_t reg_entry_i(const uint32_t (&ri)[NR], int e) {
+    if (NR == 1 || e < 64) return (uint32_t)__builtin_amdgcn_readlane(ri[0], e);
+    return (uint32_t)__builtin_amdgcn_readlane(ri[NR - 1], e - 64);
+}
+
+template <int METRIC, bool PQ, int NR>
 __device__ __forceinline__ void search_layer_reg(const HnswParams& p, WaveState& w, int level, int ef, uint32_t ep,
-                                                 float epd, float& rd, uint32_t& ri, int& Rl, uint32_t& n_dist,
-                                                 uint32_t& n_exp, Stamps& ts) {
+                                                 float epd, float (&rd)[NR], uint32_t (&ri)[NR], int& Rl,
+                                                 uint32_t& n_dist, uint32_t& n_exp, Stamps& ts) {
+    static_assert(NR == 1 || NR == 2, "64 or 128 results per wave");
     const int lane = threadIdx.x & 63;
     const int VC = 1 << p.vc_log2;
     for (int i = lane; i < VC; i += 64) w.vc[i] = WV_NIL;
     wave_sync();
     if (lane == 0) w.vc[hash32(ep) >> (32 - p.vc_log2)] = ep;
-    rd = lane == 0 ? epd : FLT_MAX;
-    ri = lane == 0 ? ep : WV_NIL;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        rd[r] = lane == 0 && r == 0 ? epd : FLT_MAX;
+        ri[r] = lane == 0 && r == 0 ? ep : WV_NIL;
+    }
     Rl = 1;
     float worst = epd;
     wave_sync();
@@ -417,13 +434,19 @@ __device__ __forceinline__ void search_layer_reg(const HnswParams& p, WaveState&
     ts.start();
     for (;;) {
         // ---- pop the best unexpanded result ----
-        const uint64_t um = __ballot(lane < Rl && !(ri & WV_FLAG));
-        if (!um) break;
-        const int ridx = __builtin_ctzll(um);
-        const float cd = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(rd), ridx));
-        const uint32_t cid = (uint32_t)__builtin_amdgcn_readlane(ri, ridx) & WV_IDMASK;
+        int ridx = -1;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            const uint64_t um = __ballot(64 * r + lane < Rl && !(ri[r] & WV_FLAG));
+            if (ridx < 0 && um) ridx = 64 * r + __builtin_ctzll(um);
+        }
+        if (ridx < 0) break;
+        const float cd = reg_entry_d<NR>(rd, ridx);
+        const uint32_t cid = reg_entry_i<NR>(ri, ridx) & WV_IDMASK;
         if (cd > worst) break;   // :213-215
-        if (lane == ridx) ri |= WV_FLAG;
+#pragma unroll
+        for (int r = 0; r < NR; ++r)
+            if (64 * r + lane == ridx) ri[r] |= WV_FLAG;
         ts.lap(0);
         uint32_t pre0 = WV_NIL, pre1 = WV_NIL;
         if (level == 0) {
@@ -498,17 +521,33 @@ __device__ __forceinline__ void search_layer_reg(const HnswParams& p, WaveState&
                     km &= km - 1;
                     const float d = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(bd[h]), src));
                     const uint32_t id = (uint32_t)__builtin_amdgcn_readlane(bi[h], src);
-                    const int pos = __popcll(__ballot(lane < Rl && key_less(rd, ri & WV_IDMASK, d, id)));
+                    int pos = 0;
+#pragma unroll
+                    for (int r = 0; r < NR; ++r)
+                        pos += __popcll(__ballot(64 * r + lane < Rl && key_less(rd[r], ri[r] & WV_IDMASK, d, id)));
                     if (pos >= ef) continue;
-                    if (pos < Rl && __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(rd), pos)) == d &&
-                        ((uint32_t)__builtin_amdgcn_readlane(ri, pos) & WV_IDMASK) == id)
+                    if (pos < Rl && reg_entry_d<NR>(rd, pos) == d && (reg_entry_i<NR>(ri, pos) & WV_IDMASK) == id)
                         continue;   // already a result (a neighbour the visited cache forgot)
-                    const float sd = wave_shr1(rd);
-                    const uint32_t si = wave_shr1(ri);
-                    if (lane > pos) { rd = sd; ri = si; }
-                    if (lane == pos) { rd = d; ri = id; }
+                    float sd[NR];
+                    uint32_t si[NR];
+#pragma unroll
+                    for (int r = 0; r < NR; ++r) {
+                        sd[r] = wave_shr1(rd[r]);
+                        si[r] = wave_shr1(ri[r]);
+                        if (r > 0) {   // (lane 63 of the register below moves to lane 0)
+                            const float cdv = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(rd[r - 1]), 63));
+                            const uint32_t civ = (uint32_t)__builtin_amdgcn_readlane(ri[r - 1], 63);
+                            if (lane == 0) { sd[r] = cdv; si[r] = civ; }
+                        }
+                    }
+#pragma unroll
+                    for (int r = 0; r < NR; ++r) {
+                        const int e = 64 * r + lane;
+                        if (e > pos) { rd[r] = sd[r]; ri[r] = si[r]; }
+                        if (e == pos) { rd[r] = d; ri[r] = id; }
+                    }
                     Rl = min(Rl + 1, ef);
-                    worst = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(rd), Rl - 1));
+                    worst = reg_entry_d<NR>(rd, Rl - 1);
                 }
             }
             ts.lap(4);
@@ -516,7 +555,7 @@ __device__ __forceinline__ void search_layer_reg(const HnswParams& p, WaveState&
     }
 }
 
-template <int METRIC, bool PQ>
+template <int METRIC, bool PQ, int NR>
 __device__ __forceinline__ void knn_one_reg(const HnswParams& p, WaveState& w, int q) {
     const int lane = threadIdx.x & 63;
     const int g = lane & 7;
@@ -532,20 +571,24 @@ __device__ __forceinline__ void knn_one_reg(const HnswParams& p, WaveState& w, i
                    : exact_dist_group8<METRIC>(w.qv, p.X + (uint64_t)ep * p.ldx, p.D, g);
     epd = __shfl(epd, 0, 64);
     n_dist++;
-    float rd;
-    uint32_t ri;
+    float rd[NR];
+    uint32_t ri[NR];
     int Rl;
     for (int level = p.max_level; level >= 1; --level) {
-        search_layer_reg<METRIC, PQ>(p, w, level, 1, ep, epd, rd, ri, Rl, n_dist, n_exp, ts);
+        search_layer_reg<METRIC, PQ, NR>(p, w, level, 1, ep, epd, rd, ri, Rl, n_dist, n_exp, ts);
         // (no nil nodes on this path: the closest result is the next entry)
-        ep = (uint32_t)__builtin_amdgcn_readlane(ri, 0) & WV_IDMASK;
-        epd = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(rd), 0));
+        ep = (uint32_t)__builtin_amdgcn_readlane(ri[0], 0) & WV_IDMASK;
+        epd = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(rd[0]), 0));
     }
-    search_layer_reg<METRIC, PQ>(p, w, 0, p.ef, ep, epd, rd, ri, Rl, n_dist, n_exp, ts);
+    search_layer_reg<METRIC, PQ, NR>(p, w, 0, p.ef, ep, epd, rd, ri, Rl, n_dist, n_exp, ts);
     const int n = min(Rl, p.k);
-    if (lane < n) {
-        p.out_ids[(uint64_t)q * p.k + lane] = p.id_base + (ri & WV_IDMASK);
-        p.out_d[(uint64_t)q * p.k + lane] = rd;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const int e = 64 * r + lane;
+        if (e < n) {
+            p.out_ids[(uint64_t)q * p.k + e] = p.id_base + (ri[r] & WV_IDMASK);
+            p.out_d[(uint64_t)q * p.k + e] = rd[r];
+        }
     }
     if (lane == 0) {
         p.out_n[q] = n;
@@ -627,10 +670,11 @@ __device__ __forceinline__ void knn_one(const HnswParams& p, WaveState& w, int q
     }
 }
 
-// One instantiation per (metric, raw / PQ, register / LDS results): each gets
-// its own register allocation (one kernel holding all six inlined searches
-// spilled 431 SGPRs into VGPR lanes); the host launches the matching one.
-template <int METRIC, bool PQ, bool REG>
+// One instantiation per (metric, raw / PQ, LDS results / 64 / 128 register
+// results): each gets its own register allocation (one kernel holding all six
+// inlined searches spilled 431 SGPRs into VGPR lanes); the host launches the
+// matching one.
+template <int METRIC, bool PQ, int NR>
 __global__ __launch_bounds__(256) void wv_hnsw_kernel(HnswParams p) {
     extern __shared__ float lds[];
     const int wave = threadIdx.x >> 6;
@@ -649,7 +693,7 @@ __global__ __launch_bounds__(256) void wv_hnsw_kernel(HnswParams p) {
     w.vc = reinterpret_cast<uint32_t*>(cur); cur += (1 << p.vc_log2);
     w.xs = reinterpret_cast<uint32_t*>(cur); cur += (1 << p.xs_log2);
     w.ltomb = reinterpret_cast<uint32_t*>(cur); cur += MAX_LOCAL_TOMB;
-    if constexpr (REG) knn_one_reg<METRIC, PQ>(p, w, q);
+    if constexpr (NR > 0) knn_one_reg<METRIC, PQ, NR>(p, w, q);
     else knn_one<METRIC, PQ>(p, w, q);
 }
 
@@ -925,14 +969,17 @@ hipError_t wv_launch_hnsw(const wv::HnswParams* p, int waves_per_block, hipStrea
     const size_t lds = (size_t)waves_per_block * p->per_wave_words * sizeof(float);
     const unsigned blocks = (unsigned)((p->nq + waves_per_block - 1) / waves_per_block);
     if (blocks == 0) return hipSuccess;
-    // results in registers: unfiltered (no side set) with ef <= 64
-    const bool reg = p->sc == 0 && p->efc == 64 && !p->allow;
-#define WV_HNSW_LAUNCH(M, PQ)                                                                                     \
-    do {                                                                                                          \
-        if (reg) hipLaunchKernelGGL((wv::wv_hnsw_kernel<M, PQ, true>), dim3(blocks), dim3(64 * waves_per_block), \
-                                    lds, s, *p);                                                                  \
-        else hipLaunchKernelGGL((wv::wv_hnsw_kernel<M, PQ, false>), dim3(blocks), dim3(64 * waves_per_block),    \
-                                lds, s, *p);                                                                      \
+    // results in registers: unfiltered (no side set) with ef <= 64 (one
+    // register) or ef <= 128 (two)
+    const int nr = p->sc == 0 && !p->allow ? (p->efc == 64 ? 1 : p->efc == 128 ? 2 : 0) : 0;
+#define WV_HNSW_LAUNCH(M, PQ)                                                                                        \
+    do {                                                                                                             \
+        if (nr == 1) hipLaunchKernelGGL((wv::wv_hnsw_kernel<M, PQ, 1>), dim3(blocks), dim3(64 * waves_per_block),   \
+                                        lds, s, *p);                                                                 \
+        else if (nr == 2) hipLaunchKernelGGL((wv::wv_hnsw_kernel<M, PQ, 2>), dim3(blocks),                          \
+                                             dim3(64 * waves_per_block), lds, s, *p);                                \
+        else hipLaunchKernelGGL((wv::wv_hnsw_kernel<M, PQ, 0>), dim3(blocks), dim3(64 * waves_per_block), lds, s,   \
+                                *p);                                                                                 \
     } while (0)
     // a compressed index (PQ codes) is its own instantiation: the raw-vector
     // kernel keeps its registers and schedule
