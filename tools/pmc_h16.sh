@@ -1,5 +1,7 @@
 #!/bin/bash
-# f16 key pass on the harness (build/h16/abl_base, tools/h16_ablate.sh):
+# f16 key pass on the harness (build/h16/abl_base, tools/h16_ablate.sh)
+# (KNAME=wv_bf_h16w_kernel KSUB=wv_bf_h16w_kernel N=1250000 NQ=1000 D=768: the
+# wide pass on the C4 shape):
 # rocprofv3 kernel trace + stats, then separate PMC passes (no tracing in
 # the counter runs).  Output under gpurun_out/pmc_h16/.
 set -e
@@ -42,7 +44,8 @@ for f in glob.glob("gpurun_out/pmc_h16/trace/run_kernel_stats.csv"):
             avg_ns = float(r["AverageNs"])
 if "FETCH_SIZE" in out:
     rd = 2.0 * out["FETCH_SIZE"] * 1024
-    js = {"kernel": "wv_bf_h16_kernel", "N": int(os.environ.get("N", 1000000)), "nq": int(os.environ.get("NQ", 10000)),
+    kname = os.environ.get("KNAME", "wv_bf_h16_kernel")
+    js = {"kernel": kname, "N": int(os.environ.get("N", 1000000)), "nq": int(os.environ.get("NQ", 10000)),
           "dim": int(os.environ.get("D", 128)), "data": "uniform", "avg_kernel_ns": avg_ns,
           "hbm_read_bytes_per_launch": rd, "hbm_bytes_per_launch": rd,
           "algorithmic_bytes_per_launch": None,
@@ -50,7 +53,7 @@ if "FETCH_SIZE" in out:
           "note": "read = 2*FETCH_SIZE*1024 (gfx950 half-count correction); U[0,1) corpus/queries of the "
                   "tools/h16_ablate.cpp harness (same shape as bench.py's configs[1]); write traffic is the "
                   "candidate lists only (not collected)",
-          "source": "profiles/pmc_wv_bf_h16_kernel.json (tools/pmc_h16.sh)"}
+          "source": "profiles/pmc_%s.json (tools/pmc_h16.sh)" % kname}
     sq = js["sq"]
     mf = sq.get("SQ_INSTS_MFMA") or 0
     if mf:
@@ -65,5 +68,5 @@ if "FETCH_SIZE" in out:
         # MFMA pipe busy share: busy cycles summed over SIMDs / (SIMDs x cycles)
         js["mfma_busy_frac"] = sq["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024.0 * sq["GRBM_GUI_ACTIVE"] / 8.0)
     js["build"] = os.environ.get("WV_BUILD_HASH")
-    json.dump(js, open("gpurun_out/pmc_h16/pmc_wv_bf_h16_kernel.json", "w"), indent=1)
+    json.dump(js, open("gpurun_out/pmc_h16/pmc_%s.json" % kname, "w"), indent=1)
 PY
