@@ -453,12 +453,6 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16_kernel(H16Params p) {
             mfma_half(lds, 0, acc00, acc01, [](int) {}, lds, 1);   // H0(0), then the head of H1(0)
             need_mask = tile_ok(phys(t_begin), okw);
         }
-        // a full group's DMA ops of this wave: a constant per wave class when
-        // the image shares divide evenly (the usual D = 64 / 128), so the
-        // per-group wait needs no runtime switch on the scalar unit
-        constexpr bool EVEN = (St::IMG_U4 / 64) % WAVES == 0;
-        constexpr int SHARE = (St::IMG_U4 / 64) / WAVES;
-        const bool xns_wave = wave == 0 && L2;
         int slot_t = 0;   // LDS slot of tile t
         // row base of tile t (scalar; wraps with the rotation)
         uint32_t rbase = (uint32_t)(phys(t_begin) * (uint64_t)p.tile_stride * H_BN);
@@ -470,27 +464,22 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16_kernel(H16Params p) {
             if (rbase >= rb_wrap) rbase -= rb_wrap;
             WV_DBG_COUNT(0)
             const int g = t / TPS;
-#ifndef WV_H16_ABLATE_NO_FILL
-            // group g + 2 goes to stage (g + 2) % 3 = (g - 1) % 3, last read
-            // in group g - 1, before the barrier of group g's last tile
-            if (t % TPS == 0) ops_in_flight = g + 2 < ngroups ? fill_group(t_begin, g + 2, ntile) : 0;
-#endif
             const uint4* img = lds + slot_t * St::U4;
             slot_t = next_slot(slot_t);
             const bool more = t + 1 < ntile;
-            // the group's last tile: group g + 1 landed (at most the newest
-            // group's ops outstanding) and everyone is past its reads of
-            // group g - 1's stage, before A prefetches tile t + 1
+            // the group's last tile: group g + 1 landed and every wave is
+            // done with tile t - 1, hence with group g - 1's stage (its last
+            // reads: phase A of that group's last tile); only then is group
+            // g + 2 issued into it -- (g + 2) % 3 = (g - 1) % 3 -- a group's
+            // time ahead of its first read.  (Issued at the start of group g
+            // instead, a wave could overwrite that stage while a slower wave
+            // still ran phase A of group g - 1's last tile.)
             if (t % TPS == TPS - 1 && g + 1 < ngroups) {
-                if (EVEN && ops_in_flight == TPS * (SHARE + (xns_wave ? 1 : 0))) {
-                    if (xns_wave) vm_wait(TPS * (SHARE + 1));
-                    else vm_wait(TPS * SHARE);
-                } else if (EVEN) {
-                    vm_wait(0);   // (a partial group at the segment's end)
-                } else {
-                    vm_wait(ops_in_flight);
-                }
+                vm_wait(0);
                 block_barrier();
+#ifndef WV_H16_ABLATE_NO_FILL
+                if (g + 2 < ngroups) fill_group(t_begin, g + 2, ntile);
+#endif
             }
             // lanes l and l ^ 32 keep lists for the same query column (see the split pass)
             const bool mask_t = need_mask;
