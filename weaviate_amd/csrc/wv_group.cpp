@@ -30,8 +30,10 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -122,27 +124,96 @@ struct wv_group {
     DBuf r_ids, r_d, r_n, o_ids, o_d, o_n;   // on the root (member 0's device)
     HBuf h_q;                                // the batch, staged once for every member's upload
     std::mutex mu;
+    // one persistent host thread per member (more than one member): a call
+    // hands every worker the same task instead of spawning a thread per
+    // member per search
+    struct Pool {
+        std::mutex mu, call;
+        std::condition_variable cv, done;
+        uint64_t gen = 0;
+        int pending = 0;
+        bool stop = false;
+        const std::function<int(int)>* task = nullptr;
+        std::vector<std::thread> th;
+    } pool;
 };
 
 namespace {
 
-// run f(i) for every member on its own host thread; first error wins
+// member i's pool worker: its device set once, then every task handed out
+void pool_worker(wv_group* g, int i) {
+    Member& mb = g->m[i];
+    const bool dev_ok = hipSetDevice(mb.dev) == hipSuccess;
+    auto& P = g->pool;
+    uint64_t seen = 0;
+    std::unique_lock<std::mutex> l(P.mu);
+    for (;;) {
+        P.cv.wait(l, [&] { return P.stop || P.gen != seen; });
+        if (P.stop) return;
+        seen = P.gen;
+        const std::function<int(int)>* task = P.task;
+        l.unlock();
+        if (!dev_ok) {
+            mb.rc = WV_EDEVICE;
+            mb.err = "hipSetDevice";
+        } else {
+            mb.rc = (*task)(i);
+            if (mb.rc) mb.err = wv_last_error();
+        }
+        l.lock();
+        if (--P.pending == 0) P.done.notify_all();
+    }
+}
+
+void pool_start(wv_group* g) {
+    if (g->m.size() < 2) return;
+    for (size_t i = 0; i < g->m.size(); ++i) g->pool.th.emplace_back(pool_worker, g, (int)i);
+}
+
+void pool_stop(wv_group* g) {
+    {
+        std::lock_guard<std::mutex> l(g->pool.mu);
+        g->pool.stop = true;
+    }
+    g->pool.cv.notify_all();
+    for (auto& t : g->pool.th) t.join();
+    g->pool.th.clear();
+}
+
+// run f(i) for every member, each on its own device: one member inline on
+// the caller's thread (its device restored after), several on the pool's
+// workers in parallel; first error wins
 template <class F>
 int each_member(wv_group* g, F&& f) {
-    std::vector<std::thread> ts;
-    for (size_t i = 0; i < g->m.size(); ++i) {
-        ts.emplace_back([&, i] {
+    if (g->pool.th.empty()) {
+        int prev = 0;
+        (void)hipGetDevice(&prev);
+        for (size_t i = 0; i < g->m.size(); ++i) {
             Member& mb = g->m[i];
             if (hipSetDevice(mb.dev) != hipSuccess) {
                 mb.rc = WV_EDEVICE;
                 mb.err = "hipSetDevice";
-                return;
+                continue;
             }
             mb.rc = f((int)i);
             if (mb.rc) mb.err = wv_last_error();
-        });
+        }
+        (void)hipSetDevice(prev);
+    } else {
+        const std::function<int(int)> task = [&](int i) { return f(i); };
+        auto& P = g->pool;
+        std::lock_guard<std::mutex> c(P.call);
+        {
+            std::lock_guard<std::mutex> l(P.mu);
+            P.task = &task;
+            P.pending = (int)g->m.size();
+            ++P.gen;
+        }
+        P.cv.notify_all();
+        std::unique_lock<std::mutex> l(P.mu);
+        P.done.wait(l, [&] { return P.pending == 0; });
+        P.task = nullptr;
     }
-    for (auto& t : ts) t.join();
     for (auto& mb : g->m)
         if (mb.rc) return gfail(mb.rc, mb.err);
     return WV_OK;
@@ -373,12 +444,14 @@ int wv_group_create(const int* devices, int n_devices, int dim, int metric, cons
             return gfail(WV_EDEVICE, std::string("ncclCommInitAll: ") + ncclGetErrorString(r));
         }
     }
+    pool_start(g);
     *out = g;
     return WV_OK;
 }
 
 int wv_group_destroy(wv_group* g) {
     if (!g) return WV_OK;
+    pool_stop(g);
     destroy_members(g);
     delete g;
     return WV_OK;
