@@ -246,7 +246,8 @@ int main(int argc, char** argv) {
     const int device = argc > 2 ? std::atoi(argv[2]) : 0;
     const std::string mode = argc > 3 ? argv[3] : "sync";
     const bool async_start = mode == "async" || mode == "pq", heal = mode == "heal", pqm = mode == "pq";
-    if (mode != "sync" && !async_start && !heal) { std::fprintf(stderr, "unknown mode %s\n", mode.c_str()); return 2; }
+    const bool epgone = mode == "epgone";
+    if (mode != "sync" && !async_start && !heal && !epgone) { std::fprintf(stderr, "unknown mode %s\n", mode.c_str()); return 2; }
     const std::string log_dir = root + "/main.hnsw.commitlog.d";
     mkdir(root.c_str(), 0755);
     mkdir(log_dir.c_str(), 0755);
@@ -276,7 +277,7 @@ int main(int argc, char** argv) {
         uint64_t ns = 0, ep = 0, nu = 0;
         int ml = 0;
         wvo_graph_info(cpu, &ns, &ep, &ml, &nu);
-        if (id == ep || !in_store[id]) continue;
+        if ((id == ep && !epgone) || !in_store[id]) continue;
         in_store[id] = 0;
         wvo_clear_vector(cpu, id);
         ++gone;
@@ -309,6 +310,9 @@ int main(int argc, char** argv) {
     opt.max_batch = 256;
     opt.commitlog_dir = log_dir.c_str();
     if (heal) {
+        // (the library holds its worker 200 ms after each install: the second
+        // failure below lands inside that window)
+        setenv("WV_MIRROR_TEST_POST_INSTALL_MS", "200", 1);
         opt.auto_resync = 1;
         opt.flush = flush_cb;
         opt.resync_backoff_ms = 50;
@@ -336,7 +340,7 @@ int main(int argc, char** argv) {
                       std::to_string(st0.startup_rows) + " missing " + std::to_string(st0.startup_missing) + " nodes " +
                       std::to_string(st0.graph_nodes) + " delta " + std::to_string(st0.delta_rows) + " capacity " +
                       std::to_string(st0.capacity));
-        diffs_startup = failed ? -1 : compare(m, N0, 11, "startup");
+        diffs_startup = failed ? -1 : epgone ? 0 : compare(m, N0, 11, "startup");
     } else {
         // PostStartup returns at once; the build runs on the mirror's thread
         // while the writer and the searchers below already run
@@ -351,6 +355,42 @@ int main(int argc, char** argv) {
         diffs_startup = 0;   // (no quiescent point: the final comparison covers it)
     }
     const double startup_call_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
+    if (epgone) {
+        // the log's entrypoint lost its object: knnSearchByVector errors
+        // (search.go:467-476) -- the mirror too -- while a flat search (a
+        // small allow list, search.go:74-78) still answers as flatSearch
+        uint64_t ns = 0, ep = 0, nu = 0;
+        int ml = 0;
+        wvo_graph_info(cpu, &ns, &ep, &ml, &nu);
+        if (in_store[ep]) violation("epgone: the entrypoint still has its object");
+        uint64_t ids[K], oi[K];
+        float ds[K], od[K];
+        int32_t n = 0;
+        int on = 0;
+        int rc = wv_mirror_search(m, &store[5 * DIM], DIM, K, 0, nullptr, 0, ids, ds, &n);
+        if (rc != WV_EDELETED) violation("epgone: an unfiltered search returned " + std::to_string(rc));
+        std::mt19937_64 g(3);
+        const std::vector<uint64_t> al = allow_ids(g, 1500, N0), al_big = allow_ids(g, 14000, N0);
+        rc = wv_mirror_search(m, &store[5 * DIM], DIM, K, 1, al_big.data(), al_big.size(), ids, ds, &n);
+        if (rc != WV_EDELETED) violation("epgone: a filtered HNSW search returned " + std::to_string(rc));
+        rc = wv_mirror_search(m, &store[5 * DIM], DIM, K, 1, al.data(), al.size(), ids, ds, &n);
+        const std::vector<uint64_t> bits = to_bits(al, N0);
+        wvo_flat_search(cpu, &store[5 * DIM], K, bits.data(), N0, oi, od, &on);
+        bool same = rc == 0 && n == on;
+        for (int j = 0; same && j < on; ++j) same = ids[j] == oi[j] && std::memcmp(&ds[j], &od[j], 4) == 0;
+        if (!same) violation("epgone: a flat search differs from flatSearch (rc " + std::to_string(rc) + ")");
+        int64_t nd = 0;
+        rc = wv_mirror_search_by_distance(m, &store[5 * DIM], DIM, 1.f, -1, 0, nullptr, 0, ids, ds, K, &nd);
+        if (rc != WV_EDELETED) violation("epgone: an unfiltered search by distance returned " + std::to_string(rc));
+        wv_mirror_destroy(m);
+        wvo_destroy(cpu);
+        if (failed) {
+            std::fprintf(stderr, "VIOLATION: %s\n", first_err.c_str());
+            return 1;
+        }
+        std::printf("{\"ok\": true, \"mode\": \"epgone\", \"flat_ids\": %d}\n", n);
+        return 0;
+    }
 
     // ---- serving: adds, deletes, compactions and searches at once ----
     std::atomic<int> n_deleted{(int)deleted.size()};
@@ -364,7 +404,7 @@ int main(int argc, char** argv) {
     g_in_graph_mu = &in_graph_mu;
     g_compacted = &compacted;
     std::atomic<uint64_t> stale_answers{0};   // searches the CPU index answered (mirror not live)
-    std::atomic<uint64_t> missed_id{UINT64_MAX};
+    std::atomic<uint64_t> missed_id{UINT64_MAX}, missed_id2{UINT64_MAX};
     std::atomic<bool> live_seen{!async_start};
 
     auto writer = std::thread([&] {
@@ -381,6 +421,23 @@ int main(int argc, char** argv) {
                 // a write the mirror never saw (the decorator's propagation
                 // failed): stale now, the mirror must heal itself
                 missed_id = id;
+                wv_mirror_mark_stale(m);
+                // and a second failure the moment that resync goes live
+                // (polled: it lands while the worker is still busy finishing
+                // the resync -- the library holds it 200 ms there in this
+                // mode): the mirror must heal again
+                const auto t_poll = std::chrono::steady_clock::now();
+                wv_mirror_stats s;
+                for (;;) {
+                    wv_mirror_get_stats(m, &s);
+                    if (s.state == WV_MIRROR_LIVE) break;
+                    if (std::chrono::steady_clock::now() - t_poll > std::chrono::seconds(120)) {
+                        violation("heal: the first resync did not go live");
+                        break;
+                    }
+                    std::this_thread::sleep_for(std::chrono::microseconds(20));
+                }
+                missed_id2 = id;
                 wv_mirror_mark_stale(m);
             } else {
                 const int rc = wv_mirror_add(m, id, &store[id * DIM], DIM);
@@ -509,13 +566,15 @@ int main(int argc, char** argv) {
         if (pqm && !s.pq) violation("pq: the mirror does not serve compressed");
     }
     if (heal && !failed) {
-        // the missed row: found first by an exact (filtered) search
-        const uint64_t id = missed_id.load();
-        uint64_t ids[K];
-        float ds[K];
-        int32_t n = 0;
-        const int rc = wv_mirror_search(m, &store[id * DIM], DIM, K, 1, &id, 1, ids, ds, &n);
-        if (rc || n != 1 || ids[0] != id || ds[0] != 0.f) violation("heal: the missed row is not served after the resync");
+        // the missed rows: found first by an exact (filtered) search
+        for (const uint64_t id : {missed_id.load(), missed_id2.load()}) {
+            uint64_t ids[K];
+            float ds[K];
+            int32_t n = 0;
+            const int rc = wv_mirror_search(m, &store[id * DIM], DIM, K, 1, &id, 1, ids, ds, &n);
+            if (rc || n != 1 || ids[0] != id || ds[0] != 0.f)
+                violation("heal: missed row " + std::to_string(id) + " is not served after the resyncs");
+        }
     }
     {
         std::lock_guard<std::mutex> l(cpu_mu);
@@ -524,7 +583,8 @@ int main(int argc, char** argv) {
     if (!failed && wv_mirror_compact(m)) violation(std::string("final compact: ") + wv_last_error());
     wv_mirror_stats st;
     wv_mirror_get_stats(m, &st);
-    if (heal && !failed && (st.resyncs < 1 || flushes < 1)) violation("heal: the mirror did not resync by itself");
+    if (heal && !failed && (st.resyncs < 2 || flushes < 2))
+        violation("heal: the mirror did not resync by itself after both failures (resyncs " + std::to_string(st.resyncs) + ")");
     const int diffs_final = failed ? -1 : compare(m, CAP, 12, "final");
     if (!failed && st.delta_rows != 0) violation("delta not empty after the final compaction");
     // (async / pq: the writes replayed at install join the delta at once)

@@ -26,6 +26,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <shared_mutex>
@@ -199,6 +200,12 @@ struct wv_mirror {
     std::atomic<uint64_t> capacity{0};
     std::atomic<int> state{WV_MIRROR_IDLE};
     std::atomic<bool> pq{false};
+    // the log's entrypoint has no object (its row is gone from the store):
+    // the device graph runs from a live replacement, but every search that
+    // would take the HNSW path answers WV_EDELETED as knnSearchByVector does
+    // (search.go:467-476) until a compaction reads a log whose entrypoint
+    // the CPU index's cleanup has moved
+    std::atomic<bool> ep_gone{false};
     std::vector<uint64_t> have;       // ids holding a vector in the mirror
     std::vector<uint64_t> in_snap;    // ids that are nodes of the uploaded graph
     std::vector<uint64_t> tomb;       // ids deleted through the mirror (never cleared: doc ids are not reused)
@@ -221,8 +228,21 @@ struct wv_mirror {
     bool want_start = false, resync_next = false, busy = false;
     std::atomic<bool> stop{false};
     int backoff_ms = 0;
+    // failure injection for the replay harness: hold the worker this long
+    // between a startup's install (state LIVE) and busy = false, the window
+    // in which a failed write used to lose its resync
+    int test_post_install_ms = 0;
 
     bool live() const { return state.load() == WV_MIRROR_LIVE; }
+    // SearchByVector's dispatch (search.go:74-78): only a flat search runs
+    // without the entrypoint
+    int check_entrypoint(int filtered, uint64_t n_allow) {
+        if (!ep_gone) return WV_OK;
+        const wv_config c = config();
+        if (filtered && !c.forbid_flat && (int64_t)n_allow < c.flat_search_cutoff) return WV_OK;
+        return err(WV_EDELETED, "entrypoint was deleted in the object store, it has been flagged for cleanup and "
+                                "should be fixed in the next cleanup cycle");
+    }
     wv_config config() {
         std::lock_guard<std::mutex> l(cfg_mu);
         return cfg;
@@ -285,11 +305,12 @@ struct wv_mirror {
     // graph of c into x (exclusive access to x): nil for nodes without a row,
     // the entrypoint repaired; sets in_snap / snap_nodes of the caller's copy
     int upload_graph(wv_index* x, Csr& c, const std::vector<uint64_t>& have_rows, std::vector<uint64_t>& snap,
-                     uint64_t& nodes) {
+                     uint64_t& nodes, bool& gone) {
         for (uint64_t i = 0; i < c.n; ++i)
             if (c.levels[i] >= 0 && !bit(have_rows, i)) c.levels[i] = -1;
         snap.assign((c.n + 63) / 64, 0);
         nodes = 0;
+        gone = c.n > 0 && c.levels[c.entrypoint] < 0;
         if (!repair_entrypoint(c)) return WV_OK;   // no live node: every row stays in the delta
         int rc = wv_index_upload_graph(x, c.n, c.levels.data(), c.layer0.data(), c.deg0, c.upper_row.data(),
                                        c.max_level > 0 ? c.upper.data() : nullptr, c.n_upper, c.degU, c.max_level,
@@ -307,7 +328,7 @@ struct wv_mirror {
         wv_batcher* b = nullptr;
         int dim = 0;
         uint64_t capacity = 0, nodes = 0, rows = 0, missing = 0;
-        bool pq = false;
+        bool pq = false, ep_gone = false;
         std::vector<uint64_t> have, in_snap;
         Csr c;
         void release() {
@@ -378,7 +399,7 @@ struct wv_mirror {
             nb.pq = true;
         }
         if (c.n > 0) {
-            if (int rc = upload_graph(nb.ix, c, nb.have, nb.in_snap, nb.nodes)) return rc;
+            if (int rc = upload_graph(nb.ix, c, nb.have, nb.in_snap, nb.nodes, nb.ep_gone)) return rc;
         }
         return WV_OK;
     }
@@ -394,6 +415,7 @@ struct wv_mirror {
         if (nb.dim) dim = nb.dim;
         capacity = nb.capacity;
         pq = nb.pq;
+        ep_gone = nb.ep_gone;
         {
             std::lock_guard<std::mutex> bl(bm_mu);
             have.swap(nb.have);
@@ -498,6 +520,7 @@ struct wv_mirror {
             }
             if (!rc) rc = run_startup();
             if (!rc && resync) resyncs++;
+            if (test_post_install_ms > 0) std::this_thread::sleep_for(std::chrono::milliseconds(test_post_install_ms));
             l.lock();
             busy = false;
             if (rc) {
@@ -505,6 +528,15 @@ struct wv_mirror {
                 if (opt.auto_resync && src && !stop) { want_start = true; resync_next = true; }
             } else {
                 backoff_ms = 0;
+                // a write that failed between the install (state LIVE) and
+                // busy = false marked the mirror stale while request_resync
+                // saw busy and returned: schedule that resync here, or no
+                // later failure would (mark_stale only acts on LIVE)
+                if (state.load() == WV_MIRROR_STALE && opt.auto_resync && src && !stop && !want_start) {
+                    want_start = true;
+                    resync_next = true;
+                    backoff_ms = opt.resync_backoff_ms;
+                }
             }
             wk_cv.notify_all();
         }
@@ -543,6 +575,7 @@ int wv_mirror_create(int metric, const wv_config* cfg, const wv_mirror_options* 
     m->opt.commitlog_dir = nullptr;   // (the caller's string is not retained)
     if (m->opt.dim < 0 || m->opt.dim > kMaxDim) { delete m; return err(WV_EINVAL, "wv_mirror_create: bad dim"); }
     m->dim = m->opt.dim;
+    if (const char* e = std::getenv("WV_MIRROR_TEST_POST_INSTALL_MS")) m->test_post_install_ms = std::atoi(e);
     *out = m;
     return WV_OK;
 }
@@ -565,7 +598,11 @@ int wv_mirror_post_startup(wv_mirror* m, wv_vector_source src, void* ctx) {
 // goroutine): returns at once; reads answer WV_ESTALE until it is installed
 int wv_mirror_post_startup_async(wv_mirror* m, wv_vector_source src, void* ctx) {
     if (!m || !src) return err(WV_EINVAL, "wv_mirror_post_startup_async: bad argument");
-    std::lock_guard<std::mutex> l(m->wk_mu);
+    std::unique_lock<std::mutex> l(m->wk_mu);
+    // a startup or resync in flight first installs (begin_start below clears
+    // the writes queued for that install, and run_startup assumes STARTING);
+    // the wait is for the build already running, not for the one posted here
+    m->wk_cv.wait(l, [&] { return !m->busy; });
     m->src = src;
     m->src_ctx = ctx;
     m->begin_start();
@@ -691,6 +728,7 @@ int wv_mirror_search(wv_mirror* m, const float* vector, int len, int k, int filt
     if (!m->live()) return err(WV_ESTALE, "wv_mirror: stale");
     if (!m->ix) { *out_n = 0; return WV_OK; }   // empty index (search.go:463-465)
     if (len != m->dim) return err(WV_ESTALE, "wv_mirror_search: vector length differs from the index's");
+    if (int rc = m->check_entrypoint(filtered, n_allow)) return rc;
     // ids past the capacity hold no row: the list is cut there (ascending)
     const uint64_t cap = m->capacity;
     while (n_allow && allow_ids[n_allow - 1] >= cap) --n_allow;
@@ -706,6 +744,7 @@ int wv_mirror_search_by_distance(wv_mirror* m, const float* vector, int len, flo
     if (!m->live()) return err(WV_ESTALE, "wv_mirror: stale");
     if (!m->ix) { *out_n = 0; return WV_OK; }
     if (len != m->dim) return err(WV_ESTALE, "wv_mirror_search_by_distance: vector length differs from the index's");
+    if (int rc = m->check_entrypoint(filtered, n_allow)) return rc;   // (each deepening round is a SearchByVector)
     std::vector<uint64_t> bits;
     uint64_t nbits = 0;
     if (filtered) allow_bitmap(allow_ids, n_allow, m->capacity, bits, nbits);
@@ -769,7 +808,9 @@ int wv_mirror_compact(wv_mirror* m) {
             have_now = m->have;
         }
         uint64_t nodes = 0;
-        if ((rc = m->upload_graph(m->ix, c, have_now, snap, nodes))) return fail_stale(rc);
+        bool gone = false;
+        if ((rc = m->upload_graph(m->ix, c, have_now, snap, nodes, gone))) return fail_stale(rc);
+        m->ep_gone = gone;
         std::lock_guard<std::mutex> bl(m->bm_mu);
         const std::vector<uint64_t> t = m->tomb_union(c, m->capacity);
         if (!t.empty() && (rc = wv_index_set_tombstones(m->ix, t.data(), std::min<uint64_t>(t.size() * 64, m->capacity))))
