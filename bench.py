@@ -283,6 +283,60 @@ def _allow_words(args, lo, n_local):
     return words, int(keep.sum())
 
 
+def device_rows(ctx, kind, seed, row0, n, dim):
+    """rows [row0, row0 + n) of a counter-based corpus generated on the device
+    (tools/wv_synth.hip; measurement infrastructure)"""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import synth
+    t = ctx.torch.empty((n, dim), dtype=ctx.torch.float32, device=ctx.dev)
+    synth.fill(kind, seed, row0, t, stream=ctx.stream)
+    return t
+
+
+def upload_device_rows(ctx, ix, kind, seed, row0, n, dim, chunk=1 << 23, host_copy=False):
+    """the index's rows [0, n) = corpus rows [row0, row0 + n), generated on the
+    device chunk by chunk and uploaded from device memory; host_copy: also
+    returned as a host array (for the CPU restatement)"""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import synth
+    torch = ctx.torch
+    host = np.empty((n, dim), np.float32) if host_copy else None
+    chunk = max(1, min(chunk, (1 << 31) // (4 * dim)))
+    t = torch.empty((min(n, chunk), dim), dtype=torch.float32, device=ctx.dev)
+    for r0 in range(0, n, chunk):
+        m = min(chunk, n - r0)
+        synth.fill(kind, seed, row0 + r0, t[:m], stream=ctx.stream)
+        torch.cuda.synchronize(ctx.dev)
+        ix.upload_vectors_device(t.data_ptr(), m, first_id=r0)
+        if host is not None:
+            host[r0:r0 + m] = t[:m].cpu().numpy()
+    del t
+    torch.cuda.empty_cache()
+    return host
+
+
+_PHASE = ["start", time.time()]
+
+
+def phase(name: str):
+    """the bench's current phase, echoed to stderr (and every 30 s by the
+    heartbeat: long silent phases -- a 100M-row graph build -- stay visible)"""
+    _PHASE[0], _PHASE[1] = name, time.time()
+    print(f"[bench] {name}", file=sys.stderr, flush=True)
+
+
+def _heartbeat():
+    import threading
+
+    def run():
+        t0 = time.time()
+        while True:
+            time.sleep(30)
+            print(f"[bench] ... {_PHASE[0]} ({time.time() - _PHASE[1]:.0f} s in phase, {time.time() - t0:.0f} s total)",
+                  file=sys.stderr, flush=True)
+    threading.Thread(target=run, daemon=True).start()
+
+
 def _oracle():
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle as O  # the checker / CPU baseline (test infrastructure), never the measured path
@@ -431,6 +485,101 @@ def run_exact(args, ctx, W):
     return res, state
 
 
+def c4_line(args, ctx, W, with_cpu):
+    """configs[3]: 10M x 768-d dot product, exact (flatSearch) 10-NN of a
+    1000-query batch under a shared allow list kept at 100 / 50 / 10 / 1 %
+    (Bernoulli over ids, seed 3) -- the corpus sharded over the N GPUs by id
+    range, the per-shard top-k all-gathered over RCCL and merged on the device
+    (index.go:967-1044, flat_search.go:19-74).  Rows generated on the device
+    (N(0,1)/sqrt(768), tools/wv_synth.hip).  The reference would take the
+    filtered HNSW path at 1 % of 10M (100k > flatSearchCutoff 40k,
+    search.go:74-78); this line is the exact search (cutoff above |allow|)."""
+    torch = ctx.torch
+    N, D, NQ, K = args.c4_rows, 768, args.c4_nq, args.k
+    ws, rank = ctx.ws, ctx.rank
+    lo, hi = N * rank // ws, N * (rank + 1) // ws
+    n_local = hi - lo
+    t0 = time.time()
+    ix = W.GPUVectorIndex(D, "dot", capacity=n_local, device=ctx.gpu, id_base=lo)
+    base = upload_device_rows(ctx, ix, "gauss", 1, lo, n_local, D, host_copy=with_cpu)
+    queries = device_rows(ctx, "gauss", 2, 0, NQ, D).cpu().numpy()
+    qt = _query_tensor(ctx, queries, ix.query_ld())
+    setup_s = time.time() - t0
+    out_ids, out_d, out_n = _out_tensors(ctx, NQ, K)
+    if ws > 1:
+        g_ids = torch.empty((ws, NQ, K), dtype=torch.int64, device=ctx.dev)
+        g_d = torch.empty((ws, NQ, K), dtype=torch.float32, device=ctx.dev)
+        g_n = torch.empty((ws, NQ), dtype=torch.int32, device=ctx.dev)
+        m_ids, m_d, m_n = _out_tensors(ctx, NQ, K)
+    O = _oracle() if with_cpu else None
+    legs = {}
+    for frac in args.c4_fracs:
+        a = argparse.Namespace(**vars(args))
+        a.allow_frac = frac
+        allow_ptr, allow_bits, n_allowed, words = 0, 0, n_local, None
+        if frac < 1.0:
+            words, n_allowed = _allow_words(a, lo, n_local)
+            allow_t = torch.from_numpy(words.view(np.int64)).to(ctx.dev)
+            allow_ptr, allow_bits = allow_t.data_ptr(), n_local
+
+        def step(timed):
+            ix.search_batch_device(qt.data_ptr(), NQ, K, out_ids.data_ptr(), out_d.data_ptr(), out_n.data_ptr(),
+                                   ef=0, mode="exact", stream=ctx.stream, allow_ptr=allow_ptr,
+                                   allow_nbits=allow_bits)
+            if ws > 1:
+                ctx.allgather(g_ids, out_ids)
+                ctx.allgather(g_d, out_d)
+                ctx.allgather(g_n, out_n)
+                W.merge_shards_device(g_d.data_ptr(), g_ids.data_ptr(), g_n.data_ptr(), ws, NQ, K, m_d.data_ptr(),
+                                      m_ids.data_ptr(), m_n.data_ptr(), stream=ctx.stream)
+
+        ix.set_timing(True)
+        el = ctx.time_steps(step, args.steps, args.warmup, before_timed=ix.last_kernel_times)
+        km = ix.last_kernel_times()
+        stats = ix.last_batch_stats()
+        ix.set_timing(False)
+        roof, kind = exact_roofline(a, ix, [km], stats, D, n_allowed, n_local, NQ)
+        attach_traffic(roof, n_local, NQ, D, "gauss" if frac >= 1.0 else f"gauss_allow{frac}")
+        ms = 1000 * el / args.steps
+        leg = {"value": round(NQ * args.steps / el, 1), "unit": "queries/s", "ms_per_step": round(ms, 3),
+               "allowed_rows_rank0": int(n_allowed), "roofline": roof,
+               "outside_key_pass_frac": round(max(0.0, 1.0 - roof["kernel_ms"] / ms), 3)}
+        fin_ids, fin_d = (m_ids, m_d) if ws > 1 else (out_ids, out_d)
+        if with_cpu:
+            # flatSearch restated in C on the same rows and list (parity + baseline)
+            cpu = {}
+            for threads, secs in ((args.cpu_threads, args.c4_cpu_seconds), (1, args.c4_cpu_seconds_t1)):
+                probe = max(1, min(8, threads))
+                tp = time.perf_counter()
+                O.flat_scan(O.DOT, base, queries[:probe], K, allow_bits=words, threads=threads)
+                per_q = (time.perf_counter() - tp) / probe
+                ns = int(min(NQ, max(probe, secs / max(per_q, 1e-9))))
+                tp = time.perf_counter()
+                oi, od, on = O.flat_scan(O.DOT, base, queries[:ns], K, allow_bits=words, threads=threads)
+                cpu[threads] = (ns, time.perf_counter() - tp, oi, od)
+            ns, ct, oi, od = cpu[args.cpu_threads]
+            gi = fin_ids.cpu().numpy().view(np.uint64)[:ns]
+            gd = fin_d.cpu().numpy()[:ns]
+            id_eq, d_eq, tie_ok = parity_stats(gi, gd, oi, od)
+            leg["parity_sample"] = {"queries": ns, "ids_and_dists_bit_identical": id_eq == 1.0 and d_eq == 1.0,
+                                    "dists_bitwise_equal_frac": d_eq, "tie_aware_identical_frac": tie_ok}
+            n1, t1 = cpu[1][0], cpu[1][1]
+            leg["cpu_baseline"] = {"value": round(ns / ct, 2), "unit": "queries/s", "cores": args.cpu_threads,
+                                   "kind": "port", "value_t1": round(n1 / t1, 2), "cores_t1": 1,
+                                   "sample": f"{ns} (T={args.cpu_threads}) / {n1} (T=1) of the {NQ} queries over "
+                                             f"the full {N:,}-row corpus and list; flatSearch restated in C (AVX2 "
+                                             f"asm-order dot, oracle/)"}
+        legs["allow_%g%%" % (100 * frac)] = leg
+    ix.close()
+    del base
+    return {"workload": f"exact {K}-NN, {N:,} x {D}-d dot, {NQ}-query batch, shared allow list (BASELINE configs[3])",
+            "parallelism": (f"corpus sharded over {ws} GPU(s) by id range ({n_local:,} rows per GPU), RCCL all-gather "
+                            f"of per-shard top-k + device merge" if ws > 1 else "one GPU holding the whole corpus"),
+            "scaling": "strong (fixed corpus and batch)", "setup_s": round(setup_s, 1),
+            "data": "N(0,1)/sqrt(768) rows and queries generated on the device (counter-based, seeds 1 / 2)",
+            "legs": legs}
+
+
 def wide_k_line(args, ctx, st, W):
     """Secondary exact lines on the same index (N=1): k=100 through the batched
     wide path (search.go:90-158 asks limit 100 first), and SearchByVectorDistance
@@ -572,10 +721,18 @@ def run_hnsw(args, ctx, W, with_cpu):
     gen = {"uniform": counter_uniform, "gauss": counter_gauss, "sift": counter_sift, "glove": counter_glove}[data]
     lo, hi = (N * rank // ws, N * (rank + 1) // ws) if corpus else (0, N)
     n_local = hi - lo
-    base = gen(1, lo, n_local, D)
-    queries = gen(2, 0 if corpus else rank * NQ, NQ, D)
     ix = W.GPUVectorIndex(D, args.metric, capacity=n_local, device=ctx.gpu, max_connections=args.M, id_base=lo)
-    ix.upload_vectors(base)
+    if getattr(args, "device_data", False):
+        # configs[4]-sized shards: rows generated in HBM (tools/wv_synth.hip,
+        # the same construction as the numpy generator) and uploaded from
+        # there; the host never holds the corpus
+        base = None
+        queries = device_rows(ctx, data, 2, 0 if corpus else rank * NQ, NQ, D).cpu().numpy()
+        upload_device_rows(ctx, ix, data, 1, lo, n_local, D)
+    else:
+        base = gen(1, lo, n_local, D)
+        queries = gen(2, 0 if corpus else rank * NQ, NQ, D)
+        ix.upload_vectors(base)
     O = _oracle() if (with_cpu or args.graph_build != "gpu") else None
     graph = build_hnsw_graph(args, ctx, ix, base, n_local, O)
     graph["max_level"] = int(ix.graph_info()["max_level"])
@@ -683,7 +840,7 @@ def run_hnsw(args, ctx, W, with_cpu):
         res["ef_sweep"] = sweep
     if args.concurrency and ws == 1:
         res["concurrent_callers"] = concurrent_callers(args, ix, queries)
-    if not with_cpu and getattr(args, "counts_sample", 0) > 0:
+    if not with_cpu and getattr(args, "counts_sample", 0) > 0 and base is not None:
         # SURVEY 8d's byte basis from the restatement's own evaluation counts
         # on a query sample of this shard's graph (no CPU timing): the GPU's
         # visited-cache re-evaluations are not counted as useful bytes
@@ -700,6 +857,29 @@ def run_hnsw(args, ctx, W, with_cpu):
                                 "dist_evals_per_query": round(e_q, 1), "expansions_per_query": round(x_q, 1),
                                 "gpu_dist_evals_per_query": round(stats[-1]["dist_evals"] / NQ, 1)})
         del ref
+    if base is None and getattr(args, "exact_counts_sample", 0) > 0:
+        # corpora too large to restate on the host (configs[4]): the same
+        # traversal counted on the GPU with an exact per-query visited bitmap
+        # (WV_HNSW_UNIQUE_COUNTS) -- each node's layer-0 evaluation once, as
+        # the reference's visited list allows, not the lossy cache's repeats
+        ns_ = min(NQ, args.exact_counts_sample)
+        os.environ["WV_HNSW_UNIQUE_COUNTS"] = "1"
+        try:
+            ix.search_batch_device(qt.data_ptr(), ns_, K, out_ids.data_ptr(), out_d.data_ptr(), out_n.data_ptr(),
+                                   ef=args.ef, mode="hnsw", stream=ctx.stream)
+            torch.cuda.synchronize(ctx.dev)
+            su = ix.last_batch_stats()
+        finally:
+            del os.environ["WV_HNSW_UNIQUE_COUNTS"]
+        e_q, x_q = su["dist_evals"] / ns_, su["expansions"] / ns_
+        by = (4.0 * D * e_q + 4.0 * 2 * args.M * x_q) * NQ
+        achieved = by / (hnsw_ms * 1e-3) / 1e9
+        res["roofline"].update({"achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4),
+                                "counts_from": f"GPU traversal with an exact per-query visited bitmap (each node's "
+                                               f"evaluation counted once, as the reference's visited list), "
+                                               f"{ns_}-query sample",
+                                "dist_evals_per_query": round(e_q, 1), "expansions_per_query": round(x_q, 1),
+                                "gpu_dist_evals_per_query": round(stats[-1]["dist_evals"] / NQ, 1)})
     if with_cpu:
         ref = O.Index(D, args.metric, args.M, args.efc, capacity=N, seed=1)
         ref.import_graph(base, ix.download_graph())   # the restatement searches the very same graph
@@ -740,6 +920,8 @@ def run_hnsw(args, ctx, W, with_cpu):
                                "kind": "port", "value_t1": round(n1 / t1, 1), "cores_t1": 1,
                                "sample": f"all {NQ} queries x {reps} passes (T={args.cpu_threads}), {n1} queries "
                                          f"(T=1); knnSearchByVector restated in C on the same graph (oracle/)"}
+        if getattr(args, "filtered_fracs", None):
+            res["filtered_hnsw"] = filtered_hnsw_legs(args, ctx, ix, ref, queries, qt, NQ, K, D, n_local)
         if args.seq_build:
             # north_star: recall within 0.5 pt of the reference index -- whose
             # graph is built by inserting one node at a time (insert.go:103-217,
@@ -765,6 +947,59 @@ def run_hnsw(args, ctx, W, with_cpu):
                 "sequential_build_s": round(build_s, 1), "threads": args.hnsw_build_threads}
     ix.close()
     return res
+
+
+def filtered_hnsw_legs(args, ctx, ix, ref, queries, qt, NQ, K, D, n_local):
+    """Filtered HNSW on the configs[0] graph (search.go:74-78 with forbidFlat,
+    or |allow| >= flatSearchCutoff: the allow list is applied at layer 0,
+    :282-298): a shared Bernoulli(p) list (seed 3), ef = the line's ef.  QPS,
+    HBM fraction from the restatement's counts on the same graph, parity
+    with the restatement (knnSearchByVector with the list), recall against
+    the filtered exact answer, and the rate of queries whose ineligible side
+    set outgrew the wave's LDS (answered by the exact filtered scan)."""
+    torch = ctx.torch
+    out = {}
+    oi_, od_, on_ = _out_tensors(ctx, NQ, K)
+    for frac in args.filtered_fracs:
+        a = argparse.Namespace(**vars(args))
+        a.allow_frac = frac
+        words, n_allowed = _allow_words(a, 0, n_local)
+        allow_t = torch.from_numpy(words.view(np.int64)).to(ctx.dev)
+
+        def step(timed, mode="hnsw"):
+            ix.search_batch_device(qt.data_ptr(), NQ, K, oi_.data_ptr(), od_.data_ptr(), on_.data_ptr(), ef=args.ef,
+                                   mode=mode, stream=ctx.stream, allow_ptr=allow_t.data_ptr(), allow_nbits=n_local)
+
+        ix.set_timing(True)
+        el = ctx.time_steps(step, args.steps, args.warmup, before_timed=ix.last_kernel_times)
+        km = ix.last_kernel_times()["hnsw_ms"]
+        st = ix.last_batch_stats()
+        ix.set_timing(False)
+        gi = oi_.cpu().numpy().view(np.uint64).copy()
+        gd = od_.cpu().numpy().copy()
+        step(False, mode="exact")
+        torch.cuda.synchronize(ctx.dev)
+        truth = oi_.cpu().numpy().view(np.uint64).copy()
+        ri, rd, rn, rst = ref.search_batch(queries, K, args.ef, allow=words, threads=args.cpu_threads)
+        id_eq, d_eq, tie_ok = parity_stats(gi, gd, ri, rd)
+        rec = float(np.mean([len(set(x) & set(y)) / K for x, y in zip(gi.tolist(), truth.tolist())]))
+        rec_cpu = float(np.mean([len(set(x) & set(y)) / K for x, y in zip(ri.tolist(), truth.tolist())]))
+        e, x = rst["dist_evals"], rst["expansions"]
+        by = 4.0 * D * e + 4.0 * 2 * args.M * x
+        achieved = by / (km * 1e-3) / 1e9
+        out["allow_%g%%" % (100 * frac)] = {
+            "value": round(NQ * args.steps / el, 1), "unit": "queries/s", "ms_per_step": round(1000 * el / args.steps, 3),
+            "allowed_rows": int(n_allowed), "ef": args.ef, "recall@10_vs_filtered_exact": round(rec, 4),
+            "recall@10_cpu_restatement": round(rec_cpu, 4),
+            "exact_fallback_queries": int(st["fallbacks"]), "exact_fallback_rate": round(st["fallbacks"] / NQ, 4),
+            "parity_sample": {"queries": NQ, "id_match_frac": id_eq, "dists_bitwise_equal_frac": d_eq,
+                              "tie_aware_identical_frac": tie_ok},
+            "roofline": {"bound": "hbm", "kernel": "wv_hnsw_kernel", "achieved": round(achieved, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "kernel_ms": round(km, 3), "counts_from": "CPU restatement (oracle/) on the same graph and list",
+                         "dist_evals_per_query": round(e / NQ, 1), "expansions_per_query": round(x / NQ, 1),
+                         "gpu_dist_evals_per_query": round(st["dist_evals"] / NQ, 1)}}
+    return out
 
 
 def concurrent_callers(args, ix, queries):
@@ -905,11 +1140,21 @@ def main():
                          "beside the GPU-built graph's (north_star's 0.5-pt criterion; ~40 s of CPU at 1M; on by "
                          "default for the C1 line beside the exact value)")
     ap.add_argument("--no-seq-build", action="store_true", help="skip the C1 line's sequential-build recall check")
-    ap.add_argument("--c5-fixed-corpus", action="store_true",
-                    help="N > 1: the configs[4] line shards a fixed 100M corpus (100M / N rows per GPU) instead of "
-                         "12.5M rows per GPU")
+    ap.add_argument("--c5-rows", type=int, default=100_000_000,
+                    help="configs[4] corpus rows, sharded N ways (100M / N rows and graph per GPU)")
+    ap.add_argument("--c5-weak", action="store_true",
+                    help="the configs[4] line with 12.5M rows per GPU (weak scaling) instead of the fixed corpus")
     ap.add_argument("--no-c5-line", action="store_true",
-                    help="skip the configs[4] line (12.5M x 96 rows per GPU, sharded hnsw + RCCL merge)")
+                    help="skip the configs[4] line (100M x 96 corpus sharded over the N GPUs, hnsw + RCCL merge)")
+    ap.add_argument("--no-filtered-hnsw", action="store_true",
+                    help="skip the filtered-HNSW legs (allow 10 / 50 %%, forbidFlat) on the configs[0] graph")
+    ap.add_argument("--no-c4-line", action="store_true",
+                    help="skip the configs[3] line (10M x 768 dot, allow lists 100/50/10/1 %%, sharded over the N GPUs)")
+    ap.add_argument("--c4-rows", type=int, default=10_000_000)
+    ap.add_argument("--c4-nq", type=int, default=1000)
+    ap.add_argument("--c4-fracs", default="1,0.5,0.1,0.01", help="configs[3] allow-list selectivities")
+    ap.add_argument("--c4-cpu-seconds", type=float, default=4.0)
+    ap.add_argument("--c4-cpu-seconds-t1", type=float, default=2.0)
     ap.add_argument("--no-c3-line", action="store_true",
                     help="skip the configs[2] GloVe-shaped hnsw ef-sweep line reported beside the default value")
     ap.add_argument("--hnsw-build-threads", type=int, default=16)
@@ -935,6 +1180,7 @@ def main():
     if args.cpu_threads <= 0:
         args.cpu_threads = args.host_cores["cores"]
     args.ef_sweep = [int(x) for x in args.ef_sweep.split(",") if x]
+    args.c4_fracs = [float(x) for x in args.c4_fracs.split(",") if x]
     args.concurrency = [int(x) for x in args.concurrency.split(",") if x]
     GLOVE_NOISE = args.glove_noise
     if args.group_leg:
@@ -961,6 +1207,7 @@ def main():
     args.hnsw_data = args.data if args.workload == "hnsw" else "sift"
 
     import weaviate_amd as W
+    _heartbeat()
     ctx = Ctx(args)
     with_cpu = rank == 0 and ws == 1 and not args.no_cpu_baseline
 
@@ -978,6 +1225,7 @@ def main():
             if key in h:
                 result[key] = h[key]
     else:
+        phase("exact headline (configs[1])")
         e, st = run_exact(args, ctx, W)
         result = {
             "metric": METRIC, "value": e["value"], "unit": "queries/s", "n_gpus": ws, "devices": ctx.n_devices,
@@ -993,9 +1241,11 @@ def main():
             "roofline": e["roofline"],
         }
         if with_cpu:
+            phase("exact CPU baseline + parity sample")
             O = _oracle()
             result["cpu_baseline"], result["parity_sample"] = exact_cpu_baseline(args, st, O)
         if ws == 1 and args.allow_frac == 0 and not args.no_wide_line:
+            phase("wide k / SearchByVectorDistance")
             result["wide_k"] = wide_k_line(args, ctx, st, W)
         if args.dump_ids and rank == 0:
             np.savez(args.dump_ids, ids=st["final_ids"], dists=st["final_d"])
@@ -1023,6 +1273,8 @@ def main():
             # within 0.5 pt of the insert-by-insert graph; --no-seq-build skips it)
             a1 = argparse.Namespace(**vars(args))
             a1.seq_build = (args.seq_build or (not args.no_seq_build and args.rows == 1_000_000)) and ws == 1
+            a1.filtered_fracs = [] if args.no_filtered_hnsw else [0.1, 0.5]
+            phase("configs[0] hnsw line")
             h = run_hnsw(a1, ctx, W, with_cpu)
             h.pop("metric", None)
             result["hnsw_c1"] = h
@@ -1032,36 +1284,45 @@ def main():
             a3.rows, a3.dim, a3.metric, a3.hnsw_data = 1_200_000, 100, "cosine-dot", "glove"
             a3.ef, a3.ef_sweep, a3.concurrency, a3.split = 64, [32, 64, 128, 256], [], "corpus"
             a3.cpu_seconds, a3.cpu_seconds_t1, a3.graph_build = 4.0, 2.0, "gpu"
+            phase("configs[2] hnsw ef sweep")
             h = run_hnsw(a3, ctx, W, with_cpu)
             h.pop("metric", None)
             result["hnsw_c3"] = h
+        if not args.no_c4_line and args.rows == 1_000_000 and args.metric == "l2-squared":
+            try:
+                phase("configs[3] exact 10M x 768 dot")
+                result["exact_c4"] = c4_line(args, ctx, W, with_cpu)
+            except Exception as e:   # reported, not fatal to the headline line
+                result["exact_c4"] = {"error": f"{type(e).__name__}: {e}"}
         if not args.no_c5_line and args.rows == 1_000_000 and args.metric == "l2-squared":
             # configs[4]'s layout: a Deep/SIFT-shaped 96-d corpus sharded by id
             # range over the N GPUs, every GPU building and searching the graph
             # of its shard, per-shard top-k all-gathered over RCCL and merged on
-            # the device (index.go:967-1044).  Default: 12.5M rows per GPU (the
-            # 100M corpus at N = 8, weak scaling below).  --c5-fixed-corpus
-            # shards a fixed 100M corpus (100M / N rows per GPU, strong
-            # scaling): the 50M-row shard graph of N = 2 takes > 185 s to build
-            # on one MI355X (12.5M: 17 s), too long for the default run.
+            # the device (index.go:967-1044).  The corpus is the fixed 100M
+            # rows at every N (100M / N rows and graph per GPU, strong
+            # scaling; N = 1 holds all of it: 38.4 GB of rows + a 51 GB
+            # layer-0 CSR in 288 GB).  The rows are generated on the device
+            # and the graph built there: linear, 14.2 s per 12.5M rows
+            # (profiles/r05/build_scaling_probe.log).  --c5-weak: 12.5M rows
+            # per GPU instead.
             a5 = argparse.Namespace(**vars(args))
-            c5_fixed = args.c5_fixed_corpus and ws > 1
-            c5_rows = 100_000_000 if c5_fixed else 12_500_000 * ws
+            c5_fixed = not args.c5_weak
+            c5_rows = args.c5_rows if c5_fixed else 12_500_000 * ws
             a5.rows, a5.dim, a5.metric, a5.hnsw_data = c5_rows, 96, "l2-squared", "sift"
             a5.ef, a5.ef_sweep, a5.concurrency, a5.split = 64, [128], [], "corpus"
             a5.graph_build, a5.dump_ids, a5.seq_build = "gpu", "", False
-            a5.counts_sample = 1000 if ws == 1 else 0   # (N > 1: the 100M / N shards are large to restate)
+            a5.device_data = True
+            a5.counts_sample, a5.exact_counts_sample = 0, 1000
             try:
+                phase("configs[4] hnsw over the 100M corpus")
                 h = run_hnsw(a5, ctx, W, False)
                 h.pop("metric", None)
                 if c5_fixed:
-                    h["scaling"] = f"strong (fixed 100M-row corpus, {c5_rows // ws:,} rows per GPU)"
-                elif ws > 1:
-                    h["scaling"] = "weak (12.5M rows per GPU; the 100M corpus at N = 8)"
+                    h["scaling"] = f"strong (fixed {c5_rows:,}-row corpus, {c5_rows // ws:,} rows per GPU)"
                 else:
-                    h["scaling"] = "one shard: 12.5M rows = the per-GPU share of 100M over 8 GPUs"
-                h["value_units"] = (f"queries/s over the whole {a5.rows:,}-row corpus (every rank searches the batch)"
-                                    if ws > 1 else "queries/s over one 12,500,000-row shard (not the 100M corpus)")
+                    h["scaling"] = "weak (12.5M rows per GPU; the 100M corpus at N = 8)"
+                h["value_units"] = (f"queries/s over the whole {a5.rows:,}-row corpus"
+                                    + (" (every rank searches the batch over its shard)" if ws > 1 else " on one GPU"))
                 result["hnsw_c5_sharded"] = h
             except Exception as e:   # reported, not fatal to the headline line
                 result["hnsw_c5_sharded"] = {"error": f"{type(e).__name__}: {e}"}

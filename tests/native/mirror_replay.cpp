@@ -277,9 +277,18 @@ int main(int argc, char** argv) {
         uint64_t ns = 0, ep = 0, nu = 0;
         int ml = 0;
         wvo_graph_info(cpu, &ns, &ep, &ml, &nu);
-        if ((id == ep && !epgone) || !in_store[id]) continue;
+        if (id == ep || !in_store[id]) continue;
         in_store[id] = 0;
         wvo_clear_vector(cpu, id);
+        ++gone;
+    }
+    if (epgone) {   // the entrypoint's object deleted from the store, its node not cleaned up yet
+        uint64_t ns = 0, ep = 0, nu = 0;
+        int ml = 0;
+        wvo_graph_info(cpu, &ns, &ep, &ml, &nu);
+        wvo_add_tombstone(cpu, ep);
+        in_store[ep] = 0;
+        wvo_clear_vector(cpu, ep);
         ++gone;
     }
     flush_log();

@@ -98,6 +98,40 @@ def test_configs0_sift_hnsw_m64_efc128_ef64():
     ix.close()
 
 
+def test_exact_visited_counts_equal_restatement(monkeypatch):
+    """The configs[4] line's byte basis (E and X of the reference's
+    traversal) is measured on the GPU where the corpus is too large to restate
+    on the host: WV_HNSW_UNIQUE_COUNTS counts each node's layer-0 evaluation
+    once (an exact per-query visited bitmap beside the lossy LDS cache, as the
+    reference's visited list, search.go:256-264).  On a graph the restatement
+    also searches, those counts equal the restatement's E and X -- with the
+    visited cache squeezed so that the GPU re-evaluates."""
+    n, d, nq, k, ef = 24000, 96, 300, 10, 64
+    base = counter_sift(1, 0, n, d)
+    qs = counter_sift(2, 0, nq, d)
+    ref = O.Index(d, "l2-squared", 64, 128, capacity=n, seed=1)
+    ref.add_batch(base, threads=THREADS)
+    ix = W.GPUVectorIndex(d, "l2-squared", capacity=n, max_connections=64)
+    ix.upload_vectors(base)
+    ix.upload_graph(ref.export_graph())
+    oi, od, on, ost = ref.search_batch(qs, k, ef, threads=THREADS)
+    monkeypatch.setenv("WV_HNSW_WAVE_KB", "6")   # a small visited cache: re-evaluations
+    gi, gd, gn = ix.search_batch(qs, k, ef=ef, mode="hnsw")
+    lossy = ix.last_batch_stats()
+    monkeypatch.setenv("WV_HNSW_UNIQUE_COUNTS", "1")
+    ui, ud, un = ix.search_batch(qs, k, ef=ef, mode="hnsw")
+    exact = ix.last_batch_stats()
+    ix.close()
+    same(ui, ud, gi, gd)   # counting changes nothing in the search
+    assert not _unexplained(ref, qs, k, ef, gi, gd, oi, od)
+    print(f"E per query: restatement {ost['dist_evals'] / nq:.1f}, GPU lossy {lossy['dist_evals'] / nq:.1f}, "
+          f"GPU exact-visited {exact['dist_evals'] / nq:.1f}; X {ost['expansions'] / nq:.1f} / "
+          f"{exact['expansions'] / nq:.1f}")
+    assert lossy["dist_evals"] > ost["dist_evals"]   # the squeezed cache did re-evaluate
+    assert abs(exact["expansions"] - ost["expansions"]) <= 0.001 * ost["expansions"]
+    assert abs(exact["dist_evals"] - ost["dist_evals"]) <= 0.001 * ost["dist_evals"]
+
+
 @pytest.mark.parametrize("ef", [64, 128, 256])
 def test_configs2_glove_cosine_d100_large_ef(ef):
     """configs[2]: 100-d cosine (stored rows normalized on upload, queries

@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <array>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -1216,9 +1217,19 @@ int run_hnsw(wv_index* ix, const float* d_q, int nq, int k, int ef, const uint64
     hp.status = ix->status.as<int32_t>();
     hp.counters = ix->counters.as<uint32_t>();
     if (ix->pq_on) hp.pq = pq_params(ix);   // compressed: PQ distances (search.go:171-199)
+    // diagnostic: exact per-query visited bitmaps for the evaluation counts
+    // (a bounded sample: nq x N bits of scratch, freed after the launch)
+    void* uniq = nullptr;
+    if (std::getenv("WV_HNSW_UNIQUE_COUNTS") && nq <= 4096) {
+        hp.uniq_words = (ix->gn + 63) / 64;
+        HIP_TRY(hipMallocAsync(&uniq, (size_t)nq * hp.uniq_words * 8, s));
+        HIP_TRY(hipMemsetAsync(uniq, 0, (size_t)nq * hp.uniq_words * 8, s));
+        hp.uniq = static_cast<unsigned long long*>(uniq);
+    }
     TREC(4);
     HIP_TRY(wv_launch_hnsw(&hp, wpb, s));
     TREC(5);
+    if (uniq) HIP_TRY(hipFreeAsync(uniq, s));
     HIP_TRY(ix->stat_acc.ensure(32));
     HIP_TRY(wv_launch_hnsw_stats(ix->counters.as<uint32_t>(), nq, ix->stat_acc.as<unsigned long long>(), s));
     if (!ix->pq_on) {
@@ -1954,6 +1965,15 @@ int wv_index_build_graph(wv_index* ix, int ef_construction, uint64_t seed, int b
     while (wpb > 1 && (size_t)wpb * per_wave * 4 > 160 * 1024) --wpb;
     const int bmax = 16384;
     uint64_t done = 1;
+    // WV_BUILD_TRACE=1 (diagnostic): per-phase device times (events) summed
+    // over intervals of 64 batches, printed to stderr with the host time
+    const bool trace = std::getenv("WV_BUILD_TRACE") != nullptr;
+    hipEvent_t tev[5] = {};
+    double tph[4] = {0, 0, 0, 0};
+    uint64_t tbatches = 0, treq = 0, truns = 0;
+    auto thost = std::chrono::steady_clock::now();
+    if (trace)
+        for (auto& e : tev) HIP_TRY(hipEventCreate(&e));
     while (done < n) {
         const int nb = (int)std::min<uint64_t>(n - done, std::max<uint64_t>(1, std::min<uint64_t>(bmax, done / batch_div)));
         int lb = 1;
@@ -2011,8 +2031,11 @@ int wv_index_build_graph(wv_index* ix, int ef_construction, uint64_t seed, int b
         b.countsU = ix->b_cntu.as<uint32_t>();
         b.req_key = ix->b_rk.as<uint64_t>();
         b.req_node = ix->b_rn.as<uint32_t>();
+        if (trace) HIP_TRY(hipEventRecord(tev[0], s));
         HIP_TRY(wv_launch_build_search(&b, wpb, s));
+        if (trace) HIP_TRY(hipEventRecord(tev[1], s));
         HIP_TRY(wv_launch_build_select(&b, s));
+        if (trace) HIP_TRY(hipEventRecord(tev[2], s));
         // reverse links grouped by (level, neighbour), batch order kept (stable)
         size_t tb = 0, tb2 = 0, tb3 = 0;
         HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, ix->b_rk.as<uint64_t>(), ix->b_rk2.as<uint64_t>(),
@@ -2033,6 +2056,7 @@ int wv_index_build_graph(wv_index* ix, int ef_construction, uint64_t seed, int b
         HIP_TRY(hipcub::DeviceScan::ExclusiveSum(ix->b_tmp.p, tb3, ix->b_ul.as<uint32_t>(), ix->b_uo.as<uint32_t>(),
                                                  (int)nreq, s));
         uint32_t n_runs = 0;
+        if (trace) HIP_TRY(hipEventRecord(tev[3], s));
         HIP_TRY(hipMemcpyAsync(&n_runs, ix->b_nr.p, 4, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
         b.run_key = ix->b_uk.as<uint64_t>();
@@ -2041,6 +2065,30 @@ int wv_index_build_graph(wv_index* ix, int ef_construction, uint64_t seed, int b
         b.sorted_node = ix->b_rn2.as<uint32_t>();
         b.n_runs = (int)n_runs;
         HIP_TRY(wv_launch_build_link(&b, s));
+        if (trace) {
+            HIP_TRY(hipEventRecord(tev[4], s));
+            HIP_TRY(hipEventSynchronize(tev[4]));
+            for (int i = 0; i < 4; ++i) {
+                float ms = 0.f;
+                HIP_TRY(hipEventElapsedTime(&ms, tev[i], tev[i + 1]));
+                tph[i] += ms;
+            }
+            ++tbatches;
+            treq += nreq;
+            truns += n_runs;
+            if (tbatches % 64 == 0 || done + nb >= n) {
+                const auto now = std::chrono::steady_clock::now();
+                std::fprintf(stderr,
+                             "[build] done %llu nb %d lb %d | %llu batches: host %.1f ms, search %.1f select %.1f "
+                             "sort %.1f link %.1f ms, req %.2fM runs %.2fM\n",
+                             (unsigned long long)(done + nb), nb, lb, (unsigned long long)tbatches,
+                             std::chrono::duration<double, std::milli>(now - thost).count(), tph[0], tph[1], tph[2],
+                             tph[3], treq / 1e6, truns / 1e6);
+                thost = now;
+                tph[0] = tph[1] = tph[2] = tph[3] = 0;
+                tbatches = treq = truns = 0;
+            }
+        }
         // the batch is in the graph: its levels make it reachable for the next one
         HIP_TRY(hipMemcpyAsync(ix->levels.as<int8_t>() + done, lv.data() + done, nb, hipMemcpyHostToDevice, s));
         for (int i = 0; i < nb; ++i)   // insert.go:202-213: a higher node becomes the entrypoint
@@ -2048,6 +2096,8 @@ int wv_index_build_graph(wv_index* ix, int ef_construction, uint64_t seed, int b
         done += nb;
     }
     HIP_TRY(hipStreamSynchronize(s));
+    if (trace)
+        for (auto& e : tev) HIP_TRY(hipEventDestroy(e));
     ix->nil_host.assign(ix->bm_words, ~0ull);
     for (uint64_t i = 0; i < lv.size(); ++i)
         if (lv[i] >= 0) ix->nil_host[i >> 6] &= ~(1ull << (i & 63));

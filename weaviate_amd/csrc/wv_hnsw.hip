@@ -88,7 +88,25 @@ struct WaveState {
     uint32_t* vc;
     uint32_t* xs;
     uint32_t* ltomb;
+    unsigned long long* ub;   // this query's exact visited bitmap (diagnostic counts; nullable)
 };
+
+// the diagnostic count of a batch's layer-0 evaluations: nodes first
+// evaluated now (their bit set by this wave); every evaluation otherwise
+__device__ __forceinline__ uint32_t eval_count(const WaveState& w, int level, int nb, bool v0, uint32_t id0, bool v1,
+                                               uint32_t id1) {
+    if (level != 0 || !w.ub) return (uint32_t)nb;
+    bool f0 = false, f1 = false;
+    if (v0) {
+        const unsigned long long b = 1ull << (id0 & 63);
+        f0 = !(atomicOr(w.ub + (id0 >> 6), b) & b);
+    }
+    if (v1) {
+        const unsigned long long b = 1ull << (id1 & 63);
+        f1 = !(atomicOr(w.ub + (id1 >> 6), b) & b);
+    }
+    return (uint32_t)(__popcll(__ballot(f0)) + __popcll(__ballot(f1)));
+}
 
 __device__ __forceinline__ uint32_t hash32(uint32_t x) { return x * 2654435761u; }
 
@@ -245,7 +263,7 @@ __device__ __forceinline__ void search_layer(const HnswParams& p, WaveState& w_i
                     exact_dist_rows<METRIC, WV_HNSW_RPG>(w.qv, p.X, p.ldx, p.D, w.Bi + base, nb - base, w.Bd + base,
                                                          lane);
             }
-            n_dist += nb;
+            n_dist += eval_count(w, level, nb, v0, id0, v1, id1);
             wave_sync();
             ts.lap(3);
 
@@ -497,7 +515,7 @@ __device__ __forceinline__ void search_layer_reg(const HnswParams& p, WaveState&
                     exact_dist_rows<METRIC, WV_HNSW_RPG, true>(w.qv, p.X, p.ldx, p.D, w.Bi + base, nb - base, w.Bd + base,
                                                          lane);
             }
-            n_dist += nb;
+            n_dist += eval_count(w, level, nb, v0, id0, v1, id1);
             wave_sync();
             ts.lap(3);
             // ---- keep test against the batch's starting R (as the LDS path's
@@ -693,6 +711,7 @@ __global__ __launch_bounds__(256) void wv_hnsw_kernel(HnswParams p) {
     w.vc = reinterpret_cast<uint32_t*>(cur); cur += (1 << p.vc_log2);
     w.xs = reinterpret_cast<uint32_t*>(cur); cur += (1 << p.xs_log2);
     w.ltomb = reinterpret_cast<uint32_t*>(cur); cur += MAX_LOCAL_TOMB;
+    w.ub = p.uniq ? p.uniq + (uint64_t)q * p.uniq_words : nullptr;
     if constexpr (NR > 0) knn_one_reg<METRIC, PQ, NR>(p, w, q);
     else knn_one<METRIC, PQ>(p, w, q);
 }
@@ -757,6 +776,7 @@ __global__ __launch_bounds__(256) void wv_build_search_kernel(BuildParams b) {
     const HnswParams& p = b.h;
     float* cur = lds + (uint64_t)wave * p.per_wave_words;
     WaveState w;
+    w.ub = nullptr;
     w.qv = cur; cur += p.dpad;
     w.Rd = cur; cur += p.efc; w.Ri = reinterpret_cast<uint32_t*>(cur); cur += p.efc;
     w.Rd2 = cur; cur += p.efc; w.Ri2 = reinterpret_cast<uint32_t*>(cur); cur += p.efc;

@@ -322,6 +322,13 @@ struct HnswParams {
     int32_t* status;     // bit0 side overflow, bit1 expanded-set overflow
     uint32_t* counters;  // [nq][2]: distance evaluations, expansions (nullable)
     PqParams pq;         // compressed index: distances from codes (search.go:171-199)
+    // diagnostic (WV_HNSW_UNIQUE_COUNTS): one exact visited bitmap per query
+    // ([nq][uniq_words], zeroed): layer-0 evaluations are counted once per
+    // node, as the reference's exact visited list does (search.go:256-264) --
+    // the lossy LDS cache's re-evaluations are not -- so the count equals the
+    // restatement's E on the same traversal (nullable: off)
+    unsigned long long* uniq;
+    uint64_t uniq_words;
 };
 
 // Flat search over PQ codes (flat_search.go:19-74 on a compressed index):
