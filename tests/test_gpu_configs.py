@@ -98,6 +98,40 @@ def test_configs0_sift_hnsw_m64_efc128_ef64():
     ix.close()
 
 
+@pytest.mark.parametrize("frac", [0.1, 0.5])
+def test_filtered_hnsw_selective_list_parity_and_fallback_rate(frac):
+    """Filtered HNSW (search.go:74-78 with |allow| >= flatSearchCutoff or
+    forbidFlat; the list applied at layer 0, :282-298) on the configs[0]
+    graph shape at 10 % and 50 % of the rows: the traversal keeps every
+    ineligible node with d <= worst as a side candidate -- hundreds to ~2k
+    per query at 10 % -- so the first pass's 256-entry side set overflows and
+    a second pass with 2048 entries completes the search; results equal the
+    restatement's knnSearchByVector with the list, and at most 1 % of the
+    queries fall back to the exact filtered scan."""
+    import bench
+    n, d, nq, k, ef = 100_000, 128, 500, 10, 64
+    base = counter_sift(1, 0, n, d)
+    qs = counter_sift(2, 0, nq, d)
+    ref = O.Index(d, "l2-squared", 64, 128, capacity=n, seed=1)
+    ref.add_batch(base, threads=THREADS)
+    a = type("A", (), {"allow_frac": frac})()
+    words, n_allowed = bench._allow_words(a, 0, n)
+    allow = W.AllowList.from_ids(np.nonzero(counter_uniform(3, 0, n, 1)[:, 0] < frac)[0], n)
+    ix = W.GPUVectorIndex(d, "l2-squared", capacity=n, max_connections=64)
+    ix.upload_vectors(base)
+    ix.upload_graph(ref.export_graph())
+    gi, gd, gn = ix.search_batch(qs, k, ef=ef, allow=allow, mode="hnsw")
+    st = ix.last_batch_stats()
+    oi, od, on, _ = ref.search_batch(qs, k, ef, allow=words, threads=THREADS)
+    ix.close()
+    fb = st["fallbacks"]
+    print(f"allow {frac:.0%} ({n_allowed} rows): exact fallbacks {fb} of {nq}")
+    assert fb <= 0.01 * nq, fb
+    assert gn.tolist() == on.tolist()
+    bad = [i for i in range(nq) if not tie_aware_equal(gi[i], gd[i], oi[i], od[i])]
+    assert len(bad) <= fb + 0.002 * nq, bad[:10]   # (a fallback answers exactly: a superset in quality)
+
+
 def test_exact_visited_counts_equal_restatement(monkeypatch):
     """The configs[4] line's byte basis (E and X of the reference's
     traversal) is measured on the GPU where the corpus is too large to restate

@@ -32,7 +32,8 @@ hipError_t wv_launch_bf_finalize_wide(const wv::BfFinParams* p, hipStream_t s);
 hipError_t wv_launch_exact_scan(const wv::ScanParams* p, hipStream_t s);
 hipError_t wv_launch_fb(const wv::FbParams* p, hipStream_t s);
 hipError_t wv_launch_fbd(const int32_t* flags, int nq, const wv::FbParams* fb, hipStream_t s);
-hipError_t wv_launch_fbd_mark(const int32_t* status, int nq, int32_t* flags, float* thr, hipStream_t s);
+hipError_t wv_launch_fbd_mark(const int32_t* status, int nq, int32_t* flags, float* thr, const float* out_d,
+                              const int32_t* out_n, int k, hipStream_t s);
 hipError_t wv_launch_hnsw_stats(const uint32_t* counters, int nq, unsigned long long* acc, hipStream_t s);
 hipError_t wv_launch_rownorm(const float* X, uint64_t N, int D, int ldx, float* norm2, unsigned int* maxbits,
                              hipStream_t s);
@@ -1228,6 +1229,25 @@ int run_hnsw(wv_index* ix, const float* d_q, int nq, int k, int ef, const uint64
     }
     TREC(4);
     HIP_TRY(wv_launch_hnsw(&hp, wpb, s));
+    if (filtered && !std::getenv("WV_HNSW_NO_WIDE_SIDE")) {
+        // second pass for the queries whose side set or expanded-set table
+        // overflowed (status != 0; the others' waves exit at once): the same
+        // search with a 2048-entry side set and a 2048-slot expanded set --
+        // selective filters traverse many ineligible nodes (search.go:282-298:
+        // at 10 % of the rows the reference's candidate heap reaches ~1.8k).
+        // Only what still overflows here takes the exact fallback.
+        wv::HnswParams h2 = hp;
+        h2.redo = ix->status.as<int32_t>();
+        h2.sc = 2048;
+        h2.xs_log2 = 11;
+        const int fixed2 = wv_hnsw_per_wave_words(ix->dpad, efc, h2.sc, 0, h2.xs_log2) - 1;
+        h2.vc_log2 = choose_vc_log2(fixed2 + 1024, fixed2);
+        int pw2 = (wv_hnsw_per_wave_words(ix->dpad, efc, h2.sc, h2.vc_log2, h2.xs_log2) + 3) & ~3;
+        h2.per_wave_words = pw2;
+        int wpb2 = 4;
+        while (wpb2 > 1 && (size_t)wpb2 * pw2 * 4 > 160 * 1024) --wpb2;
+        if ((size_t)pw2 * 4 <= 160 * 1024) HIP_TRY(wv_launch_hnsw(&h2, wpb2, s));
+    }
     TREC(5);
     if (uniq) HIP_TRY(hipFreeAsync(uniq, s));
     HIP_TRY(ix->stat_acc.ensure(32));
@@ -1236,7 +1256,8 @@ int run_hnsw(wv_index* ix, const float* d_q, int nq, int k, int ef, const uint64
         // queries whose side state outgrew LDS: exact answer on the device
         HIP_TRY(ix->fail.ensure((size_t)nq * 4));
         HIP_TRY(ix->fail_thr.ensure((size_t)nq * 4));
-        HIP_TRY(wv_launch_fbd_mark(ix->status.as<int32_t>(), nq, ix->fail.as<int32_t>(), ix->fail_thr.as<float>(), s));
+        HIP_TRY(wv_launch_fbd_mark(ix->status.as<int32_t>(), nq, ix->fail.as<int32_t>(), ix->fail_thr.as<float>(),
+                                   d_out_d, d_out_n, k, s));
         return queue_fbd(ix, d_q, nq, k, d_allow, allow_nbits, allow_stride, d_out_ids, d_out_d, d_out_n, s);
     }
     std::vector<int32_t> st(nq);

@@ -1216,12 +1216,17 @@ __global__ void wv_hnsw_stats_kernel(const uint32_t* __restrict__ ct, int nq, un
 }
 
 __global__ void wv_fbd_mark_kernel(const int32_t* __restrict__ status, int nq, int32_t* __restrict__ flags,
-                                   float* __restrict__ thr) {
-    // HNSW queries whose side state overflowed: exact answer, no threshold
+                                   float* __restrict__ thr, const float* __restrict__ out_d,
+                                   const int32_t* __restrict__ out_n, int k) {
+    // HNSW queries whose side state overflowed: exact answer.  Their results
+    // so far are eligible rows with exact distances, so the k-th of them (when
+    // there are k) bounds the true k-th distance: the filter keeps only rows
+    // at or under it (no threshold otherwise)
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= nq) return;
-    flags[q] = status[q] != 0;
-    thr[q] = __builtin_inff();
+    const bool f = status[q] != 0;
+    flags[q] = f;
+    thr[q] = f && out_n && out_n[q] >= k && k > 0 ? out_d[(size_t)q * k + k - 1] : __builtin_inff();
 }
 
 template <int METRIC>
@@ -1644,9 +1649,11 @@ hipError_t wv_launch_hnsw_stats(const uint32_t* counters, int nq, unsigned long 
     return hipGetLastError();
 }
 
-hipError_t wv_launch_fbd_mark(const int32_t* status, int nq, int32_t* flags, float* thr, hipStream_t s) {
+hipError_t wv_launch_fbd_mark(const int32_t* status, int nq, int32_t* flags, float* thr, const float* out_d,
+                              const int32_t* out_n, int k, hipStream_t s) {
     if (nq == 0) return hipSuccess;
-    hipLaunchKernelGGL(wv::wv_fbd_mark_kernel, dim3((nq + 255) / 256), dim3(256), 0, s, status, nq, flags, thr);
+    hipLaunchKernelGGL(wv::wv_fbd_mark_kernel, dim3((nq + 255) / 256), dim3(256), 0, s, status, nq, flags, thr, out_d,
+                       out_n, k);
     return hipGetLastError();
 }
 

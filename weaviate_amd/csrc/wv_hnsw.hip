@@ -698,6 +698,7 @@ __global__ __launch_bounds__(256) void wv_hnsw_kernel(HnswParams p) {
     const int wave = threadIdx.x >> 6;
     const int q = blockIdx.x * (blockDim.x >> 6) + wave;
     if (q >= p.nq) return;
+    if (p.redo && p.redo[q] == 0) return;   // (second pass: this query completed)
     float* base = lds + (uint64_t)wave * p.per_wave_words;
     WaveState w;
     float* cur = base;

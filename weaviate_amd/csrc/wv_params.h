@@ -329,6 +329,9 @@ struct HnswParams {
     // restatement's E on the same traversal (nullable: off)
     unsigned long long* uniq;
     uint64_t uniq_words;
+    // a second pass (nullable): only the queries whose entry here is non-zero
+    // (the first pass's status: its side state overflowed) search again
+    const int32_t* redo;
 };
 
 // Flat search over PQ codes (flat_search.go:19-74 on a compressed index):
