@@ -248,6 +248,15 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16_kernel(H16Params p) {
                                                               0, 0, 0);
                 accB = __builtin_amdgcn_mfma_f32_32x32x16_f16(ak, __builtin_bit_cast(half8, bq1[k]), k == 0 ? xc : accB,
                                                               0, 0, 0);
+#ifndef WV_H16_XC_INPLACE
+                // (xc stays live past both first MFMAs: neither accumulator
+                // is allocated in place of the C-in, whose registers the next
+                // half's head then reuses -- in place, the head landed on a
+                // live accumulator and the compiler copied it out: 8
+                // v_mov_b64 + s_nop per half, and the loop-carried C-in once
+                // more per tile)
+                if (k == 0) asm volatile("" ::"v"(xc));
+#endif
                 between(k);
             }
             __builtin_amdgcn_sched_barrier(0);
@@ -256,6 +265,10 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16_kernel(H16Params p) {
         // v_min3 chains per accumulator, two ops per k-step
         auto min_steps = [&](const floatx16& A, const floatx16& B, float& mA, float& mB) {
             return [&](int k) {
+                // (each step pinned by an asm use: IR sinking otherwise moved
+                // the whole chain past the MFMAs of phase E to the join with
+                // the last tile's min16 -- 16 serial v_min3 per tile)
+
                 // chain c of A covers keys 4c .. 4c + 3; B likewise
                 if (k == 0) { mA = fminf(fminf(A[0], A[1]), A[2]); mB = fminf(fminf(B[0], B[1]), B[2]); }
                 else if (k == 1) { mA = fminf(fminf(mA, A[3]), A[4]); mB = fminf(fminf(mB, B[3]), B[4]); }
@@ -270,6 +283,7 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16_kernel(H16Params p) {
 #pragma unroll
                     for (int r = NS <= 7 ? 2 * NS + 1 : 15; r < 16; ++r) { mA = fminf(mA, A[r]); mB = fminf(mB, B[r]); }
                 }
+                asm volatile("" : "+v"(mA), "+v"(mB));
             };
         };
         // eligibility of a tile's 64 rows for this lane's two columns (bits of
