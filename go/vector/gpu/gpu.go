@@ -27,7 +27,10 @@
 //	Delete(ids...)   -> cpu.Delete, then wv_mirror_delete (delete.go:29-84)
 //	SearchByVector   -> wv_mirror_search (micro-batched; search.go:64-79)
 //	SearchByVectorDistance -> wv_mirror_search_by_distance (search.go:90-158)
-//	UpdateUserConfig -> cpu.UpdateUserConfig, then wv_mirror_update_config
+//	UpdateUserConfig -> cpu.UpdateUserConfig, then wv_mirror_update_config;
+//	                    PQ enabled at runtime: the CPU index answers until a
+//	                    flush + wv_mirror_compact after Compress turned the
+//	                    mirror to the codes (config_update.go:97-120)
 //
 // Rows added after the last graph snapshot are searched exactly beside the
 // graph; once wv_mirror_needs_compaction reports enough of them, a background
@@ -125,6 +128,7 @@ type Index struct {
 	mu         sync.RWMutex // calls shared; the log flushes, PostStartup and close exclusive
 	compacting atomic.Bool
 	closed     atomic.Bool
+	pqPending  atomic.Bool // PQ enabled at runtime, the mirror not yet serving the codes: the CPU index answers
 	handle     cgo.Handle      // this Index, for the library's callbacks (its threads call them)
 	ctx        *C.uintptr_t    // C memory holding handle: the callbacks' ctx, valid until close
 	metrics    *mirrorMetrics  // nil unless Options.Metrics
@@ -318,7 +322,7 @@ func allowIDs(allow helpers.AllowList) (*C.uint64_t, C.uint64_t, C.int) {
 func (g *Index) SearchByVector(vector []float32, k int, allow helpers.AllowList) ([]uint64, []float32, error) {
 	g.mu.RLock()
 	defer g.mu.RUnlock()
-	if len(vector) == 0 || k <= 0 || g.closed.Load() {
+	if len(vector) == 0 || k <= 0 || g.closed.Load() || g.pqPending.Load() {
 		return g.cpuIndex.SearchByVector(vector, k, allow)
 	}
 	ids := make([]uint64, k)
@@ -345,7 +349,7 @@ func (g *Index) SearchByVectorDistance(vector []float32, dist float32, maxLimit 
 ) ([]uint64, []float32, error) {
 	g.mu.RLock()
 	defer g.mu.RUnlock()
-	if len(vector) == 0 || g.closed.Load() {
+	if len(vector) == 0 || g.closed.Load() || g.pqPending.Load() {
 		return g.cpuIndex.SearchByVectorDistance(vector, dist, maxLimit, allow)
 	}
 	ap, an, filtered := allowIDs(allow)
@@ -370,19 +374,71 @@ func (g *Index) SearchByVectorDistance(vector []float32, dist float32, maxLimit 
 	}
 }
 
-// UpdateUserConfig mirrors hnsw.UpdateUserConfig (config_update.go:79-120): ef,
-// dynamic ef and flatSearchCutoff change the search path.
+// UpdateUserConfig mirrors hnsw.UpdateUserConfig (config_update.go:79-128): ef,
+// dynamic ef and flatSearchCutoff change the search path at once.  Enabling
+// PQ starts hnsw's Compress in a goroutine (:97-120 -> compress.go:39-99),
+// which ends with the AddPQ record in the commit log and calls the callback:
+// from the request on, searches go to the CPU index (it serves uncompressed
+// while it fits, then compressed), and each callback flushes the log and
+// compacts the mirror -- the compaction that reads the AddPQ record encodes
+// every row on the device and serves the codes (wv_mirror.cpp enable_pq),
+// with no write needed to trigger it; then the mirror answers again.
 func (g *Index) UpdateUserConfig(updated schema.VectorIndexConfig, callback func()) error {
-	if err := g.cpuIndex.UpdateUserConfig(updated, callback); err != nil {
+	uc, isUC := updated.(ent.UserConfig)
+	g.mu.RLock() // (the mirror is not destroyed under mu)
+	enablePQ := isUC && uc.PQ.Enabled && !g.closed.Load() && !g.mirrorCompressed()
+	if enablePQ {
+		g.pqPending.Store(true)
+	}
+	g.mu.RUnlock()
+	err := g.cpuIndex.UpdateUserConfig(updated, func() {
+		callback()
+		if enablePQ {
+			go g.syncCompression()
+		}
+	})
+	if err != nil {
+		if enablePQ {
+			g.pqPending.Store(false)
+		}
 		return err
 	}
 	g.mu.RLock()
 	defer g.mu.RUnlock()
-	if uc, ok := updated.(ent.UserConfig); ok && !g.closed.Load() {
+	if isUC && !g.closed.Load() {
 		cfg := configOf(uc, g.device)
 		C.wv_mirror_update_config(g.m, &cfg)
 	}
 	return nil
+}
+
+// mirrorCompressed: the mirror serves PQ codes (wv_mirror_stats.pq).
+func (g *Index) mirrorCompressed() bool {
+	var st C.wv_mirror_stats
+	return C.wv_mirror_get_stats(g.m, &st) == 0 && st.pq != 0
+}
+
+// syncCompression: a flush of the CPU index's log and a compaction, so the
+// mirror reads the AddPQ record Compress wrote; it clears pqPending once the
+// mirror serves the codes (hnsw calls the callback before Compress starts
+// too -- that pass finds no record and leaves the CPU index answering).
+func (g *Index) syncCompression() {
+	g.mu.Lock()
+	if g.closed.Load() {
+		g.mu.Unlock()
+		return
+	}
+	err := g.cpuIndex.Flush()
+	g.mu.Unlock()
+	g.mu.RLock()
+	defer g.mu.RUnlock()
+	if err != nil || g.closed.Load() {
+		return
+	}
+	C.wv_mirror_compact(g.m)
+	if g.mirrorCompressed() {
+		g.pqPending.Store(false)
+	}
 }
 
 func (g *Index) close() {

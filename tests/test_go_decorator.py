@@ -52,6 +52,15 @@ def test_go_decorator_binds_only_header_symbols():
     add = re.search(r"func \(g \*Index\) Add\(.*?\n}\n", src, re.S).group(0)
     assert add.index("C.wv_mirror_needs_compaction(") < add.rindex("g.mu.RUnlock()") < add.index("g.startCompaction()")
     assert "!g.closed.Load()" in add
+    # runtime PQ enablement (config_update.go:97-128): the CPU index answers
+    # while pending, each callback flushes the log and compacts the mirror
+    uuc = re.search(r"func \(g \*Index\) UpdateUserConfig\(.*?\n}\n", src, re.S).group(0)
+    assert "g.pqPending.Store(true)" in uuc and "go g.syncCompression()" in uuc
+    sc = re.search(r"func \(g \*Index\) syncCompression\(.*?\n}\n", src, re.S).group(0)
+    assert sc.index("cpuIndex.Flush()") < sc.index("C.wv_mirror_compact(") < sc.index("g.pqPending.Store(false)")
+    for method in ("SearchByVector", "SearchByVectorDistance"):
+        body = re.search(r"func \(g \*Index\) %s\(.*?\n}\n" % method, src, re.S).group(0)
+        assert "g.pqPending.Load()" in body, method
     # close releases mu before joining the library's thread (a resync's flush takes mu)
     cl = re.search(r"func \(g \*Index\) close\(.*?\n}\n", src, re.S).group(0)
     assert cl.index("g.mu.Unlock()") < cl.index("C.wv_mirror_destroy(") < cl.index("g.freeHandles()")
@@ -87,7 +96,7 @@ def test_mirror_lifecycle_from_commit_log(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["async", "heal", "pq", "epgone"])
+@pytest.mark.parametrize("mode", ["async", "heal", "pq", "epgone", "pqlive"])
 def test_mirror_lifecycle_modes(tmp_path, mode):
     """async: PostStartup returns at once and the mirror builds on its own
     thread while writers and searchers run (the CPU index answers until it is
@@ -98,7 +107,11 @@ def test_mirror_lifecycle_modes(tmp_path, mode):
     restatement's PQ searches (compress.go:39-99, search.go:172-197);
     epgone: the log's entrypoint lost its object -- HNSW searches answer
     WV_EDELETED as knnSearchByVector errors (search.go:467-476), a flat one
-    equals flatSearch's."""
+    equals flatSearch's; pqlive: the class is compressed while serving
+    (UpdateUserConfig with PQ.Enabled -> Compress, config_update.go:97-120,
+    compress.go:39-99) with no later write, the decorator's callback flushes
+    and compacts, and the mirror then answers as the restatement's PQ
+    searches."""
     binp = os.path.join(ROOT, "tests", "native", "mirror_replay")
     assert os.path.exists(binp), "build tests/native first (__graft_entry__.build())"
     p = subprocess.run([binp, str(tmp_path), "0", mode], capture_output=True, text=True, timeout=240)
@@ -115,7 +128,7 @@ def test_mirror_lifecycle_modes(tmp_path, mode):
     if mode == "heal":
         # two failures: the second the moment the first resync went live
         assert r["resyncs"] >= 2 and r["stale_answers"] > 0
-    if mode == "pq":
+    if mode in ("pq", "pqlive"):
         assert r["pq"] == 1
     print(r)
 
@@ -150,8 +163,8 @@ def test_host_runtime_under_thread_sanitizer(tmp_path):
         return mode, p
 
     with ThreadPoolExecutor(2) as ex:
-        for mode, p in ex.map(run, ["sync", "async", "heal", "pq"]):
+        for mode, p in ex.map(run, ["sync", "async", "heal", "pq", "epgone", "pqlive"]):
             races = p.stderr.count("WARNING: ThreadSanitizer")
             assert races == 0 and p.returncode == 0, (mode, races, p.stderr[-4000:])
             r = json.loads(p.stdout.strip().splitlines()[-1])
-            assert r["ok"] and r["mode"] == mode and r["compactions"] >= 1
+            assert r["ok"] and r["mode"] == mode and (mode == "epgone" or r["compactions"] >= 1)
