@@ -224,6 +224,33 @@ class Ctx:
         if self.ws > 1:
             self.dist.barrier()
 
+    def per_rank(self, x: int) -> list:
+        """x from every rank, in rank order (a collective: every rank calls it)"""
+        if self.ws == 1:
+            return [int(x)]
+        torch = self.torch
+        t = torch.tensor([int(x)], dtype=torch.int64, device="cpu" if self.gloo else self.dev)
+        parts = [torch.zeros_like(t) for _ in range(self.ws)]
+        self.dist.all_gather(parts, t)
+        return [int(p.item()) for p in parts]
+
+    def info(self) -> dict:
+        """what the first multi-GPU run must be checked against line by line:
+        the backend (torch "nccl" = RCCL on ROCm), the world it saw, the
+        devices behind the ranks"""
+        d = {"world_size": self.ws, "distinct_devices": self.n_devices, "rank0_device": self.gpu}
+        if self.ws > 1:
+            d["backend"] = str(self.dist.get_backend())
+            d["uses_rccl"] = d["backend"] == "nccl"
+            d["process_group_size"] = self.dist.get_world_size()
+            try:
+                d["rccl_version"] = ".".join(str(v) for v in self.torch.cuda.nccl.version())
+            except Exception as e:  # (informational)
+                d["rccl_version"] = f"unavailable: {type(e).__name__}"
+        else:
+            d["uses_rccl"] = False
+        return d
+
     def max_over_ranks(self, x: float) -> float:
         if self.ws == 1:
             return x
@@ -572,7 +599,9 @@ def c4_line(args, ctx, W, with_cpu):
         legs["allow_%g%%" % (100 * frac)] = leg
     ix.close()
     del base
+    rows_per_rank = ctx.per_rank(n_local)
     return {"workload": f"exact {K}-NN, {N:,} x {D}-d dot, {NQ}-query batch, shared allow list (BASELINE configs[3])",
+            "rows_per_rank": rows_per_rank,
             "parallelism": (f"corpus sharded over {ws} GPU(s) by id range ({n_local:,} rows per GPU), RCCL all-gather "
                             f"of per-shard top-k + device merge" if ws > 1 else "one GPU holding the whole corpus"),
             "scaling": "strong (fixed corpus and batch)", "setup_s": round(setup_s, 1),
@@ -814,8 +843,9 @@ def run_hnsw(args, ctx, W, with_cpu):
                  ids=hi_ids, dists=hi_d, shard_ids=shard_ids, shard_dists=shard_d, lo=lo, n_local=n_local,
                  **{"g_" + k: np.asarray(v) for k, v in ix.download_graph().items()})
     units = NQ * (1 if corpus else ws)
+    rows_per_rank = ctx.per_rank(n_local)
     res = {
-        "metric": METRIC, "value": round(units * args.steps / elapsed, 1), "unit": "queries/s",
+        "metric": METRIC, "value": round(units * args.steps / elapsed, 1), "unit": "queries/s", "rows_per_rank": rows_per_rank,
         "ms_per_step": round(1000 * elapsed / args.steps, 3), "recall@10": round(rec, 4),
         "recall_truth": "exact path on the same queries (all of them)",
         "scaling": "strong" if corpus else "weak",
@@ -1328,6 +1358,7 @@ def main():
                 result["hnsw_c5_sharded"] = h
             except Exception as e:   # reported, not fatal to the headline line
                 result["hnsw_c5_sharded"] = {"error": f"{type(e).__name__}: {e}"}
+    result["distributed"] = ctx.info()
     if ws > 1:
         ctx.barrier()
         ctx.dist.destroy_process_group()

@@ -252,7 +252,8 @@ int search_shards(wv_group* g, const float* queries, int nq, int k, int ef, cons
     const int n = (int)g->m.size();
     const size_t nk = (size_t)nq * k;
     // 0. the batch into pinned staging once (a previous call's copies from
-    // it have landed: every call ends with its members' streams drained)
+    // it have landed: every call ends after its root stream, which waited
+    // for every member's results, hence for their copies of the staging)
     G_HIP(g->h_q.ensure((size_t)nq * g->dim * 4));
     std::memcpy(g->h_q.p, queries, (size_t)nq * g->dim * 4);
     // 1. every member: its queries, its slice of the allow list, its search
@@ -317,10 +318,10 @@ int search_shards(wv_group* g, const float* queries, int nq, int k, int ef, cons
                 G_NCCL(ncclGather(mb.n.p, is_root ? rn : nullptr, (size_t)nq, ncclInt32, 0, g->comms[i], mb.s));
             }
             G_NCCL(ncclGroupEnd());
-            for (int i = 1; i < n; ++i) {   // senders done before their buffers are reused
-                G_HIP(hipSetDevice(g->m[i].dev));
-                G_HIP(hipStreamSynchronize(g->m[i].s));
-            }
+            // (no drain of the senders: their next writes to ids / d / n are
+            // queued on the same streams, after these sends; and the root's
+            // gather completing -- waited for below -- means every sender's
+            // data left, so the staging the next call rewrites is free)
             G_HIP(hipSetDevice(root.dev));
         } else {
             for (int i = 0; i < n; ++i) {
@@ -341,12 +342,11 @@ int search_shards(wv_group* g, const float* queries, int nq, int k, int ef, cons
         G_HIP(hipMemcpyAsync(out_ids, g->o_ids.p, nk * 8, hipMemcpyDeviceToHost, root.s));
         G_HIP(hipMemcpyAsync(out_d, g->o_d.p, nk * 4, hipMemcpyDeviceToHost, root.s));
         G_HIP(hipMemcpyAsync(out_n, g->o_n.p, (size_t)nq * 4, hipMemcpyDeviceToHost, root.s));
+        // the one wait of a call (its results go to the host): the root's
+        // stream waited for every member's copies (events) or gather, so the
+        // members' streams need no drain -- the next call's work queues
+        // behind this call's on each of them
         G_HIP(hipStreamSynchronize(root.s));
-        if (g->comms.empty())
-            for (int i = 1; i < n; ++i) {
-                G_HIP(hipSetDevice(g->m[i].dev));
-                G_HIP(hipStreamSynchronize(g->m[i].s));
-            }
         return WV_OK;
     }();
     if (rc) drain_members(g);
