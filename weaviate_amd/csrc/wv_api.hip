@@ -53,7 +53,7 @@ hipError_t wv_launch_split_rows(const float* in, int ld_in, const uint64_t* ids,
                                 float scale, void* out, int ld_out, uint64_t out_row0, hipStream_t s);
 hipError_t wv_launch_h16_rows(const float* in, int ld_in, const uint64_t* ids, uint64_t n, int D, int ns, float sign,
                               float scale, const unsigned int* scale_from_max, void* out, uint64_t out_row0,
-                              unsigned int* res_max_bits, float* res_out, int quad, hipStream_t s);
+                              unsigned int* res_max_bits, float* res_out, int wide_layout, hipStream_t s);
 hipError_t wv_launch_h16_rows_gather(const float* in, int ld_in, const uint32_t* gather, uint64_t n, uint64_t n_pad,
                                      int D, int ns, float scale, void* out, hipStream_t s);
 hipError_t wv_launch_h16_compact_aux(const float* xnorm, const uint32_t* rowidx, uint64_t n, float* cxnorm,
@@ -477,8 +477,20 @@ __global__ void pad_rowidx_kernel(uint32_t* rowidx, uint64_t from, uint64_t to) 
 
 // Ascending list of the rows a shared allow list keeps (allowed, not excluded,
 // < N) into ix->rowidx, padded to whole tiles; *n_ok = its length.
+// The f16 pass runs over a shared allow list's gathered rows when gathering
+// costs less than masking the rest of the corpus: a gathered row moves ~6 D
+// bytes once, a masked row costs the pass ~nq x D of MFMA work (measured at
+// 10M x 768: 0.9 ns per gathered row, 1.6 ns per scanned row per 1000
+// queries) and at least one read of its 2 D-byte image, so compacting pays
+// below n_ok / N = max(1/3, nq / (nq + 560)) -- 64 % at configs[3]'s 1000
+// queries (round 4's fixed rule, 50 %, left the 50 % leg a coin flip).
+static bool worth_compacting(uint64_t n_ok, uint64_t N, int nq) {
+    const double f = std::max(1.0 / 3.0, (double)nq / ((double)nq + 560.0));
+    return (double)n_ok < (double)N * f;
+}
+
 int compact_allowed(wv_index* ix, const uint64_t* d_allow, uint64_t allow_nbits, uint64_t N, uint64_t* n_ok,
-                    hipStream_t s, bool always = false) {
+                    hipStream_t s, bool always = false, int nq = 1) {
     const uint64_t words = (N + 63) / 64;
     const uint64_t allow_words = (allow_nbits + 63) / 64;
     HIP_TRY(ix->ac_cnt.ensure((words + 1) * 4));
@@ -498,8 +510,10 @@ int compact_allowed(wv_index* ix, const uint64_t* d_allow, uint64_t allow_nbits,
     HIP_TRY(hipMemcpyAsync(&total, ix->ac_off.as<uint32_t>() + words, 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     *n_ok = total;
-    if (total == 0 || (2 * (uint64_t)total >= N && !always)) return WV_OK;
-    const uint64_t padded = (total + wv::BF_BN - 1) / wv::BF_BN * wv::BF_BN;
+    // (the row list also serves the fp32 pass, which compacts below 1/2)
+    if (total == 0 || (!worth_compacting(total, N, nq) && 2 * (uint64_t)total >= N && !always)) return WV_OK;
+    // (whole 256-row tiles: the wide-D pass reads the list per tile)
+    const uint64_t padded = (total + wv::HW_BN - 1) / wv::HW_BN * wv::HW_BN;
     HIP_TRY(ix->rowidx.ensure(padded * 4));
     hipLaunchKernelGGL(allowed_scatter_kernel, dim3(blocks), dim3(256), 0, s, d_allow, allow_words,
                        ix->excl.as<uint64_t>(), N, ix->ac_off.as<uint32_t>(), ix->rowidx.as<uint32_t>());
@@ -612,16 +626,18 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
         // the allowed rows' image in list order (whole tiles, zero padded),
         // their |x|^2, and exclusion bits set only past N
         const uint64_t rows = ntl * tile_rows, ew = rows / 64 + 2;
-        const size_t ib = rows * (size_t)ns * 16 * 2;
-        HIP_TRY(ix->cimg16.ensure(ib));
         HIP_TRY(ix->cxnorm.ensure(rows * 4));
         HIP_TRY(ix->cexcl.ensure(ew * 8));
         HIP_TRY(hipMemsetAsync(ix->cxnorm.p, 0, rows * 4, s));
-        HIP_TRY(wv_launch_h16_rows_gather(ix->vecs.as<float>(), ix->ldx, rowidx, N, rows, ix->dim, ns, ix->h16_sx,
-                                          ix->cimg16.p, s));
+        if (!wd) {   // (D > 128: the pass reads the row-major image through the list itself)
+            const size_t ib = rows * (size_t)ns * 16 * 2;
+            HIP_TRY(ix->cimg16.ensure(ib));
+            HIP_TRY(wv_launch_h16_rows_gather(ix->vecs.as<float>(), ix->ldx, rowidx, N, rows, ix->dim, ns, ix->h16_sx,
+                                              ix->cimg16.p, s));
+            ximg = ix->cimg16.p;
+        }
         HIP_TRY(wv_launch_h16_compact_aux(ix->xnorm.as<float>(), rowidx, N, ix->cxnorm.as<float>(),
                                           ix->cexcl.as<uint64_t>(), ew, s));
-        ximg = ix->cimg16.p;
         xnorm = ix->cxnorm.as<float>();
         excl = ix->cexcl.as<uint64_t>();
         allow = nullptr;
@@ -630,6 +646,7 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
         HIP_TRY(wv_launch_h16_xns(xnorm, ntl * tile_rows, ix->h16_sx, ix->qscale.as<float>(), ix->xns.as<float>(), s));
     wv::H16Params hp{};
     hp.X = ximg;
+    hp.rowidx = wd ? rowidx : nullptr;
     hp.Q = ix->qimg16.p;
     hp.xns = ix->xns.as<float>();
     hp.excl = excl;
@@ -872,16 +889,16 @@ int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
         const uint64_t cbits = d_allow && !allow_stride ? allow_nbits : rowmask_nbits;
         if (cmask) {
             uint64_t n_ok = 0;
-            int rc = compact_allowed(ix, cmask, cbits, N, &n_ok, s, d_rowmask != nullptr);
+            int rc = compact_allowed(ix, cmask, cbits, N, &n_ok, s, d_rowmask != nullptr, nq);
             if (rc) return rc;
             if (n_ok == 0) {
                 HIP_TRY(hipMemsetAsync(d_out_n, 0, sizeof(int32_t) * nq, s));
                 return WV_OK;
             }
-            // a list keeping under half the corpus: the scan runs over its
-            // rows -- on the f16 pass over their gathered image (h16_ok), else
-            // on the fp32 pass over the row list
-            const bool compact = (2 * n_ok < N && !std::getenv("WV_BF_NO_COMPACT")) || d_rowmask;
+            // a list worth compacting (worth_compacting): the scan runs over
+            // its rows -- on the f16 pass over their gathered image (h16_ok),
+            // else (below 1/2 or 1/8) on the fp32 pass over the row list
+            const bool compact = (worth_compacting(n_ok, N, nq) && !std::getenv("WV_BF_NO_COMPACT")) || d_rowmask;
             if (compact && h16_ok) {
                 std::vector<int32_t> none;
                 int rc2 = run_h16(ix, d_q, nq, k, nullptr, 0, n_ok, d_out_ids, d_out_d, d_out_n, s, none,
@@ -1599,16 +1616,16 @@ static int rows_written(wv_index* ix, const uint64_t* d_ids, uint64_t n, uint64_
     if (rebuild) HIP_TRY(hipMemsetAsync(exb, 0, 4, ix->stream));
     {
         void* img = ix->ximg16.p;
-        const int quad = 0;
+        const int wide_layout = ix->h16_wide ? 1 : 0;   // (the wide-D kernel's h16w_index image)
         if (rebuild) {
             HIP_TRY(wv_launch_h16_rows(ix->vecs.as<float>(), ix->ldx, nullptr, ix->n_rows, ix->dim, ix->h16_ns, 1.f,
-                                       ix->h16_sx, nullptr, img, 0, exb, nullptr, quad, ix->stream));
+                                       ix->h16_sx, nullptr, img, 0, exb, nullptr, wide_layout, ix->stream));
         } else if (d_ids) {
             HIP_TRY(wv_launch_h16_rows(ix->vecs.as<float>(), ix->ldx, d_ids, n, ix->dim, ix->h16_ns, 1.f, ix->h16_sx,
-                                       nullptr, img, 0, exb, nullptr, quad, ix->stream));
+                                       nullptr, img, 0, exb, nullptr, wide_layout, ix->stream));
         } else {
             HIP_TRY(wv_launch_h16_rows(ix->vecs.as<float>() + first_id * ix->ldx, ix->ldx, nullptr, n, ix->dim,
-                                       ix->h16_ns, 1.f, ix->h16_sx, nullptr, img, first_id, exb, nullptr, quad,
+                                       ix->h16_ns, 1.f, ix->h16_sx, nullptr, img, first_id, exb, nullptr, wide_layout,
                                        ix->stream));
         }
     }

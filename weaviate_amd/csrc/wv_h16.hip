@@ -612,7 +612,6 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16w_kernel(H16Params p) {
     const int l31 = lane & 31;
     const int rh = wave & 1, qq = wave >> 1;
     const int ns = p.ns, nch = ns / KC;
-    const uint4* __restrict__ X = reinterpret_cast<const uint4*>(p.X);
     const uint4* __restrict__ Qg = reinterpret_cast<const uint4*>(p.Q);
     const bool has_allow = p.allow != nullptr;
     int lb = (int)blockIdx.x;
@@ -653,11 +652,37 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16w_kernel(H16Params p) {
         const int wg = wave / KC, wsk = wave % KC;
         const uint64_t gstride = (uint64_t)(8 / KC) * ns * 64;   // 8 / KC groups, in uint4
         const uint4* b_src0 = Qg + (((uint64_t)qb * (HW_BQ / 32) + wg) * ns + wsk) * 64;
+        // Corpus side (round 5): the image is h16w_index (16-row groups of
+        // 1 KiB panels, 64 B of a row per chunk), and the stage's A image is
+        // the tile's 256 rows x 64 B, row after row.  This wave fills pieces
+        // wave and wave + 8 (16 rows each); lane i loads 16 B of row 16 piece
+        // + i / 4 -- row (tile, that row), or that entry of the compacted row
+        // list: a compacted scan needs no gathered image.  The list entries of
+        // tile t + 1 are LDS-DMA'd with tile t's first chunk into a 2-slot
+        // ring and read at the tile change (nch - 1 >= 5 counted waits later;
+        // a VGPR load the compiler does not track could be copied before it
+        // lands).  The 16 B slot i % 4 of a row holds its chunk (i % 4) ^
+        // ((row >> 2) & 3): the MFMA's ds_read_b128 lane groups then hit 16
+        // distinct bank slots.
+        static_assert(KC == 2, "a chunk is one 64 B panel per row");
+        const uint64_t gsb = (uint64_t)ns * 512;   // bytes per 16-row group
+        const char* Xb = reinterpret_cast<const char*>(p.X) + 16 * ((lane & 3) ^ ((lane >> 4) & 3));
+        auto rid_of = [&](uint64_t tile, int j) -> uint64_t {
+            return tile * BN + 16 * (wave + 8 * j) + (lane >> 2);
+        };
+        uint32_t rid_cur[2];
+        const uint32_t rid_ring = ex0 + (uint32_t)(2 * St::EX_U4 * 16 + 8 * 256 + wave * 512);   // + slot 4 KiB + j 256
+        const uint32_t* rid_lds = reinterpret_cast<const uint32_t*>(ex_lds + 2 * St::EX_U4) + 8 * 64 + wave * 128 + lane;
+        // a row's first panel in the image (row group, row in group)
+        uint64_t rbase[2];
+        auto set_rbase = [&] {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) rbase[j] = (uint64_t)(rid_cur[j] >> 4) * gsb + (uint64_t)((rid_cur[j] & 15) * 64);
+        };
         // running sources of the next chunk to fill: +1 chunk (KC KiB steps)
         // per chunk; at a tile's end the corpus side moves on to the next
         // tile's row groups (2 RG ns steps per tile: + (2 RG - 1) ns past the
         // last chunk) and the query side starts over
-        const uint4* a_cur = X + (((uint64_t)t_begin * 2 * RG + wg) * ns + wsk) * 64;
         const uint4* b_cur = b_src0;
         int ft = 0, fc = 0;   // the next chunk to fill
         auto fill_next = [&](int stage) {
@@ -670,11 +695,13 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16w_kernel(H16Params p) {
             const uint32_t dst = lds0 + (uint32_t)(stage * St::U4 * 16) + (uint32_t)(wave * 1024);
             // (wave-uniform by construction; readfirstlane tells the compiler,
             // which must keep the LDS-DMA bases in SGPRs)
-            const uint4* a = uniform_ptr(a_cur);
             const uint4* b = uniform_ptr(b_cur);
 #ifndef WV_H16W_ABLATE_NO_A
-            glds16s(a, (uint32_t)(lane * 16), dst);
-            glds16s(uniform_ptr(a + gstride), (uint32_t)(lane * 16), dst + 8 * 1024);
+            {
+                const uint32_t kofs = (uint32_t)(fc * 1024);
+                glds16(Xb + rbase[0] + kofs, dst);
+                glds16(Xb + rbase[1] + kofs, dst + 8 * 1024);
+            }
 #endif
 #ifndef WV_H16W_ABLATE_NO_B
 #pragma unroll
@@ -682,6 +709,12 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16w_kernel(H16Params p) {
                 glds16s(uniform_ptr(b + j * gstride), (uint32_t)(lane * 16), dst + (uint32_t)(St::A_U4 * 16 + 8 * j * 1024));
 #endif
             if (fc == 0) {
+                if (p.rowidx) {
+                    const uint64_t tn = tile + 1 < p.ntiles_real ? tile + 1 : p.ntiles_real - 1;
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        glds4(p.rowidx + rid_of(tn, j), rid_ring + (uint32_t)(((ft + 1) & 1) * 4096 + 256 * j));
+                }
                 const uint32_t xd = ex0 + (uint32_t)((ft & 1) * St::EX_U4 * 16);
                 if (wave == 0 && L2) {
 #pragma unroll
@@ -695,13 +728,17 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16w_kernel(H16Params p) {
                     if (lane < 2 * St::WORDS || (lane < 4 * St::WORDS && has_allow)) glds4(w, xd + (BN / 4) * 16);
                 }
             }
-            a_cur = a + KC * 64;
             b_cur = b + KC * 64;
             if (++fc == nch) {
                 fc = 0;
                 ++ft;
-                a_cur += (uint64_t)(2 * RG - 1) * ns * 64;
                 b_cur = b_src0;
+                // the next tile's rows: fetched a tile ago, covered by every
+                // chunk's counted wait since (nch >= 3 chunks of >= 4 ops)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    rid_cur[j] = p.rowidx ? rid_lds[(ft & 1) * 1024 + 64 * j] : (uint32_t)rid_of(t_begin + ft, j);
+                set_rbase();
             }
         };
 
@@ -768,7 +805,13 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16w_kernel(H16Params p) {
             m1 = fminf(fminf(m1, A[14]), A[15]);
             return fminf(fminf(m0, m1), fminf(m2, m3));
         };
-        // (the previous segment ended with every stage read and every DMA landed)
+        // (the previous segment ended with every stage read and every DMA
+        // landed: the first tile's rows are waited for alone)
+        if (nchunks > 0) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) rid_cur[j] = p.rowidx ? p.rowidx[rid_of(t_begin, j)] : (uint32_t)rid_of(t_begin, j);
+            set_rbase();
+        }
         if (nchunks > 0) fill_next(0);
         if (nchunks > 1) fill_next(1);
         int t = 0, c = 0, stg = 0;   // the chunk computed: (tile, chunk), its stage
@@ -819,9 +862,11 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16w_kernel(H16Params p) {
             for (int k = 0; k < KC; ++k) {
                 const half8 b0 = __builtin_bit_cast(half8, st[St::A_U4 + ((2 * qq) * KC + k) * 64 + lane]);
                 const half8 b1 = __builtin_bit_cast(half8, st[St::A_U4 + ((2 * qq + 1) * KC + k) * 64 + lane]);
+                // row 32 G + l31's chunk 2 k + khalf (swizzled slot)
+                const int aslot = 4 * l31 + ((2 * k + khalf) ^ ((l31 >> 2) & 3));
 #pragma unroll
                 for (int i = 0; i < RG; ++i) {
-                    const half8 a = __builtin_bit_cast(half8, st[((RG * rh + i) * KC + k) * 64 + lane]);
+                    const half8 a = __builtin_bit_cast(half8, st[128 * (RG * rh + i) + aslot]);
                     acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b0, acc[i][0], 0, 0, 0);
                     acc[i][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b1, acc[i][1], 0, 0, 0);
                 }
@@ -1046,7 +1091,7 @@ __device__ __forceinline__ float pow2_scale_for(float maxabs) {
 __global__ void wv_h16_rows_kernel(const float* in, int ld_in, const uint64_t* ids, const uint32_t* gather,
                                    uint64_t n, int D, int ns, float sign, float scale,
                                    const unsigned int* scale_from_max, uint16_t* out, uint64_t out_row0,
-                                   unsigned int* res_max_bits, float* res_out, int quad) {
+                                   unsigned int* res_max_bits, float* res_out, int wide_layout) {
     const uint64_t r = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (r >= n) return;
@@ -1064,7 +1109,7 @@ __global__ void wv_h16_rows_kernel(const float* in, int ld_in, const uint64_t* i
         const float back = (float)h / scale;
         const float e = x - back;           // exact (Sterbenz) unless h overflowed
         acc = __builtin_fmaf(e, e, acc);
-        out[h16_index(out_row0 + row, k, ns)] =
+        out[wide_layout ? h16w_index(out_row0 + row, k, ns) : h16_index(out_row0 + row, k, ns)] =
             __builtin_bit_cast(uint16_t, h);
     }
     for (int m = 32; m >= 1; m >>= 1) acc += __shfl_xor(acc, m, 64);
@@ -1127,13 +1172,13 @@ float wv_h16_pow2_scale(float maxabs) {
 
 hipError_t wv_launch_h16_rows(const float* in, int ld_in, const uint64_t* ids, uint64_t n, int D, int ns, float sign,
                               float scale, const unsigned int* scale_from_max, void* out, uint64_t out_row0,
-                              unsigned int* res_max_bits, float* res_out, int quad, hipStream_t s) {
+                              unsigned int* res_max_bits, float* res_out, int wide_layout, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    // (quad: unused, always 0 -- the 16x16x32 layout was retired in round 4)
-    if (ns < 1 || ns > wv::HW_NS_MAX || D > ns * 16 || (quad && ns % 2)) return hipErrorInvalidValue;
+    // (wide_layout: the h16w_index image of the wide-D kernel; 0: h16_index)
+    if (ns < 1 || ns > wv::HW_NS_MAX || D > ns * 16) return hipErrorInvalidValue;
     hipLaunchKernelGGL(wv::wv_h16_rows_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, in, ld_in, ids,
                        (const uint32_t*)nullptr, n, D, ns, sign, scale, scale_from_max, static_cast<uint16_t*>(out),
-                       out_row0, res_max_bits, res_out, quad);
+                       out_row0, res_max_bits, res_out, wide_layout);
     return hipGetLastError();
 }
 
@@ -1318,7 +1363,8 @@ hipError_t wv_launch_bf_h16w(const wv::H16Params* p, hipStream_t s) {
     if (l2 && !p->xns) return hipErrorInvalidValue;
     if (p->wide_rows != 128) return hipErrorInvalidValue;
     using St = wv::HWStage<128>;
-    const size_t lds = ((size_t)wv::HW_STAGES * St::U4 + 2 * St::EX_U4) * 16 + 8 * 256;   // + the gtau return slots
+    // + the gtau return slots and the row-list ring (2 slots x 8 waves x 2 x 64 ids)
+    const size_t lds = ((size_t)wv::HW_STAGES * St::U4 + 2 * St::EX_U4) * 16 + 8 * 256 + 2 * 8 * 2 * 256;
     if (l2) hipLaunchKernelGGL((wv::wv_bf_h16w_kernel<true, 128>), dim3(nb), dim3(512), lds, s, *p);
     else hipLaunchKernelGGL((wv::wv_bf_h16w_kernel<false, 128>), dim3(nb), dim3(512), lds, s, *p);
     return hipGetLastError();

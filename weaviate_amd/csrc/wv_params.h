@@ -132,6 +132,18 @@ inline uint64_t h16_index(uint64_t row, int k, int ns) {
     return (block * 64 + lane) * 8 + (uint64_t)(k & 7);
 }
 
+// The wide-D (D > 128) corpus image: 16-row groups of ns * 512 B, each a
+// sequence of 1 KiB panels (32 k, i.e. 64 B, of the group's 16 rows, row
+// after row).  A run of 16 consecutive rows' panel is one contiguous 1 KiB
+// piece (an unfiltered scan's LDS-DMA), and any single row's panel is 64
+// contiguous bytes (a compacted scan's per-lane fill, no gathered copy).
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+inline uint64_t h16w_index(uint64_t row, int k, int ns) {
+    return (row >> 4) * (uint64_t)ns * 256 + (uint64_t)(k >> 5) * 512 + (row & 15) * 32 + (uint64_t)(k & 31);
+}
+
 struct H16Params {
     const void* X;            // corpus image (h16_index), rows padded to whole tiles (zeros)
     const void* Q;            // query image (h16_index over query rows), padded to whole H_BQ blocks
@@ -166,6 +178,11 @@ struct H16Params {
     int xslot;                // 1: use gslot instead of the gtau publish
     int ns;                   // 16-k steps of the images (the wide-D kernel: a multiple of HW_KC)
     int wide_rows;            // the wide-D kernel's rows per wave: 128 (256-row tiles) or 64 (128-row tiles)
+    // the wide-D kernel (round 5): X is row-major (row r's ns * 16 halves at
+    // r * ns * 32 bytes) and its operand blocks are filled per lane; rowidx
+    // (nullable): scan rows rowidx[0 .. N) (a compacted allow list, ascending,
+    // padded to whole 256-row tiles) instead of rows 0 .. N -- no gathered image
+    const uint32_t* rowidx;
 };
 
 // ---- f16 key pass for D > 128 (wv_bf_h16w_kernel, wv_h16.hip) --------------
