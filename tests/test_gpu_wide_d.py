@@ -100,3 +100,41 @@ def test_gathered_allow_list_pass_equals_restatement(d, metric):
             if k <= 64:
                 assert st["fallbacks"] <= len(qs) // 50, (frac, k, st)
     ix.close()
+
+
+@pytest.mark.parametrize("metric", [O.L2, O.DOT])
+def test_device_counted_compaction_edge_lists(metric, monkeypatch):
+    """The wide-D pass compacts a shared allow list without reading its
+    length back (compact_allowed_dev + H16Params.n_dev: the kernel sizes its
+    slots' tile runs from the device count).  Equal to the restatement and to
+    the read-back path (WV_BF_SYNC_COMPACT=1) bit for bit over the edges: an
+    empty list, a list of tombstoned rows only (length 0 on the device), one
+    row, every row, a list shorter than the corpus's bitmap, and a
+    single-query batch (one query block, 256 slots)."""
+    n, d = 30_001, 256
+    base, qs = _gauss(n, d, 21), _gauss(300, d, 22)
+    ix = W.GPUVectorIndex(d, NAMES[metric], capacity=n)
+    ix.upload_vectors(base)
+    rng = np.random.default_rng(23)
+    dead = rng.choice(n, 900, replace=False)
+    ix.add_tombstones(dead)
+    tomb = O.bits_from_ids(dead, n)
+    cases = {
+        "empty": np.zeros(0, np.int64),
+        "dead_only": np.sort(dead[:50]),
+        "one": np.array([12_345]),
+        "all": np.arange(n),
+        "prefix": np.arange(0, 7_000, 3),
+        "random_30": np.nonzero(rng.random(n) < 0.3)[0],
+    }
+    for name, ids_a in cases.items():
+        al = W.AllowList.from_ids(ids_a, n)
+        for q in (qs, qs[:1]):
+            _check(ix, base, q, 10, metric, allow_bits=al.words, allow=al, tomb=tomb)
+            a = ix.search_batch(q, 10, mode="exact", allow=al)
+            monkeypatch.setenv("WV_BF_SYNC_COMPACT", "1")
+            b = ix.search_batch(q, 10, mode="exact", allow=al)
+            monkeypatch.delenv("WV_BF_SYNC_COMPACT")
+            for x, y in zip(a, b):
+                assert np.array_equal(x, y), name
+    ix.close()

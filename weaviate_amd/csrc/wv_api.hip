@@ -56,10 +56,11 @@ hipError_t wv_launch_h16_rows(const float* in, int ld_in, const uint64_t* ids, u
                               unsigned int* res_max_bits, float* res_out, int wide_layout, hipStream_t s);
 hipError_t wv_launch_h16_rows_gather(const float* in, int ld_in, const uint32_t* gather, uint64_t n, uint64_t n_pad,
                                      int D, int ns, float scale, void* out, hipStream_t s);
-hipError_t wv_launch_h16_compact_aux(const float* xnorm, const uint32_t* rowidx, uint64_t n, float* cxnorm,
-                                     uint64_t* excl, uint64_t excl_words, hipStream_t s);
+hipError_t wv_launch_h16_compact_aux(const float* xnorm, const uint32_t* rowidx, uint64_t n, const uint32_t* n_dev,
+                                     float* cxnorm, uint64_t* excl, uint64_t excl_words, hipStream_t s);
 hipError_t wv_launch_remap_ids(uint32_t* ids, int nq, int n_slots, int per_slot, int bq, uint64_t ntiles,
-                               uint64_t units_per_block, const uint32_t* rowidx, uint64_t n_rows, hipStream_t s);
+                               uint64_t units_per_block, const uint32_t* rowidx, uint64_t n_rows, const uint32_t* n_dev,
+                               hipStream_t s);
 hipError_t wv_launch_absmax(const float* in, int ld, uint64_t n, int D, unsigned int* max_bits, hipStream_t s);
 hipError_t wv_launch_h16_qscale(const float* part, int nparts, unsigned int* max_bits, float bsign, float* qscale,
                                 hipStream_t s);
@@ -470,7 +471,11 @@ __global__ void allowed_scatter_kernel(const uint64_t* allow, uint64_t allow_wor
     }
 }
 
-__global__ void pad_rowidx_kernel(uint32_t* rowidx, uint64_t from, uint64_t to) {
+__global__ void pad_rowidx_kernel(uint32_t* rowidx, uint64_t from, uint64_t to, const uint32_t* n_dev) {
+    if (n_dev) {   // (the device's count: pad it to a whole tile)
+        from = *n_dev;
+        to = (from + wv::HW_BN - 1) / wv::HW_BN * wv::HW_BN;
+    }
     const uint64_t i = from + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < to) rowidx[i] = 0;   // padded tile rows read row 0 and are masked by the row count
 }
@@ -520,7 +525,39 @@ int compact_allowed(wv_index* ix, const uint64_t* d_allow, uint64_t allow_nbits,
     HIP_TRY(hipGetLastError());
     if (padded > total)
         hipLaunchKernelGGL(pad_rowidx_kernel, dim3(1), dim3(256), 0, s, ix->rowidx.as<uint32_t>(), (uint64_t)total,
-                           padded);
+                           padded, nullptr);
+    HIP_TRY(hipGetLastError());
+    return WV_OK;
+}
+
+// The same list without reading its length back: ix->rowidx holds it, padded
+// to whole tiles, and *n_dev (device memory) its length, which the compacted
+// f16 wide-D pass reads itself (H16Params.n_dev) -- no host round trip
+// between the allow list and the scan.
+int compact_allowed_dev(wv_index* ix, const uint64_t* d_allow, uint64_t allow_nbits, uint64_t N, const uint32_t** n_dev,
+                        hipStream_t s) {
+    const uint64_t words = (N + 63) / 64;
+    const uint64_t allow_words = (allow_nbits + 63) / 64;
+    HIP_TRY(ix->ac_cnt.ensure((words + 1) * 4));
+    HIP_TRY(ix->ac_off.ensure((words + 1) * 4));
+    const unsigned blocks = (unsigned)((words + 255) / 256);
+    hipLaunchKernelGGL(allowed_count_kernel, dim3(blocks), dim3(256), 0, s, d_allow, allow_words,
+                       ix->excl.as<uint64_t>(), N, ix->ac_cnt.as<uint32_t>());
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemsetAsync(ix->ac_cnt.as<uint32_t>() + words, 0, 4, s));
+    size_t tmp = 0;
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, ix->ac_cnt.as<uint32_t>(), ix->ac_off.as<uint32_t>(),
+                                             (int)(words + 1), s));
+    HIP_TRY(ix->sort_tmp.ensure(tmp));
+    HIP_TRY(hipcub::DeviceScan::ExclusiveSum(ix->sort_tmp.p, tmp, ix->ac_cnt.as<uint32_t>(), ix->ac_off.as<uint32_t>(),
+                                             (int)(words + 1), s));
+    const uint64_t padded = (N + wv::HW_BN - 1) / wv::HW_BN * wv::HW_BN;
+    HIP_TRY(ix->rowidx.ensure(padded * 4));
+    hipLaunchKernelGGL(allowed_scatter_kernel, dim3(blocks), dim3(256), 0, s, d_allow, allow_words,
+                       ix->excl.as<uint64_t>(), N, ix->ac_off.as<uint32_t>(), ix->rowidx.as<uint32_t>());
+    HIP_TRY(hipGetLastError());
+    *n_dev = ix->ac_off.as<uint32_t>() + words;
+    hipLaunchKernelGGL(pad_rowidx_kernel, dim3(1), dim3(256), 0, s, ix->rowidx.as<uint32_t>(), 0ull, 0ull, *n_dev);
     HIP_TRY(hipGetLastError());
     return WV_OK;
 }
@@ -578,7 +615,7 @@ int block_order(wv_index* ix, uint64_t nqb, const wv::BfSchedule& sch, hipStream
 
 int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_allow, uint64_t allow_nbits, uint64_t N,
             uint64_t* d_out_ids, float* d_out_d, int32_t* d_out_n, hipStream_t s, std::vector<int32_t>& fails,
-            const uint32_t* rowidx = nullptr) {
+            const uint32_t* rowidx = nullptr, const uint32_t* n_dev = nullptr) {
     const int ns = ix->h16_ns;
     const bool wd = ix->h16_wide;   // D > 128: the wide-D kernel
     // D <= 128: 8-wave (512-query) workgroups, one per CU; D > 128: 256-row
@@ -636,7 +673,7 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
                                               ix->cimg16.p, s));
             ximg = ix->cimg16.p;
         }
-        HIP_TRY(wv_launch_h16_compact_aux(ix->xnorm.as<float>(), rowidx, N, ix->cxnorm.as<float>(),
+        HIP_TRY(wv_launch_h16_compact_aux(ix->xnorm.as<float>(), rowidx, N, n_dev, ix->cxnorm.as<float>(),
                                           ix->cexcl.as<uint64_t>(), ew, s));
         xnorm = ix->cxnorm.as<float>();
         excl = ix->cexcl.as<uint64_t>();
@@ -742,7 +779,19 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     // the wide pass: query blocks cut at the same tile offsets where that
     // costs no work (bf_schedule_aligned)
     wv::BfSchedule sch{};
-    if (wd && !wide) sch = wv::bf_schedule_aligned(nq, N, target(ntl), bq, tile_rows, false);
+    if (n_dev) {
+        // a device-counted list (N its bound): S slots per query block, the
+        // kernel sizes their runs (H16Params.n_dev); finalize and remap see
+        // S one-tile slots, which index the lists the same way
+        if (!wd || wide) return fail(WV_ESTATE, "run_h16: device-counted rows need the wide-D pass");
+        const int S = std::max(1, target(ntl) / nqb);
+        sch.bq = bq;
+        sch.ntiles = (uint64_t)S;
+        sch.units_per_block = 1;
+        sch.n_blocks = nqb * S;
+        sch.n_slots = S + 1;
+    }
+    if (wd && !wide && sch.n_blocks == 0) sch = wv::bf_schedule_aligned(nq, N, target(ntl), bq, tile_rows, false);
     if (sch.n_blocks == 0) sch = wv::bf_schedule(nq, N, target(ntl), bq, tile_rows);
     if (wide && (uint64_t)sch.n_slots * prod * kp > (uint64_t)wv::FINW_NE)
         return fail(WV_ESTATE, "run_h16: too many lists for the wide finalize");
@@ -752,6 +801,7 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     hp.ntiles_real = ntl;
     hp.units_per_block = sch.units_per_block;
     hp.n_slots = sch.n_slots;
+    hp.n_dev = n_dev;
     hp.tile_stride = 1;
     hp.tau = nullptr;
     // the running threshold (k <= 2 BF_KP), started at the seed's
@@ -796,7 +846,7 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     TREC(1);
     if (rowidx)
         HIP_TRY(wv_launch_remap_ids(ix->cand_id.as<uint32_t>(), nq, sch.n_slots, prod * kp, bq, sch.ntiles,
-                                    sch.units_per_block, rowidx, N, s));
+                                    sch.units_per_block, rowidx, N, n_dev, s));
     fp.cand_d = ix->cand_d.as<float>();
     fp.cand_id = ix->cand_id.as<uint32_t>();
     fp.n_slots = sch.n_slots;
@@ -887,6 +937,25 @@ int run_exact(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
         const uint32_t* d_rowidx = nullptr;
         const uint64_t* cmask = d_allow && !allow_stride ? d_allow : d_rowmask;
         const uint64_t cbits = d_allow && !allow_stride ? allow_nbits : rowmask_nbits;
+        // The wide-D f16 pass (k <= FIN_KF) compacts every shared list with
+        // no host round trip: its per-lane fill reads a compacted tile at the
+        // cost of a contiguous one, so the list's length need not steer the
+        // scan (WV_BF_SYNC_COMPACT=1: the read-back rule below, measurements)
+        if (cmask && !d_rowmask && h16_ok && ix->h16_wide && k <= wv::FIN_KF && !std::getenv("WV_BF_SYNC_COMPACT") &&
+            !std::getenv("WV_BF_NO_COMPACT")) {
+            const uint32_t* n_dev = nullptr;
+            const uint64_t n_bound = std::min<uint64_t>(N, cbits);
+            if (n_bound == 0) {
+                HIP_TRY(hipMemsetAsync(d_out_n, 0, sizeof(int32_t) * nq, s));
+                return WV_OK;
+            }
+            if (int rc = compact_allowed_dev(ix, cmask, cbits, N, &n_dev, s)) return rc;
+            std::vector<int32_t> none;
+            if (int rc = run_h16(ix, d_q, nq, k, nullptr, 0, n_bound, d_out_ids, d_out_d, d_out_n, s, none,
+                                 ix->rowidx.as<uint32_t>(), n_dev))
+                return rc;
+            return queue_fbd(ix, d_q, nq, k, d_allow, allow_nbits, allow_stride, d_out_ids, d_out_d, d_out_n, s);
+        }
         if (cmask) {
             uint64_t n_ok = 0;
             int rc = compact_allowed(ix, cmask, cbits, N, &n_ok, s, d_rowmask != nullptr, nq);

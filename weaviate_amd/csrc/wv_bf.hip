@@ -723,20 +723,34 @@ __device__ __forceinline__ void finalize_one(const BfFinParams& p, int q, float*
         uint32_t ti[FIN_KF];
 #pragma unroll
         for (int i = 0; i < FIN_KF; ++i) { td[i] = FLT_MAX; ti[i] = WV_NIL; }
-        for (int e = lane; e < n_ent; e += 64) {
-            float d = cd[e];
-            uint32_t id = ci[e];
-            if (id == WV_NIL) continue;
-            if (!key_less(d, id, td[FIN_KF - 1], ti[FIN_KF - 1])) continue;
+        // (8 entries per lane loaded before any is inserted: one memory
+        // round trip per 512 entries, not per 64 -- the wide-D pass's 1000-query
+        // batches run one wave per SIMD, where each trip is exposed)
+        for (int e0 = lane; e0 < n_ent; e0 += 64 * 8) {
+            float dd[8];
+            uint32_t ii[8];
 #pragma unroll
-            for (int i = 0; i < FIN_KF; ++i) {
-                const bool lt = key_less(d, id, td[i], ti[i]);
-                const float a = td[i];
-                const uint32_t b = ti[i];
-                td[i] = lt ? d : td[i];
-                ti[i] = lt ? id : ti[i];
-                d = lt ? a : d;
-                id = lt ? b : id;
+            for (int u = 0; u < 8; ++u) {
+                const int e = e0 + 64 * u;
+                ii[u] = e < n_ent ? ci[e] : WV_NIL;
+                dd[u] = e < n_ent ? cd[e] : FLT_MAX;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                float d = dd[u];
+                uint32_t id = ii[u];
+                if (id == WV_NIL) continue;
+                if (!key_less(d, id, td[FIN_KF - 1], ti[FIN_KF - 1])) continue;
+#pragma unroll
+                for (int i = 0; i < FIN_KF; ++i) {
+                    const bool lt = key_less(d, id, td[i], ti[i]);
+                    const float a = td[i];
+                    const uint32_t b = ti[i];
+                    td[i] = lt ? d : td[i];
+                    ti[i] = lt ? id : ti[i];
+                    d = lt ? a : d;
+                    id = lt ? b : id;
+                }
             }
         }
         // wave merge: FIN_KF rounds of argmin over the lane heads
@@ -775,22 +789,14 @@ __device__ __forceinline__ void finalize_one(const BfFinParams& p, int q, float*
     for (int i = lane; i < ((p.D + 3) & ~3); i += 64) qv[i] = i < p.D ? p.Q[(size_t)q * p.ldq + i] : 0.f;
     __builtin_amdgcn_wave_barrier();
 
-    // exact re-rank of the FIN_KF candidates: 8 lanes per row
-    const int g = lane & 7, grp = lane >> 3;
-    float ex[FIN_KF / 8];
-#pragma unroll
-    for (int pass = 0; pass < FIN_KF / 8; ++pass) {
-        const int c = pass * 8 + grp;
-        const uint32_t id = si[c];
-        float d = FLT_MAX;
-        if (id != WV_NIL) d = exact_dist_group8<METRIC, 8>(qv, p.X + (size_t)id * p.ldx, p.D, g);
-        ex[pass] = d;
-    }
+    // exact re-rank of the FIN_KF candidates: 8 lanes per row, all FIN_KF
+    // rows' loads of a slab in flight together (exact_dist_rows; the same
+    // arithmetic as exact_dist_group8).  The selection put the nil entries
+    // (key FLT_MAX, largest id) last, and their keys stay FLT_MAX.
+    int n_sel = 0;
+    for (int j = 0; j < FIN_KF; ++j) n_sel += (si[j] != WV_NIL);
     __builtin_amdgcn_wave_barrier();
-    // write exact distances back (group leader)
-#pragma unroll
-    for (int pass = 0; pass < FIN_KF / 8; ++pass)
-        if (g == 0) sd[pass * 8 + grp] = ex[pass];
+    exact_dist_rows<METRIC, FIN_KF / 8>(qv, p.X, p.ldx, p.D, si, n_sel, sd, lane);
     __builtin_amdgcn_wave_barrier();
     // sort the FIN_KF exact keys (rank by counting: lane c < FIN_KF)
     float myd = FLT_MAX;

@@ -614,6 +614,13 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16w_kernel(H16Params p) {
     const int ns = p.ns, nch = ns / KC;
     const uint4* __restrict__ Qg = reinterpret_cast<const uint4*>(p.Q);
     const bool has_allow = p.allow != nullptr;
+    if (p.n_dev) {   // the schedule of a device-counted row list
+        const uint64_t S = (uint64_t)(p.n_slots - 1), nt = ((uint64_t)*p.n_dev + BN - 1) / BN;
+        const uint64_t U = nt > S ? (nt + S - 1) / S : 1;
+        p.ntiles = S * U;
+        p.ntiles_real = nt;
+        p.units_per_block = U;
+    }
     int lb = (int)blockIdx.x;
     if ((p.locality & 1) && gridDim.x >= 8) {
         const int nwg = (int)gridDim.x, q8 = nwg / 8, r8 = nwg % 8, xcd = (int)blockIdx.x % 8;
@@ -1232,8 +1239,10 @@ hipError_t wv_launch_h16_rows_gather(const float* in, int ld_in, const uint32_t*
     return hipGetLastError();
 }
 
-__global__ void wv_gather_f32_kernel(const float* src, const uint32_t* idx, uint64_t n, float* dst) {
+__global__ void wv_gather_f32_kernel(const float* src, const uint32_t* idx, uint64_t n, const uint32_t* n_dev,
+                                     float* dst) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (n_dev) n = *n_dev;   // (n: the launch's bound)
     if (i < n) dst[i] = src[idx[i]];
 }
 
@@ -1244,9 +1253,11 @@ __global__ void wv_gather_f32_kernel(const float* src, const uint32_t* idx, uint
 // stale words.  A position >= n_rows cannot come out of the pass; it would
 // become WV_NIL here rather than an out-of-range read.
 __global__ void wv_remap_ids_kernel(uint32_t* ids, int nq, int n_slots, int per_slot, int bq, uint64_t ntiles,
-                                    uint64_t units_per_block, const uint32_t* rowidx, uint64_t n_rows) {
+                                    uint64_t units_per_block, const uint32_t* rowidx, uint64_t n_rows,
+                                    const uint32_t* n_dev) {
     const int q = blockIdx.x;
     if (q >= nq) return;
+    if (n_dev) n_rows = *n_dev;
     const int n_valid = wv::bf_slots_of((uint64_t)(q / bq), ntiles, units_per_block) * per_slot;
     uint32_t* e = ids + (size_t)q * n_slots * per_slot;
     for (int i = threadIdx.x; i < n_valid; i += blockDim.x) {
@@ -1256,27 +1267,30 @@ __global__ void wv_remap_ids_kernel(uint32_t* ids, int nq, int n_slots, int per_
 }
 
 // exclusion bits of a compacted scan: rows >= n (the last tile's padding)
-__global__ void wv_excl_tail_kernel(uint64_t* excl, uint64_t n, uint64_t words) {
+__global__ void wv_excl_tail_kernel(uint64_t* excl, uint64_t n, const uint32_t* n_dev, uint64_t words) {
     const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= words) return;
+    if (n_dev) n = *n_dev;
     const uint64_t lo = w * 64;
     excl[w] = lo >= n ? ~0ull : (n - lo >= 64 ? 0ull : ~0ull << (n - lo));
 }
 
-hipError_t wv_launch_h16_compact_aux(const float* xnorm, const uint32_t* rowidx, uint64_t n, float* cxnorm,
-                                     uint64_t* excl, uint64_t excl_words, hipStream_t s) {
+// n_dev (nullable): the list's length on the device, n then its bound
+hipError_t wv_launch_h16_compact_aux(const float* xnorm, const uint32_t* rowidx, uint64_t n, const uint32_t* n_dev,
+                                     float* cxnorm, uint64_t* excl, uint64_t excl_words, hipStream_t s) {
     if (n) hipLaunchKernelGGL(wv_gather_f32_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, xnorm, rowidx, n,
-                              cxnorm);
+                              n_dev, cxnorm);
     hipLaunchKernelGGL(wv_excl_tail_kernel, dim3((unsigned)((excl_words + 255) / 256)), dim3(256), 0, s, excl, n,
-                       excl_words);
+                       n_dev, excl_words);
     return hipGetLastError();
 }
 
 hipError_t wv_launch_remap_ids(uint32_t* ids, int nq, int n_slots, int per_slot, int bq, uint64_t ntiles,
-                               uint64_t units_per_block, const uint32_t* rowidx, uint64_t n_rows, hipStream_t s) {
+                               uint64_t units_per_block, const uint32_t* rowidx, uint64_t n_rows, const uint32_t* n_dev,
+                               hipStream_t s) {
     if (nq == 0) return hipSuccess;
     hipLaunchKernelGGL(wv_remap_ids_kernel, dim3((unsigned)nq), dim3(64), 0, s, ids, nq, n_slots, per_slot, bq, ntiles,
-                       units_per_block, rowidx, n_rows);
+                       units_per_block, rowidx, n_rows, n_dev);
     return hipGetLastError();
 }
 

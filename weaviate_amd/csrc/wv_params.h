@@ -178,11 +178,17 @@ struct H16Params {
     int xslot;                // 1: use gslot instead of the gtau publish
     int ns;                   // 16-k steps of the images (the wide-D kernel: a multiple of HW_KC)
     int wide_rows;            // the wide-D kernel's rows per wave: 128 (256-row tiles) or 64 (128-row tiles)
-    // the wide-D kernel (round 5): X is row-major (row r's ns * 16 halves at
-    // r * ns * 32 bytes) and its operand blocks are filled per lane; rowidx
+    // the wide-D kernel (round 5): X is h16w_index (row r's 64 B panels per
+    // 16-row group) and its operand blocks are filled per lane; rowidx
     // (nullable): scan rows rowidx[0 .. N) (a compacted allow list, ascending,
     // padded to whole 256-row tiles) instead of rows 0 .. N -- no gathered image
     const uint32_t* rowidx;
+    // (nullable, wide-D kernel) the row count as the device computed it (a
+    // compacted list's length, never read back by the host): the schedule is
+    // then n_slots - 1 slots per query block of U = ceil(tiles / slots) tiles
+    // each, fixed at kernel start; the host passes ntiles = n_slots - 1 and
+    // units_per_block = 1 (the same grid, slots and block order)
+    const uint32_t* n_dev;
 };
 
 // ---- f16 key pass for D > 128 (wv_bf_h16w_kernel, wv_h16.hip) --------------
