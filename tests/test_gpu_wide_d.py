@@ -138,3 +138,37 @@ def test_device_counted_compaction_edge_lists(metric, monkeypatch):
             for x, y in zip(a, b):
                 assert np.array_equal(x, y), name
     ix.close()
+
+
+@pytest.mark.parametrize("metric", [O.L2, O.DOT])
+def test_duplicate_rows_ties_by_id(metric):
+    """Rows repeated many times: equal keys everywhere, so the finalize's
+    selection (the FIN_KF-th list head bounds the entries it sorts; more than
+    256 such entries fall back to the per-lane selection) must order ties by
+    id exactly as the restatement does.  600 queries: 3 query blocks of 85
+    slots, 170 lists of 8 entries per query."""
+    distinct, reps, d = 500, 40, 256
+    base = np.tile(_gauss(distinct, d, 31), (reps, 1))
+    qs = _gauss(600, d, 32)
+    ix = W.GPUVectorIndex(d, NAMES[metric], capacity=len(base))
+    ix.upload_vectors(base)
+    for k in (10, 32):
+        _check(ix, base, qs, k, metric)
+    ix.close()
+
+
+@pytest.mark.parametrize("d", [64, 256])
+def test_finalize_many_lists_small_batches(d):
+    """Small batches spread a corpus over many slots: 1 or 3 queries over
+    ~9k rows give each query 100-300 lists (800-2400 entries), so the
+    finalize bounds them by the FIN_KF-th list head and compacts the entries
+    at or below it over several 512-entry rounds (a wave-uniform count), or
+    falls back past 256 lists.  Equal to the restatement."""
+    n = 9_001
+    base, qs = _gauss(n, d, 41), _gauss(700, d, 42)
+    for metric in (O.L2, O.DOT):
+        ix = W.GPUVectorIndex(d, NAMES[metric], capacity=n)
+        ix.upload_vectors(base)
+        for nq in (1, 3, 700):
+            _check(ix, base, qs[:nq], 10, metric)
+        ix.close()

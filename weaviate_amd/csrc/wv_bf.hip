@@ -629,11 +629,80 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void wv_bf_split_kernel(BfParams 
 // ---------------------------------------------------------------------------
 // Finalize: one wave per query.
 
-// FAST: every query has <= 256 list entries (n_slots * prod * kp): the
-// bitonic selection; otherwise per-lane top-KF runs and a KF-round merge
-// (separate instantiations: one kernel holding both needs 210 VGPRs)
+// Finalize sort keys: (dist, id) as one u64 whose unsigned order is
+// key_less's (dist's bits made monotonic -- -0 folded into +0 first, as the
+// float compare ties them -- then the id's 31 bits; nil ids come back as nil:
+// no row id reaches 2^31 - 1).  One v_cmp_lt_u64 per compare: key_less's
+// short-circuit form compiled to exec-mask branches in these sorts, ~10x
+// their shuffle cost at one wave per SIMD (in-kernel stamps).
+__device__ __forceinline__ uint64_t fin_key(float d, uint32_t id) {
+    uint32_t u = __float_as_uint(d + 0.0f);
+    u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+    return ((uint64_t)u << 32) | (uint64_t)(id & WV_IDMASK);
+}
+__device__ __forceinline__ void fin_unkey(uint64_t k, float& d, uint32_t& id) {
+    uint32_t u = (uint32_t)(k >> 32);
+    u = (u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u;
+    d = __uint_as_float(u);
+    const uint32_t lo = (uint32_t)k;
+    id = lo == WV_IDMASK ? WV_NIL : lo;
+}
+
+// A wave-wide bitonic sort of 256 fin_key keys, element i = 64 j + lane in
+// register j: strides >= 64 inside the lane, smaller ones by shuffles; the
+// smallest FIN_KF end in lanes 0 .. FIN_KF - 1 of j = 0.
+__device__ __forceinline__ void bitonic256_wave(uint64_t (&kk)[4], int lane) {
+#pragma unroll
+    for (int k = 2; k <= 256; k <<= 1) {
+#pragma unroll
+        for (int jj = k >> 1; jj > 0; jj >>= 1) {
+            if (jj >= 64) {
+                // (register pairs named by literal indices: a runtime
+                // j ^ (jj / 64) made the arrays dynamically indexed)
+                auto cas = [&](auto jc, auto pc) {
+                    constexpr int j = decltype(jc)::value, pj = decltype(pc)::value;
+                    const bool up = ((64 * j + lane) & k) == 0;   // element j is the lower index
+                    // (operands selected, then one compare: a ternary of two
+                    // compares compiled to exec-mask branches)
+                    const uint64_t a = up ? kk[pj] : kk[j], b = up ? kk[j] : kk[pj];
+                    const bool sw = a < b;
+                    const uint64_t t = kk[j];
+                    kk[j] = sw ? kk[pj] : kk[j];
+                    kk[pj] = sw ? t : kk[pj];
+                };
+                using I0 = std::integral_constant<int, 0>;
+                using I1 = std::integral_constant<int, 1>;
+                using I2 = std::integral_constant<int, 2>;
+                using I3 = std::integral_constant<int, 3>;
+                if (jj == 64) { cas(I0{}, I1{}); cas(I2{}, I3{}); }
+                else { cas(I0{}, I2{}); cas(I1{}, I3{}); }
+            } else {
+                const bool lower = (lane & jj) == 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t plo = (uint32_t)__shfl_xor((int)(uint32_t)kk[j], jj, 64);
+                    const uint32_t phi = (uint32_t)__shfl_xor((int)(uint32_t)(kk[j] >> 32), jj, 64);
+                    const uint64_t pk = ((uint64_t)phi << 32) | plo;
+                    const bool up = ((64 * j + lane) & k) == 0;
+                    // the lower index of an ascending pair keeps the min
+                    const bool c = lower == up;
+                    const uint64_t a = c ? pk : kk[j], b = c ? kk[j] : pk;
+                    const bool take = a < b;
+                    kk[j] = take ? pk : kk[j];
+                }
+            }
+        }
+    }
+}
+
+// FAST: every query has <= 256 list entries (n_slots * prod * kp): one
+// bitonic selection; otherwise the list heads bound a short list that is
+// sorted the same way, or (over 256 entries at or below that bound) per-lane
+// top-KF runs and a KF-round merge (separate instantiations: one kernel
+// holding both needs 210 VGPRs)
 template <int METRIC, bool FAST>
-__device__ __forceinline__ void finalize_one(const BfFinParams& p, int q, float* sd, uint32_t* si, float* qv) {
+__device__ __forceinline__ void finalize_one(const BfFinParams& p, int q, float* sd, uint32_t* si, float* qv,
+                                             float* kept_d, uint32_t* kept_i) {
     const int lane = threadIdx.x & 63;
     const int n_lists = bf_slots_of((uint64_t)(q / p.bq), p.ntiles, p.units_per_block) * p.prod;
     const int kp = p.kp ? p.kp : BF_KP;   // entries per list
@@ -642,134 +711,144 @@ __device__ __forceinline__ void finalize_one(const BfFinParams& p, int q, float*
     const uint32_t* ci = p.cand_id + (size_t)q * p.n_slots * p.prod * kp;
 
     // bound from the producers' last entries: anything a producer dropped is >= its KP-th key
-    float bound = FLT_MAX;
-    uint32_t bound_id = WV_NIL;
+    uint64_t bkey = fin_key(FLT_MAX, WV_NIL);
     for (int l = lane; l < n_lists; l += 64) {
-        const float d = cd[l * kp + kp - 1];
-        const uint32_t i = ci[l * kp + kp - 1];
-        if (key_less(d, i, bound, bound_id)) { bound = d; bound_id = i; }
+        const uint64_t t = fin_key(cd[l * kp + kp - 1], ci[l * kp + kp - 1]);
+        bkey = t < bkey ? t : bkey;
     }
     for (int m = 32; m >= 1; m >>= 1) {
-        const float od = __shfl_xor(bound, m, 64);
-        const uint32_t oi = __shfl_xor(bound_id, m, 64);
-        if (key_less(od, oi, bound, bound_id)) { bound = od; bound_id = oi; }
+        const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)bkey, m, 64);
+        const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(bkey >> 32), m, 64);
+        const uint64_t t = ((uint64_t)hi << 32) | lo;
+        bkey = t < bkey ? t : bkey;
     }
+    float bound;
+    uint32_t bound_id;
+    fin_unkey(bkey, bound, bound_id);
 
     // select the FIN_KF smallest (key, id) among all entries
     if constexpr (FAST) {
-        // a wave-wide bitonic sort of the (<= 256) entries, element i = 64 j +
-        // lane in register j: strides >= 64 inside the lane, smaller ones by
-        // shuffles; the FIN_KF smallest end in lanes 0 .. FIN_KF - 1 of j = 0
-        float kd[4];
-        uint32_t ki[4];
+        // a wave-wide bitonic sort of the (<= 256) entries
+        uint64_t kk[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int e = 64 * j + lane;
-            kd[j] = FLT_MAX;
-            ki[j] = WV_NIL;
-            if (e < n_ent) {
-                ki[j] = ci[e];
-                if (ki[j] != WV_NIL) kd[j] = cd[e];
+            const uint32_t id = e < n_ent ? ci[e] : WV_NIL;
+            kk[j] = fin_key(id != WV_NIL ? cd[e] : FLT_MAX, id);
+        }
+        bitonic256_wave(kk, lane);
+        if (lane < FIN_KF) fin_unkey(kk[0], sd[lane], si[lane]);
+    } else {
+        // More entries (the wide-D pass's 64-slot schedules: 1024).  The
+        // lists are sorted, so the FIN_KF-th smallest list head T bounds the
+        // FIN_KF smallest entries (FIN_KF heads are <= T): sort the heads,
+        // keep the entries <= T (a few dozen; compacted into LDS by ballot)
+        // and sort those -- two 256-sorts instead of a private top-KF per lane
+        // and KF merge rounds (66 + 28 us of dependent VALU / shuffle chains
+        // per 1024-entry query at one wave per SIMD; in-kernel stamps)
+        bool done = false;
+        if (n_lists <= 256) {
+            uint64_t hk[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int l = 64 * j + lane;
+                const uint32_t id = l < n_lists ? ci[l * kp] : WV_NIL;
+                hk[j] = fin_key(id != WV_NIL ? cd[l * kp] : FLT_MAX, id);
+            }
+            bitonic256_wave(hk, lane);
+            const uint64_t T = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(hk[0] >> 32), FIN_KF - 1, 64) << 32) |
+                               (uint32_t)__shfl((int)(uint32_t)hk[0], FIN_KF - 1, 64);
+            int n_keep = 0;   // (wave-uniform: the loop runs on every lane)
+            for (int e0 = 0; e0 < n_ent; e0 += 64 * 8) {
+                float dd[8];
+                uint32_t ii[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int e = e0 + 64 * u + lane;
+                    ii[u] = e < n_ent ? ci[e] : WV_NIL;
+                    dd[u] = e < n_ent ? cd[e] : FLT_MAX;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const bool keep = ii[u] != WV_NIL && fin_key(dd[u], ii[u]) <= T;
+                    const uint64_t m = __ballot(keep);
+                    const int pos = n_keep + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                    if (keep && pos < 256) { kept_d[pos] = dd[u]; kept_i[pos] = ii[u]; }
+                    n_keep += __popcll(m);
+                }
+            }
+            if (n_keep <= 256) {
+                __builtin_amdgcn_wave_barrier();
+                uint64_t kk[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int e = 64 * j + lane;
+                    kk[j] = e < n_keep ? fin_key(kept_d[e], kept_i[e]) : fin_key(FLT_MAX, WV_NIL);
+                }
+                bitonic256_wave(kk, lane);
+                if (lane < FIN_KF) fin_unkey(kk[0], sd[lane], si[lane]);
+                done = true;
             }
         }
+        if (!done) {
+            // more entries: each lane keeps a private sorted top-KF of its share,
+            // then KF rounds of a wave-wide argmin over the lane heads
+            if (lane < FIN_KF) { sd[lane] = FLT_MAX; si[lane] = WV_NIL; }
+            __builtin_amdgcn_wave_barrier();
+            // each lane scans its share and keeps a private top-KF in LDS-free registers
+            float td[FIN_KF];
+            uint32_t ti[FIN_KF];
 #pragma unroll
-        for (int k = 2; k <= 256; k <<= 1) {
+            for (int i = 0; i < FIN_KF; ++i) { td[i] = FLT_MAX; ti[i] = WV_NIL; }
+            // (8 entries per lane loaded before any is inserted: one memory
+            // round trip per 512 entries, not per 64 -- the wide-D pass's 1000-query
+            // batches run one wave per SIMD, where each trip is exposed)
+            for (int e0 = lane; e0 < n_ent; e0 += 64 * 8) {
+                float dd[8];
+                uint32_t ii[8];
 #pragma unroll
-            for (int jj = k >> 1; jj > 0; jj >>= 1) {
-                if (jj >= 64) {
-                    // (register pairs named by literal indices: a runtime
-                    // j ^ (jj / 64) made the arrays dynamically indexed, i.e.
-                    // 208 bytes of scratch per lane)
-                    auto cas = [&](auto jc, auto pc) {
-                        constexpr int j = decltype(jc)::value, pj = decltype(pc)::value;
-                        const bool up = ((64 * j + lane) & k) == 0;   // element j is the lower index
-                        const bool sw = up ? key_less(kd[pj], ki[pj], kd[j], ki[j]) : key_less(kd[j], ki[j], kd[pj], ki[pj]);
-                        const float td = kd[j];
-                        const uint32_t ti = ki[j];
-                        kd[j] = sw ? kd[pj] : kd[j];
-                        ki[j] = sw ? ki[pj] : ki[j];
-                        kd[pj] = sw ? td : kd[pj];
-                        ki[pj] = sw ? ti : ki[pj];
-                    };
-                    using I0 = std::integral_constant<int, 0>;
-                    using I1 = std::integral_constant<int, 1>;
-                    using I2 = std::integral_constant<int, 2>;
-                    using I3 = std::integral_constant<int, 3>;
-                    if (jj == 64) { cas(I0{}, I1{}); cas(I2{}, I3{}); }
-                    else { cas(I0{}, I2{}); cas(I1{}, I3{}); }
-                } else {
-                    const bool lower = (lane & jj) == 0;
+                for (int u = 0; u < 8; ++u) {
+                    const int e = e0 + 64 * u;
+                    ii[u] = e < n_ent ? ci[e] : WV_NIL;
+                    dd[u] = e < n_ent ? cd[e] : FLT_MAX;
+                }
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const float pd = __shfl_xor(kd[j], jj, 64);
-                        const uint32_t pi = __shfl_xor(ki[j], jj, 64);
-                        const bool up = ((64 * j + lane) & k) == 0;
-                        // the lower index of an ascending pair keeps the min
-                        const bool take = (lower == up) ? key_less(pd, pi, kd[j], ki[j]) : key_less(kd[j], ki[j], pd, pi);
-                        kd[j] = take ? pd : kd[j];
-                        ki[j] = take ? pi : ki[j];
+                for (int u = 0; u < 8; ++u) {
+                    float d = dd[u];
+                    uint32_t id = ii[u];
+                    if (id == WV_NIL) continue;
+                    if (!key_less(d, id, td[FIN_KF - 1], ti[FIN_KF - 1])) continue;
+#pragma unroll
+                    for (int i = 0; i < FIN_KF; ++i) {
+                        const bool lt = key_less(d, id, td[i], ti[i]);
+                        const float a = td[i];
+                        const uint32_t b = ti[i];
+                        td[i] = lt ? d : td[i];
+                        ti[i] = lt ? id : ti[i];
+                        d = lt ? a : d;
+                        id = lt ? b : id;
                     }
                 }
             }
-        }
-        if (lane < FIN_KF) { sd[lane] = kd[0]; si[lane] = ki[0]; }
-    } else {
-        // more entries: each lane keeps a private sorted top-KF of its share,
-        // then KF rounds of a wave-wide argmin over the lane heads
-        if (lane < FIN_KF) { sd[lane] = FLT_MAX; si[lane] = WV_NIL; }
-        __builtin_amdgcn_wave_barrier();
-        // each lane scans its share and keeps a private top-KF in LDS-free registers
-        float td[FIN_KF];
-        uint32_t ti[FIN_KF];
+            // wave merge: FIN_KF rounds of argmin over the lane heads
+            int head = 0;
+            for (int r = 0; r < FIN_KF; ++r) {
+                float hd = FLT_MAX;
+                uint32_t hi = WV_NIL;
 #pragma unroll
-        for (int i = 0; i < FIN_KF; ++i) { td[i] = FLT_MAX; ti[i] = WV_NIL; }
-        // (8 entries per lane loaded before any is inserted: one memory
-        // round trip per 512 entries, not per 64 -- the wide-D pass's 1000-query
-        // batches run one wave per SIMD, where each trip is exposed)
-        for (int e0 = lane; e0 < n_ent; e0 += 64 * 8) {
-            float dd[8];
-            uint32_t ii[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int e = e0 + 64 * u;
-                ii[u] = e < n_ent ? ci[e] : WV_NIL;
-                dd[u] = e < n_ent ? cd[e] : FLT_MAX;
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                float d = dd[u];
-                uint32_t id = ii[u];
-                if (id == WV_NIL) continue;
-                if (!key_less(d, id, td[FIN_KF - 1], ti[FIN_KF - 1])) continue;
-#pragma unroll
-                for (int i = 0; i < FIN_KF; ++i) {
-                    const bool lt = key_less(d, id, td[i], ti[i]);
-                    const float a = td[i];
-                    const uint32_t b = ti[i];
-                    td[i] = lt ? d : td[i];
-                    ti[i] = lt ? id : ti[i];
-                    d = lt ? a : d;
-                    id = lt ? b : id;
+                for (int i = 0; i < FIN_KF; ++i)
+                    if (i == head) { hd = td[i]; hi = ti[i]; }
+                float md = hd;
+                uint32_t mi = hi;
+                for (int m = 32; m >= 1; m >>= 1) {
+                    const float od = __shfl_xor(md, m, 64);
+                    const uint32_t oi = __shfl_xor(mi, m, 64);
+                    if (key_less(od, oi, md, mi)) { md = od; mi = oi; }
                 }
+                if (hi == mi && hd == md && mi != WV_NIL) head++;
+                if (lane == 0) { sd[r] = md; si[r] = mi; }
             }
-        }
-        // wave merge: FIN_KF rounds of argmin over the lane heads
-        int head = 0;
-        for (int r = 0; r < FIN_KF; ++r) {
-            float hd = FLT_MAX;
-            uint32_t hi = WV_NIL;
-#pragma unroll
-            for (int i = 0; i < FIN_KF; ++i)
-                if (i == head) { hd = td[i]; hi = ti[i]; }
-            float md = hd;
-            uint32_t mi = hi;
-            for (int m = 32; m >= 1; m >>= 1) {
-                const float od = __shfl_xor(md, m, 64);
-                const uint32_t oi = __shfl_xor(mi, m, 64);
-                if (key_less(od, oi, md, mi)) { md = od; mi = oi; }
-            }
-            if (hi == mi && hd == md && mi != WV_NIL) head++;
-            if (lane == 0) { sd[r] = md; si[r] = mi; }
         }
     }
     __builtin_amdgcn_wave_barrier();
@@ -805,8 +884,9 @@ __device__ __forceinline__ void finalize_one(const BfFinParams& p, int q, float*
     if (lane < FIN_KF) {
         myd = sd[lane];
         myi = si[lane];
+        const uint64_t mykey = fin_key(myd, myi);
         for (int j = 0; j < FIN_KF; ++j)
-            if (key_less(sd[j], si[j], myd, myi)) rank++;
+            rank += fin_key(sd[j], si[j]) < mykey;
     }
     __builtin_amdgcn_wave_barrier();
     const int k = p.k;
@@ -876,11 +956,14 @@ __global__ __launch_bounds__(64) void wv_bf_finalize_kernel(BfFinParams p) {
     const int dpad = (p.D + 3) & ~3;
     float* sd = qv + dpad;
     uint32_t* si = reinterpret_cast<uint32_t*>(sd + FIN_KF);
+    // (non-FAST: + 256 kept entries)
+    float* kept_d = reinterpret_cast<float*>(si + FIN_KF);
+    uint32_t* kept_i = reinterpret_cast<uint32_t*>(kept_d + 256);
     const int q = blockIdx.x;
     if (q >= p.nq) return;
-    if (p.metric == WV_METRIC_L2) finalize_one<WV_METRIC_L2, FAST>(p, q, sd, si, qv);
-    else if (p.metric == WV_METRIC_DOT) finalize_one<WV_METRIC_DOT, FAST>(p, q, sd, si, qv);
-    else finalize_one<WV_METRIC_COSINE, FAST>(p, q, sd, si, qv);
+    if (p.metric == WV_METRIC_L2) finalize_one<WV_METRIC_L2, FAST>(p, q, sd, si, qv, kept_d, kept_i);
+    else if (p.metric == WV_METRIC_DOT) finalize_one<WV_METRIC_DOT, FAST>(p, q, sd, si, qv, kept_d, kept_i);
+    else finalize_one<WV_METRIC_COSINE, FAST>(p, q, sd, si, qv, kept_d, kept_i);
 }
 
 // ---------------------------------------------------------------------------
@@ -1590,8 +1673,8 @@ hipError_t wv_launch_split_rows(const float* in, int ld_in, const uint64_t* ids,
 }
 
 hipError_t wv_launch_bf_finalize(const wv::BfFinParams* p, hipStream_t s) {
-    const size_t lds = (((p->D + 3) & ~3) + 2 * wv::FIN_KF) * sizeof(float);
     const bool fast = (uint64_t)p->n_slots * p->prod * (p->kp ? p->kp : wv::BF_KP) <= 256;
+    const size_t lds = (((p->D + 3) & ~3) + 2 * wv::FIN_KF + (fast ? 0 : 512)) * sizeof(float);
     if (fast) hipLaunchKernelGGL(wv::wv_bf_finalize_kernel<true>, dim3(p->nq), dim3(64), lds, s, *p);
     else hipLaunchKernelGGL(wv::wv_bf_finalize_kernel<false>, dim3(p->nq), dim3(64), lds, s, *p);
     return hipGetLastError();
