@@ -1234,9 +1234,17 @@ int run_pq_flat(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d
     return WV_OK;
 }
 
-int choose_vc_log2(int per_wave_budget_words, int fixed_words) {
-    int l = 12;
-    while (l > 8 && fixed_words + (1 << l) > per_wave_budget_words) --l;
+// Visited-cache size (2^vc_log2 16-bit slots) for a per-wave LDS budget, and
+// the tag width that makes slot + tag identify ids below n_nodes exactly
+// (HnswParams.vc_tbits <= 15; a graph past 2^(vc_log2 + 15) nodes gets more
+// slots than the budget would give).
+int choose_vc_log2(int per_wave_budget_words, int fixed_words, uint64_t n_nodes, int* tbits) {
+    int l = 13;
+    while (l > 8 && fixed_words + ((1 << l) + 1) / 2 > per_wave_budget_words) --l;
+    int hb = 1;
+    while (hb < 32 && (1ull << hb) < n_nodes) ++hb;
+    if (hb - l > 15) l = hb - 15;
+    *tbits = hb > l ? hb - l : 0;
     return l;
 }
 
@@ -1258,7 +1266,8 @@ int run_hnsw(wv_index* ix, const float* d_q, int nq, int k, int ef, const uint64
     int wave_kb = filtered ? 20 : 12;
     if (const char* e = std::getenv("WV_HNSW_WAVE_KB")) wave_kb = std::max(4, std::atoi(e));
     const int budget = wave_kb * 1024 / 4;
-    const int vc_log2 = choose_vc_log2(budget, fixed);
+    int vc_tbits = 0;
+    const int vc_log2 = choose_vc_log2(budget, fixed, ix->gn, &vc_tbits);
     int per_wave = wv_hnsw_per_wave_words(ix->dpad, efc, sc, vc_log2, xs_log2);
     per_wave = (per_wave + 3) & ~3;
     int wpb = 4;
@@ -1295,6 +1304,7 @@ int run_hnsw(wv_index* ix, const float* d_q, int nq, int k, int ef, const uint64
     hp.efc = efc;
     hp.sc = sc;
     hp.vc_log2 = vc_log2;
+    hp.vc_tbits = vc_tbits;
     hp.xs_log2 = xs_log2;
     hp.dpad = ix->dpad;
     hp.per_wave_words = per_wave;
@@ -1327,7 +1337,7 @@ int run_hnsw(wv_index* ix, const float* d_q, int nq, int k, int ef, const uint64
         h2.sc = 2048;
         h2.xs_log2 = 11;
         const int fixed2 = wv_hnsw_per_wave_words(ix->dpad, efc, h2.sc, 0, h2.xs_log2) - 1;
-        h2.vc_log2 = choose_vc_log2(fixed2 + 1024, fixed2);
+        h2.vc_log2 = choose_vc_log2(fixed2 + 1024, fixed2, ix->gn, &h2.vc_tbits);
         int pw2 = (wv_hnsw_per_wave_words(ix->dpad, efc, h2.sc, h2.vc_log2, h2.xs_log2) + 3) & ~3;
         h2.per_wave_words = pw2;
         int wpb2 = 4;
@@ -2066,7 +2076,8 @@ int wv_index_build_graph(wv_index* ix, int ef_construction, uint64_t seed, int b
     // per-wave search state as in run_hnsw (unfiltered layout)
     const int efc = std::max(64, (ef_construction + 63) / 64 * 64);
     const int fixed = wv_hnsw_per_wave_words(ix->dpad, efc, 0, 0, 0) - 1;
-    const int vc_log2 = choose_vc_log2(12 * 1024 / 4, fixed);
+    int vc_tbits = 0;
+    const int vc_log2 = choose_vc_log2(12 * 1024 / 4, fixed, n, &vc_tbits);
     int per_wave = (wv_hnsw_per_wave_words(ix->dpad, efc, 0, vc_log2, 0) + 3) & ~3;
     int wpb = 4;
     while (wpb > 1 && (size_t)wpb * per_wave * 4 > 160 * 1024) --wpb;
@@ -2122,6 +2133,7 @@ int wv_index_build_graph(wv_index* ix, int ef_construction, uint64_t seed, int b
         h.efc = efc;
         h.sc = 0;
         h.vc_log2 = vc_log2;
+        h.vc_tbits = vc_tbits;
         h.xs_log2 = 0;
         h.dpad = ix->dpad;
         h.per_wave_words = per_wave;

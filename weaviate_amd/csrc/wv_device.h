@@ -272,6 +272,14 @@ __device__ __forceinline__ float asm_l2_serial(const float* __restrict__ x, cons
 __device__ __forceinline__ bool key_less(float da, uint32_t ia, float db, uint32_t ib) {
     return da < db || (da == db && (ia & WV_IDMASK) < (ib & WV_IDMASK));
 }
+// The same order without short-circuit evaluation, for compares inside
+// ballots and selection chains: the || / && form can compile to exec-mask
+// branches around each compare (round 5, finalize sorts: ~10x their cost);
+// this one is three compares and two mask ops.  (Not the default: in the
+// HNSW LDS-path kernels it raised VGPRs 72 -> 139.)
+__device__ __forceinline__ bool key_less_nb(float da, uint32_t ia, float db, uint32_t ib) {
+    return (da < db) | ((da == db) & ((ia & WV_IDMASK) < (ib & WV_IDMASK)));
+}
 
 __device__ __forceinline__ bool bit_test(const uint64_t* __restrict__ bits, uint64_t nbits, uint64_t id) {
     return id < nbits && ((bits[id >> 6] >> (id & 63)) & 1ull);

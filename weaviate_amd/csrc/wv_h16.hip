@@ -871,12 +871,28 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16w_kernel(H16Params p) {
                 const half8 b1 = __builtin_bit_cast(half8, st[St::A_U4 + ((2 * qq + 1) * KC + k) * 64 + lane]);
                 // row 32 G + l31's chunk 2 k + khalf (swizzled slot)
                 const int aslot = 4 * l31 + ((2 * k + khalf) ^ ((l31 >> 2) & 3));
+#ifndef WV_H16W_JIT_READS
+                // every operand of the k-step read before its first MFMA: the
+                // scheduler otherwise reuses one A register set, each A read
+                // then waits for the MFMAs of the last (lgkmcnt(0) per MFMA
+                // pair: the LDS latency exposed RG times per k-step)
+                half8 a[RG];
+#pragma unroll
+                for (int i = 0; i < RG; ++i) a[i] = __builtin_bit_cast(half8, st[128 * (RG * rh + i) + aslot]);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int i = 0; i < RG; ++i) {
+                    acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i], b0, acc[i][0], 0, 0, 0);
+                    acc[i][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[i], b1, acc[i][1], 0, 0, 0);
+                }
+#else
 #pragma unroll
                 for (int i = 0; i < RG; ++i) {
                     const half8 a = __builtin_bit_cast(half8, st[128 * (RG * rh + i) + aslot]);
                     acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b0, acc[i][0], 0, 0, 0);
                     acc[i][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b1, acc[i][1], 0, 0, 0);
                 }
+#endif
 #ifndef WV_H16W_FILL_EARLY
                 // the next fill between this chunk's MFMAs, not beside the
                 // partner wave's fill after the barrier (2.33 -> 2.23 ms per

@@ -85,7 +85,7 @@ struct WaveState {
     float* Sd2; uint32_t* Si2;
     float* Bd; uint32_t* Bi;    // raw batch (distance by batch slot)
     float* Cd; uint32_t* Ci;    // sorted batch
-    uint32_t* vc;
+    uint16_t* vc;   // visited cache (HnswParams.vc_tbits)
     uint32_t* xs;
     uint32_t* ltomb;
     unsigned long long* ub;   // this query's exact visited bitmap (diagnostic counts; nullable)
@@ -109,6 +109,16 @@ __device__ __forceinline__ uint32_t eval_count(const WaveState& w, int level, in
 }
 
 __device__ __forceinline__ uint32_t hash32(uint32_t x) { return x * 2654435761u; }
+
+// visited-cache slot and tag of a node id (HnswParams.vc_tbits)
+__device__ __forceinline__ uint32_t vc_hash(const HnswParams& p, uint32_t id) {
+    return hash32(id) & ((1u << (p.vc_log2 + p.vc_tbits)) - 1u);
+}
+__device__ __forceinline__ uint32_t vc_slot(const HnswParams& p, uint32_t h) { return h >> p.vc_tbits; }
+__device__ __forceinline__ uint16_t vc_tag(const HnswParams& p, uint32_t h) {
+    return (uint16_t)(h & ((1u << p.vc_tbits) - 1u));
+}
+constexpr uint16_t VC_EMPTY = 0xFFFF;
 
 // lower bound: number of entries of a sorted (d,id) array with key < (d,id)
 __device__ __forceinline__ int lower_bound(const float* ad, const uint32_t* ai, int n, float d, uint32_t id) {
@@ -136,7 +146,7 @@ __device__ __forceinline__ void search_layer(const HnswParams& p, WaveState& w_i
     const int lane = threadIdx.x & 63;
     const int VC = 1 << p.vc_log2;
     const int XS = 1 << p.xs_log2;
-    for (int i = lane; i < VC; i += 64) w.vc[i] = WV_NIL;
+    for (int i = lane; i < VC; i += 64) w.vc[i] = VC_EMPTY;
     for (int i = lane; i < XS; i += 64) w.xs[i] = WV_NIL;
     wave_sync();
 
@@ -149,7 +159,10 @@ __device__ __forceinline__ void search_layer(const HnswParams& p, WaveState& w_i
     };
 
     // insertViableEntrypointsAsCandidatesAndResults (search.go:329-353)
-    if (lane == 0) w.vc[hash32(ep) >> (32 - p.vc_log2)] = ep;
+    if (lane == 0) {
+        const uint32_t he = vc_hash(p, ep);
+        w.vc[vc_slot(p, he)] = vc_tag(p, he);
+    }
     const bool ep_ok = eligible(ep);
     if (lane == 0) {
         float* dd = ep_ok ? w.Rd : w.Sd;
@@ -237,13 +250,14 @@ __device__ __forceinline__ void search_layer(const HnswParams& p, WaveState& w_i
             }
             bool v0 = id0 != WV_NIL && id0 < p.N;
             bool v1 = id1 != WV_NIL && id1 < p.N;
-            const uint32_t h0 = v0 ? hash32(id0) >> (32 - p.vc_log2) : 0;
-            const uint32_t h1 = v1 ? hash32(id1) >> (32 - p.vc_log2) : 0;
-            if (v0 && w.vc[h0] == id0) v0 = false;
-            if (v1 && w.vc[h1] == id1) v1 = false;
+            const uint32_t e0 = vc_hash(p, id0), e1 = vc_hash(p, id1);
+            const uint32_t h0 = v0 ? vc_slot(p, e0) : 0, h1 = v1 ? vc_slot(p, e1) : 0;
+            const uint16_t t0 = vc_tag(p, e0), t1 = vc_tag(p, e1);
+            if (v0 && w.vc[h0] == t0) v0 = false;
+            if (v1 && w.vc[h1] == t1) v1 = false;
             wave_sync();
-            if (v0) w.vc[h0] = id0;
-            if (v1) w.vc[h1] = id1;
+            if (v0) w.vc[h0] = t0;
+            if (v1) w.vc[h1] = t1;
             const uint64_t m0 = __ballot(v0), m1 = __ballot(v1);
             const int n0 = __popcll(m0);
             const int nb = n0 + __popcll(m1);
@@ -436,9 +450,12 @@ __device__ __forceinline__ void search_layer_reg(const HnswParams& p, WaveState&
     static_assert(NR == 1 || NR == 2, "64 or 128 results per wave");
     const int lane = threadIdx.x & 63;
     const int VC = 1 << p.vc_log2;
-    for (int i = lane; i < VC; i += 64) w.vc[i] = WV_NIL;
+    for (int i = lane; i < VC; i += 64) w.vc[i] = VC_EMPTY;
     wave_sync();
-    if (lane == 0) w.vc[hash32(ep) >> (32 - p.vc_log2)] = ep;
+    if (lane == 0) {
+        const uint32_t he = vc_hash(p, ep);
+        w.vc[vc_slot(p, he)] = vc_tag(p, he);
+    }
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
         rd[r] = lane == 0 && r == 0 ? epd : FLT_MAX;
@@ -492,13 +509,14 @@ __device__ __forceinline__ void search_layer_reg(const HnswParams& p, WaveState&
             }
             bool v0 = id0 != WV_NIL && id0 < p.N;
             bool v1 = id1 != WV_NIL && id1 < p.N;
-            const uint32_t h0 = v0 ? hash32(id0) >> (32 - p.vc_log2) : 0;
-            const uint32_t h1 = v1 ? hash32(id1) >> (32 - p.vc_log2) : 0;
-            if (v0 && w.vc[h0] == id0) v0 = false;
-            if (v1 && w.vc[h1] == id1) v1 = false;
+            const uint32_t e0 = vc_hash(p, id0), e1 = vc_hash(p, id1);
+            const uint32_t h0 = v0 ? vc_slot(p, e0) : 0, h1 = v1 ? vc_slot(p, e1) : 0;
+            const uint16_t t0 = vc_tag(p, e0), t1 = vc_tag(p, e1);
+            if (v0 && w.vc[h0] == t0) v0 = false;
+            if (v1 && w.vc[h1] == t1) v1 = false;
             wave_sync();
-            if (v0) w.vc[h0] = id0;
-            if (v1) w.vc[h1] = id1;
+            if (v0) w.vc[h0] = t0;
+            if (v1) w.vc[h1] = t1;
             const uint64_t m0 = __ballot(v0), m1 = __ballot(v1);
             const int n0 = __popcll(m0);
             const int nb = n0 + __popcll(m1);
@@ -542,7 +560,7 @@ __device__ __forceinline__ void search_layer_reg(const HnswParams& p, WaveState&
                     int pos = 0;
 #pragma unroll
                     for (int r = 0; r < NR; ++r)
-                        pos += __popcll(__ballot(64 * r + lane < Rl && key_less(rd[r], ri[r] & WV_IDMASK, d, id)));
+                        pos += __popcll(__ballot((64 * r + lane < Rl) & key_less_nb(rd[r], ri[r] & WV_IDMASK, d, id)));
                     if (pos >= ef) continue;
                     if (pos < Rl && reg_entry_d<NR>(rd, pos) == d && (reg_entry_i<NR>(ri, pos) & WV_IDMASK) == id)
                         continue;   // already a result (a neighbour the visited cache forgot)
@@ -709,7 +727,7 @@ __global__ __launch_bounds__(256) void wv_hnsw_kernel(HnswParams p) {
     w.Sd2 = cur; cur += p.sc; w.Si2 = reinterpret_cast<uint32_t*>(cur); cur += p.sc;
     w.Bd = cur; cur += BATCH; w.Bi = reinterpret_cast<uint32_t*>(cur); cur += BATCH;
     w.Cd = cur; cur += BATCH; w.Ci = reinterpret_cast<uint32_t*>(cur); cur += BATCH;
-    w.vc = reinterpret_cast<uint32_t*>(cur); cur += (1 << p.vc_log2);
+    w.vc = reinterpret_cast<uint16_t*>(cur); cur += ((1 << p.vc_log2) + 1) / 2;
     w.xs = reinterpret_cast<uint32_t*>(cur); cur += (1 << p.xs_log2);
     w.ltomb = reinterpret_cast<uint32_t*>(cur); cur += MAX_LOCAL_TOMB;
     w.ub = p.uniq ? p.uniq + (uint64_t)q * p.uniq_words : nullptr;
@@ -785,7 +803,7 @@ __global__ __launch_bounds__(256) void wv_build_search_kernel(BuildParams b) {
     w.Sd2 = cur; cur += p.sc; w.Si2 = reinterpret_cast<uint32_t*>(cur); cur += p.sc;
     w.Bd = cur; cur += BATCH; w.Bi = reinterpret_cast<uint32_t*>(cur); cur += BATCH;
     w.Cd = cur; cur += BATCH; w.Ci = reinterpret_cast<uint32_t*>(cur); cur += BATCH;
-    w.vc = reinterpret_cast<uint32_t*>(cur); cur += (1 << p.vc_log2);
+    w.vc = reinterpret_cast<uint16_t*>(cur); cur += ((1 << p.vc_log2) + 1) / 2;
     w.xs = reinterpret_cast<uint32_t*>(cur); cur += (1 << p.xs_log2);
     w.ltomb = reinterpret_cast<uint32_t*>(cur);
     if (p.metric == WV_METRIC_L2) build_search_one<WV_METRIC_L2>(b, w, slot);
@@ -953,7 +971,7 @@ __global__ __launch_bounds__(64) void wv_build_link_kernel(BuildParams b) {
 }
 
 int hnsw_per_wave_words(int dpad, int efc, int sc, int vc_log2, int xs_log2) {
-    return dpad + 4 * efc + 4 * sc + 4 * BATCH + (1 << vc_log2) + (1 << xs_log2) + MAX_LOCAL_TOMB;
+    return dpad + 4 * efc + 4 * sc + 4 * BATCH + ((1 << vc_log2) + 1) / 2 + (1 << xs_log2) + MAX_LOCAL_TOMB;
 }
 
 }  // namespace wv

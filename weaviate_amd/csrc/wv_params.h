@@ -339,6 +339,12 @@ struct HnswParams {
     int upper_levels;    // level stride of `upper` (>= max_level)
     int nq, k, ef;
     int efc, sc, vc_log2, xs_log2, dpad, per_wave_words;
+    // visited cache (round 5): 2^vc_log2 16-bit slots; node id -> h = id *
+    // 2654435761 mod 2^(vc_log2 + vc_tbits) (a bijection on ids below that
+    // power of two, which covers N), slot = h >> vc_tbits, tag = the low
+    // vc_tbits <= 15 bits (0xFFFF: empty) -- an exact membership test per
+    // slot in half the LDS of a 32-bit id
+    int vc_tbits;
     uint64_t* out_ids;   // [nq][k]
     float* out_d;
     int32_t* out_n;
