@@ -946,3 +946,33 @@ def test_h16_cross_slot_threshold_without_seed_equals_restatement(data):
             assert gn.tolist() == on.tolist()
             for i in range(nq):
                 _same_tie_aware(gi[i], gd[i], oi[i], od[i])
+
+
+@pytest.mark.parametrize("metric,d,M", [(O.L2, 48, 16), (O.COSINE, 100, 64), (O.DOT, 128, 32)])
+def test_hnsw_workgroup_per_query_small_batches(metric, d, M, monkeypatch):
+    """Batches of up to 64 unfiltered queries run one 4-wave workgroup per
+    query (wv_hnsw_wg_kernel: helper waves take rows 32..127 of each distance
+    batch): identical to the restatement and, bit for bit, to the one-wave
+    kernel (WV_HNSW_WG_MAX=0), at batch sizes 1, 7 and 64, ef 10 / 64 / 100
+    (one and two result registers), M = 64 (128 neighbours per batch) and a
+    D = 32 m + 4 row tail."""
+    n = 4000
+    base, idx = _build_graph(n, d, metric, M=M)
+    qs = np.random.default_rng(77).random((64, d), dtype=np.float32)
+    g = idx.export_graph()
+    ix = W.GPUVectorIndex(d, METRIC_NAMES[metric], capacity=n, max_connections=M)
+    ix.upload_vectors(base)
+    ix.upload_graph(g)
+    for ef in (10, 64, 100):
+        oi, od, on, st = idx.search_batch(qs, 10, ef, threads=8)
+        for nb in (1, 7, 64):
+            q = qs[:nb]
+            ids, ds, cnt = ix.search_batch(q, 10, ef=ef, mode="hnsw")
+            assert cnt.tolist() == on[:nb].tolist()
+            _same(ids, ds, oi[:nb], od[:nb])
+            monkeypatch.setenv("WV_HNSW_WG_MAX", "0")
+            ids1, ds1, cnt1 = ix.search_batch(q, 10, ef=ef, mode="hnsw")
+            monkeypatch.delenv("WV_HNSW_WG_MAX")
+            assert np.array_equal(ids, ids1) and np.array_equal(ds.view(np.uint32), ds1.view(np.uint32))
+            assert np.array_equal(cnt, cnt1)
+    ix.close()

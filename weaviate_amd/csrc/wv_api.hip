@@ -42,6 +42,7 @@ hipError_t wv_launch_scale(const float* in, float* out, uint64_t n, float scale,
 hipError_t wv_launch_qnorm(const float* Q, int nq, int D, int ldq, int metric, float* out, float* absmax_part,
                            hipStream_t s);
 hipError_t wv_launch_hnsw(const wv::HnswParams* p, int waves_per_block, hipStream_t s);
+hipError_t wv_launch_hnsw_wg(const wv::HnswParams* p, hipStream_t s);
 hipError_t wv_launch_build_search(const wv::BuildParams* b, int waves_per_block, hipStream_t s);
 hipError_t wv_launch_build_select(const wv::BuildParams* b, hipStream_t s);
 hipError_t wv_launch_build_link(const wv::BuildParams* b, hipStream_t s);
@@ -1324,7 +1325,18 @@ int run_hnsw(wv_index* ix, const float* d_q, int nq, int k, int ef, const uint64
         hp.uniq = static_cast<unsigned long long*>(uniq);
     }
     TREC(4);
-    HIP_TRY(wv_launch_hnsw(&hp, wpb, s));
+    // small unfiltered batches (the batcher's lone callers): a workgroup per
+    // query, whose three helper waves take the distance batches' other rows
+    // (WV_HNSW_WG_MAX: the largest such batch; 0 turns it off)
+    int wg_max = 64;
+    if (const char* e = std::getenv("WV_HNSW_WG_MAX")) wg_max = std::atoi(e);
+    const bool wg = !filtered && !ix->pq_on && (efc == 64 || efc == 128) && nq <= wg_max;
+    if (wg) {
+        hp.wg_helpers = 3;
+        HIP_TRY(wv_launch_hnsw_wg(&hp, s));
+    } else {
+        HIP_TRY(wv_launch_hnsw(&hp, wpb, s));
+    }
     if (filtered && !std::getenv("WV_HNSW_NO_WIDE_SIDE")) {
         // second pass for the queries whose side set or expanded-set table
         // overflowed (status != 0; the others' waves exit at once): the same

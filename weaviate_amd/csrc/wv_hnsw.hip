@@ -89,6 +89,7 @@ struct WaveState {
     uint32_t* xs;
     uint32_t* ltomb;
     unsigned long long* ub;   // this query's exact visited bitmap (diagnostic counts; nullable)
+    volatile int* wg_nb;      // workgroup-per-query launch: the batch size the helpers read (-1: done)
 };
 
 // the diagnostic count of a batch's layer-0 evaluations: nodes first
@@ -443,6 +444,31 @@ __device__ __forceinline__ uint32_t reg_entry_i(const uint32_t (&ri)[NR], int e)
     return (uint32_t)__builtin_amdgcn_readlane(ri[NR - 1], e - 64);
 }
 
+// Distances of a batch in a workgroup-per-query launch: wave v computes rows
+// 32 v .. 32 v + 31 (all of them at once, one memory round trip: a lone
+// wave's two trips of 32 rows were 66 % of an expansion, and one CU's
+// gathers are bound by the bytes it has in flight).  Wave 0 publishes nb; the
+// helpers (wg_helper) wait at the same two barriers.
+template <int METRIC>
+__device__ __forceinline__ void wg_dist(const HnswParams& p, const WaveState& w, int nb, int lane) {
+    if (lane == 0) *w.wg_nb = nb;
+    __syncthreads();
+    exact_dist_rows<METRIC, 4, true>(w.qv, p.X, p.ldx, p.D, w.Bi, min(nb, 32), w.Bd, lane);
+    __syncthreads();
+}
+template <int METRIC>
+__device__ void wg_helper(const HnswParams& p, const WaveState& w, int wave, int lane) {
+    for (;;) {
+        __syncthreads();
+        const int nb = *w.wg_nb;
+        if (nb < 0) break;
+        const int base = 32 * wave;
+        if (base < nb)
+            exact_dist_rows<METRIC, 4, true>(w.qv, p.X, p.ldx, p.D, w.Bi + base, min(nb - base, 32), w.Bd + base, lane);
+        __syncthreads();
+    }
+}
+
 template <int METRIC, bool PQ, int NR>
 __device__ __forceinline__ void search_layer_reg(const HnswParams& p, WaveState& w, int level, int ef, uint32_t ep,
                                                  float epd, float (&rd)[NR], uint32_t (&ri)[NR], int& Rl,
@@ -528,6 +554,8 @@ __device__ __forceinline__ void search_layer_reg(const HnswParams& p, WaveState&
             if (PQ) {
                 for (int base = 0; base < nb; base += 64)
                     if (base + lane < nb) w.Bd[base + lane] = pq_dist_row<METRIC>(w.qv, p.pq, w.Bi[base + lane]);
+            } else if (p.wg_helpers) {
+                wg_dist<METRIC>(p, w, nb, lane);
             } else {
                 for (int base = 0; base < nb; base += 8 * WV_HNSW_RPG)
                     exact_dist_rows<METRIC, WV_HNSW_RPG, true>(w.qv, p.X, p.ldx, p.D, w.Bi + base, nb - base, w.Bd + base,
@@ -733,6 +761,39 @@ __global__ __launch_bounds__(256) void wv_hnsw_kernel(HnswParams p) {
     w.ub = p.uniq ? p.uniq + (uint64_t)q * p.uniq_words : nullptr;
     if constexpr (NR > 0) knn_one_reg<METRIC, PQ, NR>(p, w, q);
     else knn_one<METRIC, PQ>(p, w, q);
+}
+
+// Small unfiltered batches (wv_search_batch under ~64 queries: the batcher's
+// single callers): one 4-wave workgroup per query, wave 0 running the search
+// of wv_hnsw_kernel's register path and waves 1..3 its distance batches
+// (wg_dist).  Same expansion order and results, bit for bit.
+template <int METRIC, int NR>
+__global__ __launch_bounds__(256) void wv_hnsw_wg_kernel(HnswParams p) {
+    extern __shared__ float lds[];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int q = blockIdx.x;
+    if (q >= p.nq) return;
+    float* cur = lds;
+    WaveState w;
+    w.wg_nb = reinterpret_cast<volatile int*>(lds + p.per_wave_words);
+    w.qv = cur; cur += p.dpad;
+    w.Rd = cur; cur += p.efc; w.Ri = reinterpret_cast<uint32_t*>(cur); cur += p.efc;
+    w.Rd2 = cur; cur += p.efc; w.Ri2 = reinterpret_cast<uint32_t*>(cur); cur += p.efc;
+    w.Sd = cur; cur += p.sc; w.Si = reinterpret_cast<uint32_t*>(cur); cur += p.sc;
+    w.Sd2 = cur; cur += p.sc; w.Si2 = reinterpret_cast<uint32_t*>(cur); cur += p.sc;
+    w.Bd = cur; cur += BATCH; w.Bi = reinterpret_cast<uint32_t*>(cur); cur += BATCH;
+    w.Cd = cur; cur += BATCH; w.Ci = reinterpret_cast<uint32_t*>(cur); cur += BATCH;
+    w.vc = reinterpret_cast<uint16_t*>(cur); cur += ((1 << p.vc_log2) + 1) / 2;
+    w.xs = reinterpret_cast<uint32_t*>(cur); cur += (1 << p.xs_log2);
+    w.ltomb = reinterpret_cast<uint32_t*>(cur); cur += MAX_LOCAL_TOMB;
+    w.ub = p.uniq ? p.uniq + (uint64_t)q * p.uniq_words : nullptr;
+    if (wave == 0) {
+        knn_one_reg<METRIC, false, NR>(p, w, q);
+        if (lane == 0) *w.wg_nb = -1;
+        __syncthreads();
+    } else {
+        wg_helper<METRIC>(p, w, wave, lane);
+    }
 }
 
 // ===========================================================================
@@ -1001,6 +1062,24 @@ hipError_t wv_launch_build_link(const wv::BuildParams* b, hipStream_t s) {
     const size_t lds = 6 * ((size_t)b->M0 + 1) * sizeof(float);
     if (b->n_runs == 0) return hipSuccess;
     hipLaunchKernelGGL(wv::wv_build_link_kernel, dim3((unsigned)b->n_runs), dim3(64), lds, s, *b);
+    return hipGetLastError();
+}
+
+// workgroup-per-query launch of an unfiltered register-path search (no PQ)
+hipError_t wv_launch_hnsw_wg(const wv::HnswParams* p, hipStream_t s) {
+    if (p->nq == 0) return hipSuccess;
+    const int nr = p->sc == 0 && !p->allow ? (p->efc == 64 ? 1 : p->efc == 128 ? 2 : 0) : 0;
+    if (nr == 0 || p->pq.codes || !p->wg_helpers) return hipErrorInvalidValue;
+    const size_t lds = (size_t)p->per_wave_words * sizeof(float) + 16;
+#define WV_HNSW_WG(M)                                                                                              \
+    do {                                                                                                           \
+        if (nr == 1) hipLaunchKernelGGL((wv::wv_hnsw_wg_kernel<M, 1>), dim3(p->nq), dim3(256), lds, s, *p);       \
+        else hipLaunchKernelGGL((wv::wv_hnsw_wg_kernel<M, 2>), dim3(p->nq), dim3(256), lds, s, *p);               \
+    } while (0)
+    if (p->metric == WV_METRIC_L2) WV_HNSW_WG(WV_METRIC_L2);
+    else if (p->metric == WV_METRIC_DOT) WV_HNSW_WG(WV_METRIC_DOT);
+    else WV_HNSW_WG(WV_METRIC_COSINE);
+#undef WV_HNSW_WG
     return hipGetLastError();
 }
 

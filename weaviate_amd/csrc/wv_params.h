@@ -361,6 +361,10 @@ struct HnswParams {
     // a second pass (nullable): only the queries whose entry here is non-zero
     // (the first pass's status: its side state overflowed) search again
     const int32_t* redo;
+    // (round 5) workgroup per query (wv_hnsw_wg_kernel, small unfiltered
+    // batches): wave 0 searches, waves 1..3 compute rows 32 v .. 32 v + 31 of
+    // every distance batch -- one memory round trip for up to 128 rows
+    int wg_helpers;
 };
 
 // Flat search over PQ codes (flat_search.go:19-74 on a compressed index):
