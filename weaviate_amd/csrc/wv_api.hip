@@ -1325,10 +1325,12 @@ int run_hnsw(wv_index* ix, const float* d_q, int nq, int k, int ef, const uint64
         hp.uniq = static_cast<unsigned long long*>(uniq);
     }
     TREC(4);
-    // small unfiltered batches (the batcher's lone callers): a workgroup per
+    // small unfiltered batches (the batcher's callers): a workgroup per
     // query, whose three helper waves take the distance batches' other rows
-    // (WV_HNSW_WG_MAX: the largest such batch; 0 turns it off)
-    int wg_max = 64;
+    // -- while every workgroup is resident (up to 3 per CU at 158 VGPRs; a
+    // 256-query batch 898 -> 705 us p50, profiles/r05/wg_latency.log).
+    // WV_HNSW_WG_MAX: the largest such batch; 0 turns it off.
+    int wg_max = 512;
     if (const char* e = std::getenv("WV_HNSW_WG_MAX")) wg_max = std::atoi(e);
     const bool wg = !filtered && !ix->pq_on && (efc == 64 || efc == 128) && nq <= wg_max;
     if (wg) {
