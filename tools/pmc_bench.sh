@@ -7,10 +7,13 @@
 #   LINE=head  wv_bf_h16_kernel main pass, configs[1] (1M x 128, 10k queries)
 #   LINE=c4    wv_bf_h16w_kernel, configs[3] 100 % leg (10M x 768, 1000 queries)
 #   LINE=c5    wv_hnsw_kernel, configs[4] over the 100M corpus (ef 128)
-# Output: gpurun_out/pmc_bench/<LINE>/ and gpurun_out/pmc_bench/pmc_<kernel>[_<shape>].json
+# Output: gpurun_out/pmc_bench/<LINE>/ (logs, kernel stats) and
+# gpurun_out/pmc_bench/pmc_<kernel>[_<shape>].json; the raw traces and counter
+# tables stay in /tmp (a full run's trace exceeds what gpurun merges back).
 set -e
 LINE=${LINE:-head}
-O=gpurun_out/pmc_bench/$LINE; mkdir -p $O
+G=gpurun_out/pmc_bench; mkdir -p $G/$LINE
+O=/tmp/pmc_bench/$LINE; rm -rf $O; mkdir -p $O
 export TMPDIR=/tmp
 OFF="--no-cpu-baseline --no-corpus-leg --no-group-leg --no-wide-line --steps 5 --warmup 2"
 case $LINE in
@@ -70,6 +73,8 @@ if mf and sq.get("SQ_VALU_MFMA_BUSY_CYCLES") is not None and sq.get("GRBM_GUI_AC
     js["mfma_busy_frac"] = sq["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024.0 * sq["GRBM_GUI_ACTIVE"] / 8.0)
 if avg_ns and js.get("hbm_bytes_per_launch"):
     js["hbm_gbs_measured"] = js["hbm_bytes_per_launch"] / (avg_ns * 1e-9) / 1e9
-json.dump(js, open(os.path.join(os.path.dirname(O), os.environ["OUTJ"]), "w"), indent=1)
+json.dump(js, open(os.path.join("gpurun_out/pmc_bench", os.environ["OUTJ"]), "w"), indent=1)
 print(json.dumps(js))
 PY
+cp $O/*.log $G/$LINE/
+find $O/trace -name run_kernel_stats.csv -exec cp {} $G/$LINE/kernel_stats.csv \;
