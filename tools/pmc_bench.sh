@@ -9,7 +9,8 @@
 #   LINE=c5    wv_hnsw_kernel, configs[4] over the 100M corpus (ef 128)
 # Output: gpurun_out/pmc_bench/<LINE>/ (logs, kernel stats) and
 # gpurun_out/pmc_bench/pmc_<kernel>[_<shape>].json; the raw traces and counter
-# tables stay in /tmp (a full run's trace exceeds what gpurun merges back).
+# tables stay in /tmp (a full run's trace exceeds what gpurun merges back);
+# the bench logs (with its 30-s heartbeat) are written under gpurun_out.
 set -e
 LINE=${LINE:-head}
 G=gpurun_out/pmc_bench; mkdir -p $G/$LINE
@@ -24,17 +25,17 @@ case $LINE in
         KNAME=wv_bf_h16w_kernel; KSUB="wv_bf_h16w_kernel<false, 128>"; SHAPE="10000000 1000 768 gauss"
         OUTJ=pmc_wv_bf_h16w_kernel_c4.json; T=300;;
   c5)   ARGS="$OFF --no-hnsw-line --no-c3-line --no-c4-line"
-        KNAME=wv_hnsw_kernel; KSUB="wv_hnsw_kernel"; SHAPE="100000000 10000 96 sift"
+        KNAME=wv_hnsw_kernel; KSUB="wv_hnsw_kernel<0, false, 2>"; SHAPE="100000000 10000 96 sift"
         OUTJ=pmc_wv_hnsw_kernel_c5.json; T=900;;
 esac
 export KNAME KSUB SHAPE OUTJ O
 export WV_BUILD_HASH=$(python3 -c "import sys; sys.path.insert(0, 'tools'); from build_hash import build_hash; print(build_hash('$KNAME'))")
-timeout -k 10 $T rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 bench.py $ARGS > $O/trace.log 2>&1
+timeout -k 10 $T rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 bench.py $ARGS > $G/$LINE/trace.log 2>&1
 i=0
 for set in "FETCH_SIZE" \
            "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
   i=$((i+1))
-  timeout -s KILL $T rocprofv3 --pmc $set --output-format csv -d $O/p$i -o run -- python3 bench.py $ARGS > $O/p$i.log 2>&1
+  timeout -s KILL $T rocprofv3 --pmc $set --output-format csv -d $O/p$i -o run -- python3 bench.py $ARGS > $G/$LINE/p$i.log 2>&1
 done
 python3 - <<'PY'
 import csv, glob, json, os, statistics
@@ -76,5 +77,4 @@ if avg_ns and js.get("hbm_bytes_per_launch"):
 json.dump(js, open(os.path.join("gpurun_out/pmc_bench", os.environ["OUTJ"]), "w"), indent=1)
 print(json.dumps(js))
 PY
-cp $O/*.log $G/$LINE/
 find $O/trace -name run_kernel_stats.csv -exec cp {} $G/$LINE/kernel_stats.csv \;
