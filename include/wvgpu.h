@@ -200,11 +200,14 @@ int wv_search_batch(wv_index *ix, const float *queries, int nq, int k, int ef, c
  * written d_queries) and ordered after every earlier call on the index; later
  * calls on the index are ordered after it.  The
  * results are complete when the stream reaches the end of the queued work.
- * Exact searches (k <= 256 on the f16 key pass, k <= 32 otherwise) and HNSW
- * searches without an allow list queue everything, certificate fallbacks
- * included (resolved on the device), and return without waiting for the GPU;
- * allow lists (AUTO's per-query flat/HNSW decision, row compaction), the
- * exact scan for larger k and PQ-compressed fallbacks still read counts back.
+ * Exact searches (k <= 256 on the f16 key pass, k <= 32 otherwise) without an
+ * allow list or, for D > 128, with a shared one (compacted on the device), and
+ * HNSW searches with or without allow lists queue everything, certificate
+ * and side-set fallbacks included (resolved on the device), and return
+ * without waiting for the GPU; AUTO's per-query flat/HNSW decision over allow
+ * lists, the D <= 128 exact pass over a shared allow list (row compaction),
+ * the exact scan for larger k and PQ-compressed fallbacks still read counts
+ * back.
  * Batch stats and kernel times are read (one sync) only when asked for. */
 int wv_search_batch_device(wv_index *ix, const float *d_queries, int nq, int k, int ef,
                            const uint64_t *d_allow_bits, uint64_t allow_nbits, uint64_t allow_stride_words,
