@@ -845,9 +845,17 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     TREC(0);
     HIP_TRY(wd ? wv_launch_bf_h16w(&hp, s) : wv_launch_bf_h16(&hp, ns, 0, s));
     TREC(1);
-    if (rowidx)
+    // compacted scan: the candidate positions map to rows -- inside the
+    // finalize for its FIN_KF selected entries, or (the wide finalize) all
+    // of them first
+    if (rowidx && wide)
         HIP_TRY(wv_launch_remap_ids(ix->cand_id.as<uint32_t>(), nq, sch.n_slots, prod * kp, bq, sch.ntiles,
                                     sch.units_per_block, rowidx, N, n_dev, s));
+    if (rowidx && !wide) {
+        fp.rowidx = rowidx;
+        fp.rowidx_n = N;
+        fp.rowidx_ndev = n_dev;
+    }
     fp.cand_d = ix->cand_d.as<float>();
     fp.cand_id = ix->cand_id.as<uint32_t>();
     fp.n_slots = sch.n_slots;

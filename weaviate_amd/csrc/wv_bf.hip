@@ -875,6 +875,11 @@ __device__ __forceinline__ void finalize_one(const BfFinParams& p, int q, float*
     int n_sel = 0;
     for (int j = 0; j < FIN_KF; ++j) n_sel += (si[j] != WV_NIL);
     __builtin_amdgcn_wave_barrier();
+    if (p.rowidx) {   // compacted scan: positions -> rows (order-preserving)
+        const uint64_t nr = p.rowidx_ndev ? (uint64_t)*p.rowidx_ndev : p.rowidx_n;
+        if (lane < FIN_KF && si[lane] != WV_NIL) si[lane] = si[lane] < nr ? p.rowidx[si[lane]] : WV_NIL;
+        __builtin_amdgcn_wave_barrier();
+    }
     exact_dist_rows<METRIC, FIN_KF / 8>(qv, p.X, p.ldx, p.D, si, n_sel, sd, lane);
     __builtin_amdgcn_wave_barrier();
     // sort the FIN_KF exact keys (rank by counting: lane c < FIN_KF)

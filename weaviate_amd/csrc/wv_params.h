@@ -267,6 +267,14 @@ struct BfFinParams {
     const float* qres;      // [nq] |b - f16(s_q b) / s_q| (rounded up)
     const float* tau_in;    // [nq] seed threshold the key pass dropped keys above (nullable)
     float* tau_out;         // seed pre-pass: [nq] threshold in true key units, no results written
+    // (nullable, finalize_one) the candidates' ids are positions in this
+    // ascending row list (a compacted allow list): the selected positions are
+    // mapped to rows before the re-rank -- the map is increasing, so every
+    // (key, id) order on positions is the order on rows.  Positions at or
+    // past the list's length (rowidx_n, or *rowidx_ndev when set) map to nil.
+    const uint32_t* rowidx;
+    uint64_t rowidx_n;
+    const uint32_t* rowidx_ndev;
 };
 
 // Certificate fallback: exact distances of every row for a batch of failed
