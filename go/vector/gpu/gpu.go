@@ -78,6 +78,7 @@ import (
 	"runtime/cgo"
 	"sync"
 	"sync/atomic"
+	"time"
 	"unsafe"
 
 	"github.com/pkg/errors"
@@ -129,6 +130,8 @@ type Index struct {
 	compacting atomic.Bool
 	closed     atomic.Bool
 	pqPending  atomic.Bool // PQ enabled at runtime, the mirror not yet serving the codes: the CPU index answers
+	pqGen      atomic.Int64 // one per runtime PQ enablement (its callbacks count against it)
+	pqCalls    atomic.Int32 // callbacks seen for the current pqGen: the second one follows Compress's end
 	handle     cgo.Handle      // this Index, for the library's callbacks (its threads call them)
 	ctx        *C.uintptr_t    // C memory holding handle: the callbacks' ctx, valid until close
 	metrics    *mirrorMetrics  // nil unless Options.Metrics
@@ -387,14 +390,22 @@ func (g *Index) UpdateUserConfig(updated schema.VectorIndexConfig, callback func
 	uc, isUC := updated.(ent.UserConfig)
 	g.mu.RLock() // (the mirror is not destroyed under mu)
 	enablePQ := isUC && uc.PQ.Enabled && !g.closed.Load() && !g.mirrorCompressed()
+	var gen int64
 	if enablePQ {
+		gen = g.pqGen.Add(1)
+		g.pqCalls.Store(0)
 		g.pqPending.Store(true)
 	}
 	g.mu.RUnlock()
 	err := g.cpuIndex.UpdateUserConfig(updated, func() {
 		callback()
-		if enablePQ {
-			go g.syncCompression()
+		if enablePQ && g.pqGen.Load() == gen {
+			// hnsw calls back once when UpdateUserConfig returns and once when
+			// its Compress goroutine ends, with or without an error
+			// (config_update.go:113-127): after the second, the log holds the
+			// AddPQ record or never will
+			final := g.pqCalls.Add(1) >= 2
+			go g.syncCompression(gen, final)
 		}
 	})
 	if err != nil {
@@ -419,25 +430,47 @@ func (g *Index) mirrorCompressed() bool {
 }
 
 // syncCompression: a flush of the CPU index's log and a compaction, so the
-// mirror reads the AddPQ record Compress wrote; it clears pqPending once the
-// mirror serves the codes (hnsw calls the callback before Compress starts
-// too -- that pass finds no record and leaves the CPU index answering).
-func (g *Index) syncCompression() {
-	g.mu.Lock()
-	if g.closed.Load() {
+// mirror reads the AddPQ record Compress wrote.  pqPending is cleared once
+// the mirror serves the codes, or -- after Compress has ended (final) -- once
+// a compaction of the flushed log succeeded without finding one: Compress
+// failed, the CPU index stays uncompressed, and so does the mirror.  A
+// compaction refused while the mirror is not live (an async startup or a
+// resync in flight: WV_ESTALE) is retried, 1 s apart, for up to 10 minutes.
+func (g *Index) syncCompression(gen int64, final bool) {
+	for try := 0; try < 600; try++ {
+		if try > 0 {
+			time.Sleep(time.Second)
+		}
+		if g.pqGen.Load() != gen {
+			return // a later enablement owns the flag
+		}
+		g.mu.Lock()
+		if g.closed.Load() {
+			g.mu.Unlock()
+			return
+		}
+		err := g.cpuIndex.Flush()
 		g.mu.Unlock()
-		return
-	}
-	err := g.cpuIndex.Flush()
-	g.mu.Unlock()
-	g.mu.RLock()
-	defer g.mu.RUnlock()
-	if err != nil || g.closed.Load() {
-		return
-	}
-	C.wv_mirror_compact(g.m)
-	if g.mirrorCompressed() {
-		g.pqPending.Store(false)
+		g.mu.RLock()
+		if g.closed.Load() {
+			g.mu.RUnlock()
+			return
+		}
+		rc := C.int(C.WV_ESTATE)
+		if err == nil {
+			rc = C.wv_mirror_compact(g.m)
+		}
+		compressed := rc == 0 && g.mirrorCompressed()
+		g.mu.RUnlock()
+		if compressed || (final && rc == 0) {
+			if g.pqGen.Load() == gen {
+				g.pqPending.Store(false)
+			}
+			return
+		}
+		if !final {
+			return // (the callback before Compress ends: the final one settles the flag)
+		}
 	}
 }
 

@@ -228,6 +228,13 @@ int wv_merge_shards_device(const float *d_in_dists, const uint64_t *d_in_ids, co
  * by the certificate fallback.  Waits for the batch to finish. */
 int wv_last_batch_stats(wv_index *ix, uint64_t *dist_evals, uint64_t *expansions, uint64_t *fallbacks);
 
+/* The last batch's filtered-HNSW state (nullable outputs): the queries whose
+ * side candidates outgrew the first launch's capacity and were re-run with
+ * twice of it, and that first launch's side columns (rows of 64 entries) and
+ * expanded-side set slots (0 when no filtered HNSW search ran).  Waits for
+ * the batch to finish.  A measurement hook (no reference counterpart). */
+int wv_last_side_stats(wv_index *ix, uint64_t *second_pass, int *side_rows, int *side_set);
+
 /* Kernel timing with HIP events on the launch stream (off by default).  When
  * enabled, every batch records the device time of its dominant kernels: the
  * MFMA brute-force kernel, the exact re-rank/finalize kernel and the HNSW

@@ -27,6 +27,9 @@ class Stats(C.Structure):
         ("max_cand", C.c_uint64),
         ("layer0_visited_max", C.c_uint64),
         ("ties", C.c_uint64),
+        ("side_live_max", C.c_uint64),
+        ("side_exp", C.c_uint64),
+        ("side_exp_max", C.c_uint64),
     ]
 
     def asdict(self):
@@ -89,6 +92,7 @@ def lib():
             "wvo_pq_distance": (C.c_float, [C.c_int, fp, vp, fp, C.c_int, C.c_int, C.c_int, C.c_int]),
             "wvo_pq_encode_kmeans": (C.c_int, [fp, C.c_uint64, C.c_int, C.c_int, C.c_int, fp, C.c_int, vp]),
             "wvo_compress": (C.c_int, [vp, C.c_int, C.c_int, C.c_int, fp, vp, vp, C.c_uint64]),
+            "wvo_set_side_diag": (None, [C.c_int]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)

@@ -852,6 +852,9 @@ static void conn_append(conn_list *cl, uint32_t id) {
     cl->ids[cl->len++] = id;
 }
 
+static int side_diag = 0;
+void wvo_set_side_diag(int on) { side_diag = on; }
+
 /* ---- searchLayerByVector -- search.go:160-327 ---------------------------- */
 /* entrypoints: min-heap consumed; results: caller-initialised max heap. */
 static void search_layer(wvo_index *h, ctx_t *c, const float *q, pq_t *eps,
@@ -880,8 +883,18 @@ static void search_layer(wvo_index *h, ctx_t *c, const float *q, pq_t *eps,
         worst = FLT_MAX;
     }
 
+    uint64_t side_exp = 0;
     while (cand->len > 0) {
         if (cand->len > c->st.max_cand) c->st.max_cand = cand->len;
+        if (side_diag && level == 0) {
+            uint64_t live = 0;
+            for (size_t i = 0; i < cand->len; i++) {
+                const uint64_t id = cand->it[i].id;
+                const int inel = (allow && !allow_contains(allow, allow_nbits, id)) || (id < h->cap && h->tomb[id]);
+                if (inel && (cand->it[i].dist <= worst || (int)results->len < ef)) live++;
+            }
+            if (live > c->st.side_live_max) c->st.side_live_max = live;
+        }
         /* :192-215 -- the top's distance is recomputed by the reference; it is
          * bit-identical to the stored value, so the stored one is used. */
         uint64_t top = cand->it[0].id;
@@ -912,6 +925,9 @@ static void search_layer(wvo_index *h, ctx_t *c, const float *q, pq_t *eps,
         nunlock(h, cid);
         c->st.expansions++;
         c->st.nbr_slots += nn;
+        if (side_diag && level == 0 &&
+            ((allow && !allow_contains(allow, allow_nbits, cid)) || (cid < h->cap && h->tomb[cid])))
+            side_exp++;
 
         /* :256-315 */
         for (uint32_t i = 0; i < nn; i++) {
@@ -931,6 +947,8 @@ static void search_layer(wvo_index *h, ctx_t *c, const float *q, pq_t *eps,
             }
         }
     }
+    c->st.side_exp += side_exp;
+    if (side_exp > c->st.side_exp_max) c->st.side_exp_max = side_exp;
     c->st.visited += c->vis_count;
     if (level == 0 && c->vis_count > c->st.layer0_visited_max) c->st.layer0_visited_max = c->vis_count;
 }
@@ -1615,6 +1633,9 @@ int wvo_search_batch(wvo_index *h, const float *qs, int nq, int k, int ef,
         tot.visited += args[t].st.visited;
         tot.ties += args[t].st.ties;
         if (args[t].st.max_cand > tot.max_cand) tot.max_cand = args[t].st.max_cand;
+        tot.side_exp += args[t].st.side_exp;
+        if (args[t].st.side_exp_max > tot.side_exp_max) tot.side_exp_max = args[t].st.side_exp_max;
+        if (args[t].st.side_live_max > tot.side_live_max) tot.side_live_max = args[t].st.side_live_max;
         if (args[t].st.layer0_visited_max > tot.layer0_visited_max)
             tot.layer0_visited_max = args[t].st.layer0_visited_max;
     }

@@ -63,7 +63,17 @@ typedef struct {
     uint64_t max_cand;     /* high-water mark of the candidate heap               */
     uint64_t layer0_visited_max; /* max visited count of one layer-0 search      */
     uint64_t ties;         /* decisions taken between equal distances (heap order) */
+    /* diagnostics of the side candidates (traversed but ineligible: filtered
+     * out or tombstoned, search.go:282-298), collected only after
+     * wvo_set_side_diag(1): the high-water mark of the live ones (distance
+     * <= worst, or all of them while the results are not full) over one
+     * layer-0 search, and how many were expanded (total / max per search) */
+    uint64_t side_live_max;
+    uint64_t side_exp;
+    uint64_t side_exp_max;
 } wvo_stats;
+
+void wvo_set_side_diag(int on);
 
 wvo_index *wvo_create(int dim, int metric, int max_connections,
                       int ef_construction, uint64_t capacity, uint64_t seed);

@@ -46,6 +46,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <future>
 #include <mutex>
 #include <random>
 #include <string>
@@ -174,7 +175,12 @@ std::atomic<uint64_t>* g_n_added = nullptr;
 std::mutex* g_in_graph_mu = nullptr;
 std::vector<uint8_t>* g_compacted = nullptr;
 std::atomic<int> flushes{0};
+// postheal mode: the lock the decorator's PostStartup holds around
+// wv_mirror_post_startup_async (g.mu) -- wvgpuFlush takes it too
+std::mutex* g_caller_mu = nullptr;
 int flush_cb(void*) {
+    std::unique_lock<std::mutex> cl;
+    if (g_caller_mu) cl = std::unique_lock<std::mutex>(*g_caller_mu);
     std::lock_guard<std::mutex> l(cpu_mu);
     flush_log();
     const uint64_t na = g_n_added ? g_n_added->load() : 0;
@@ -245,13 +251,20 @@ int main(int argc, char** argv) {
     const std::string root = argv[1];
     const int device = argc > 2 ? std::atoi(argv[2]) : 0;
     const std::string mode = argc > 3 ? argv[3] : "sync";
-    const bool async_start = mode == "async" || mode == "pq", heal = mode == "heal", pqm = mode == "pq";
+    const bool async_start = mode == "async" || mode == "pq", pqm = mode == "pq";
+    bool heal = mode == "heal";
     const bool epgone = mode == "epgone";
     // pqlive: the class is compressed while serving (UpdateUserConfig with
     // PQ.Enabled, config_update.go:97-120 -> Compress, compress.go:39-99),
     // with no write after it: the decorator's callback flushes the log and
     // compacts, and the mirror serves PQ codes from then on
     const bool pqlive = mode == "pqlive";
+    // postheal: heal's self-healing mirror, and a PostStartup posted (under
+    // the decorator's lock, which the resync's flush callback also takes)
+    // while that resync waits in its flush: post_startup_async must return
+    // without waiting for the worker, which then runs the posted startup
+    const bool postheal = mode == "postheal";
+    if (postheal) heal = true;
     if (mode != "sync" && !async_start && !heal && !epgone && !pqlive) { std::fprintf(stderr, "unknown mode %s\n", mode.c_str()); return 2; }
     const std::string log_dir = root + "/main.hnsw.commitlog.d";
     mkdir(root.c_str(), 0755);
@@ -331,6 +344,8 @@ int main(int argc, char** argv) {
         opt.flush = flush_cb;
         opt.resync_backoff_ms = 50;
     }
+    std::mutex caller_mu;
+    if (postheal) g_caller_mu = &caller_mu;
     wv_mirror* m = nullptr;
     if (wv_mirror_create(WV_L2_SQUARED, &cfg, &opt, &m)) { std::fprintf(stderr, "create: %s\n", wv_last_error()); return 1; }
     {
@@ -436,7 +451,41 @@ int main(int argc, char** argv) {
                 std::lock_guard<std::mutex> l(cpu_mu);
                 wvo_add(cpu, id, &store[id * DIM]);
             }
-            if (heal && a == N_ADD / 3) {
+            if (postheal && a == N_ADD / 3) {
+                missed_id = missed_id2 = id;
+                wv_mirror_stats s0;
+                wv_mirror_get_stats(m, &s0);
+                std::unique_lock<std::mutex> cl(caller_mu);   // PostStartup's g.mu.Lock()
+                wv_mirror_mark_stale(m);
+                // the resync has begun (STARTING) and blocks in the flush
+                // callback on caller_mu
+                const auto t_poll = std::chrono::steady_clock::now();
+                for (;;) {
+                    wv_mirror_stats s;
+                    wv_mirror_get_stats(m, &s);
+                    if (s.state == WV_MIRROR_STARTING) break;
+                    if (std::chrono::steady_clock::now() - t_poll > std::chrono::seconds(60)) {
+                        violation("postheal: the resync did not start");
+                        break;
+                    }
+                    std::this_thread::sleep_for(std::chrono::microseconds(50));
+                }
+                std::this_thread::sleep_for(std::chrono::milliseconds(20));   // (into the callback)
+                auto call = std::async(std::launch::async, [&] { return wv_mirror_post_startup_async(m, vector_for_id, nullptr); });
+                if (call.wait_for(std::chrono::seconds(20)) != std::future_status::ready) {
+                    std::fprintf(stderr, "VIOLATION: postheal: post_startup_async waits for the resync whose flush "
+                                         "needs the caller's lock (deadlock)\n");
+                    std::_Exit(1);
+                }
+                if (call.get()) violation(std::string("postheal post_startup_async: ") + wv_last_error());
+                cl.unlock();
+                if (wv_mirror_wait_live(m, 120000)) violation("postheal: the posted startup did not go live");
+                wv_mirror_stats s1;
+                wv_mirror_get_stats(m, &s1);
+                if (s1.startups < s0.startups + 2)
+                    violation("postheal: the posted startup did not run after the resync (startups " +
+                              std::to_string(s0.startups) + " -> " + std::to_string(s1.startups) + ")");
+            } else if (heal && a == N_ADD / 3) {
                 // a write the mirror never saw (the decorator's propagation
                 // failed): stale now, the mirror must heal itself
                 missed_id = id;
@@ -628,7 +677,7 @@ int main(int argc, char** argv) {
     if (!failed && wv_mirror_compact(m)) violation(std::string("final compact: ") + wv_last_error());
     wv_mirror_stats st;
     wv_mirror_get_stats(m, &st);
-    if (heal && !failed && (st.resyncs < 2 || flushes < 2))
+    if (heal && !postheal && !failed && (st.resyncs < 2 || flushes < 2))
         violation("heal: the mirror did not resync by itself after both failures (resyncs " + std::to_string(st.resyncs) + ")");
     const int diffs_final = failed ? -1 : compare(m, CAP, 12, "final");
     if (!failed && st.delta_rows != 0) violation("delta not empty after the final compaction");

@@ -96,13 +96,16 @@ def test_mirror_lifecycle_from_commit_log(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["async", "heal", "pq", "epgone", "pqlive"])
+@pytest.mark.parametrize("mode", ["async", "heal", "postheal", "pq", "epgone", "pqlive"])
 def test_mirror_lifecycle_modes(tmp_path, mode):
     """async: PostStartup returns at once and the mirror builds on its own
     thread while writers and searchers run (the CPU index answers until it is
     live; writes made meanwhile are replayed); heal: a write the mirror never
     saw marks it stale and it resyncs by itself (flush callback, then a
-    rebuild), serving the missed row afterwards; pq: a KMeans-compressed
+    rebuild), serving the missed row afterwards; postheal: a PostStartup
+    posted under the decorator's lock while a resync waits for that lock in
+    its flush callback returns at once and runs after the resync (ADVICE r5:
+    no deadlock); pq: a KMeans-compressed
     index (AddPQ record in the log) is served compressed, equal to the
     restatement's PQ searches (compress.go:39-99, search.go:172-197);
     epgone: the log's entrypoint lost its object -- HNSW searches answer
@@ -128,6 +131,8 @@ def test_mirror_lifecycle_modes(tmp_path, mode):
     if mode == "heal":
         # two failures: the second the moment the first resync went live
         assert r["resyncs"] >= 2 and r["stale_answers"] > 0
+    if mode == "postheal":
+        assert r["resyncs"] >= 1 and r["stale_answers"] > 0
     if mode in ("pq", "pqlive"):
         assert r["pq"] == 1
     print(r)
@@ -163,7 +168,7 @@ def test_host_runtime_under_thread_sanitizer(tmp_path):
         return mode, p
 
     with ThreadPoolExecutor(2) as ex:
-        for mode, p in ex.map(run, ["sync", "async", "heal", "pq", "epgone", "pqlive"]):
+        for mode, p in ex.map(run, ["sync", "async", "heal", "postheal", "pq", "epgone", "pqlive"]):
             races = p.stderr.count("WARNING: ThreadSanitizer")
             assert races == 0 and p.returncode == 0, (mode, races, p.stderr[-4000:])
             r = json.loads(p.stdout.strip().splitlines()[-1])

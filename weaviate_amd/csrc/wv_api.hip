@@ -47,6 +47,8 @@ hipError_t wv_launch_build_search(const wv::BuildParams* b, int waves_per_block,
 hipError_t wv_launch_build_select(const wv::BuildParams* b, hipStream_t s);
 hipError_t wv_launch_build_link(const wv::BuildParams* b, hipStream_t s);
 int wv_hnsw_per_wave_words(int dpad, int efc, int sc, int vc_log2, int xs_log2);
+int wv_hnsw_side_per_wave_words(int dpad, int side_rows, int vc_log2, int xs_log2);
+hipError_t wv_launch_hnsw_side(const wv::HnswParams* p, int waves_per_block, hipStream_t s);
 hipError_t wv_launch_pq_encode(const float* X, int ldx, const uint64_t* ids, uint64_t n_rows, const wv::PqParams* pq,
                                uint8_t* codes, hipStream_t s);
 hipError_t wv_launch_pq_scan(const wv::PqScanParams* p, hipStream_t s);
@@ -216,6 +218,14 @@ __global__ void merge_shards_kernel(const float* in_d, const uint64_t* in_ids, c
     out_n[q] = n;
 }
 
+// queries whose search reported an overflow (status != 0) into *acc
+__global__ void count_nonzero_kernel(const int32_t* st, int n, unsigned long long* acc) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool nz = i < n && st[i] != 0;
+    const unsigned long long c = __popcll(__ballot(nz));
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(acc, c);
+}
+
 __global__ void popcount_rows_kernel(const uint64_t* bits, uint64_t words, uint64_t stride, int nrows,
                                      unsigned long long* out) {
     const int r = blockIdx.x;
@@ -272,6 +282,8 @@ struct wv_index {
     // bitmaps
     std::vector<uint64_t> tomb_host;
     bool any_tomb = false, any_nil = false;   // any tombstone / nil node below gn
+    uint64_t n_tomb = 0;                      // tombstones (sizes the side-register path's state)
+    int last_side_rows = 0, last_side_xs = 0;  // the last side-register launch's capacities
     DevBuf tomb;            // tombstones (HNSW eligibility)
     DevBuf excl;            // tombstone | nil node | no vector (flatSearch skips)
     uint64_t bm_words = 0;
@@ -1333,6 +1345,85 @@ int run_hnsw(wv_index* ix, const float* d_q, int nq, int k, int ef, const uint64
         hp.uniq = static_cast<unsigned long long*>(uniq);
     }
     TREC(4);
+    // Filtered / tombstoned / nil-node searches with ef <= 128 (round 6):
+    // the side-register path, its side columns and expanded-side set sized
+    // from the eligible fraction p (the live side set peaks near
+    // 1.4 ef (1-p)/p, the side expansions likewise: oracle side diagnostics,
+    // DESIGN 3.3); what overflows re-runs once with twice the capacity,
+    // then exactly.  WV_HNSW_NO_SIDE=1 keeps the LDS path.
+    const bool side = filtered && !ix->pq_on && efc <= 128 && !std::getenv("WV_HNSW_NO_SIDE");
+    if (side) {
+        double p_el = 1.0;
+        if (d_allow) {
+            const int rows = allow_stride ? nq : 1;
+            const uint64_t words = std::min<uint64_t>((allow_nbits + 63) / 64, (ix->gn + 63) / 64);
+            HIP_TRY(ix->g_cnt.ensure((size_t)rows * 8));
+            HIP_TRY(hipMemsetAsync(ix->g_cnt.p, 0, (size_t)rows * 8, s));
+            hipLaunchKernelGGL(popcount_rows_kernel, dim3(rows), dim3(256), 0, s, d_allow, words,
+                               allow_stride ? allow_stride : words, rows, ix->g_cnt.as<unsigned long long>());
+            HIP_TRY(hipGetLastError());
+            std::vector<unsigned long long> cnt(rows);
+            HIP_TRY(hipMemcpyAsync(cnt.data(), ix->g_cnt.p, 8 * (size_t)rows, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipStreamSynchronize(s));
+            const unsigned long long mn = *std::min_element(cnt.begin(), cnt.end());
+            p_el = (double)mn / (double)std::max<uint64_t>(1, ix->gn);
+        }
+        p_el *= 1.0 - std::min(1.0, (double)ix->n_tomb / (double)std::max<uint64_t>(1, ix->gn));
+        p_el = std::max(p_el, 1e-4);
+        const double side_need = 1.5 * ef * (1.0 - p_el) / p_el;
+        int side_rows = std::max(2, (int)std::ceil((side_need + 128.0) / 64.0));
+        int x_log2 = 8;
+        while (x_log2 < 20 && (double)(1 << x_log2) < 1.3 * (side_need + 64.0)) ++x_log2;
+        if (const char* e = std::getenv("WV_HNSW_SIDE_ROWS")) side_rows = std::max(1, std::atoi(e));
+        if (const char* e = std::getenv("WV_HNSW_SIDE_XS")) x_log2 = std::max(6, std::atoi(e));
+        // per-wave LDS budget: 13 KiB (12 waves per CU) while the side state
+        // leaves a 4 KiB visited cache beside it, else 20 KiB (8 waves)
+        const int fixed_b = 4 * wv_hnsw_side_per_wave_words(ix->dpad, side_rows, 0, x_log2);
+        int side_kb = fixed_b + 4096 <= 13 * 1024 ? 13 : 20;
+        if (const char* e = std::getenv("WV_HNSW_SIDE_KB")) side_kb = std::max(4, std::atoi(e));
+        auto layout = [&](wv::HnswParams& h, int rows, int xl, int budget_words) -> bool {
+            // shrink to the CU's LDS (status then reports what no longer fits)
+            while (rows > 1 && wv_hnsw_side_per_wave_words(ix->dpad, rows, 10, xl) * 4 > 160 * 1024) {
+                if (xl > 10 && (1 << xl) > 128 * rows) --xl;
+                else --rows;
+            }
+            h.side_rows = rows;
+            h.xs_log2 = xl;
+            const int fixed = wv_hnsw_side_per_wave_words(ix->dpad, rows, 0, xl) - 1;
+            h.vc_log2 = choose_vc_log2(std::max(budget_words, fixed + 512), fixed, ix->gn, &h.vc_tbits);
+            h.vc_log2 = std::max(h.vc_log2, 10);
+            int pw = (wv_hnsw_side_per_wave_words(ix->dpad, rows, h.vc_log2, xl) + 3) & ~3;
+            while (pw * 4 > 160 * 1024 && h.vc_log2 > 8) {
+                --h.vc_log2;
+                pw = (wv_hnsw_side_per_wave_words(ix->dpad, rows, h.vc_log2, xl) + 3) & ~3;
+            }
+            h.per_wave_words = pw;
+            return pw * 4 <= 160 * 1024;
+        };
+        auto wpb_of = [](int pw) {
+            int w = 4;
+            while (w > 1 && (size_t)w * pw * 4 > 160 * 1024) --w;
+            return w;
+        };
+        wv::HnswParams hs = hp;
+        hs.sc = 0;
+        if (!layout(hs, side_rows, x_log2, side_kb * 256)) return fail(WV_EINVAL, "hnsw side state too large");
+        ix->last_side_rows = hs.side_rows;
+        ix->last_side_xs = 1 << hs.xs_log2;
+        HIP_TRY(wv_launch_hnsw_side(&hs, wpb_of(hs.per_wave_words), s));
+        HIP_TRY(ix->stat_acc.ensure(32));
+        hipLaunchKernelGGL(count_nonzero_kernel, dim3((nq + 255) / 256), dim3(256), 0, s, ix->status.as<int32_t>(), nq,
+                           ix->stat_acc.as<unsigned long long>() + 3);
+        HIP_TRY(hipGetLastError());
+        if (!std::getenv("WV_HNSW_NO_WIDE_SIDE")) {
+            // overflowed queries (status != 0; the others' waves exit at
+            // once): twice the columns and the set, the LDS permitting
+            wv::HnswParams h2 = hs;
+            h2.redo = ix->status.as<int32_t>();
+            if (layout(h2, 2 * hs.side_rows, std::min(20, hs.xs_log2 + 1), 2 * side_kb * 256))
+                HIP_TRY(wv_launch_hnsw_side(&h2, wpb_of(h2.per_wave_words), s));
+        }
+    } else {
     // small unfiltered batches (the batcher's callers): a workgroup per
     // query, whose three helper waves take the distance batches' other rows
     // -- while every workgroup is resident (up to 3 per CU at 158 VGPRs; a
@@ -1365,6 +1456,7 @@ int run_hnsw(wv_index* ix, const float* d_q, int nq, int k, int ef, const uint64
         int wpb2 = 4;
         while (wpb2 > 1 && (size_t)wpb2 * pw2 * 4 > 160 * 1024) --wpb2;
         if ((size_t)pw2 * 4 <= 160 * 1024) HIP_TRY(wv_launch_hnsw(&h2, wpb2, s));
+    }
     }
     TREC(5);
     if (uniq) HIP_TRY(hipFreeAsync(uniq, s));
@@ -1453,6 +1545,7 @@ int search_core(wv_index* ix, const float* d_q, int nq, int k, int ef, const uin
     int rc = refresh_bitmaps(ix);
     if (rc) return rc;
     ix->last_dist = ix->last_exp = ix->last_fallbacks = 0;
+    ix->last_side_rows = ix->last_side_xs = 0;
     HIP_TRY(ix->stat_acc.ensure(32));
     HIP_TRY(hipMemsetAsync(ix->stat_acc.p, 0, 32, s));
     ix->stat_stream = s;
@@ -1867,9 +1960,9 @@ int wv_index_set_tombstones(wv_index* ix, const uint64_t* bits, uint64_t nbits) 
     const uint64_t w = std::min<uint64_t>((nbits + 63) / 64, ix->bm_words);
     for (uint64_t i = 0; i < w; ++i) ix->tomb_host[i] = bits ? bits[i] : 0;
     if (nbits & 63 && w == (nbits + 63) / 64 && w > 0) ix->tomb_host[w - 1] &= (1ull << (nbits & 63)) - 1;
-    ix->any_tomb = false;
-    for (uint64_t i = 0; i < ix->bm_words; ++i)
-        if (ix->tomb_host[i]) { ix->any_tomb = true; break; }
+    ix->n_tomb = 0;
+    for (uint64_t i = 0; i < ix->bm_words; ++i) ix->n_tomb += (uint64_t)__builtin_popcountll(ix->tomb_host[i]);
+    ix->any_tomb = ix->n_tomb > 0;
     ix->bitmaps_dirty = true;
     return WV_OK;
 }
@@ -1957,10 +2050,11 @@ static int edit_tombstones(wv_index* ix, const uint64_t* ids, uint64_t n, bool a
     for (uint64_t i = 0; i < n; ++i) {
         if (ids[i] >= ix->capacity) return fail(WV_EINVAL, "tombstone id beyond capacity");
         const uint64_t bit = 1ull << (ids[i] & 63);
-        if (add) ix->tomb_host[ids[i] >> 6] |= bit;
-        else ix->tomb_host[ids[i] >> 6] &= ~bit;
+        uint64_t& w = ix->tomb_host[ids[i] >> 6];
+        if (add && !(w & bit)) { w |= bit; ix->n_tomb++; }
+        else if (!add && (w & bit)) { w &= ~bit; ix->n_tomb--; }
     }
-    ix->any_tomb = std::any_of(ix->tomb_host.begin(), ix->tomb_host.end(), [](uint64_t w) { return w != 0; });
+    ix->any_tomb = ix->n_tomb > 0;
     ix->bitmaps_dirty = true;
     return WV_OK;
 }
@@ -2689,6 +2783,21 @@ int wv_last_batch_stats(wv_index* ix, uint64_t* dist_evals, uint64_t* expansions
     if (dist_evals) *dist_evals = ix->last_dist + acc[0];
     if (expansions) *expansions = ix->last_exp + acc[1];
     if (fallbacks) *fallbacks = ix->last_fallbacks + acc[2];
+    return WV_OK;
+}
+
+int wv_last_side_stats(wv_index* ix, uint64_t* second_pass, int* side_rows, int* side_set) {
+    if (check(ix)) return WV_EINVAL;
+    std::lock_guard<std::mutex> g(ix->mu);
+    HIP_TRY(hipSetDevice(ix->cfg.device));
+    unsigned long long acc[4] = {0, 0, 0, 0};
+    if (ix->stat_acc.p) {
+        HIP_TRY(hipMemcpyAsync(acc, ix->stat_acc.p, 32, hipMemcpyDeviceToHost, ix->stat_stream));
+        HIP_TRY(hipStreamSynchronize(ix->stat_stream));
+    }
+    if (second_pass) *second_pass = acc[3];
+    if (side_rows) *side_rows = ix->last_side_rows;
+    if (side_set) *side_set = ix->last_side_xs;
     return WV_OK;
 }
 

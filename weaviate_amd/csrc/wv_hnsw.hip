@@ -31,6 +31,7 @@
 #include "wv_params.h"
 
 #include <float.h>
+#include <cstdlib>
 
 namespace wv {
 
@@ -40,6 +41,12 @@ constexpr int MAX_LOCAL_TOMB = 4;
 // rows per 8-lane group in one distance round trip (exact_dist_rows)
 #ifndef WV_HNSW_RPG
 #define WV_HNSW_RPG 4
+#endif
+// rows per 8-lane group on the side-register path (its occupancy is bound
+// by LDS, not VGPRs: a wider trip serves a filtered expansion's ~40 new
+// neighbours in one memory round trip)
+#ifndef WV_HNSW_SIDE_RPG
+#define WV_HNSW_SIDE_RPG 4
 #endif
 
 // Diagnostic build only (-DWV_HNSW_STAMPS, tools/hnsw_latency.sh): per-phase
@@ -797,6 +804,405 @@ __global__ __launch_bounds__(256) void wv_hnsw_wg_kernel(HnswParams p) {
 }
 
 // ===========================================================================
+// Side-register path (round 6): filtered, tombstoned or nil-node searches with
+// ef <= 128.  The results R live in registers as on the unfiltered register
+// path (search_layer_reg); the side candidates S -- traversed but ineligible
+// (filtered out at layer 0, tombstoned, or a nil node the descent tombstoned:
+// search.go:282-298, :496-507) -- live unsorted in an LDS array of
+// side_rows x 64 entries, appended batch by batch, with the minimum key and
+// its position kept wave-uniform: a side pop moves the last entry into the
+// popped one's place and rescans (n / 64 LDS reads per lane and one DPP
+// reduction).  The expanded side candidates are an exact set X in LDS (open
+// addressing, probed 64 slots per step), checked when a side candidate is
+// popped: a copy re-inserted after a visited-cache miss is dropped there,
+// never expanded twice.
+//
+// Capacity.  A full array first sheds its dead entries (d > worst once R is
+// full: never expandable, search.go:213-215); the new entries that still do
+// not fit are dropped and the smallest dropped key (xd) is remembered.  The
+// search stays exact while every pop is below xd (the reference would have
+// popped the dropped entry first) and it ends with xd > worst (the
+// reference's loop would not reach it); otherwise -- or when X fills --
+// status != 0 and the host re-runs the query with larger capacities, then
+// exactly.  Sizes come from the list's selectivity (the live side
+// set peaks near 1.4 ef (1-p)/p).
+
+// one step of a (d, id) minimum by DPP (no LDS): lanes whose source is out
+// of range or masked take the identity
+template <int CTRL, int RM>
+__device__ __forceinline__ void kmin_step(float& d, uint32_t& i) {
+    const float od = __uint_as_float((uint32_t)__builtin_amdgcn_update_dpp(
+        (int)__float_as_uint(FLT_MAX), (int)__float_as_uint(d), CTRL, RM, 0xF, false));
+    const uint32_t oi = (uint32_t)__builtin_amdgcn_update_dpp((int)WV_NIL, (int)i, CTRL, RM, 0xF, false);
+    const bool lt = key_less_nb(od, oi, d, i);
+    d = lt ? od : d;
+    i = lt ? oi : i;
+}
+// (d, id) minimum over the wave (row_shr 1/2/4/8 within rows, row_bcast
+// 15/31 across them, lane 63 read out): every lane returns it
+__device__ __forceinline__ void wave_min_key(float& d, uint32_t& i) {
+    kmin_step<0x111, 0xF>(d, i);
+    kmin_step<0x112, 0xF>(d, i);
+    kmin_step<0x114, 0xF>(d, i);
+    kmin_step<0x118, 0xF>(d, i);
+    kmin_step<0x142, 0xA>(d, i);
+    kmin_step<0x143, 0xC>(d, i);
+    d = __uint_as_float((uint32_t)__builtin_amdgcn_readlane((int)__float_as_uint(d), 63));
+    i = (uint32_t)__builtin_amdgcn_readlane((int)i, 63);
+}
+
+template <int METRIC, int NR, int RPG>
+__device__ __forceinline__ void search_layer_side(const HnswParams& p, WaveState& w, int level, int ef, uint32_t ep,
+                                                  float epd, const uint64_t* allow, int nlt, float (&rd)[NR],
+                                                  uint32_t (&ri)[NR], int& Rl, int& status, uint32_t& n_dist,
+                                                  uint32_t& n_exp) {
+    static_assert(NR == 1 || NR == 2, "64 or 128 results per wave");
+    const int lane = threadIdx.x & 63;
+    const int VC = 1 << p.vc_log2;
+    const int XS = 1 << p.xs_log2;
+    const int SC = 64 * p.side_rows;
+    float* Sd = w.Sd;
+    uint32_t* Si = w.Si;
+    for (int i = lane; i < VC; i += 64) w.vc[i] = VC_EMPTY;
+    for (int i = lane; i < XS; i += 64) w.xs[i] = WV_NIL;
+    wave_sync();
+    if (lane == 0) {
+        const uint32_t he = vc_hash(p, ep);
+        w.vc[vc_slot(p, he)] = vc_tag(p, he);
+    }
+    auto eligible = [&](uint32_t id) -> bool {
+        if (p.tomb && bit_test(p.tomb, p.tomb_nbits, id)) return false;
+        for (int t = 0; t < nlt; ++t)
+            if (w.ltomb[t] == id) return false;
+        if (level == 0 && allow && !bit_test(allow, p.allow_nbits, id)) return false;
+        return true;
+    };
+    // insertViableEntrypointsAsCandidatesAndResults (search.go:329-353)
+    const bool ep_ok = eligible(ep);
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        rd[r] = ep_ok && lane == 0 && r == 0 ? epd : FLT_MAX;
+        ri[r] = ep_ok && lane == 0 && r == 0 ? ep : WV_NIL;
+    }
+    Rl = ep_ok ? 1 : 0;
+    // currentWorstResultDistanceToFloat (:355-377)
+    float worst = ep_ok ? epd : FLT_MAX;
+    // S: n entries, minimum (smd, smi) at spos; xd/xi the smallest dropped key
+    int n = 0, spos = 0;
+    float smd = FLT_MAX, xd = FLT_MAX;
+    uint32_t smi = WV_NIL, xi = WV_NIL;
+    if (!ep_ok) {
+        if (lane == 0) { Sd[0] = epd; Si[0] = ep; }
+        n = 1; smd = epd; smi = ep;
+    }
+    // rescan S for its minimum (after a pop or a shed)
+    auto rescan = [&]() {
+        float bd_ = FLT_MAX;
+        uint32_t bi_ = WV_NIL;
+        int bp = 0;
+        for (int j = lane; j < n; j += 64) {
+            const float d = Sd[j];
+            const uint32_t id = Si[j];
+            const bool lt = key_less_nb(d, id, bd_, bi_);
+            bd_ = lt ? d : bd_;
+            bi_ = lt ? id : bi_;
+            bp = lt ? j : bp;
+        }
+        float md = bd_;
+        uint32_t mi = bi_;
+        wave_min_key(md, mi);
+        const uint64_t wm = __ballot(bd_ == md && bi_ == mi);
+        spos = wm ? __builtin_amdgcn_readlane(bp, __builtin_ctzll(wm)) : 0;
+        smd = md;
+        smi = mi;
+    };
+    wave_sync();
+    const uint32_t* nbr_base;
+    int deg;
+    for (;;) {
+        // ---- pop: the first unexpanded result vs the side minimum ----
+        int ridx = -1;
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            const uint64_t um = __ballot(64 * r + lane < Rl && !(ri[r] & WV_FLAG));
+            if (ridx < 0 && um) ridx = 64 * r + __builtin_ctzll(um);
+        }
+        if (ridx < 0 && n == 0) {   // candidates exhausted
+            if (xi != WV_NIL) status |= 1;   // (a dropped one was still to be expanded)
+            break;
+        }
+        float cd = smd;
+        uint32_t cid = smi;
+        bool fromR = false;
+        if (ridx >= 0) {
+            const float rdv = reg_entry_d<NR>(rd, ridx);
+            const uint32_t riv = reg_entry_i<NR>(ri, ridx) & WV_IDMASK;
+            if (n == 0 || key_less(rdv, riv, smd, smi)) { cd = rdv; cid = riv; fromR = true; }
+        }
+        if (cd > worst) {   // :213-215
+            if (xi != WV_NIL && !(xd > worst)) status |= 1;
+            break;
+        }
+        if (xi != WV_NIL && key_less(xd, xi, cd, cid)) { status |= 1; break; }
+        if (fromR) {
+#pragma unroll
+            for (int r = 0; r < NR; ++r)
+                if (64 * r + lane == ridx) ri[r] |= WV_FLAG;
+        } else {
+            // remove it: the last entry takes its place
+            --n;
+            if (lane == 0 && spos != n) { Sd[spos] = Sd[n]; Si[spos] = Si[n]; }
+            wave_sync();
+            rescan();
+            // X: expanded once (search.go:256-264 by way of the exact set)
+            const uint32_t h0 = hash32(cid) >> (32 - p.xs_log2);
+            bool dup = false, placed = false;
+            for (int b = 0; b < XS; b += 64) {
+                const uint32_t slot = (h0 + b + lane) & (XS - 1);
+                const uint32_t v = w.xs[slot];
+                const uint64_t fm = __ballot(v == cid), em = __ballot(v == WV_NIL);
+                const int fe = em ? __builtin_ctzll(em) : 64;
+                if (fm && __builtin_ctzll(fm) < fe) { dup = true; break; }
+                if (em) {
+                    if (lane == fe) w.xs[slot] = cid;
+                    placed = true;
+                    break;
+                }
+            }
+            if (dup) continue;
+            if (!placed) { status |= 2; break; }
+        }
+        uint32_t pre0 = WV_NIL, pre1 = WV_NIL;
+        if (level == 0) {
+            nbr_base = p.layer0 + (uint64_t)cid * p.deg0;
+            deg = p.deg0;
+            if (lane < deg) pre0 = nbr_base[lane];
+            if (64 + lane < deg) pre1 = nbr_base[64 + lane];
+            if (p.levels[cid] < 0) continue;   // :217-234
+        } else {
+            if (p.levels[cid] < level) continue;
+            const uint32_t row = p.upper_row[cid];
+            nbr_base = p.upper + ((uint64_t)row * p.upper_levels + (level - 1)) * p.degU;
+            deg = p.degU;
+        }
+        n_exp++;
+        for (int c0 = 0; c0 < deg; c0 += BATCH) {
+            uint32_t id0 = WV_NIL, id1 = WV_NIL;
+            if (level == 0 && c0 == 0) {
+                id0 = pre0;
+                id1 = pre1;
+            } else {
+                if (c0 + lane < deg) id0 = nbr_base[c0 + lane];
+                if (c0 + 64 + lane < deg) id1 = nbr_base[c0 + 64 + lane];
+            }
+            bool v0 = id0 != WV_NIL && id0 < p.N;
+            bool v1 = id1 != WV_NIL && id1 < p.N;
+            const uint32_t e0 = vc_hash(p, id0), e1 = vc_hash(p, id1);
+            const uint32_t h0 = v0 ? vc_slot(p, e0) : 0, h1 = v1 ? vc_slot(p, e1) : 0;
+            const uint16_t t0 = vc_tag(p, e0), t1 = vc_tag(p, e1);
+            if (v0 && w.vc[h0] == t0) v0 = false;
+            if (v1 && w.vc[h1] == t1) v1 = false;
+            wave_sync();
+            if (v0) w.vc[h0] = t0;
+            if (v1) w.vc[h1] = t1;
+            const uint64_t m0 = __ballot(v0), m1 = __ballot(v1);
+            const int n0 = __popcll(m0);
+            const int nb = n0 + __popcll(m1);
+            if (v0) w.Bi[mbcnt64(m0)] = id0;
+            if (v1) w.Bi[n0 + mbcnt64(m1)] = id1;
+            // eligibility (tombstone / allow words) loads issued beside the
+            // row loads, consumed after them (no round trip of their own)
+            const bool el0 = v0 && eligible(id0), el1 = v1 && eligible(id1);
+            wave_sync();
+            if (nb == 0) continue;
+            for (int base = 0; base < nb; base += 8 * RPG)
+                exact_dist_rows<METRIC, RPG, true>(w.qv, p.X, p.ldx, p.D, w.Bi + base, nb - base, w.Bd + base, lane);
+            n_dist += eval_count(w, level, nb, v0, id0, v1, id1);
+            wave_sync();
+            // ---- keep test against the batch's starting state (search.go:282),
+            // on the neighbours' own lanes (batch order = lane order, id0s
+            // first): eligible keys into R one by one, ineligible ones to S ----
+            float bd[2];
+            uint32_t bi[2];
+            uint64_t kmask[2], smask[2];
+            bd[0] = v0 ? w.Bd[mbcnt64(m0)] : FLT_MAX;
+            bd[1] = v1 ? w.Bd[n0 + mbcnt64(m1)] : FLT_MAX;
+            bi[0] = id0;
+            bi[1] = id1;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const bool keep = (h ? v1 : v0) && (bd[h] < worst || Rl < ef);
+                const bool el = h ? el1 : el0;
+                kmask[h] = __ballot(keep && el);
+                smask[h] = __ballot(keep && !el);
+            }
+            const int ns0 = __popcll(smask[0]);
+            const int ns = ns0 + __popcll(smask[1]);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                uint64_t km = kmask[h];
+                while (km) {
+                    const int src = __builtin_ctzll(km);
+                    km &= km - 1;
+                    const float d = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(bd[h]), src));
+                    const uint32_t id = (uint32_t)__builtin_amdgcn_readlane(bi[h], src);
+                    int pos = 0;
+#pragma unroll
+                    for (int r = 0; r < NR; ++r)
+                        pos += __popcll(__ballot((64 * r + lane < Rl) & key_less_nb(rd[r], ri[r] & WV_IDMASK, d, id)));
+                    if (pos >= ef) continue;
+                    if (pos < Rl && reg_entry_d<NR>(rd, pos) == d && (reg_entry_i<NR>(ri, pos) & WV_IDMASK) == id)
+                        continue;   // already a result (a neighbour the visited cache forgot)
+                    float sd[NR];
+                    uint32_t si[NR];
+#pragma unroll
+                    for (int r = 0; r < NR; ++r) {
+                        sd[r] = wave_shr1(rd[r]);
+                        si[r] = wave_shr1(ri[r]);
+                        if (r > 0) {
+                            const float cdv = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(rd[r - 1]), 63));
+                            const uint32_t civ = (uint32_t)__builtin_amdgcn_readlane(ri[r - 1], 63);
+                            if (lane == 0) { sd[r] = cdv; si[r] = civ; }
+                        }
+                    }
+#pragma unroll
+                    for (int r = 0; r < NR; ++r) {
+                        const int e = 64 * r + lane;
+                        if (e > pos) { rd[r] = sd[r]; ri[r] = si[r]; }
+                        if (e == pos) { rd[r] = d; ri[r] = id; }
+                    }
+                    Rl = min(Rl + 1, ef);
+                    worst = reg_entry_d<NR>(rd, Rl - 1);
+                }
+            }
+            if (ns == 0) continue;
+            // ---- the ineligible keys to S ----
+            if (n + ns > SC && Rl >= ef) {
+                // shed the dead (d > worst), in place: a chunk's reads come
+                // before its writes, which land at or below them
+                int k = 0;
+                for (int j0 = 0; j0 < n; j0 += 64) {
+                    const int j = j0 + lane;
+                    const float d = j < n ? Sd[j] : FLT_MAX;
+                    const uint32_t id = j < n ? Si[j] : WV_NIL;
+                    const bool live = j < n && !(d > worst);
+                    const uint64_t lm = __ballot(live);
+                    wave_sync();
+                    if (live) { Sd[k + mbcnt64(lm)] = d; Si[k + mbcnt64(lm)] = id; }
+                    k += __popcll(lm);
+                    wave_sync();
+                }
+                n = k;
+                rescan();
+            }
+            const int fit = min(ns, SC - n);
+            float nd_ = FLT_MAX, xd_ = FLT_MAX;
+            uint32_t ni_ = WV_NIL, xi_ = WV_NIL;
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+                if ((smask[h] >> lane) & 1) {
+                    const int r = (h ? ns0 : 0) + mbcnt64(smask[h]);
+                    if (r < fit) {
+                        Sd[n + r] = bd[h];
+                        Si[n + r] = bi[h];
+                        if (key_less(bd[h], bi[h], nd_, ni_)) { nd_ = bd[h]; ni_ = bi[h]; }
+                    } else if (key_less(bd[h], bi[h], xd_, xi_)) {
+                        xd_ = bd[h]; xi_ = bi[h];
+                    }
+                }
+            wave_min_key(nd_, ni_);
+            if (key_less(nd_, ni_, smd, smi)) {
+                smd = nd_;
+                smi = ni_;
+                const uint64_t pm0 = __ballot(((smask[0] >> lane) & 1) && bd[0] == nd_ && bi[0] == ni_);
+                const uint64_t pm1 = __ballot(((smask[1] >> lane) & 1) && bd[1] == nd_ && bi[1] == ni_);
+                spos = pm0 ? n + __popcll(smask[0] & ((1ull << __builtin_ctzll(pm0)) - 1))
+                           : n + ns0 + __popcll(smask[1] & ((1ull << __builtin_ctzll(pm1)) - 1));
+            }
+            if (fit < ns) {
+                wave_min_key(xd_, xi_);
+                if (key_less(xd_, xi_, xd, xi)) { xd = xd_; xi = xi_; }
+            }
+            n += fit;
+            wave_sync();
+        }
+    }
+}
+
+template <int METRIC, int NR, int RPG>
+__device__ __forceinline__ void knn_one_side(const HnswParams& p, WaveState& w, int q) {
+    const int lane = threadIdx.x & 63;
+    const int g = lane & 7;
+    for (int i = lane; i < p.dpad; i += 64) w.qv[i] = i < p.D ? p.Q[(uint64_t)q * p.ldq + i] : 0.f;
+    wave_sync();
+    const uint64_t* allow = p.allow ? p.allow + (p.allow_stride ? (uint64_t)q * p.allow_stride : 0) : nullptr;
+    int status = 0, nlt = 0;
+    uint32_t n_dist = 0, n_exp = 0;
+    uint32_t ep = p.entrypoint;
+    float epd = __shfl(exact_dist_group8<METRIC>(w.qv, p.X + (uint64_t)ep * p.ldx, p.D, g), 0, 64);
+    n_dist++;
+    float rd[NR];
+    uint32_t ri[NR];
+    int Rl = 0;
+    // greedy descent, levels max..1 with ef = 1 (search.go:479-521): a nil
+    // result is tombstoned for the rest of the search (:496-507)
+    for (int level = p.max_level; level >= 1 && !status; --level) {
+        search_layer_side<METRIC, NR, RPG>(p, w, level, 1, ep, epd, nullptr, nlt, rd, ri, Rl, status, n_dist, n_exp);
+        if (Rl > 0) {
+            const uint32_t cid = (uint32_t)__builtin_amdgcn_readlane(ri[0], 0) & WV_IDMASK;
+            if (p.levels[cid] < 0) {
+                if (nlt < MAX_LOCAL_TOMB) {
+                    if (lane == 0) w.ltomb[nlt] = cid;
+                    nlt++;
+                }
+                wave_sync();
+            } else {
+                ep = cid;
+                epd = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(rd[0]), 0));
+            }
+        }
+    }
+    if (!status)
+        search_layer_side<METRIC, NR, RPG>(p, w, 0, p.ef, ep, epd, allow, nlt, rd, ri, Rl, status, n_dist, n_exp);
+    const int n = status ? 0 : min(Rl, p.k);
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const int e = 64 * r + lane;
+        if (e < n) {
+            p.out_ids[(uint64_t)q * p.k + e] = p.id_base + (ri[r] & WV_IDMASK);
+            p.out_d[(uint64_t)q * p.k + e] = rd[r];
+        }
+    }
+    if (lane == 0) {
+        p.out_n[q] = n;
+        p.status[q] = status;
+        if (p.counters) { p.counters[2 * q] = n_dist; p.counters[2 * q + 1] = n_exp; }
+    }
+}
+
+// LDS per wave: query, batch, visited cache, side columns, X, local tombstones
+// WPS: waves per SIMD the register allocation targets (2: no spills, 3: a
+// few VGPRs spilled to scratch for 12 waves per CU when the LDS allows it)
+template <int METRIC, int NR, int RPG, int WPS>
+__global__ __launch_bounds__(256, WPS) void wv_hnsw_side_kernel(HnswParams p) {
+    extern __shared__ float lds[];
+    const int wave = threadIdx.x >> 6;
+    const int q = blockIdx.x * (blockDim.x >> 6) + wave;
+    if (q >= p.nq) return;
+    if (p.redo && p.redo[q] == 0) return;   // (second pass: this query completed)
+    float* cur = lds + (uint64_t)wave * p.per_wave_words;
+    WaveState w{};
+    w.qv = cur; cur += p.dpad;
+    w.Bd = cur; cur += BATCH; w.Bi = reinterpret_cast<uint32_t*>(cur); cur += BATCH;
+    w.Sd = cur; cur += 64 * p.side_rows; w.Si = reinterpret_cast<uint32_t*>(cur); cur += 64 * p.side_rows;
+    w.xs = reinterpret_cast<uint32_t*>(cur); cur += (1 << p.xs_log2);
+    w.ltomb = reinterpret_cast<uint32_t*>(cur); cur += MAX_LOCAL_TOMB;
+    w.vc = reinterpret_cast<uint16_t*>(cur);
+    w.ub = p.uniq ? p.uniq + (uint64_t)q * p.uniq_words : nullptr;
+    knn_one_side<METRIC, NR, RPG>(p, w, q);
+}
+
+// ===========================================================================
 // GPU graph construction -- insert.go:103-217 in batches.
 // A batch of new nodes is inserted against the graph of every node before it:
 //   1. wv_build_search_kernel (one wave per node): findBestEntrypointForNode
@@ -1031,6 +1437,10 @@ __global__ __launch_bounds__(64) void wv_build_link_kernel(BuildParams b) {
     else build_link_one<WV_METRIC_COSINE>(b, r, ci, cd, ui, ud, sel, rowl);
 }
 
+int hnsw_side_per_wave_words(int dpad, int side_rows, int vc_log2, int xs_log2) {
+    return dpad + 2 * BATCH + 128 * side_rows + (1 << xs_log2) + MAX_LOCAL_TOMB + ((1 << vc_log2) + 1) / 2;
+}
+
 int hnsw_per_wave_words(int dpad, int efc, int sc, int vc_log2, int xs_log2) {
     return dpad + 4 * efc + 4 * sc + 4 * BATCH + ((1 << vc_log2) + 1) / 2 + (1 << xs_log2) + MAX_LOCAL_TOMB;
 }
@@ -1041,6 +1451,39 @@ extern "C" {
 
 int wv_hnsw_per_wave_words(int dpad, int efc, int sc, int vc_log2, int xs_log2) {
     return wv::hnsw_per_wave_words(dpad, efc, sc, vc_log2, xs_log2);
+}
+
+int wv_hnsw_side_per_wave_words(int dpad, int side_rows, int vc_log2, int xs_log2) {
+    return wv::hnsw_side_per_wave_words(dpad, side_rows, vc_log2, xs_log2);
+}
+
+// side-register path (filtered / tombstoned / nil nodes, ef <= 128, no PQ)
+hipError_t wv_launch_hnsw_side(const wv::HnswParams* p, int waves_per_block, hipStream_t s) {
+    const size_t lds = (size_t)waves_per_block * p->per_wave_words * sizeof(float);
+    const unsigned blocks = (unsigned)((p->nq + waves_per_block - 1) / waves_per_block);
+    if (blocks == 0) return hipSuccess;
+    const int nr = p->efc == 64 ? 1 : p->efc == 128 ? 2 : 0;
+    if (nr == 0 || p->pq.codes || p->side_rows < 1) return hipErrorInvalidValue;
+#define WV_HNSW_SIDE_W(M, NRV, W)                                                                                   \
+    hipLaunchKernelGGL((wv::wv_hnsw_side_kernel<M, NRV, WV_HNSW_SIDE_RPG, W>), dim3(blocks),                          \
+                       dim3(64 * waves_per_block), lds, s, *p)
+#define WV_HNSW_SIDE(M)                                                                                             \
+    do {                                                                                                            \
+        if (nr == 1 && wps == 3) WV_HNSW_SIDE_W(M, 1, 3);                                                           \
+        else if (nr == 1) WV_HNSW_SIDE_W(M, 1, 2);                                                                  \
+        else if (wps == 3) WV_HNSW_SIDE_W(M, 2, 3);                                                                 \
+        else WV_HNSW_SIDE_W(M, 2, 2);                                                                               \
+    } while (0)
+    // 12 waves per CU need <= 168 VGPRs (spilling a few) and <= 13 KiB of LDS
+    // per wave; otherwise the LDS caps it at 8 anyway
+    int wps = (size_t)p->per_wave_words * 4 <= 13 * 1024 ? 3 : 2;
+    if (const char* e = std::getenv("WV_HNSW_SIDE_WPS")) wps = std::atoi(e) == 3 ? 3 : 2;
+    if (p->metric == WV_METRIC_L2) WV_HNSW_SIDE(WV_METRIC_L2);
+    else if (p->metric == WV_METRIC_DOT) WV_HNSW_SIDE(WV_METRIC_DOT);
+    else WV_HNSW_SIDE(WV_METRIC_COSINE);
+#undef WV_HNSW_SIDE
+#undef WV_HNSW_SIDE_W
+    return hipGetLastError();
 }
 
 hipError_t wv_launch_build_search(const wv::BuildParams* b, int waves_per_block, hipStream_t s) {

@@ -226,6 +226,13 @@ struct wv_mirror {
     std::condition_variable wk_cv;
     std::thread worker;
     bool want_start = false, resync_next = false, busy = false;
+    // a startup posted while another build ran (wv_mirror_post_startup_async
+    // does not wait for it: its Go caller may hold the lock the running
+    // resync's flush callback takes): the worker adopts this source and
+    // starts it after the current install
+    bool fresh_pending = false;
+    wv_vector_source next_src = nullptr;
+    void* next_ctx = nullptr;
     std::atomic<bool> stop{false};
     int backoff_ms = 0;
     // failure injection for the replay harness: hold the worker this long
@@ -498,9 +505,16 @@ struct wv_mirror {
         for (;;) {
             wk_cv.wait(l, [&] { return stop.load() || want_start; });
             if (stop) return;
-            const bool resync = resync_next;
+            bool resync = resync_next;
             want_start = false;
             resync_next = false;
+            if (fresh_pending) {   // (a posted startup supersedes a queued resync)
+                fresh_pending = false;
+                resync = false;
+                src = next_src;
+                src_ctx = next_ctx;
+                begin_start();   // (wk_mu -> pend_mu: no path takes them the other way)
+            }
             if (resync) {
                 const int delay = backoff_ms;
                 if (delay > 0 && wk_cv.wait_until(l, wait_clock::now() + std::chrono::milliseconds(delay), [&] { return stop.load(); }))
@@ -599,10 +613,20 @@ int wv_mirror_post_startup(wv_mirror* m, wv_vector_source src, void* ctx) {
 int wv_mirror_post_startup_async(wv_mirror* m, wv_vector_source src, void* ctx) {
     if (!m || !src) return err(WV_EINVAL, "wv_mirror_post_startup_async: bad argument");
     std::unique_lock<std::mutex> l(m->wk_mu);
-    // a startup or resync in flight first installs (begin_start below clears
-    // the writes queued for that install, and run_startup assumes STARTING);
-    // the wait is for the build already running, not for the one posted here
-    m->wk_cv.wait(l, [&] { return !m->busy; });
+    if (m->busy) {
+        // a startup or resync in flight installs first (begin_start would
+        // clear the writes queued for that install, and run_startup assumes
+        // STARTING): the worker starts this one after it.  No wait here --
+        // the running build may call the flush callback, which takes the
+        // caller's lock (PostStartup holds g.mu)
+        m->next_src = src;
+        m->next_ctx = ctx;
+        m->fresh_pending = true;
+        m->want_start = true;
+        m->resync_next = false;
+        m->wk_cv.notify_all();
+        return WV_OK;
+    }
     m->src = src;
     m->src_ctx = ctx;
     m->begin_start();
@@ -616,7 +640,7 @@ int wv_mirror_post_startup_async(wv_mirror* m, wv_vector_source src, void* ctx) 
 int wv_mirror_wait_live(wv_mirror* m, int timeout_ms) {
     if (!m) return err(WV_EINVAL, "wv_mirror_wait_live: bad argument");
     std::unique_lock<std::mutex> l(m->wk_mu);
-    auto done = [&] { return m->live() || (!m->busy && !m->want_start); };
+    auto done = [&] { return (m->live() && !m->fresh_pending) || (!m->busy && !m->want_start); };
     if (timeout_ms < 0) m->wk_cv.wait(l, done);
     else m->wk_cv.wait_until(l, wait_clock::now() + std::chrono::milliseconds(timeout_ms), done);
     return m->live() ? WV_OK : err(WV_ESTALE, "wv_mirror: not live");

@@ -373,6 +373,11 @@ struct HnswParams {
     // batches): wave 0 searches, waves 1..3 compute rows 32 v .. 32 v + 31 of
     // every distance batch -- one memory round trip for up to 128 rows
     int wg_helpers;
+    // (round 6) side-register path (wv_hnsw_side_kernel: filtered,
+    // tombstoned or nil-node searches with ef <= 128): results in registers,
+    // side candidates in side_rows x 64 swizzled per-lane LDS columns, the
+    // expanded side candidates in an exact 2^xs_log2-slot set
+    int side_rows;
 };
 
 // Flat search over PQ codes (flat_search.go:19-74 on a compressed index):

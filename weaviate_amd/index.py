@@ -351,6 +351,13 @@ class GPUVectorIndex:
         check(lib().wv_last_batch_stats(self._h, C.byref(a), C.byref(b), C.byref(c)))
         return {"dist_evals": a.value, "expansions": b.value, "fallbacks": c.value}
 
+    def last_side_stats(self):
+        """filtered HNSW: queries re-run with twice the side capacity, and the
+        first launch's side columns / expanded-side set slots"""
+        a, b, c = C.c_uint64(), C.c_int(), C.c_int()
+        check(lib().wv_last_side_stats(self._h, C.byref(a), C.byref(b), C.byref(c)))
+        return {"second_pass": a.value, "side_rows": b.value, "side_set": c.value}
+
 
 class CommitLogGraph:
     """A graph replayed from HNSW commit logs (wv_graph_*, deserializer.go:80-158).
