@@ -870,6 +870,8 @@ def run_hnsw(args, ctx, W, with_cpu):
         res["ef_sweep"] = sweep
     if args.concurrency and ws == 1:
         res["concurrent_callers"] = concurrent_callers(args, ix, queries)
+        if args.open_loop:
+            res["open_loop"] = open_loop(args, ix, queries, res["concurrent_callers"])
     if not with_cpu and getattr(args, "counts_sample", 0) > 0 and base is not None:
         # SURVEY 8d's byte basis from the restatement's own evaluation counts
         # on a query sample of this shard's graph (no CPU timing): the GPU's
@@ -1065,6 +1067,47 @@ def concurrent_callers(args, ix, queries):
     return out
 
 
+def open_loop(args, ix, queries, closed):
+    """Open-loop arrivals through the micro-batcher: Poisson requests at 10 %
+    and 50 % of the closed-loop capacity (the largest caller count's QPS),
+    each issued at its time by a pool of native threads -- the reference
+    answers every SearchByVector on its own (shard_read.go:252), so an
+    arrival must not wait for callers that are not coming (wv_batcher.cpp:
+    the refill wait runs only while the last batch's callers resubmit).
+    Latency from the scheduled arrival (no coordinated omission)."""
+    import ctypes as C
+    path = os.path.join(ROOT, "tests", "native", "libwvload.so")
+    lib = C.CDLL(path)
+    if not hasattr(lib, "wvl_open_loop"):
+        return {"error": "libwvload.so lacks wvl_open_loop"}
+    lib.wvl_open_loop.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_double, C.c_double, C.c_int,
+                                  C.c_int, C.c_void_p]
+    caps = [v["value"] for v in closed.values() if isinstance(v, dict) and "value" in v]
+    if not caps:
+        return {"error": "no closed-loop capacity"}
+    cap = max(caps)
+    q = np.ascontiguousarray(queries, dtype=np.float32)
+    ix.update_user_config(ef=args.ef)
+    out = {"capacity_qps": round(cap, 1)}
+    for f in args.open_loop:
+        rate = f * cap
+        r = np.zeros(8, np.float64)
+        rc = lib.wvl_open_loop(C.c_void_p(ix._h.value if hasattr(ix._h, "value") else ix._h), q.ctypes.data,
+                               q.shape[0], q.shape[1], args.k, rate, args.open_loop_seconds, args.max_batch, 512,
+                               r.ctypes.data)
+        if rc:
+            out[f"{f:.0%}"] = {"error": f"status {rc}"}
+            continue
+        out[f"{f:.0%}"] = {"offered_qps": round(rate, 1), "achieved_qps": round(r[0], 1), "p50_us": round(r[1], 1),
+                           "p99_us": round(r[2], 1), "p999_us": round(r[3], 1), "max_us": round(r[4], 1),
+                           "mean_batch": round(r[5], 1), "requests": int(r[6]), "late_starts": int(r[7])}
+    ix.update_user_config(ef=-1)
+    out["note"] = ("Poisson arrivals (seed 7) at the given share of the closed-loop capacity, 512 pool threads, "
+                   f"k={args.k}, ef={args.ef}; latency from the scheduled arrival; late_starts = requests issued "
+                   ">50 us after their time (pool saturated)")
+    return out
+
+
 def group_leg(args):
     """Child process (no torch.distributed): one process drives `--group-devices`
     through libwvgpu.so's in-process group (wv_group_*, the layout a single Go
@@ -1153,6 +1196,9 @@ def main():
     ap.add_argument("--concurrency", default="1,8,64,256",
                     help="hnsw: concurrent single-query caller counts timed through the micro-batcher ('' = skip)")
     ap.add_argument("--concurrency-seconds", type=float, default=2.0)
+    ap.add_argument("--open-loop", default="0.1,0.5",
+                    help="hnsw: open-loop Poisson arrival rates as shares of the closed-loop capacity ('' = skip)")
+    ap.add_argument("--open-loop-seconds", type=float, default=1.5)
     ap.add_argument("--max-batch", type=int, default=1024, help="micro-batcher: queries per launch")
     ap.add_argument("--allow-frac", type=float, default=0.0,
                     help="exact mode: shared allow list, Bernoulli(p) over ids (seed 3, BASELINE configs[3])")
@@ -1212,6 +1258,7 @@ def main():
     args.ef_sweep = [int(x) for x in args.ef_sweep.split(",") if x]
     args.c4_fracs = [float(x) for x in args.c4_fracs.split(",") if x]
     args.concurrency = [int(x) for x in args.concurrency.split(",") if x]
+    args.open_loop = [float(x) for x in args.open_loop.split(",") if x]
     GLOVE_NOISE = args.glove_noise
     if args.group_leg:
         if args.data == "auto":

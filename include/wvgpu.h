@@ -229,11 +229,12 @@ int wv_merge_shards_device(const float *d_in_dists, const uint64_t *d_in_ids, co
 int wv_last_batch_stats(wv_index *ix, uint64_t *dist_evals, uint64_t *expansions, uint64_t *fallbacks);
 
 /* The last batch's filtered-HNSW state (nullable outputs): the queries whose
- * side candidates outgrew the first launch's capacity and were re-run with
- * twice of it, and that first launch's side columns (rows of 64 entries) and
- * expanded-side set slots (0 when no filtered HNSW search ran).  Waits for
- * the batch to finish.  A measurement hook (no reference counterpart). */
-int wv_last_side_stats(wv_index *ix, uint64_t *second_pass, int *side_rows, int *side_set);
+ * side candidates outgrew the per-query spill (answered by the exact
+ * fallback), and the side-register launch's LDS side array (rows of 64
+ * entries) and spill capacity (entries per query; 0 when no filtered HNSW
+ * search ran).  Waits for the batch to finish.  A measurement hook (no
+ * reference counterpart). */
+int wv_last_side_stats(wv_index *ix, uint64_t *overflowed, int *side_rows, int *spill_cap);
 
 /* Kernel timing with HIP events on the launch stream (off by default).  When
  * enabled, every batch records the device time of its dominant kernels: the

@@ -7,6 +7,8 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cmath>
+#include <random>
 #include <thread>
 #include <vector>
 
@@ -70,6 +72,75 @@ int wvl_concurrent(wv_index* ix, const float* queries, int nq, int dim, int k, i
     out[3] = b1 > b0 ? (double)(r1 - r0) / (double)(b1 - b0) : 0.0;
     out[4] = (double)(r1 - r0);
     out[5] = el;
+    return WV_OK;
+}
+
+// Open loop: requests arrive at Poisson times of rate `rate` (seed 7) for
+// `seconds`, each issued at its time by one of `pool` threads (a pool larger
+// than rate x latency keeps arrivals independent of completions); latency is
+// measured from the scheduled arrival, so a request that waits for a free
+// thread is charged for it.  out[0] achieved QPS, out[1] p50 (us), out[2] p99,
+// out[3] p99.9, out[4] max, out[5] mean batch size, out[6] requests, out[7]
+// requests that started > 50 us late (pool saturated).
+int wvl_open_loop(wv_index* ix, const float* queries, int nq, int dim, int k, double rate, double seconds,
+                  int max_batch, int pool, double* out) {
+    if (!ix || !queries || nq <= 0 || dim <= 0 || k <= 0 || rate <= 0 || seconds <= 0 || pool <= 0 || !out)
+        return WV_EINVAL;
+    wv_batcher* b = nullptr;
+    int rc = wv_batcher_create(ix, dim, max_batch, 0, &b);
+    if (rc) return rc;
+    using clk = std::chrono::steady_clock;
+    const size_t n = (size_t)std::max(1.0, std::ceil(rate * seconds));
+    std::vector<double> at(n);   // arrival offsets (s)
+    std::mt19937_64 rng(7);
+    std::exponential_distribution<double> gap(rate);
+    double t = 0.0;
+    for (size_t i = 0; i < n; ++i) { t += gap(rng); at[i] = t; }
+    std::vector<float> lat(n, 0.f);
+    std::atomic<size_t> next{0};
+    std::atomic<int> failed{0}, late{0};
+    uint64_t r0 = 0, b0 = 0, r1 = 0, b1 = 0;
+    wv_batcher_stats(b, &r0, &b0);
+    const auto t0 = clk::now() + std::chrono::milliseconds(20);
+    std::vector<std::thread> ts;
+    for (int w = 0; w < pool; ++w) {
+        ts.emplace_back([&] {
+            std::vector<uint64_t> ids(k);
+            std::vector<float> ds(k);
+            int32_t cnt = 0;
+            for (;;) {
+                const size_t i = next.fetch_add(1);
+                if (i >= n || failed.load()) return;
+                const auto due = t0 + std::chrono::duration_cast<clk::duration>(std::chrono::duration<double>(at[i]));
+                // sleep to just before the arrival, then spin
+                if (due - clk::now() > std::chrono::microseconds(200))
+                    std::this_thread::sleep_until(due - std::chrono::microseconds(100));
+                while (clk::now() < due) std::this_thread::yield();
+                if (clk::now() - due > std::chrono::microseconds(50)) late++;
+                const float* q = queries + (i % (size_t)nq) * dim;
+                if (wv_batcher_search(b, q, k, nullptr, 0, ids.data(), ds.data(), &cnt)) { failed = 1; return; }
+                lat[i] = std::chrono::duration<float, std::micro>(clk::now() - due).count();
+            }
+        });
+    }
+    for (auto& th : ts) th.join();
+    const double el = std::chrono::duration<double>(clk::now() - t0).count();
+    wv_batcher_stats(b, &r1, &b1);
+    wv_batcher_destroy(b);
+    if (failed) return WV_EDEVICE;
+    const size_t skip = n / 10;   // (warm-up)
+    std::vector<float> all(lat.begin() + skip, lat.end());
+    if (all.empty()) return WV_ESTATE;
+    std::sort(all.begin(), all.end());
+    auto pct = [&](double f) { return (double)all[std::min(all.size() - 1, (size_t)(f * (double)all.size()))]; };
+    out[0] = (double)n / el;
+    out[1] = pct(0.5);
+    out[2] = pct(0.99);
+    out[3] = pct(0.999);
+    out[4] = (double)all.back();
+    out[5] = b1 > b0 ? (double)(r1 - r0) / (double)(b1 - b0) : 0.0;
+    out[6] = (double)n;
+    out[7] = (double)late.load();
     return WV_OK;
 }
 

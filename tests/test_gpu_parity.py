@@ -976,3 +976,29 @@ def test_hnsw_workgroup_per_query_small_batches(metric, d, M, monkeypatch):
             assert np.array_equal(ids, ids1) and np.array_equal(ds.view(np.uint32), ds1.view(np.uint32))
             assert np.array_equal(cnt, cnt1)
     ix.close()
+
+
+@pytest.mark.parametrize("n", [1, 2, 40])
+def test_hnsw_workgroup_launch_edge_graphs(n, monkeypatch):
+    """The workgroup-per-query launch's barrier pairing (wv_hnsw.hip, above
+    wg_dist) on edge shapes: a one- and two-node graph and a small one whose
+    top level is 0 or 1, k = 1 and ef = 1, one and three queries -- every
+    launch drains (no early return past a pending barrier) and answers as the
+    one-wave kernel and the restatement do."""
+    d = 32
+    base, idx = _build_graph(n, d, O.L2, M=64)
+    qs = np.random.default_rng(5).random((3, d), dtype=np.float32)
+    ix = W.GPUVectorIndex(d, "l2-squared", capacity=n, max_connections=64)
+    ix.upload_vectors(base)
+    ix.upload_graph(idx.export_graph())
+    for k, ef in ((1, 1), (1, 10), (10, 64)):
+        oi, od, on, _ = idx.search_batch(qs, k, ef, threads=2)
+        for nb in (1, 3):
+            ids, ds, cnt = ix.search_batch(qs[:nb], k, ef=ef, mode="hnsw")
+            assert cnt.tolist() == on[:nb].tolist()
+            _same(ids, ds, oi[:nb], od[:nb])
+            monkeypatch.setenv("WV_HNSW_WG_MAX", "0")
+            ids1, ds1, cnt1 = ix.search_batch(qs[:nb], k, ef=ef, mode="hnsw")
+            monkeypatch.delenv("WV_HNSW_WG_MAX")
+            assert np.array_equal(ids, ids1) and np.array_equal(cnt, cnt1)
+    ix.close()

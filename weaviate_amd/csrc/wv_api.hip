@@ -283,7 +283,8 @@ struct wv_index {
     std::vector<uint64_t> tomb_host;
     bool any_tomb = false, any_nil = false;   // any tombstone / nil node below gn
     uint64_t n_tomb = 0;                      // tombstones (sizes the side-register path's state)
-    int last_side_rows = 0, last_side_xs = 0;  // the last side-register launch's capacities
+    int last_side_rows = 0, last_side_xs = 0;  // the last side-register launch's LDS rows / spill capacity
+    DevBuf side_vb, side_sp;                   // its visited bitmaps and spills (HBM scratch)
     DevBuf tomb;            // tombstones (HNSW eligibility)
     DevBuf excl;            // tombstone | nil node | no vector (flatSearch skips)
     uint64_t bm_words = 0;
@@ -1338,7 +1339,8 @@ int run_hnsw(wv_index* ix, const float* d_q, int nq, int k, int ef, const uint64
     // diagnostic: exact per-query visited bitmaps for the evaluation counts
     // (a bounded sample: nq x N bits of scratch, freed after the launch)
     void* uniq = nullptr;
-    if (std::getenv("WV_HNSW_UNIQUE_COUNTS") && nq <= 4096) {
+    // (bounded by bytes too: a 100M-node graph would take 51 GB at nq 4096)
+    if (std::getenv("WV_HNSW_UNIQUE_COUNTS") && nq <= 4096 && (size_t)nq * ((ix->gn + 63) / 64) * 8 <= ((size_t)1 << 30)) {
         hp.uniq_words = (ix->gn + 63) / 64;
         HIP_TRY(hipMallocAsync(&uniq, (size_t)nq * hp.uniq_words * 8, s));
         HIP_TRY(hipMemsetAsync(uniq, 0, (size_t)nq * hp.uniq_words * 8, s));
@@ -1346,11 +1348,12 @@ int run_hnsw(wv_index* ix, const float* d_q, int nq, int k, int ef, const uint64
     }
     TREC(4);
     // Filtered / tombstoned / nil-node searches with ef <= 128 (round 6):
-    // the side-register path, its side columns and expanded-side set sized
-    // from the eligible fraction p (the live side set peaks near
-    // 1.4 ef (1-p)/p, the side expansions likewise: oracle side diagnostics,
-    // DESIGN 3.3); what overflows re-runs once with twice the capacity,
-    // then exactly.  WV_HNSW_NO_SIDE=1 keeps the LDS path.
+    // the side-register path.  Layer 0 has an exact visited bitmap per query
+    // in HBM (nothing evaluated or queued twice) and a side set whose smallest
+    // keys sit in LDS, sized from the eligible fraction p (the live side set
+    // peaks near 1.4 ef (1-p)/p: oracle side diagnostics), the
+    // rest spilled to HBM.  Only a spill past its capacity takes the exact
+    // fallback.  WV_HNSW_NO_SIDE=1 keeps the LDS path.
     const bool side = filtered && !ix->pq_on && efc <= 128 && !std::getenv("WV_HNSW_NO_SIDE");
     if (side) {
         double p_el = 1.0;
@@ -1369,60 +1372,68 @@ int run_hnsw(wv_index* ix, const float* d_q, int nq, int k, int ef, const uint64
             p_el = (double)mn / (double)std::max<uint64_t>(1, ix->gn);
         }
         p_el *= 1.0 - std::min(1.0, (double)ix->n_tomb / (double)std::max<uint64_t>(1, ix->gn));
-        p_el = std::max(p_el, 1e-4);
-        const double side_need = 1.5 * ef * (1.0 - p_el) / p_el;
-        int side_rows = std::max(2, (int)std::ceil((side_need + 128.0) / 64.0));
-        int x_log2 = 8;
-        while (x_log2 < 20 && (double)(1 << x_log2) < 1.3 * (side_need + 64.0)) ++x_log2;
-        if (const char* e = std::getenv("WV_HNSW_SIDE_ROWS")) side_rows = std::max(1, std::atoi(e));
-        if (const char* e = std::getenv("WV_HNSW_SIDE_XS")) x_log2 = std::max(6, std::atoi(e));
-        // per-wave LDS budget: 13 KiB (12 waves per CU) while the side state
-        // leaves a 4 KiB visited cache beside it, else 20 KiB (8 waves)
-        const int fixed_b = 4 * wv_hnsw_side_per_wave_words(ix->dpad, side_rows, 0, x_log2);
-        int side_kb = fixed_b + 4096 <= 13 * 1024 ? 13 : 20;
+        p_el = std::max(p_el, 1e-5);
+        const double side_need = 1.4 * ef * (1.0 - p_el) / p_el;
+        // per-wave LDS: 13 KiB (12 waves per CU); the side array takes what a
+        // 2K-slot visited cache leaves, up to the live-set estimate
+        int side_kb = 13;
         if (const char* e = std::getenv("WV_HNSW_SIDE_KB")) side_kb = std::max(4, std::atoi(e));
-        auto layout = [&](wv::HnswParams& h, int rows, int xl, int budget_words) -> bool {
-            // shrink to the CU's LDS (status then reports what no longer fits)
-            while (rows > 1 && wv_hnsw_side_per_wave_words(ix->dpad, rows, 10, xl) * 4 > 160 * 1024) {
-                if (xl > 10 && (1 << xl) > 128 * rows) --xl;
-                else --rows;
-            }
-            h.side_rows = rows;
-            h.xs_log2 = xl;
-            const int fixed = wv_hnsw_side_per_wave_words(ix->dpad, rows, 0, xl) - 1;
-            h.vc_log2 = choose_vc_log2(std::max(budget_words, fixed + 512), fixed, ix->gn, &h.vc_tbits);
-            h.vc_log2 = std::max(h.vc_log2, 10);
-            int pw = (wv_hnsw_side_per_wave_words(ix->dpad, rows, h.vc_log2, xl) + 3) & ~3;
-            while (pw * 4 > 160 * 1024 && h.vc_log2 > 8) {
-                --h.vc_log2;
-                pw = (wv_hnsw_side_per_wave_words(ix->dpad, rows, h.vc_log2, xl) + 3) & ~3;
-            }
-            h.per_wave_words = pw;
-            return pw * 4 <= 160 * 1024;
-        };
-        auto wpb_of = [](int pw) {
-            int w = 4;
-            while (w > 1 && (size_t)w * pw * 4 > 160 * 1024) --w;
-            return w;
-        };
+        const int xl = 8;   // the upper levels' expanded set
+        const int budget_words = side_kb * 256;
+        const int base_words = wv_hnsw_side_per_wave_words(ix->dpad, 0, 11, xl);
+        const int max_rows = std::max(4, (budget_words - base_words) / 128);
+        int side_rows = std::min(max_rows, std::max(4, (int)std::ceil((side_need + 64.0) / 64.0)));
+        if (const char* e = std::getenv("WV_HNSW_SIDE_ROWS")) side_rows = std::max(4, std::atoi(e));
         wv::HnswParams hs = hp;
         hs.sc = 0;
-        if (!layout(hs, side_rows, x_log2, side_kb * 256)) return fail(WV_EINVAL, "hnsw side state too large");
-        ix->last_side_rows = hs.side_rows;
-        ix->last_side_xs = 1 << hs.xs_log2;
-        HIP_TRY(wv_launch_hnsw_side(&hs, wpb_of(hs.per_wave_words), s));
+        hs.side_rows = side_rows;
+        hs.xs_log2 = xl;
+        const int fixed = wv_hnsw_side_per_wave_words(ix->dpad, side_rows, 0, xl) - 1;
+        hs.vc_log2 = std::max(10, choose_vc_log2(std::max(budget_words, fixed + 512), fixed, ix->gn, &hs.vc_tbits));
+        int pw = (wv_hnsw_side_per_wave_words(ix->dpad, side_rows, hs.vc_log2, xl) + 3) & ~3;
+        while (pw * 4 > 160 * 1024 && hs.vc_log2 > 8) {
+            --hs.vc_log2;
+            pw = (wv_hnsw_side_per_wave_words(ix->dpad, side_rows, hs.vc_log2, xl) + 3) & ~3;
+        }
+        if (pw * 4 > 160 * 1024) return fail(WV_EINVAL, "hnsw side state too large");
+        hs.per_wave_words = pw;
+        int wpb = 4;
+        while (wpb > 1 && (size_t)wpb * pw * 4 > 160 * 1024) --wpb;
+        // HBM scratch per query: the visited bitmap and the spill, in chunks
+        // of at most WV_HNSW_SIDE_SCRATCH_MB (4 GiB) -- a 10M-row graph takes
+        // 1.25 MB of bitmap a query
+        hs.vwords = (ix->gn + 31) / 32;
+        double cap = std::ceil(8.0 * side_need) + 4096.0;
+        if (const char* e = std::getenv("WV_HNSW_SPILL_CAP")) cap = std::max(64, std::atoi(e));
+        hs.spill_cap = (int)std::min(cap, (double)(1 << 22));
+        const size_t per_q = hs.vwords * 4 + (size_t)hs.spill_cap * 8;
+        size_t budget_b = (size_t)4 << 30;
+        if (const char* e = std::getenv("WV_HNSW_SIDE_SCRATCH_MB")) budget_b = (size_t)std::max(1, std::atoi(e)) << 20;
+        const int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)nq, budget_b / per_q));
+        HIP_TRY(ix->side_vb.ensure((size_t)chunk * hs.vwords * 4));
+        HIP_TRY(ix->side_sp.ensure((size_t)chunk * hs.spill_cap * 8));
+        hs.vbits = ix->side_vb.as<uint32_t>();
+        hs.spill = ix->side_sp.as<uint32_t>();
+        ix->last_side_rows = side_rows;
+        ix->last_side_xs = hs.spill_cap;
+        for (int c0 = 0; c0 < nq; c0 += chunk) {
+            const int cn = std::min(chunk, nq - c0);
+            wv::HnswParams hc = hs;
+            hc.nq = cn;
+            hc.Q = d_q + (size_t)c0 * hp.ldq;
+            if (hc.allow && allow_stride) hc.allow = d_allow + (size_t)c0 * allow_stride;
+            hc.out_ids = d_out_ids + (size_t)c0 * k;
+            hc.out_d = d_out_d + (size_t)c0 * k;
+            hc.out_n = d_out_n + c0;
+            hc.status = hp.status + c0;
+            hc.counters = hp.counters + 2 * (size_t)c0;
+            HIP_TRY(hipMemsetAsync(hs.vbits, 0, (size_t)cn * hs.vwords * 4, s));
+            HIP_TRY(wv_launch_hnsw_side(&hc, wpb, s));
+        }
         HIP_TRY(ix->stat_acc.ensure(32));
         hipLaunchKernelGGL(count_nonzero_kernel, dim3((nq + 255) / 256), dim3(256), 0, s, ix->status.as<int32_t>(), nq,
                            ix->stat_acc.as<unsigned long long>() + 3);
         HIP_TRY(hipGetLastError());
-        if (!std::getenv("WV_HNSW_NO_WIDE_SIDE")) {
-            // overflowed queries (status != 0; the others' waves exit at
-            // once): twice the columns and the set, the LDS permitting
-            wv::HnswParams h2 = hs;
-            h2.redo = ix->status.as<int32_t>();
-            if (layout(h2, 2 * hs.side_rows, std::min(20, hs.xs_log2 + 1), 2 * side_kb * 256))
-                HIP_TRY(wv_launch_hnsw_side(&h2, wpb_of(h2.per_wave_words), s));
-        }
     } else {
     // small unfiltered batches (the batcher's callers): a workgroup per
     // query, whose three helper waves take the distance batches' other rows
@@ -2786,7 +2797,7 @@ int wv_last_batch_stats(wv_index* ix, uint64_t* dist_evals, uint64_t* expansions
     return WV_OK;
 }
 
-int wv_last_side_stats(wv_index* ix, uint64_t* second_pass, int* side_rows, int* side_set) {
+int wv_last_side_stats(wv_index* ix, uint64_t* overflowed, int* side_rows, int* spill_cap) {
     if (check(ix)) return WV_EINVAL;
     std::lock_guard<std::mutex> g(ix->mu);
     HIP_TRY(hipSetDevice(ix->cfg.device));
@@ -2795,9 +2806,9 @@ int wv_last_side_stats(wv_index* ix, uint64_t* second_pass, int* side_rows, int*
         HIP_TRY(hipMemcpyAsync(acc, ix->stat_acc.p, 32, hipMemcpyDeviceToHost, ix->stat_stream));
         HIP_TRY(hipStreamSynchronize(ix->stat_stream));
     }
-    if (second_pass) *second_pass = acc[3];
+    if (overflowed) *overflowed = acc[3];
     if (side_rows) *side_rows = ix->last_side_rows;
-    if (side_set) *side_set = ix->last_side_xs;
+    if (spill_cap) *spill_cap = ix->last_side_xs;
     return WV_OK;
 }
 

@@ -82,7 +82,14 @@ struct Request {
     std::condition_variable cv;
     bool done = false;
     Request* chain_next = nullptr;   // the caller this one wakes once it is woken
+    uint64_t batch = 0;              // the batch that answered it (set before the wakeup)
+    bool resub = false;              // its thread's previous call was answered by the last batch
 };
+
+// the batch that answered this thread's last call, per batcher: a caller
+// resubmitting right after its answer is one the refill wait may expect
+thread_local const void* tl_batcher = nullptr;
+thread_local uint64_t tl_batch = 0;
 
 void wake(Request* r) {
     std::lock_guard<std::mutex> g(r->m);
@@ -92,11 +99,16 @@ void wake(Request* r) {
 
 constexpr int WAKE_CHAINS = 8;
 // how long the next batch waits for the last one's callers: a base plus a
-// share per caller (the wakeup chains' hops), capped
+// share per caller (the wakeup chains' hops), capped -- and only while they
+// are coming back: the first resubmission within REFILL_GAP_US of the batch's
+// end, each next within REFILL_GAP_US of the one before (an open-loop request
+// at an idle device is launched at once)
 int refill_us(int n) { return std::min(300, 50 + n); }
+constexpr int REFILL_GAP_US = 40;
 
 // one worker's staging, reused batch after batch
 struct Staging {
+    uint64_t seq = 0;   // the batch being run
     std::vector<Request*> take, g;
     std::vector<char> used;
     std::vector<float> q, ds;
@@ -119,6 +131,9 @@ struct wv_batcher {
     bool device_busy = false;      // a worker holds the device (one batch at a time)
     wait_clock::time_point idle_since{};   // when the last batch finished
     int expect = 0;                        // its size: the callers about to resubmit
+    uint64_t seq_started = 0, seq_done = 0;   // batches taken / the last one finished
+    int resub_seen = 0;                    // its callers back in the queue since
+    wait_clock::time_point last_resub{};   // the latest of them
     // a worker waiting for company (refill or linger) wants this many queued:
     // submitters wake it only then (0: any submit at an idle device wakes)
     int wake_at = 0;
@@ -183,6 +198,7 @@ struct wv_batcher {
         for (size_t i = 0; i < n; ++i) {
             Request* r = s.g[i];
             r->rc = rc;
+            r->batch = s.seq;
             if (rc) {
                 r->err = msg;
             } else {
@@ -203,13 +219,19 @@ struct wv_batcher {
             if (queue.empty()) return;   // (stop)
             const int want = std::min(expect, max_batch);
             if (!stop && (int)queue.size() < want) {
-                // the finished batch's callers are still resubmitting
-                const auto deadline = idle_since + std::chrono::microseconds(refill_us(want));
-                if (wait_clock::now() < deadline) {
+                // the finished batch's callers are still resubmitting: wait
+                // for them while they keep coming, up to the cap
+                const auto cap = idle_since + std::chrono::microseconds(refill_us(want));
+                const auto gap = std::chrono::microseconds(REFILL_GAP_US);
+                for (;;) {
+                    const auto now = wait_clock::now();
+                    const auto until = std::min(cap, (resub_seen ? last_resub : idle_since) + gap);
+                    if (now >= until) break;
                     wake_at = want;
-                    cv_work.wait_until(l, deadline,
-                                       [&] { return stop || device_busy || (int)queue.size() >= want; });
+                    const bool full = cv_work.wait_until(
+                        l, until, [&] { return stop || device_busy || (int)queue.size() >= want; });
                     wake_at = 0;
+                    if (full) break;
                 }
                 if (device_busy || queue.empty()) continue;   // (the other worker took them)
             }
@@ -222,6 +244,7 @@ struct wv_batcher {
                 if (device_busy || queue.empty()) continue;   // (the other worker took them)
             }
             device_busy = true;
+            s.seq = ++seq_started;
             s.take.clear();
             while (!queue.empty() && (int)s.take.size() < max_batch) {
                 s.take.push_back(queue.front());
@@ -250,6 +273,8 @@ struct wv_batcher {
                     device_busy = false;
                     idle_since = wait_clock::now();
                     expect = (int)s.take.size();
+                    seq_done = s.seq;
+                    resub_seen = 0;
                     n_batches++;
                     n_launch_rows += s.take.size();
                     l.unlock();
@@ -299,6 +324,11 @@ static int submit(wv_batcher* b, Request& r) {
         }
         b->queue.push_back(&r);
         b->n_requests++;
+        if (tl_batcher == b && tl_batch == b->seq_done && b->seq_done) {
+            r.resub = true;
+            b->resub_seen++;
+            b->last_resub = r.arrived;
+        }
         // a busy device: the worker that frees it takes the queue; a worker
         // waiting for company: only once the count it waits for is there
         notify = !b->device_busy && (b->wake_at == 0 || (int)b->queue.size() >= b->wake_at);
@@ -309,6 +339,8 @@ static int submit(wv_batcher* b, Request& r) {
         r.cv.wait(l, [&] { return r.done; });
     }
     if (r.chain_next) wake(r.chain_next);
+    tl_batcher = b;
+    tl_batch = r.batch;
     if (r.rc) wv_internal_set_error(r.err.c_str());
     return r.rc;
 }

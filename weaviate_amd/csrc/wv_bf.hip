@@ -875,9 +875,20 @@ __device__ __forceinline__ void finalize_one(const BfFinParams& p, int q, float*
     int n_sel = 0;
     for (int j = 0; j < FIN_KF; ++j) n_sel += (si[j] != WV_NIL);
     __builtin_amdgcn_wave_barrier();
-    if (p.rowidx) {   // compacted scan: positions -> rows (order-preserving)
+    if (p.rowidx) {
+        // compacted scan: positions -> rows; a position past the list (none
+        // expected) drops out, and the rows stay a prefix of n_sel entries
+        // (exact_dist_rows loads exactly those), the rest keyed FLT_MAX
         const uint64_t nr = p.rowidx_ndev ? (uint64_t)*p.rowidx_ndev : p.rowidx_n;
-        if (lane < FIN_KF && si[lane] != WV_NIL) si[lane] = si[lane] < nr ? p.rowidx[si[lane]] : WV_NIL;
+        uint32_t v = WV_NIL;
+        if (lane < FIN_KF && si[lane] != WV_NIL && si[lane] < nr) v = p.rowidx[si[lane]];
+        const uint64_t vm = __ballot(v != WV_NIL);
+        __builtin_amdgcn_wave_barrier();
+        if (lane < FIN_KF) si[lane] = WV_NIL;
+        __builtin_amdgcn_wave_barrier();
+        if (v != WV_NIL) si[mbcnt64(vm)] = v;
+        n_sel = __popcll(vm);
+        if (lane < FIN_KF && lane >= n_sel) sd[lane] = FLT_MAX;
         __builtin_amdgcn_wave_barrier();
     }
     exact_dist_rows<METRIC, FIN_KF / 8>(qv, p.X, p.ldx, p.D, si, n_sel, sd, lane);

@@ -456,6 +456,14 @@ __device__ __forceinline__ uint32_t reg_entry_i(const uint32_t (&ri)[NR], int e)
 // wave's two trips of 32 rows were 66 % of an expansion, and one CU's
 // gathers are bound by the bytes it has in flight).  Wave 0 publishes nb; the
 // helpers (wg_helper) wait at the same two barriers.
+//
+// Barrier invariant (wv_hnsw_wg_kernel): wave 0 reaches __syncthreads only
+// inside wg_dist (exactly two per call) and once after knn_one_reg returns
+// (the -1 "done" barrier); the helpers pair each with their loop's two.  So
+// knn_one_reg / search_layer_reg must never return early past a pending
+// wg_dist pair nor add a barrier of their own on the wg path: every path out
+// of them ends at the kernel's final barrier.  (test_gpu_parity.py
+// test_hnsw_workgroup_launch_edge_graphs: 1- and 2-node graphs, k = ef = 1.)
 template <int METRIC>
 __device__ __forceinline__ void wg_dist(const HnswParams& p, const WaveState& w, int nb, int lane) {
     if (lane == 0) *w.wg_nb = nb;
@@ -812,20 +820,26 @@ __global__ __launch_bounds__(256) void wv_hnsw_wg_kernel(HnswParams p) {
 // side_rows x 64 entries, appended batch by batch, with the minimum key and
 // its position kept wave-uniform: a side pop moves the last entry into the
 // popped one's place and rescans (n / 64 LDS reads per lane and one DPP
-// reduction).  The expanded side candidates are an exact set X in LDS (open
-// addressing, probed 64 slots per step), checked when a side candidate is
-// popped: a copy re-inserted after a visited-cache miss is dropped there,
-// never expanded twice.
+// reduction).
 //
-// Capacity.  A full array first sheds its dead entries (d > worst once R is
-// full: never expandable, search.go:213-215); the new entries that still do
-// not fit are dropped and the smallest dropped key (xd) is remembered.  The
-// search stays exact while every pop is below xd (the reference would have
-// popped the dropped entry first) and it ends with xd > worst (the
-// reference's loop would not reach it); otherwise -- or when X fills --
-// status != 0 and the host re-runs the query with larger capacities, then
-// exactly.  Sizes come from the list's selectivity (the live side
-// set peaks near 1.4 ef (1-p)/p).
+// Layer 0 (EV): the visited list is exact -- a per-query bitmap in HBM behind
+// the LDS cache: a neighbour the cache misses is claimed by an atomic OR
+// (search.go:256-264), so every node is evaluated and queued at most once, as
+// in the reference (a selective list traverses ~15-25k nodes a query, far past
+// any LDS cache: the lossy cache alone re-evaluated 1.5x and filled S with
+// copies).  S never holds a copy, so no expanded set is needed.  S keeps its
+// smallest keys in LDS and the rest in a per-query spill in HBM: every LDS key
+// is <= the bound U < every spilled key, so the LDS minimum is S's minimum
+// while LDS is not empty; a full LDS array first drops its dead entries
+// (d > worst once R is full: never expandable, :213-215), then moves the keys
+// above a sampled median to the spill (U drops to it); an empty LDS array
+// with a live spill takes back the spill's smallest keys (U rises).  Only a
+// spill past spill_cap ends in status != 0 (the exact fallback).
+//
+// Upper levels (!EV, ef = 1, tombstones / nil nodes only): the lossy LDS
+// cache, the expanded set X (exact, open addressing) and, when S is full, the
+// smallest dropped key: exact while every pop is below it and the search ends
+// with it above worst; otherwise status != 0.
 
 // one step of a (d, id) minimum by DPP (no LDS): lanes whose source is out
 // of range or masked take the identity
@@ -851,24 +865,40 @@ __device__ __forceinline__ void wave_min_key(float& d, uint32_t& i) {
     i = (uint32_t)__builtin_amdgcn_readlane((int)i, 63);
 }
 
-template <int METRIC, int NR, int RPG>
+// the key of rank r among the wave's 64 distinct (d, id) keys (one per lane)
+__device__ __forceinline__ void wave_rank_key(float d, uint32_t i, int r, float& od, uint32_t& oi) {
+    int rank = 0;
+    for (int t = 0; t < 64; ++t) {
+        const float td = __uint_as_float((uint32_t)__builtin_amdgcn_readlane((int)__float_as_uint(d), t));
+        const uint32_t ti = (uint32_t)__builtin_amdgcn_readlane((int)i, t);
+        rank += key_less_nb(td, ti, d, i) ? 1 : 0;
+    }
+    const uint64_t m = __ballot(rank == r);
+    const int src = m ? __builtin_ctzll(m) : 0;
+    od = __uint_as_float((uint32_t)__builtin_amdgcn_readlane((int)__float_as_uint(d), src));
+    oi = (uint32_t)__builtin_amdgcn_readlane((int)i, src);
+}
+
+template <int METRIC, int NR, int RPG, bool EV>
 __device__ __forceinline__ void search_layer_side(const HnswParams& p, WaveState& w, int level, int ef, uint32_t ep,
-                                                  float epd, const uint64_t* allow, int nlt, float (&rd)[NR],
-                                                  uint32_t (&ri)[NR], int& Rl, int& status, uint32_t& n_dist,
-                                                  uint32_t& n_exp) {
+                                                  float epd, const uint64_t* allow, int nlt, uint32_t* vb,
+                                                  uint32_t* sp, float (&rd)[NR], uint32_t (&ri)[NR], int& Rl,
+                                                  int& status, uint32_t& n_dist, uint32_t& n_exp) {
     static_assert(NR == 1 || NR == 2, "64 or 128 results per wave");
     const int lane = threadIdx.x & 63;
     const int VC = 1 << p.vc_log2;
-    const int XS = 1 << p.xs_log2;
+    const int XS = EV ? 0 : 1 << p.xs_log2;
     const int SC = 64 * p.side_rows;
     float* Sd = w.Sd;
     uint32_t* Si = w.Si;
     for (int i = lane; i < VC; i += 64) w.vc[i] = VC_EMPTY;
-    for (int i = lane; i < XS; i += 64) w.xs[i] = WV_NIL;
+    if (!EV)
+        for (int i = lane; i < XS; i += 64) w.xs[i] = WV_NIL;
     wave_sync();
     if (lane == 0) {
         const uint32_t he = vc_hash(p, ep);
         w.vc[vc_slot(p, he)] = vc_tag(p, he);
+        if (EV) atomicOr(vb + (ep >> 5), 1u << (ep & 31));   // visitedList.Visit(ep) (:338)
     }
     auto eligible = [&](uint32_t id) -> bool {
         if (p.tomb && bit_test(p.tomb, p.tomb_nbits, id)) return false;
@@ -887,10 +917,12 @@ __device__ __forceinline__ void search_layer_side(const HnswParams& p, WaveState
     Rl = ep_ok ? 1 : 0;
     // currentWorstResultDistanceToFloat (:355-377)
     float worst = ep_ok ? epd : FLT_MAX;
-    // S: n entries, minimum (smd, smi) at spos; xd/xi the smallest dropped key
-    int n = 0, spos = 0;
-    float smd = FLT_MAX, xd = FLT_MAX;
-    uint32_t smi = WV_NIL, xi = WV_NIL;
+    // S in LDS: n entries, minimum (smd, smi) at spos.  !EV: xd/xi the
+    // smallest dropped key.  EV: gcnt spilled entries in sp, every one keyed
+    // above (ud, ui) >= every LDS key (while gcnt > 0)
+    int n = 0, spos = 0, gcnt = 0;
+    float smd = FLT_MAX, xd = FLT_MAX, ud = FLT_MAX;
+    uint32_t smi = WV_NIL, xi = WV_NIL, ui = WV_NIL;
     if (!ep_ok) {
         if (lane == 0) { Sd[0] = epd; Si[0] = ep; }
         n = 1; smd = epd; smi = ep;
@@ -916,6 +948,108 @@ __device__ __forceinline__ void search_layer_side(const HnswParams& p, WaveState
         smd = md;
         smi = mi;
     };
+    auto dead = [&](float d) { return Rl >= ef && d > worst; };
+    // EV: move the LDS keys above a sampled median (n >= 64) to the spill and
+    // drop the dead ones; U falls to that median
+    auto split = [&]() {
+        const int idx = (int)(((uint32_t)lane * (uint32_t)n) >> 6);
+        float md;
+        uint32_t mi;
+        wave_rank_key(Sd[idx], Si[idx], 31, md, mi);
+        int k = 0;
+        for (int j0 = 0; j0 < n; j0 += 64) {
+            const int j = j0 + lane;
+            const float d = j < n ? Sd[j] : FLT_MAX;
+            const uint32_t id = j < n ? Si[j] : WV_NIL;
+            const bool live = j < n && !dead(d);
+            const bool stay = live && !key_less_nb(md, mi, d, id);
+            const bool mv = live && !stay;
+            const uint64_t lm = __ballot(stay), sm = __ballot(mv);
+            wave_sync();
+            if (stay) { Sd[k + mbcnt64(lm)] = d; Si[k + mbcnt64(lm)] = id; }
+            if (mv) {
+                const int g = gcnt + mbcnt64(sm);
+                if (g < p.spill_cap) { sp[2 * g] = __float_as_uint(d); sp[2 * g + 1] = id; }
+            }
+            k += __popcll(lm);
+            gcnt += __popcll(sm);
+            wave_sync();
+        }
+        if (gcnt > p.spill_cap) status |= 2;
+        n = k;
+        ud = md;
+        ui = mi;
+        rescan();
+    };
+    // EV: LDS is empty and the spill is not -- take back its smallest live keys
+    auto refill = [&]() {
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // (the wave's own spill stores)
+        // drop the dead, compact the spill in place (a chunk's writes land at
+        // or below its reads) and copy the live ones to LDS while they fit
+        int m = 0;
+        for (int j0 = 0; j0 < gcnt; j0 += 64) {
+            const int j = j0 + lane;
+            const float d = j < gcnt ? __uint_as_float(sp[2 * j]) : FLT_MAX;
+            const uint32_t id = j < gcnt ? sp[2 * j + 1] : WV_NIL;
+            const bool live = j < gcnt && !dead(d);
+            const uint64_t lm = __ballot(live);
+            const int o = m + mbcnt64(lm);
+            if (live) {
+                sp[2 * o] = __float_as_uint(d);
+                sp[2 * o + 1] = id;
+                if (o < SC) { Sd[o] = d; Si[o] = id; }
+            }
+            m += __popcll(lm);
+        }
+        gcnt = m;
+        wave_sync();
+        if (m <= SC) {   // all of it fits: the spill is empty again
+            n = m;
+            gcnt = 0;
+            if (n) rescan();
+            return;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        // a bound whose keys fill about half the array, from 64 samples;
+        // halved while the exact count does not fit
+        const int idx = (int)(((uint32_t)lane * (uint32_t)m) >> 6);
+        const float sd_ = __uint_as_float(sp[2 * idx]);
+        const uint32_t si_ = sp[2 * idx + 1];
+        int r = min(63, max(0, (32 * SC) / m - 1));
+        float bd = FLT_MAX;
+        uint32_t bi = WV_NIL;
+        for (;;) {
+            wave_rank_key(sd_, si_, r, bd, bi);
+            int c = 0;
+            for (int j0 = 0; j0 < m; j0 += 64) {
+                const int j = j0 + lane;
+                const bool in = j < m && !key_less_nb(bd, bi, __uint_as_float(sp[2 * j]), sp[2 * j + 1]);
+                c += __popcll(__ballot(in));
+            }
+            if (c <= SC) break;
+            if (r == 0) { status |= 2; return; }
+            r >>= 1;
+        }
+        int k = 0, g = 0;
+        for (int j0 = 0; j0 < m; j0 += 64) {
+            const int j = j0 + lane;
+            const float d = j < m ? __uint_as_float(sp[2 * j]) : FLT_MAX;
+            const uint32_t id = j < m ? sp[2 * j + 1] : WV_NIL;
+            const bool in = j < m && !key_less_nb(bd, bi, d, id);
+            const bool out = j < m && !in;
+            const uint64_t lm = __ballot(in), om = __ballot(out);
+            if (in) { Sd[k + mbcnt64(lm)] = d; Si[k + mbcnt64(lm)] = id; }
+            if (out) { sp[2 * (g + mbcnt64(om))] = __float_as_uint(d); sp[2 * (g + mbcnt64(om)) + 1] = id; }
+            k += __popcll(lm);
+            g += __popcll(om);
+        }
+        wave_sync();
+        n = k;
+        gcnt = g;
+        ud = bd;
+        ui = bi;
+        rescan();
+    };
     wave_sync();
     const uint32_t* nbr_base;
     int deg;
@@ -927,8 +1061,20 @@ __device__ __forceinline__ void search_layer_side(const HnswParams& p, WaveState
             const uint64_t um = __ballot(64 * r + lane < Rl && !(ri[r] & WV_FLAG));
             if (ridx < 0 && um) ridx = 64 * r + __builtin_ctzll(um);
         }
+        if (EV && n == 0 && gcnt > 0) {
+            // S's minimum is in the spill (above U): a result candidate at or
+            // below U comes first; otherwise take the spill's smallest back
+            bool r_first = false;
+            if (ridx >= 0)
+                r_first = !key_less(ud, ui, reg_entry_d<NR>(rd, ridx), reg_entry_i<NR>(ri, ridx) & WV_IDMASK);
+            if (!r_first) {
+                refill();
+                if (status) break;
+                continue;
+            }
+        }
         if (ridx < 0 && n == 0) {   // candidates exhausted
-            if (xi != WV_NIL) status |= 1;   // (a dropped one was still to be expanded)
+            if (!EV && xi != WV_NIL) status |= 1;   // (a dropped one was still to be expanded)
             break;
         }
         float cd = smd;
@@ -940,10 +1086,10 @@ __device__ __forceinline__ void search_layer_side(const HnswParams& p, WaveState
             if (n == 0 || key_less(rdv, riv, smd, smi)) { cd = rdv; cid = riv; fromR = true; }
         }
         if (cd > worst) {   // :213-215
-            if (xi != WV_NIL && !(xd > worst)) status |= 1;
+            if (!EV && xi != WV_NIL && !(xd > worst)) status |= 1;
             break;
         }
-        if (xi != WV_NIL && key_less(xd, xi, cd, cid)) { status |= 1; break; }
+        if (!EV && xi != WV_NIL && key_less(xd, xi, cd, cid)) { status |= 1; break; }
         if (fromR) {
 #pragma unroll
             for (int r = 0; r < NR; ++r)
@@ -954,23 +1100,25 @@ __device__ __forceinline__ void search_layer_side(const HnswParams& p, WaveState
             if (lane == 0 && spos != n) { Sd[spos] = Sd[n]; Si[spos] = Si[n]; }
             wave_sync();
             rescan();
-            // X: expanded once (search.go:256-264 by way of the exact set)
-            const uint32_t h0 = hash32(cid) >> (32 - p.xs_log2);
-            bool dup = false, placed = false;
-            for (int b = 0; b < XS; b += 64) {
-                const uint32_t slot = (h0 + b + lane) & (XS - 1);
-                const uint32_t v = w.xs[slot];
-                const uint64_t fm = __ballot(v == cid), em = __ballot(v == WV_NIL);
-                const int fe = em ? __builtin_ctzll(em) : 64;
-                if (fm && __builtin_ctzll(fm) < fe) { dup = true; break; }
-                if (em) {
-                    if (lane == fe) w.xs[slot] = cid;
-                    placed = true;
-                    break;
+            if (!EV) {
+                // X: expanded once (search.go:256-264 by way of the exact set)
+                const uint32_t h0 = hash32(cid) >> (32 - p.xs_log2);
+                bool dup = false, placed = false;
+                for (int b = 0; b < XS; b += 64) {
+                    const uint32_t slot = (h0 + b + lane) & (XS - 1);
+                    const uint32_t v = w.xs[slot];
+                    const uint64_t fm = __ballot(v == cid), em = __ballot(v == WV_NIL);
+                    const int fe = em ? __builtin_ctzll(em) : 64;
+                    if (fm && __builtin_ctzll(fm) < fe) { dup = true; break; }
+                    if (em) {
+                        if (lane == fe) w.xs[slot] = cid;
+                        placed = true;
+                        break;
+                    }
                 }
+                if (dup) continue;
+                if (!placed) { status |= 2; break; }
             }
-            if (dup) continue;
-            if (!placed) { status |= 2; break; }
         }
         uint32_t pre0 = WV_NIL, pre1 = WV_NIL;
         if (level == 0) {
@@ -1005,6 +1153,19 @@ __device__ __forceinline__ void search_layer_side(const HnswParams& p, WaveState
             wave_sync();
             if (v0) w.vc[h0] = t0;
             if (v1) w.vc[h1] = t1;
+            if (EV) {
+                // the cache's misses claim their bit: a node another expansion
+                // evaluated (the cache forgot it) is skipped, as the exact
+                // visited list skips it
+                if (v0) {
+                    const uint32_t b = 1u << (id0 & 31);
+                    v0 = !(atomicOr(vb + (id0 >> 5), b) & b);
+                }
+                if (v1) {
+                    const uint32_t b = 1u << (id1 & 31);
+                    v1 = !(atomicOr(vb + (id1 >> 5), b) & b);
+                }
+            }
             const uint64_t m0 = __ballot(v0), m1 = __ballot(v1);
             const int n0 = __popcll(m0);
             const int nb = n0 + __popcll(m1);
@@ -1017,7 +1178,7 @@ __device__ __forceinline__ void search_layer_side(const HnswParams& p, WaveState
             if (nb == 0) continue;
             for (int base = 0; base < nb; base += 8 * RPG)
                 exact_dist_rows<METRIC, RPG, true>(w.qv, p.X, p.ldx, p.D, w.Bi + base, nb - base, w.Bd + base, lane);
-            n_dist += eval_count(w, level, nb, v0, id0, v1, id1);
+            n_dist += (uint32_t)nb;
             wave_sync();
             // ---- keep test against the batch's starting state (search.go:282),
             // on the neighbours' own lanes (batch order = lane order, id0s
@@ -1036,8 +1197,6 @@ __device__ __forceinline__ void search_layer_side(const HnswParams& p, WaveState
                 kmask[h] = __ballot(keep && el);
                 smask[h] = __ballot(keep && !el);
             }
-            const int ns0 = __popcll(smask[0]);
-            const int ns = ns0 + __popcll(smask[1]);
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 uint64_t km = kmask[h];
@@ -1075,9 +1234,67 @@ __device__ __forceinline__ void search_layer_side(const HnswParams& p, WaveState
                     worst = reg_entry_d<NR>(rd, Rl - 1);
                 }
             }
-            if (ns == 0) continue;
-            // ---- the ineligible keys to S ----
-            if (n + ns > SC && Rl >= ef) {
+            // ---- the ineligible keys to S (EV: the ones already dead against
+            // the batch's final worst are never expandable: not queued) ----
+            if (EV) {
+                smask[0] &= __ballot(!dead(bd[0]));
+                smask[1] &= __ballot(!dead(bd[1]));
+            }
+            if ((smask[0] | smask[1]) == 0) continue;
+            if (EV) {
+                // each new key to LDS (at or below U) or to the spill; a full
+                // array drops its dead, then splits
+                uint64_t lmask[2];
+                bool shed = false;
+                for (;;) {
+#pragma unroll
+                    for (int h = 0; h < 2; ++h)
+                        lmask[h] = smask[h] & __ballot(gcnt == 0 || !key_less_nb(ud, ui, bd[h], bi[h]));
+                    const int nl = __popcll(lmask[0]) + __popcll(lmask[1]);
+                    if (n + nl <= SC) break;
+                    if (!shed && Rl >= ef) {
+                        int k = 0;
+                        for (int j0 = 0; j0 < n; j0 += 64) {
+                            const int j = j0 + lane;
+                            const float d = j < n ? Sd[j] : FLT_MAX;
+                            const uint32_t id = j < n ? Si[j] : WV_NIL;
+                            const bool live = j < n && !dead(d);
+                            const uint64_t lm = __ballot(live);
+                            wave_sync();
+                            if (live) { Sd[k + mbcnt64(lm)] = d; Si[k + mbcnt64(lm)] = id; }
+                            k += __popcll(lm);
+                            wave_sync();
+                        }
+                        n = k;
+                        rescan();
+                        shed = true;
+                        continue;
+                    }
+                    split();
+                    if (status) break;
+                }
+                if (status) break;
+                const uint64_t g0 = smask[0] & ~lmask[0], g1 = smask[1] & ~lmask[1];
+                if (g0 | g1) {
+                    const int gn0 = __popcll(g0);
+                    if ((g0 >> lane) & 1) {
+                        const int g = gcnt + mbcnt64(g0);
+                        if (g < p.spill_cap) { sp[2 * g] = __float_as_uint(bd[0]); sp[2 * g + 1] = bi[0]; }
+                    }
+                    if ((g1 >> lane) & 1) {
+                        const int g = gcnt + gn0 + mbcnt64(g1);
+                        if (g < p.spill_cap) { sp[2 * g] = __float_as_uint(bd[1]); sp[2 * g + 1] = bi[1]; }
+                    }
+                    gcnt += gn0 + __popcll(g1);
+                    if (gcnt > p.spill_cap) { status |= 2; break; }
+                }
+                smask[0] = lmask[0];
+                smask[1] = lmask[1];
+                if ((smask[0] | smask[1]) == 0) continue;
+            }
+            const int ns0 = __popcll(smask[0]);
+            const int ns = ns0 + __popcll(smask[1]);
+            if (!EV && n + ns > SC && Rl >= ef) {
                 // shed the dead (d > worst), in place: a chunk's reads come
                 // before its writes, which land at or below them
                 int k = 0;
@@ -1111,7 +1328,7 @@ __device__ __forceinline__ void search_layer_side(const HnswParams& p, WaveState
                     }
                 }
             wave_min_key(nd_, ni_);
-            if (key_less(nd_, ni_, smd, smi)) {
+            if (n == 0 || key_less(nd_, ni_, smd, smi)) {
                 smd = nd_;
                 smi = ni_;
                 const uint64_t pm0 = __ballot(((smask[0] >> lane) & 1) && bd[0] == nd_ && bi[0] == ni_);
@@ -1119,13 +1336,14 @@ __device__ __forceinline__ void search_layer_side(const HnswParams& p, WaveState
                 spos = pm0 ? n + __popcll(smask[0] & ((1ull << __builtin_ctzll(pm0)) - 1))
                            : n + ns0 + __popcll(smask[1] & ((1ull << __builtin_ctzll(pm1)) - 1));
             }
-            if (fit < ns) {
+            if (!EV && fit < ns) {
                 wave_min_key(xd_, xi_);
                 if (key_less(xd_, xi_, xd, xi)) { xd = xd_; xi = xi_; }
             }
             n += fit;
             wave_sync();
         }
+        if (status) break;
     }
 }
 
@@ -1136,6 +1354,8 @@ __device__ __forceinline__ void knn_one_side(const HnswParams& p, WaveState& w, 
     for (int i = lane; i < p.dpad; i += 64) w.qv[i] = i < p.D ? p.Q[(uint64_t)q * p.ldq + i] : 0.f;
     wave_sync();
     const uint64_t* allow = p.allow ? p.allow + (p.allow_stride ? (uint64_t)q * p.allow_stride : 0) : nullptr;
+    uint32_t* vb = p.vbits + (uint64_t)q * p.vwords;
+    uint32_t* sp = p.spill + 2 * (uint64_t)q * p.spill_cap;
     int status = 0, nlt = 0;
     uint32_t n_dist = 0, n_exp = 0;
     uint32_t ep = p.entrypoint;
@@ -1147,7 +1367,8 @@ __device__ __forceinline__ void knn_one_side(const HnswParams& p, WaveState& w, 
     // greedy descent, levels max..1 with ef = 1 (search.go:479-521): a nil
     // result is tombstoned for the rest of the search (:496-507)
     for (int level = p.max_level; level >= 1 && !status; --level) {
-        search_layer_side<METRIC, NR, RPG>(p, w, level, 1, ep, epd, nullptr, nlt, rd, ri, Rl, status, n_dist, n_exp);
+        search_layer_side<METRIC, NR, RPG, false>(p, w, level, 1, ep, epd, nullptr, nlt, vb, sp, rd, ri, Rl, status,
+                                                  n_dist, n_exp);
         if (Rl > 0) {
             const uint32_t cid = (uint32_t)__builtin_amdgcn_readlane(ri[0], 0) & WV_IDMASK;
             if (p.levels[cid] < 0) {
@@ -1163,7 +1384,8 @@ __device__ __forceinline__ void knn_one_side(const HnswParams& p, WaveState& w, 
         }
     }
     if (!status)
-        search_layer_side<METRIC, NR, RPG>(p, w, 0, p.ef, ep, epd, allow, nlt, rd, ri, Rl, status, n_dist, n_exp);
+        search_layer_side<METRIC, NR, RPG, true>(p, w, 0, p.ef, ep, epd, allow, nlt, vb, sp, rd, ri, Rl, status, n_dist,
+                                                 n_exp);
     const int n = status ? 0 : min(Rl, p.k);
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
@@ -1180,16 +1402,14 @@ __device__ __forceinline__ void knn_one_side(const HnswParams& p, WaveState& w, 
     }
 }
 
-// LDS per wave: query, batch, visited cache, side columns, X, local tombstones
-// WPS: waves per SIMD the register allocation targets (2: no spills, 3: a
-// few VGPRs spilled to scratch for 12 waves per CU when the LDS allows it)
+// LDS per wave: query, batch, side array, X (upper levels), local tombstones,
+// visited cache.  WPS: waves per SIMD the register allocation targets
 template <int METRIC, int NR, int RPG, int WPS>
 __global__ __launch_bounds__(256, WPS) void wv_hnsw_side_kernel(HnswParams p) {
     extern __shared__ float lds[];
     const int wave = threadIdx.x >> 6;
     const int q = blockIdx.x * (blockDim.x >> 6) + wave;
     if (q >= p.nq) return;
-    if (p.redo && p.redo[q] == 0) return;   // (second pass: this query completed)
     float* cur = lds + (uint64_t)wave * p.per_wave_words;
     WaveState w{};
     w.qv = cur; cur += p.dpad;
@@ -1198,7 +1418,6 @@ __global__ __launch_bounds__(256, WPS) void wv_hnsw_side_kernel(HnswParams p) {
     w.xs = reinterpret_cast<uint32_t*>(cur); cur += (1 << p.xs_log2);
     w.ltomb = reinterpret_cast<uint32_t*>(cur); cur += MAX_LOCAL_TOMB;
     w.vc = reinterpret_cast<uint16_t*>(cur);
-    w.ub = p.uniq ? p.uniq + (uint64_t)q * p.uniq_words : nullptr;
     knn_one_side<METRIC, NR, RPG>(p, w, q);
 }
 

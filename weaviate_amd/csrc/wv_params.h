@@ -356,7 +356,7 @@ struct HnswParams {
     uint64_t* out_ids;   // [nq][k]
     float* out_d;
     int32_t* out_n;
-    int32_t* status;     // bit0 side overflow, bit1 expanded-set overflow
+    int32_t* status;     // bit0 side overflow, bit1 expanded-set / spill overflow
     uint32_t* counters;  // [nq][2]: distance evaluations, expansions (nullable)
     PqParams pq;         // compressed index: distances from codes (search.go:171-199)
     // diagnostic (WV_HNSW_UNIQUE_COUNTS): one exact visited bitmap per query
@@ -375,9 +375,17 @@ struct HnswParams {
     int wg_helpers;
     // (round 6) side-register path (wv_hnsw_side_kernel: filtered,
     // tombstoned or nil-node searches with ef <= 128): results in registers,
-    // side candidates in side_rows x 64 swizzled per-lane LDS columns, the
-    // expanded side candidates in an exact 2^xs_log2-slot set
+    // the side candidates' smallest keys in a side_rows x 64-entry LDS array,
+    // the rest in a per-query spill in HBM (spill_cap (d, id) pairs), and an
+    // exact layer-0 visited bitmap per query in HBM ([nq][vwords] u32, zeroed
+    // before the launch: search.go:256-264 exactly, so nothing is evaluated or
+    // queued twice).  The upper levels keep the LDS cache + expanded set
+    // (2^xs_log2 slots).
     int side_rows;
+    uint32_t* vbits;
+    uint64_t vwords;
+    uint32_t* spill;
+    int spill_cap;
 };
 
 // Flat search over PQ codes (flat_search.go:19-74 on a compressed index):

@@ -352,11 +352,11 @@ class GPUVectorIndex:
         return {"dist_evals": a.value, "expansions": b.value, "fallbacks": c.value}
 
     def last_side_stats(self):
-        """filtered HNSW: queries re-run with twice the side capacity, and the
-        first launch's side columns / expanded-side set slots"""
+        """filtered HNSW: queries whose side set outgrew its HBM spill (exact
+        fallback), the LDS side array's rows of 64 and the spill capacity"""
         a, b, c = C.c_uint64(), C.c_int(), C.c_int()
         check(lib().wv_last_side_stats(self._h, C.byref(a), C.byref(b), C.byref(c)))
-        return {"second_pass": a.value, "side_rows": b.value, "side_set": c.value}
+        return {"overflowed": a.value, "side_rows": b.value, "spill_cap": c.value}
 
 
 class CommitLogGraph:
