@@ -407,7 +407,7 @@ def exact_roofline(args, ix, kern_ms, stats, D, n_allowed, n_local, NQ):
     return roof, kind
 
 
-def attach_traffic(roof, n_local, NQ, D, data):
+def attach_traffic(roof, n_local, NQ, D, data, allow_frac=None):
     """roofline.traffic from a committed PMC summary -- only one collected from
     this build of the key pass (tools/build_hash.py) on the same shape"""
     import glob
@@ -420,7 +420,8 @@ def attach_traffic(roof, n_local, NQ, D, data):
             p = json.load(f)
         if p.get("kernel") != roof["kernel"]:
             continue
-        same_shape = (p.get("N"), p.get("nq"), p.get("dim"), p.get("data", "uniform")) == (n_local, NQ, D, data)
+        same_shape = (p.get("N"), p.get("nq"), p.get("dim"), p.get("data", "uniform"), p.get("allow_frac")) == \
+            (n_local, NQ, D, data, allow_frac)
         if same_shape and p.get("build") == want:
             roof["traffic"] = p.get("hbm_bytes_per_launch")
             roof["traffic_source"] = p.get("source", os.path.relpath(pmc, ROOT))
@@ -987,50 +988,66 @@ def filtered_hnsw_legs(args, ctx, ix, ref, queries, qt, NQ, K, D, n_local):
     :282-298): a shared Bernoulli(p) list (seed 3), ef = the line's ef.  QPS,
     HBM fraction from the restatement's counts on the same graph, parity
     with the restatement (knnSearchByVector with the list), recall against
-    the filtered exact answer, and the rate of queries whose ineligible side
-    set outgrew the wave's LDS (answered by the exact filtered scan)."""
+    the filtered exact answer, the restatement's own time on the host cores
+    (cpu_baseline), and the rate of queries whose side set outgrew its HBM
+    spill (answered by the exact filtered scan).  Lists below 40k rows
+    (flatSearchCutoff) run as forbidFlat; the 1 % leg takes 1000 queries."""
     torch = ctx.torch
     out = {}
-    oi_, od_, on_ = _out_tensors(ctx, NQ, K)
     for frac in args.filtered_fracs:
+        nq = NQ if frac >= 0.05 else min(NQ, 1000)
+        oi_, od_, on_ = _out_tensors(ctx, nq, K)
         a = argparse.Namespace(**vars(args))
         a.allow_frac = frac
         words, n_allowed = _allow_words(a, 0, n_local)
         allow_t = torch.from_numpy(words.view(np.int64)).to(ctx.dev)
 
         def step(timed, mode="hnsw"):
-            ix.search_batch_device(qt.data_ptr(), NQ, K, oi_.data_ptr(), od_.data_ptr(), on_.data_ptr(), ef=args.ef,
+            ix.search_batch_device(qt.data_ptr(), nq, K, oi_.data_ptr(), od_.data_ptr(), on_.data_ptr(), ef=args.ef,
                                    mode=mode, stream=ctx.stream, allow_ptr=allow_t.data_ptr(), allow_nbits=n_local)
 
         ix.set_timing(True)
         el = ctx.time_steps(step, args.steps, args.warmup, before_timed=ix.last_kernel_times)
         km = ix.last_kernel_times()["hnsw_ms"]
         st = ix.last_batch_stats()
+        ss = ix.last_side_stats()
         ix.set_timing(False)
         gi = oi_.cpu().numpy().view(np.uint64).copy()
         gd = od_.cpu().numpy().copy()
         step(False, mode="exact")
         torch.cuda.synchronize(ctx.dev)
         truth = oi_.cpu().numpy().view(np.uint64).copy()
-        ri, rd, rn, rst = ref.search_batch(queries, K, args.ef, allow=words, threads=args.cpu_threads)
+        t0 = time.perf_counter()
+        ri, rd, rn, rst = ref.search_batch(queries[:nq], K, args.ef, allow=words, threads=args.cpu_threads)
+        cpu_s = time.perf_counter() - t0
         id_eq, d_eq, tie_ok = parity_stats(gi, gd, ri, rd)
         rec = float(np.mean([len(set(x) & set(y)) / K for x, y in zip(gi.tolist(), truth.tolist())]))
         rec_cpu = float(np.mean([len(set(x) & set(y)) / K for x, y in zip(ri.tolist(), truth.tolist())]))
         e, x = rst["dist_evals"], rst["expansions"]
         by = 4.0 * D * e + 4.0 * 2 * args.M * x
         achieved = by / (km * 1e-3) / 1e9
-        out["allow_%g%%" % (100 * frac)] = {
-            "value": round(NQ * args.steps / el, 1), "unit": "queries/s", "ms_per_step": round(1000 * el / args.steps, 3),
-            "allowed_rows": int(n_allowed), "ef": args.ef, "recall@10_vs_filtered_exact": round(rec, 4),
-            "recall@10_cpu_restatement": round(rec_cpu, 4),
-            "exact_fallback_queries": int(st["fallbacks"]), "exact_fallback_rate": round(st["fallbacks"] / NQ, 4),
-            "parity_sample": {"queries": NQ, "id_match_frac": id_eq, "dists_bitwise_equal_frac": d_eq,
+        leg = {
+            "value": round(nq * args.steps / el, 1), "unit": "queries/s", "ms_per_step": round(1000 * el / args.steps, 3),
+            "queries": nq, "allowed_rows": int(n_allowed), "ef": args.ef,
+            "dispatch": "forbidFlat (|allow| < flatSearchCutoff 40000)" if n_allowed < 40000 else
+                        "hnsw (|allow| >= flatSearchCutoff)",
+            "recall@10_vs_filtered_exact": round(rec, 4), "recall@10_cpu_restatement": round(rec_cpu, 4),
+            "exact_fallback_queries": int(st["fallbacks"]), "exact_fallback_rate": round(st["fallbacks"] / nq, 4),
+            "side_state": {"lds_side_rows": ss["side_rows"], "spill_cap": ss["spill_cap"],
+                           "light_pass_redone": ss["redone"], "spill_overflowed": ss["overflowed"]},
+            "parity_sample": {"queries": nq, "id_match_frac": id_eq, "dists_bitwise_equal_frac": d_eq,
                               "tie_aware_identical_frac": tie_ok},
-            "roofline": {"bound": "hbm", "kernel": "wv_hnsw_kernel", "achieved": round(achieved, 1),
+            "cpu_baseline": {"value": round(nq / cpu_s, 1), "unit": "queries/s", "cores": args.cpu_threads,
+                             "kind": "port", "sample": f"the same {nq} queries and list, knnSearchByVector restated "
+                                                       f"in C (oracle/), T={args.cpu_threads}"},
+            "roofline": {"bound": "hbm", "kernel": "wv_hnsw_side_kernel", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "kernel_ms": round(km, 3), "counts_from": "CPU restatement (oracle/) on the same graph and list",
-                         "dist_evals_per_query": round(e / NQ, 1), "expansions_per_query": round(x / NQ, 1),
-                         "gpu_dist_evals_per_query": round(st["dist_evals"] / NQ, 1)}}
+                         "traffic": None, "kernel_ms": round(km, 3),
+                         "counts_from": "CPU restatement (oracle/) on the same graph and list",
+                         "dist_evals_per_query": round(e / nq, 1), "expansions_per_query": round(x / nq, 1),
+                         "gpu_dist_evals_per_query": round(st["dist_evals"] / nq, 1)}}
+        attach_traffic(leg["roofline"], n_local, nq, D, args.hnsw_data, allow_frac=frac)
+        out["allow_%g%%" % (100 * frac)] = leg
     return out
 
 
@@ -1350,7 +1367,7 @@ def main():
             # within 0.5 pt of the insert-by-insert graph; --no-seq-build skips it)
             a1 = argparse.Namespace(**vars(args))
             a1.seq_build = (args.seq_build or (not args.no_seq_build and args.rows == 1_000_000)) and ws == 1
-            a1.filtered_fracs = [] if args.no_filtered_hnsw else [0.1, 0.5]
+            a1.filtered_fracs = [] if args.no_filtered_hnsw else [0.1, 0.5, 0.01]
             phase("configs[0] hnsw line")
             h = run_hnsw(a1, ctx, W, with_cpu)
             h.pop("metric", None)

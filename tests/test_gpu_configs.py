@@ -119,8 +119,22 @@ def _unexplained_filtered(ref, qs, k, ef, words, gi, gd, gn, oi, od, on):
     return bad, flat
 
 
+def _variants_identical(ix, qs, k, ef, allow, ref_out, monkeypatch):
+    """Every launch variant of the side-register path answers bit for bit as
+    the default one: one wave per query (no workgroup launch), the exact
+    visited bitmap forced on / off for the first pass (off: overflows re-run
+    exactly)."""
+    gi, gd, gn = ref_out
+    for key, val in (("WV_HNSW_WG_MAX", "0"), ("WV_HNSW_EV_BELOW", "0"), ("WV_HNSW_EV_BELOW", "2")):
+        monkeypatch.setenv(key, val)
+        vi, vd, vn = ix.search_batch(qs, k, ef=ef, allow=allow, mode="hnsw")
+        monkeypatch.delenv(key)
+        assert np.array_equal(vn, gn), (key, val)
+        assert np.array_equal(vi, gi) and np.array_equal(vd.view(np.uint32), gd.view(np.uint32)), (key, val)
+
+
 @pytest.mark.parametrize("frac", [0.01, 0.1, 0.5])
-def test_filtered_hnsw_selective_list_parity_and_fallback_rate(frac):
+def test_filtered_hnsw_selective_list_parity_and_fallback_rate(frac, monkeypatch):
     """Filtered HNSW (search.go:74-78 with |allow| >= flatSearchCutoff or
     forbidFlat; the list applied at layer 0, :282-298) on the configs[0]
     graph shape at 1 %, 10 % and 50 % of the rows: the traversal keeps every
@@ -147,25 +161,27 @@ def test_filtered_hnsw_selective_list_parity_and_fallback_rate(frac):
     gi, gd, gn = ix.search_batch(qs, k, ef=ef, allow=allow, mode="hnsw")
     st = ix.last_batch_stats()
     ss = ix.last_side_stats()
+    _variants_identical(ix, qs, k, ef, allow, (gi, gd, gn), monkeypatch)
     oi, od, on, ost = ref.search_batch(qs, k, ef, allow=words, threads=THREADS)
     ix.close()
     fb = st["fallbacks"]
     bad, flat = _unexplained_filtered(ref, qs, k, ef, words, gi, gd, gn, oi, od, on)
     print(f"allow {frac:.0%} ({n_allowed} rows): side array {ss['side_rows']} x 64, spill {ss['spill_cap']}, "
-          f"overflowed {ss['overflowed']}, exact fallbacks {fb} of {nq}; GPU evaluations "
+          f"overflowed {ss['overflowed']}, redone {ss['redone']}, exact fallbacks {fb} of {nq}; GPU evaluations "
           f"{st['dist_evals'] / nq:.0f} vs the restatement's {ost['dist_evals'] / nq:.0f} per query")
     assert ss["side_rows"] > 0   # (the side-register path ran)
     assert not bad, bad[:10]
     assert len(flat) <= fb, (len(flat), fb)
-    # the exact layer-0 visited list: no query overflows, and the GPU
-    # evaluates what the restatement evaluates (the upper levels' lossy cache
-    # aside)
+    # no query overflows; below 40 % eligible (the exact layer-0 visited
+    # list) the GPU evaluates what the restatement evaluates (the upper
+    # levels' lossy cache aside), above it the lossy cache re-evaluates some
     assert fb == 0 and ss["overflowed"] == 0, (fb, ss)
-    assert st["dist_evals"] <= 1.02 * ost["dist_evals"], (st["dist_evals"], ost["dist_evals"])
+    bound = 1.02 if frac < 0.4 else 1.3
+    assert st["dist_evals"] <= bound * ost["dist_evals"], (st["dist_evals"], ost["dist_evals"])
 
 
 @pytest.mark.parametrize("tomb_frac", [0.01, 0.2])
-def test_tombstoned_hnsw_side_register_path(tomb_frac):
+def test_tombstoned_hnsw_side_register_path(tomb_frac, monkeypatch):
     """Tombstones (delete.go:546-551) make nodes ineligible but traversed
     (search.go:294-296, :347-349) at every level: an unfiltered search of a
     shard with tombstones runs the side-register path (results in
@@ -188,6 +204,7 @@ def test_tombstoned_hnsw_side_register_path(tomb_frac):
     for ef_ in (ef, 128):
         gi, gd, gn = ix.search_batch(qs, k, ef=ef_, mode="hnsw")
         ss = ix.last_side_stats()
+        _variants_identical(ix, qs, k, ef_, None, (gi, gd, gn), monkeypatch)
         oi, od, on, _ = ref.search_batch(qs, k, ef_, threads=THREADS)
         assert ss["side_rows"] > 0
         returned = {int(x) for i in range(nq) for x in gi[i][:gn[i]]}

@@ -48,7 +48,7 @@ hipError_t wv_launch_build_select(const wv::BuildParams* b, hipStream_t s);
 hipError_t wv_launch_build_link(const wv::BuildParams* b, hipStream_t s);
 int wv_hnsw_per_wave_words(int dpad, int efc, int sc, int vc_log2, int xs_log2);
 int wv_hnsw_side_per_wave_words(int dpad, int side_rows, int vc_log2, int xs_log2);
-hipError_t wv_launch_hnsw_side(const wv::HnswParams* p, int waves_per_block, hipStream_t s);
+hipError_t wv_launch_hnsw_side(const wv::HnswParams* p, int waves_per_block, int ev, hipStream_t s);
 hipError_t wv_launch_pq_encode(const float* X, int ldx, const uint64_t* ids, uint64_t n_rows, const wv::PqParams* pq,
                                uint8_t* codes, hipStream_t s);
 hipError_t wv_launch_pq_scan(const wv::PqScanParams* p, hipStream_t s);
@@ -896,7 +896,7 @@ int queue_fbd(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_a
     HIP_TRY(ix->fbd_ci.ensure((size_t)nq * wv::FB_CAP * 4));
     HIP_TRY(ix->fbd_cn.ensure((size_t)nq * 4));
     HIP_TRY(ix->fbd_scr.ensure((size_t)wv::FBD_SCR * std::max<uint64_t>(N, 1) * 4));
-    HIP_TRY(ix->stat_acc.ensure(32));
+    HIP_TRY(ix->stat_acc.ensure(48));
     wv::FbParams bp{};
     bp.X = ix->vecs.as<float>();
     bp.Q = d_q;
@@ -1416,24 +1416,38 @@ int run_hnsw(wv_index* ix, const float* d_q, int nq, int k, int ef, const uint64
         hs.spill = ix->side_sp.as<uint32_t>();
         ix->last_side_rows = side_rows;
         ix->last_side_xs = hs.spill_cap;
-        for (int c0 = 0; c0 < nq; c0 += chunk) {
-            const int cn = std::min(chunk, nq - c0);
-            wv::HnswParams hc = hs;
-            hc.nq = cn;
-            hc.Q = d_q + (size_t)c0 * hp.ldq;
-            if (hc.allow && allow_stride) hc.allow = d_allow + (size_t)c0 * allow_stride;
-            hc.out_ids = d_out_ids + (size_t)c0 * k;
-            hc.out_d = d_out_d + (size_t)c0 * k;
-            hc.out_n = d_out_n + c0;
-            hc.status = hp.status + c0;
-            hc.counters = hp.counters + 2 * (size_t)c0;
-            HIP_TRY(hipMemsetAsync(hs.vbits, 0, (size_t)cn * hs.vwords * 4, s));
-            HIP_TRY(wv_launch_hnsw_side(&hc, wpb, s));
+        // Layer 0 with the exact bitmap below WV_HNSW_EV_BELOW (0.4) of the
+        // rows eligible; above it (light filters, a few tombstones) the lossy
+        // cache + expanded set, whose rare overflow re-runs exactly (redo).
+        // Small batches (<= WV_HNSW_WG_MAX, 512): a workgroup per query.
+        double ev_below = 0.4;
+        if (const char* e = std::getenv("WV_HNSW_EV_BELOW")) ev_below = std::atof(e);
+        const bool ev_first = p_el < ev_below;
+        int wg_max = 512;
+        if (const char* e = std::getenv("WV_HNSW_WG_MAX")) wg_max = std::atoi(e);
+        hs.wg_helpers = nq <= wg_max ? 3 : 0;
+        HIP_TRY(ix->stat_acc.ensure(48));
+        hs.side_acc = ix->stat_acc.as<unsigned long long>();
+        const int passes = ev_first ? 1 : 2;
+        for (int pass = 0; pass < passes; ++pass) {
+            for (int c0 = 0; c0 < nq; c0 += chunk) {
+                const int cn = std::min(chunk, nq - c0);
+                wv::HnswParams hc = hs;
+                hc.nq = cn;
+                hc.Q = d_q + (size_t)c0 * hp.ldq;
+                if (hc.allow && allow_stride) hc.allow = d_allow + (size_t)c0 * allow_stride;
+                hc.out_ids = d_out_ids + (size_t)c0 * k;
+                hc.out_d = d_out_d + (size_t)c0 * k;
+                hc.out_n = d_out_n + c0;
+                hc.status = hp.status + c0;
+                hc.counters = hp.counters + 2 * (size_t)c0;
+                hc.redo = pass ? hc.status : nullptr;
+                hc.vb_host_clear = std::getenv("WV_HNSW_VB_MEMSET") ? 1 : 0;
+                if (hc.vb_host_clear && (ev_first || pass))
+                    HIP_TRY(hipMemsetAsync(hs.vbits, 0, (size_t)cn * hs.vwords * 4, s));
+                HIP_TRY(wv_launch_hnsw_side(&hc, wpb, ev_first || pass, s));
+            }
         }
-        HIP_TRY(ix->stat_acc.ensure(32));
-        hipLaunchKernelGGL(count_nonzero_kernel, dim3((nq + 255) / 256), dim3(256), 0, s, ix->status.as<int32_t>(), nq,
-                           ix->stat_acc.as<unsigned long long>() + 3);
-        HIP_TRY(hipGetLastError());
     } else {
     // small unfiltered batches (the batcher's callers): a workgroup per
     // query, whose three helper waves take the distance batches' other rows
@@ -1471,7 +1485,7 @@ int run_hnsw(wv_index* ix, const float* d_q, int nq, int k, int ef, const uint64
     }
     TREC(5);
     if (uniq) HIP_TRY(hipFreeAsync(uniq, s));
-    HIP_TRY(ix->stat_acc.ensure(32));
+    HIP_TRY(ix->stat_acc.ensure(48));
     HIP_TRY(wv_launch_hnsw_stats(ix->counters.as<uint32_t>(), nq, ix->stat_acc.as<unsigned long long>(), s));
     if (!ix->pq_on) {
         // queries whose side state outgrew LDS: exact answer on the device
@@ -1557,8 +1571,8 @@ int search_core(wv_index* ix, const float* d_q, int nq, int k, int ef, const uin
     if (rc) return rc;
     ix->last_dist = ix->last_exp = ix->last_fallbacks = 0;
     ix->last_side_rows = ix->last_side_xs = 0;
-    HIP_TRY(ix->stat_acc.ensure(32));
-    HIP_TRY(hipMemsetAsync(ix->stat_acc.p, 0, 32, s));
+    HIP_TRY(ix->stat_acc.ensure(48));
+    HIP_TRY(hipMemsetAsync(ix->stat_acc.p, 0, 48, s));
     ix->stat_stream = s;
     if (ix->timing) {
         if (ix->ev_used == ix->ev_pool.size()) {
@@ -2797,16 +2811,17 @@ int wv_last_batch_stats(wv_index* ix, uint64_t* dist_evals, uint64_t* expansions
     return WV_OK;
 }
 
-int wv_last_side_stats(wv_index* ix, uint64_t* overflowed, int* side_rows, int* spill_cap) {
+int wv_last_side_stats(wv_index* ix, uint64_t* overflowed, uint64_t* redone, int* side_rows, int* spill_cap) {
     if (check(ix)) return WV_EINVAL;
     std::lock_guard<std::mutex> g(ix->mu);
     HIP_TRY(hipSetDevice(ix->cfg.device));
-    unsigned long long acc[4] = {0, 0, 0, 0};
+    unsigned long long acc[5] = {0, 0, 0, 0, 0};
     if (ix->stat_acc.p) {
-        HIP_TRY(hipMemcpyAsync(acc, ix->stat_acc.p, 32, hipMemcpyDeviceToHost, ix->stat_stream));
+        HIP_TRY(hipMemcpyAsync(acc, ix->stat_acc.p, 40, hipMemcpyDeviceToHost, ix->stat_stream));
         HIP_TRY(hipStreamSynchronize(ix->stat_stream));
     }
     if (overflowed) *overflowed = acc[3];
+    if (redone) *redone = acc[4];
     if (side_rows) *side_rows = ix->last_side_rows;
     if (spill_cap) *spill_cap = ix->last_side_xs;
     return WV_OK;

@@ -28,6 +28,7 @@
 // which the exact set X records), so pruning with any subset of the visited
 // set is exact.
 #include "wv_device.h"
+#include "wv_h16_dev.h"
 #include "wv_params.h"
 
 #include <float.h>
@@ -42,11 +43,12 @@ constexpr int MAX_LOCAL_TOMB = 4;
 #ifndef WV_HNSW_RPG
 #define WV_HNSW_RPG 4
 #endif
-// rows per 8-lane group on the side-register path (its occupancy is bound
-// by LDS, not VGPRs: a wider trip serves a filtered expansion's ~40 new
-// neighbours in one memory round trip)
+// rows per 8-lane group on the side-register path (24 rows a trip: at 4 it
+// spilled ~25 VGPRs at 3 waves per SIMD; 3 measured fastest of 2 / 3 / 4 on
+// the C1 graph with 1 % tombstones and 10 / 50 % allow lists,
+// profiles/r06/side_rpg_wps_ab.log)
 #ifndef WV_HNSW_SIDE_RPG
-#define WV_HNSW_SIDE_RPG 4
+#define WV_HNSW_SIDE_RPG 3
 #endif
 
 // Diagnostic build only (-DWV_HNSW_STAMPS, tools/hnsw_latency.sh): per-phase
@@ -95,6 +97,7 @@ struct WaveState {
     uint16_t* vc;   // visited cache (HnswParams.vc_tbits)
     uint32_t* xs;
     uint32_t* ltomb;
+    uint32_t* ew;   // side path: the batch's eligibility words (LDS-DMA targets, 4 x 64)
     unsigned long long* ub;   // this query's exact visited bitmap (diagnostic counts; nullable)
     volatile int* wg_nb;      // workgroup-per-query launch: the batch size the helpers read (-1: done)
 };
@@ -949,6 +952,23 @@ __device__ __forceinline__ void search_layer_side(const HnswParams& p, WaveState
         smi = mi;
     };
     auto dead = [&](float d) { return Rl >= ef && d > worst; };
+    // EV: drop the spill's dead entries in place (before it would overflow;
+    // a chunk's writes land at or below its reads)
+    auto compact_spill = [&]() {
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        int m = 0;
+        for (int j0 = 0; j0 < gcnt; j0 += 64) {
+            const int j = j0 + lane;
+            const float d = j < gcnt ? __uint_as_float(sp[2 * j]) : FLT_MAX;
+            const uint32_t id = j < gcnt ? sp[2 * j + 1] : WV_NIL;
+            const bool live = j < gcnt && !dead(d);
+            const uint64_t lm = __ballot(live);
+            if (live) { sp[2 * (m + mbcnt64(lm))] = __float_as_uint(d); sp[2 * (m + mbcnt64(lm)) + 1] = id; }
+            m += __popcll(lm);
+        }
+        gcnt = m;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    };
     // EV: move the LDS keys above a sampled median (n >= 64) to the spill and
     // drop the dead ones; U falls to that median
     auto split = [&]() {
@@ -956,6 +976,7 @@ __device__ __forceinline__ void search_layer_side(const HnswParams& p, WaveState
         float md;
         uint32_t mi;
         wave_rank_key(Sd[idx], Si[idx], 31, md, mi);
+        if (gcnt + n > p.spill_cap) compact_spill();
         int k = 0;
         for (int j0 = 0; j0 < n; j0 += 64) {
             const int j = j0 + lane;
@@ -1010,26 +1031,49 @@ __device__ __forceinline__ void search_layer_side(const HnswParams& p, WaveState
             return;
         }
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-        // a bound whose keys fill about half the array, from 64 samples;
-        // halved while the exact count does not fit
-        const int idx = (int)(((uint32_t)lane * (uint32_t)m) >> 6);
-        const float sd_ = __uint_as_float(sp[2 * idx]);
-        const uint32_t si_ = sp[2 * idx + 1];
-        int r = min(63, max(0, (32 * SC) / m - 1));
+        // a bound whose keys fill about half the array: 64 keys sampled
+        // evenly among the spilled keys at or below the current bound (into
+        // the idle batch arrays), the one of the target rank taken, its keys
+        // counted exactly; a bound that still admits too many narrows the
+        // next round's sample to its own keys (each round ~64x fewer)
         float bd = FLT_MAX;
         uint32_t bi = WV_NIL;
-        for (;;) {
-            wave_rank_key(sd_, si_, r, bd, bi);
+        bool found = false;
+        int cq = m;   // keys at or below (bd, bi)
+        for (int round = 0; round < 4 && !found; ++round) {
+            const int stride = max(1, cq / 64);
+            int t = 0;
+            for (int j0 = 0; j0 < m; j0 += 64) {
+                const int j = j0 + lane;
+                const float d = j < m ? __uint_as_float(sp[2 * j]) : FLT_MAX;
+                const uint32_t id = j < m ? sp[2 * j + 1] : WV_NIL;
+                const bool qual = j < m && (round == 0 || !key_less_nb(bd, bi, d, id));
+                const uint64_t qm = __ballot(qual);
+                const int ti = t + mbcnt64(qm);
+                if (qual && ti % stride == 0 && ti / stride < 64) { w.Bd[ti / stride] = d; w.Bi[ti / stride] = id; }
+                t += __popcll(qm);
+            }
+            wave_sync();
+            const int ns_ = min(64, (cq + stride - 1) / stride);
+            const float sd_ = lane < ns_ ? w.Bd[lane] : FLT_MAX;
+            const uint32_t si_ = lane < ns_ ? w.Bi[lane] : (WV_NIL - 1 - (uint32_t)lane);   // (distinct fillers, ranked last)
+            wave_sync();
+            const int r = min(ns_ - 1, max(0, (ns_ * (SC / 2)) / cq - 1));
+            float nd;
+            uint32_t ni;
+            wave_rank_key(sd_, si_, r, nd, ni);
             int c = 0;
             for (int j0 = 0; j0 < m; j0 += 64) {
                 const int j = j0 + lane;
-                const bool in = j < m && !key_less_nb(bd, bi, __uint_as_float(sp[2 * j]), sp[2 * j + 1]);
+                const bool in = j < m && !key_less_nb(nd, ni, __uint_as_float(sp[2 * j]), sp[2 * j + 1]);
                 c += __popcll(__ballot(in));
             }
-            if (c <= SC) break;
-            if (r == 0) { status |= 2; return; }
-            r >>= 1;
+            bd = nd;
+            bi = ni;
+            cq = c;
+            found = c <= SC;
         }
+        if (!found) { status |= 2; return; }
         int k = 0, g = 0;
         for (int j0 = 0; j0 < m; j0 += 64) {
             const int j = j0 + lane;
@@ -1153,6 +1197,20 @@ __device__ __forceinline__ void search_layer_side(const HnswParams& p, WaveState
             wave_sync();
             if (v0) w.vc[h0] = t0;
             if (v1) w.vc[h1] = t1;
+            // eligibility words (tombstones, the allow list at layer 0): LDS-
+            // DMA loads issued now, beside the claims / row loads, read after
+            // the distances -- no VGPRs held across them and no branch on
+            // them before (that would wait: one more round trip an expansion)
+            const uint32_t eb = __builtin_amdgcn_readfirstlane(lds_addr(w.ew));
+            const bool use_al = level == 0 && allow;
+            if (p.tomb) {
+                if (v0 && id0 < p.tomb_nbits) glds4(reinterpret_cast<const uint32_t*>(p.tomb) + (id0 >> 5), eb);
+                if (v1 && id1 < p.tomb_nbits) glds4(reinterpret_cast<const uint32_t*>(p.tomb) + (id1 >> 5), eb + 256);
+            }
+            if (use_al) {
+                if (v0 && id0 < p.allow_nbits) glds4(reinterpret_cast<const uint32_t*>(allow) + (id0 >> 5), eb + 512);
+                if (v1 && id1 < p.allow_nbits) glds4(reinterpret_cast<const uint32_t*>(allow) + (id1 >> 5), eb + 768);
+            }
             if (EV) {
                 // the cache's misses claim their bit: a node another expansion
                 // evaluated (the cache forgot it) is skipped, as the exact
@@ -1171,18 +1229,29 @@ __device__ __forceinline__ void search_layer_side(const HnswParams& p, WaveState
             const int nb = n0 + __popcll(m1);
             if (v0) w.Bi[mbcnt64(m0)] = id0;
             if (v1) w.Bi[n0 + mbcnt64(m1)] = id1;
-            // eligibility (tombstone / allow words) loads issued beside the
-            // row loads, consumed after them (no round trip of their own)
-            const bool el0 = v0 && eligible(id0), el1 = v1 && eligible(id1);
             wave_sync();
             if (nb == 0) continue;
-            for (int base = 0; base < nb; base += 8 * RPG)
-                exact_dist_rows<METRIC, RPG, true>(w.qv, p.X, p.ldx, p.D, w.Bi + base, nb - base, w.Bd + base, lane);
+            if (p.wg_helpers) {
+                wg_dist<METRIC>(p, w, nb, lane);
+            } else {
+                for (int base = 0; base < nb; base += 8 * RPG)
+                    exact_dist_rows<METRIC, RPG, true>(w.qv, p.X, p.ldx, p.D, w.Bi + base, nb - base, w.Bd + base,
+                                                       lane);
+            }
             n_dist += (uint32_t)nb;
             wave_sync();
             // ---- keep test against the batch's starting state (search.go:282),
             // on the neighbours' own lanes (batch order = lane order, id0s
             // first): eligible keys into R one by one, ineligible ones to S ----
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (the eligibility words landed)
+            auto el_of = [&](bool v, uint32_t id, int h) -> bool {
+                const uint32_t tw = p.tomb && id < p.tomb_nbits ? w.ew[64 * h + lane] : 0u;
+                const uint32_t aw = !use_al ? ~0u : id < p.allow_nbits ? w.ew[128 + 64 * h + lane] : 0u;
+                bool e = v && !((tw >> (id & 31)) & 1u) && ((aw >> (id & 31)) & 1u);
+                for (int t = 0; t < nlt; ++t) e = e && w.ltomb[t] != id;
+                return e;
+            };
+            const bool el0 = el_of(v0, id0, 0), el1 = el_of(v1, id1, 1);
             float bd[2];
             uint32_t bi[2];
             uint64_t kmask[2], smask[2];
@@ -1277,6 +1346,7 @@ __device__ __forceinline__ void search_layer_side(const HnswParams& p, WaveState
                 const uint64_t g0 = smask[0] & ~lmask[0], g1 = smask[1] & ~lmask[1];
                 if (g0 | g1) {
                     const int gn0 = __popcll(g0);
+                    if (gcnt + gn0 + __popcll(g1) > p.spill_cap) compact_spill();
                     if ((g0 >> lane) & 1) {
                         const int g = gcnt + mbcnt64(g0);
                         if (g < p.spill_cap) { sp[2 * g] = __float_as_uint(bd[0]); sp[2 * g + 1] = bi[0]; }
@@ -1347,14 +1417,24 @@ __device__ __forceinline__ void search_layer_side(const HnswParams& p, WaveState
     }
 }
 
-template <int METRIC, int NR, int RPG>
-__device__ __forceinline__ void knn_one_side(const HnswParams& p, WaveState& w, int q) {
+template <int METRIC, int NR, int RPG, bool EV0>
+__device__ __forceinline__ int knn_one_side(const HnswParams& p, WaveState& w, int q) {
     const int lane = threadIdx.x & 63;
     const int g = lane & 7;
     for (int i = lane; i < p.dpad; i += 64) w.qv[i] = i < p.D ? p.Q[(uint64_t)q * p.ldq + i] : 0.f;
     wave_sync();
     const uint64_t* allow = p.allow ? p.allow + (p.allow_stride ? (uint64_t)q * p.allow_stride : 0) : nullptr;
-    uint32_t* vb = p.vbits + (uint64_t)q * p.vwords;
+    uint32_t* vb = EV0 ? p.vbits + (uint64_t)q * p.vwords : nullptr;
+    if (EV0 && !p.vb_host_clear) {
+        // this query's layer-0 visited bitmap starts empty (cleared here,
+        // overlapped with the other waves' searches; the fence orders the
+        // clear before the claims)
+        uint4* v4 = reinterpret_cast<uint4*>(vb);
+        const uint64_t n4 = p.vwords / 4;
+        for (uint64_t i = lane; i < n4; i += 64) v4[i] = make_uint4(0u, 0u, 0u, 0u);
+        for (uint64_t i = 4 * n4 + lane; i < p.vwords; i += 64) vb[i] = 0u;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    }
     uint32_t* sp = p.spill + 2 * (uint64_t)q * p.spill_cap;
     int status = 0, nlt = 0;
     uint32_t n_dist = 0, n_exp = 0;
@@ -1384,8 +1464,8 @@ __device__ __forceinline__ void knn_one_side(const HnswParams& p, WaveState& w, 
         }
     }
     if (!status)
-        search_layer_side<METRIC, NR, RPG, true>(p, w, 0, p.ef, ep, epd, allow, nlt, vb, sp, rd, ri, Rl, status, n_dist,
-                                                 n_exp);
+        search_layer_side<METRIC, NR, RPG, EV0>(p, w, 0, p.ef, ep, epd, allow, nlt, vb, sp, rd, ri, Rl, status, n_dist,
+                                                n_exp);
     const int n = status ? 0 : min(Rl, p.k);
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
@@ -1399,26 +1479,60 @@ __device__ __forceinline__ void knn_one_side(const HnswParams& p, WaveState& w, 
         p.out_n[q] = n;
         p.status[q] = status;
         if (p.counters) { p.counters[2 * q] = n_dist; p.counters[2 * q + 1] = n_exp; }
+        if (status && p.side_acc) atomicAdd(p.side_acc + (EV0 ? 3 : 4), 1ull);
     }
+    return status;
 }
 
-// LDS per wave: query, batch, side array, X (upper levels), local tombstones,
-// visited cache.  WPS: waves per SIMD the register allocation targets
-template <int METRIC, int NR, int RPG, int WPS>
-__global__ __launch_bounds__(256, WPS) void wv_hnsw_side_kernel(HnswParams p) {
-    extern __shared__ float lds[];
-    const int wave = threadIdx.x >> 6;
-    const int q = blockIdx.x * (blockDim.x >> 6) + wave;
-    if (q >= p.nq) return;
-    float* cur = lds + (uint64_t)wave * p.per_wave_words;
-    WaveState w{};
+// LDS per wave: query, batch, side array, X, local tombstones, visited cache
+__device__ __forceinline__ void side_wave_state(const HnswParams& p, float* cur, WaveState& w) {
     w.qv = cur; cur += p.dpad;
     w.Bd = cur; cur += BATCH; w.Bi = reinterpret_cast<uint32_t*>(cur); cur += BATCH;
     w.Sd = cur; cur += 64 * p.side_rows; w.Si = reinterpret_cast<uint32_t*>(cur); cur += 64 * p.side_rows;
     w.xs = reinterpret_cast<uint32_t*>(cur); cur += (1 << p.xs_log2);
     w.ltomb = reinterpret_cast<uint32_t*>(cur); cur += MAX_LOCAL_TOMB;
+    w.ew = reinterpret_cast<uint32_t*>(cur); cur += 256;
     w.vc = reinterpret_cast<uint16_t*>(cur);
-    knn_one_side<METRIC, NR, RPG>(p, w, q);
+}
+
+// WPS: waves per SIMD the register allocation targets.  EV0: layer 0 with the
+// exact visited bitmap (selective lists); otherwise the lossy cache + X, and
+// a query whose side state overflows is re-run with EV0 (p.redo).
+template <int METRIC, int NR, int RPG, int WPS, bool EV0>
+__global__ __launch_bounds__(256, WPS) void wv_hnsw_side_kernel(HnswParams p) {
+    extern __shared__ float lds[];
+    const int wave = threadIdx.x >> 6;
+    const int q = blockIdx.x * (blockDim.x >> 6) + wave;
+    if (q >= p.nq) return;
+    if (p.redo && p.redo[q] == 0) return;   // (second pass: this query completed)
+    WaveState w{};
+    side_wave_state(p, lds + (uint64_t)wave * p.per_wave_words, w);
+    knn_one_side<METRIC, NR, RPG, EV0>(p, w, q);
+}
+
+// Small batches (the batcher's callers): one 4-wave workgroup per query, wave
+// 0 running the side search and waves 1..3 its distance batches (wg_dist,
+// the barrier invariant above it).  Same expansion order and results.
+template <int METRIC, int NR, bool EV0>
+__global__ __launch_bounds__(256) void wv_hnsw_side_wg_kernel(HnswParams p) {
+    extern __shared__ float lds[];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int q = blockIdx.x;
+    if (q >= p.nq) return;
+    if (p.redo && p.redo[q] == 0) return;   // (uniform over the workgroup)
+    WaveState w{};
+    side_wave_state(p, lds, w);
+    w.wg_nb = reinterpret_cast<volatile int*>(lds + p.per_wave_words);
+    if (wave == 0) {
+        // (a lossy first pass that overflowed re-runs in a second launch: an
+        // in-kernel re-run with the exact visited bitmap doubled the code and
+        // took a lone tombstoned query 399 -> 509 us)
+        knn_one_side<METRIC, NR, 4, EV0>(p, w, q);
+        if (lane == 0) *w.wg_nb = -1;
+        __syncthreads();
+    } else {
+        wg_helper<METRIC>(p, w, wave, lane);
+    }
 }
 
 // ===========================================================================
@@ -1657,7 +1771,7 @@ __global__ __launch_bounds__(64) void wv_build_link_kernel(BuildParams b) {
 }
 
 int hnsw_side_per_wave_words(int dpad, int side_rows, int vc_log2, int xs_log2) {
-    return dpad + 2 * BATCH + 128 * side_rows + (1 << xs_log2) + MAX_LOCAL_TOMB + ((1 << vc_log2) + 1) / 2;
+    return dpad + 2 * BATCH + 128 * side_rows + (1 << xs_log2) + MAX_LOCAL_TOMB + 256 + ((1 << vc_log2) + 1) / 2;
 }
 
 int hnsw_per_wave_words(int dpad, int efc, int sc, int vc_log2, int xs_log2) {
@@ -1676,16 +1790,37 @@ int wv_hnsw_side_per_wave_words(int dpad, int side_rows, int vc_log2, int xs_log
     return wv::hnsw_side_per_wave_words(dpad, side_rows, vc_log2, xs_log2);
 }
 
-// side-register path (filtered / tombstoned / nil nodes, ef <= 128, no PQ)
-hipError_t wv_launch_hnsw_side(const wv::HnswParams* p, int waves_per_block, hipStream_t s) {
+// side-register path (filtered / tombstoned / nil nodes, ef <= 128, no PQ);
+// ev: layer 0 with the exact visited bitmap; wg: a workgroup per query
+hipError_t wv_launch_hnsw_side(const wv::HnswParams* p, int waves_per_block, int ev, hipStream_t s) {
+    if (p->nq == 0) return hipSuccess;
+    const int nr = p->efc == 64 ? 1 : p->efc == 128 ? 2 : 0;
+    if (nr == 0 || p->pq.codes || p->side_rows < 4 || (ev && (!p->vbits || !p->spill))) return hipErrorInvalidValue;
+    if (p->wg_helpers) {
+        const size_t lds = (size_t)p->per_wave_words * sizeof(float) + 16;
+#define WV_HNSW_SIDE_WG(M, NRV, E) \
+        hipLaunchKernelGGL((wv::wv_hnsw_side_wg_kernel<M, NRV, E>), dim3(p->nq), dim3(256), lds, s, *p)
+#define WV_HNSW_SIDE_WG_M(M)                                                                                        \
+        do {                                                                                                        \
+            if (nr == 1) { if (ev) WV_HNSW_SIDE_WG(M, 1, true); else WV_HNSW_SIDE_WG(M, 1, false); }                \
+            else { if (ev) WV_HNSW_SIDE_WG(M, 2, true); else WV_HNSW_SIDE_WG(M, 2, false); }                        \
+        } while (0)
+        if (p->metric == WV_METRIC_L2) WV_HNSW_SIDE_WG_M(WV_METRIC_L2);
+        else if (p->metric == WV_METRIC_DOT) WV_HNSW_SIDE_WG_M(WV_METRIC_DOT);
+        else WV_HNSW_SIDE_WG_M(WV_METRIC_COSINE);
+#undef WV_HNSW_SIDE_WG_M
+#undef WV_HNSW_SIDE_WG
+        return hipGetLastError();
+    }
     const size_t lds = (size_t)waves_per_block * p->per_wave_words * sizeof(float);
     const unsigned blocks = (unsigned)((p->nq + waves_per_block - 1) / waves_per_block);
-    if (blocks == 0) return hipSuccess;
-    const int nr = p->efc == 64 ? 1 : p->efc == 128 ? 2 : 0;
-    if (nr == 0 || p->pq.codes || p->side_rows < 1) return hipErrorInvalidValue;
 #define WV_HNSW_SIDE_W(M, NRV, W)                                                                                   \
-    hipLaunchKernelGGL((wv::wv_hnsw_side_kernel<M, NRV, WV_HNSW_SIDE_RPG, W>), dim3(blocks),                          \
-                       dim3(64 * waves_per_block), lds, s, *p)
+    do {                                                                                                            \
+        if (ev) hipLaunchKernelGGL((wv::wv_hnsw_side_kernel<M, NRV, WV_HNSW_SIDE_RPG, W, true>), dim3(blocks),      \
+                                   dim3(64 * waves_per_block), lds, s, *p);                                         \
+        else hipLaunchKernelGGL((wv::wv_hnsw_side_kernel<M, NRV, WV_HNSW_SIDE_RPG, W, false>), dim3(blocks),        \
+                                dim3(64 * waves_per_block), lds, s, *p);                                            \
+    } while (0)
 #define WV_HNSW_SIDE(M)                                                                                             \
     do {                                                                                                            \
         if (nr == 1 && wps == 3) WV_HNSW_SIDE_W(M, 1, 3);                                                           \

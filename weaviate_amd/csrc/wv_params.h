@@ -386,6 +386,11 @@ struct HnswParams {
     uint64_t vwords;
     uint32_t* spill;
     int spill_cap;
+    int vb_host_clear;   // the host zeroed vbits (A/B switch; default: each wave clears its own)
+    // batch stats (nullable): [3] += queries whose side state overflowed an
+    // exact-visited search (the exact fallback answers them), [4] += queries
+    // a lossy first pass handed to the exact-visited search
+    unsigned long long* side_acc;
 };
 
 // Flat search over PQ codes (flat_search.go:19-74 on a compressed index):

@@ -353,10 +353,11 @@ class GPUVectorIndex:
 
     def last_side_stats(self):
         """filtered HNSW: queries whose side set outgrew its HBM spill (exact
-        fallback), the LDS side array's rows of 64 and the spill capacity"""
-        a, b, c = C.c_uint64(), C.c_int(), C.c_int()
-        check(lib().wv_last_side_stats(self._h, C.byref(a), C.byref(b), C.byref(c)))
-        return {"overflowed": a.value, "side_rows": b.value, "spill_cap": c.value}
+        fallback), queries the light-filter pass re-ran with the exact visited
+        bitmap, the LDS side array's rows of 64 and the spill capacity"""
+        a, r, b, c = C.c_uint64(), C.c_uint64(), C.c_int(), C.c_int()
+        check(lib().wv_last_side_stats(self._h, C.byref(a), C.byref(r), C.byref(b), C.byref(c)))
+        return {"overflowed": a.value, "redone": r.value, "side_rows": b.value, "spill_cap": c.value}
 
 
 class CommitLogGraph:
