@@ -955,6 +955,8 @@ def run_hnsw(args, ctx, W, with_cpu):
                                          f"(T=1); knnSearchByVector restated in C on the same graph (oracle/)"}
         if getattr(args, "filtered_fracs", None):
             res["filtered_hnsw"] = filtered_hnsw_legs(args, ctx, ix, ref, queries, qt, NQ, K, D, n_local)
+        if getattr(args, "tomb_frac", 0) > 0:
+            res["tombstoned"] = tombstoned_leg(args, ctx, ix, ref, queries, qt, NQ, K, D, n_local, res)
         if args.seq_build:
             # north_star: recall within 0.5 pt of the reference index -- whose
             # graph is built by inserting one node at a time (insert.go:103-217,
@@ -1049,6 +1051,64 @@ def filtered_hnsw_legs(args, ctx, ix, ref, queries, qt, NQ, K, D, n_local):
         attach_traffic(leg["roofline"], n_local, nq, D, args.hnsw_data, allow_frac=frac)
         out["allow_%g%%" % (100 * frac)] = leg
     return out
+
+
+def tombstoned_leg(args, ctx, ix, ref, queries, qt, NQ, K, D, n_local, res):
+    """The same line on a shard with a fraction of its ids tombstoned
+    (delete.go:546-551: an update is a delete + insert and tombstones live
+    until cleanup): tombstoned nodes are traversed but never returned
+    (search.go:294-296, :347-349), so the side-register path runs (results
+    in registers; the lossy visited cache at this selectivity, a rare
+    overflow re-run with the exact bitmap).  QPS against the tombstone-free
+    value, the lone caller's latency through the micro-batcher, and parity
+    with the restatement under the same tombstones.  The tombstones are
+    cleared afterwards."""
+    torch = ctx.torch
+    dead = np.nonzero(counter_uniform(5, 0, n_local, 1)[:, 0] < args.tomb_frac)[0]
+    ix.add_tombstones(dead)
+    oi_, od_, on_ = _out_tensors(ctx, NQ, K)
+
+    def step(timed):
+        ix.search_batch_device(qt.data_ptr(), NQ, K, oi_.data_ptr(), od_.data_ptr(), on_.data_ptr(), ef=args.ef,
+                               mode="hnsw", stream=ctx.stream)
+
+    ix.set_timing(True)
+    el = ctx.time_steps(step, args.steps, args.warmup, before_timed=ix.last_kernel_times)
+    km = ix.last_kernel_times()["hnsw_ms"]
+    st, ss = ix.last_batch_stats(), ix.last_side_stats()
+    ix.set_timing(False)
+    gi = oi_.cpu().numpy().view(np.uint64).copy()
+    gd = od_.cpu().numpy().copy()
+    for t in dead.tolist():
+        ref.add_tombstone(int(t))
+    ri, rd, rn, rst = ref.search_batch(queries, K, args.ef, threads=args.cpu_threads)
+    for t in dead.tolist():
+        ref.remove_tombstone(int(t))
+    id_eq, d_eq, tie_ok = parity_stats(gi, gd, ri, rd)
+    leaked = int(np.isin(gi[gi != np.uint64(0xFFFFFFFFFFFFFFFF)], dead.astype(np.uint64)).sum())
+    a1 = argparse.Namespace(**vars(args))
+    a1.concurrency = [1]
+    lone = concurrent_callers(a1, ix, queries).get("1", {})
+    ix.set_tombstones([])
+    e, x = rst["dist_evals"], rst["expansions"]
+    by = 4.0 * D * e + 4.0 * 2 * args.M * x
+    achieved = by / (km * 1e-3) / 1e9
+    free = res.get("value")
+    val = NQ * args.steps / el
+    return {"value": round(val, 1), "unit": "queries/s", "ms_per_step": round(1000 * el / args.steps, 3),
+            "tombstoned_ids": int(len(dead)), "tomb_frac": args.tomb_frac,
+            "vs_tombstone_free_value": round(val / free, 4) if free else None,
+            "tombstoned_ids_returned": leaked, "exact_fallback_queries": int(st["fallbacks"]),
+            "side_state": {"lds_side_rows": ss["side_rows"], "light_pass_redone": ss["redone"],
+                           "spill_overflowed": ss["overflowed"]},
+            "parity_sample": {"queries": NQ, "id_match_frac": id_eq, "dists_bitwise_equal_frac": d_eq,
+                              "tie_aware_identical_frac": tie_ok},
+            "lone_caller_through_batcher": lone,
+            "roofline": {"bound": "hbm", "kernel": "wv_hnsw_side_kernel", "achieved": round(achieved, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "kernel_ms": round(km, 3), "counts_from": "CPU restatement (oracle/) with the same tombstones",
+                         "dist_evals_per_query": round(e / NQ, 1), "expansions_per_query": round(x / NQ, 1),
+                         "gpu_dist_evals_per_query": round(st["dist_evals"] / NQ, 1)}}
 
 
 def concurrent_callers(args, ix, queries):
@@ -1239,6 +1299,8 @@ def main():
                     help="the configs[4] line with 12.5M rows per GPU (weak scaling) instead of the fixed corpus")
     ap.add_argument("--no-c5-line", action="store_true",
                     help="skip the configs[4] line (100M x 96 corpus sharded over the N GPUs, hnsw + RCCL merge)")
+    ap.add_argument("--tomb-frac", type=float, default=0.01,
+                    help="C1 line: also time the shard with this fraction of ids tombstoned (0 = skip)")
     ap.add_argument("--no-filtered-hnsw", action="store_true",
                     help="skip the filtered-HNSW legs (allow 10 / 50 %%, forbidFlat) on the configs[0] graph")
     ap.add_argument("--no-c4-line", action="store_true",

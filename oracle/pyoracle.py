@@ -253,6 +253,9 @@ class Index:
     def add_tombstone(self, id_):
         lib().wvo_add_tombstone(self.h, id_)
 
+    def remove_tombstone(self, id_):
+        lib().wvo_remove_tombstone(self.h, id_)
+
     def compress(self, cent, codes, use_bits=False, has=None):
         """Compress (compress.go:39-89) with fitted centroids cent[m][ks][ds]
         and encoded vectors codes[n][m * bytes] for ids 0..n-1."""
