@@ -55,7 +55,10 @@ def test_go_decorator_binds_only_header_symbols():
     # runtime PQ enablement (config_update.go:97-128): the CPU index answers
     # while pending, each callback flushes the log and compacts the mirror
     uuc = re.search(r"func \(g \*Index\) UpdateUserConfig\(.*?\n}\n", src, re.S).group(0)
-    assert "g.pqPending.Store(true)" in uuc and "go g.syncCompression()" in uuc
+    assert "g.pqPending.Store(true)" in uuc and "go g.syncCompression(gen, final)" in uuc
+    # (advisor, round 5) a failed UpdateUserConfig, or a Compress that ended
+    # without codes, settles the flag instead of leaving the CPU index answering
+    assert "g.pqPending.Store(false)" in uuc
     sc = re.search(r"func \(g \*Index\) syncCompression\(.*?\n}\n", src, re.S).group(0)
     assert sc.index("cpuIndex.Flush()") < sc.index("C.wv_mirror_compact(") < sc.index("g.pqPending.Store(false)")
     for method in ("SearchByVector", "SearchByVectorDistance"):

@@ -37,6 +37,7 @@
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <mutex>
@@ -104,7 +105,7 @@ constexpr int WAKE_CHAINS = 8;
 // end, each next within REFILL_GAP_US of the one before (an open-loop request
 // at an idle device is launched at once)
 int refill_us(int n) { return std::min(300, 50 + n); }
-constexpr int REFILL_GAP_US = 40;
+constexpr int REFILL_GAP_US = 40;   // (WV_BATCHER_REFILL_GAP_US; < 0: wait to the cap, round 5)
 
 // one worker's staging, reused batch after batch
 struct Staging {
@@ -124,6 +125,7 @@ struct wv_batcher {
     int dim = 0;
     int max_batch = 256;
     int max_wait_us = 0;
+    int refill_gap_us = REFILL_GAP_US;
     std::mutex mu;
     std::condition_variable cv_work;
     std::deque<Request*> queue;
@@ -222,10 +224,10 @@ struct wv_batcher {
                 // the finished batch's callers are still resubmitting: wait
                 // for them while they keep coming, up to the cap
                 const auto cap = idle_since + std::chrono::microseconds(refill_us(want));
-                const auto gap = std::chrono::microseconds(REFILL_GAP_US);
+                const auto gap = std::chrono::microseconds(refill_gap_us);
                 for (;;) {
                     const auto now = wait_clock::now();
-                    const auto until = std::min(cap, (resub_seen ? last_resub : idle_since) + gap);
+                    const auto until = refill_gap_us < 0 ? cap : std::min(cap, (resub_seen ? last_resub : idle_since) + gap);
                     if (now >= until) break;
                     wake_at = want;
                     const bool full = cv_work.wait_until(
@@ -300,6 +302,7 @@ static int create_batcher(wv_index* ix, wv_group* grp, int dim, int max_batch, i
     b->dim = dim;
     b->max_batch = max_batch;
     b->max_wait_us = max_wait_us;
+    if (const char* e = std::getenv("WV_BATCHER_REFILL_GAP_US")) b->refill_gap_us = std::atoi(e);
     for (int w = 0; w < 2; ++w) b->th.emplace_back([b, w] { b->loop(b->st[w]); });
     *out = b;
     return WV_OK;
