@@ -815,6 +815,10 @@ def run_hnsw(args, ctx, W, with_cpu):
     exact_fb = ix.last_batch_stats()["fallbacks"]
     truth = (m_ids if corpus else out_ids).cpu().numpy().view(np.uint64)
     rec = float(np.mean([len(set(a) & set(b)) / K for a, b in zip(hi_ids.tolist(), truth.tolist())]))
+
+    def recall_of(ids):
+        return float(np.mean([len(set(a) & set(b)) / K for a, b in zip(ids.tolist(), truth.tolist())]))
+
     hnsw_ms = float(np.mean([k["hnsw_ms"] for k in kern_ms]))
     e, x = stats[-1]["dist_evals"], stats[-1]["expansions"]
     by = 4.0 * D * e + 4.0 * 2 * args.M * x   # 4*D*E + 4*deg_slots*X (deg0 = 2M)
@@ -967,18 +971,31 @@ def run_hnsw(args, ctx, W, with_cpu):
             seq.add_batch(base, threads=args.hnsw_build_threads)
             build_s = time.time() - t0
             si = seq.search_batch(queries, K, args.ef, threads=args.cpu_threads)[0]
+            # the GPU-built graph's recall at the other ef too (before the
+            # sequential graph replaces it on the device)
+            efs = [args.ef] + ([128] if args.ef != 128 and 128 in args.ef_sweep else [])
+            r_built = {args.ef: rec}
+            for ef_ in efs[1:]:
+                ix.search_batch_device(qt.data_ptr(), NQ, K, out_ids.data_ptr(), out_d.data_ptr(),
+                                       out_n.data_ptr(), ef=ef_, mode="hnsw", stream=ctx.stream)
+                torch.cuda.synchronize(ctx.dev)
+                r_built[ef_] = recall_of(out_ids.cpu().numpy().view(np.uint64))
             ix.upload_graph(seq.export_graph())
             del seq
-            ix.search_batch_device(qt.data_ptr(), NQ, K, out_ids.data_ptr(), out_d.data_ptr(), out_n.data_ptr(),
-                                   ef=args.ef, mode="hnsw", stream=ctx.stream)
-            torch.cuda.synchronize(ctx.dev)
-            gs = out_ids.cpu().numpy().view(np.uint64)
-            r_seq = float(np.mean([len(set(a) & set(b)) / K for a, b in zip(si.tolist(), truth.tolist())]))
-            r_gs = float(np.mean([len(set(a) & set(b)) / K for a, b in zip(gs.tolist(), truth.tolist())]))
+            r_seq_gpu = {}
+            for ef_ in efs:
+                ix.search_batch_device(qt.data_ptr(), NQ, K, out_ids.data_ptr(), out_d.data_ptr(),
+                                       out_n.data_ptr(), ef=ef_, mode="hnsw", stream=ctx.stream)
+                torch.cuda.synchronize(ctx.dev)
+                r_seq_gpu[ef_] = recall_of(out_ids.cpu().numpy().view(np.uint64))
+            r_seq = recall_of(si)
             res["sequential_build"] = {
                 "recall@10_restatement_on_sequential_graph": round(r_seq, 4),
-                "recall@10_gpu_on_sequential_graph": round(r_gs, 4), "recall@10_gpu_built_graph": round(rec, 4),
+                "recall@10_gpu_on_sequential_graph": round(r_seq_gpu[args.ef], 4),
+                "recall@10_gpu_built_graph": round(rec, 4),
                 "delta_pt_gpu_built_vs_sequential": round(100 * (rec - r_seq), 2),
+                "by_ef": {str(e): {"gpu_built": round(r_built[e], 4), "sequential": round(r_seq_gpu[e], 4),
+                                   "delta_pt": round(100 * (r_built[e] - r_seq_gpu[e]), 2)} for e in efs},
                 "sequential_build_s": round(build_s, 1), "threads": args.hnsw_build_threads}
     ix.close()
     return res
@@ -1440,6 +1457,9 @@ def main():
             a3.rows, a3.dim, a3.metric, a3.hnsw_data = 1_200_000, 100, "cosine-dot", "glove"
             a3.ef, a3.ef_sweep, a3.concurrency, a3.split = 64, [32, 64, 128, 256], [], "corpus"
             a3.cpu_seconds, a3.cpu_seconds_t1, a3.graph_build = 4.0, 2.0, "gpu"
+            # north_star's 0.5-pt recall check against the insert-by-insert
+            # graph at this line's ef and 128 (~50 s of CPU at 1.2M rows)
+            a3.seq_build = not args.no_seq_build and ws == 1
             phase("configs[2] hnsw ef sweep")
             h = run_hnsw(a3, ctx, W, with_cpu)
             h.pop("metric", None)
