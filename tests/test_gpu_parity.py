@@ -953,8 +953,8 @@ def test_hnsw_workgroup_per_query_small_batches(metric, d, M, monkeypatch):
     """Batches of up to 64 unfiltered queries run one 4-wave workgroup per
     query (wv_hnsw_wg_kernel: helper waves take rows 32..127 of each distance
     batch): identical to the restatement and, bit for bit, to the one-wave
-    kernel (WV_HNSW_WG_MAX=0), at batch sizes 1, 7 and 64, ef 10 / 64 / 100
-    (one and two result registers), M = 64 (128 neighbours per batch) and a
+    kernel (WV_HNSW_WG_MAX=0), at batch sizes 1, 7 and 64, ef 10 / 64 / 100 /
+    200 / 256 (one, two and four result registers), M = 64 (128 neighbours per batch) and a
     D = 32 m + 4 row tail."""
     n = 4000
     base, idx = _build_graph(n, d, metric, M=M)
@@ -963,7 +963,7 @@ def test_hnsw_workgroup_per_query_small_batches(metric, d, M, monkeypatch):
     ix = W.GPUVectorIndex(d, METRIC_NAMES[metric], capacity=n, max_connections=M)
     ix.upload_vectors(base)
     ix.upload_graph(g)
-    for ef in (10, 64, 100):
+    for ef in (10, 64, 100, 200, 256):
         oi, od, on, st = idx.search_batch(qs, 10, ef, threads=8)
         for nb in (1, 7, 64):
             q = qs[:nb]

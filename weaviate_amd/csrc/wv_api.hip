@@ -48,6 +48,7 @@ hipError_t wv_launch_build_select(const wv::BuildParams* b, hipStream_t s);
 hipError_t wv_launch_build_link(const wv::BuildParams* b, hipStream_t s);
 int wv_hnsw_per_wave_words(int dpad, int efc, int sc, int vc_log2, int xs_log2);
 int wv_hnsw_side_per_wave_words(int dpad, int side_rows, int vc_log2, int xs_log2);
+int wv_hnsw_reg_per_wave_words(int dpad, int vc_log2);
 hipError_t wv_launch_hnsw_side(const wv::HnswParams* p, int waves_per_block, int ev, hipStream_t s);
 hipError_t wv_launch_pq_encode(const float* X, int ldx, const uint64_t* ids, uint64_t n_rows, const wv::PqParams* pq,
                                uint8_t* codes, hipStream_t s);
@@ -1283,14 +1284,19 @@ int run_hnsw(wv_index* ix, const float* d_q, int nq, int k, int ef, const uint64
     const bool filtered = d_allow != nullptr || ix->any_tomb || ix->any_nil;
     const int sc = filtered ? 256 : 0;
     const int xs_log2 = filtered ? 9 : 0;
-    const int fixed = wv_hnsw_per_wave_words(ix->dpad, efc, sc, 0, xs_log2) - 1;
+    // register results (unfiltered, ef <= 256): the wave's LDS is the query,
+    // the batch and the visited cache only
+    const bool reg = !filtered && efc <= 256;
+    const int fixed = reg ? wv_hnsw_reg_per_wave_words(ix->dpad, 0) - 1
+                          : wv_hnsw_per_wave_words(ix->dpad, efc, sc, 0, xs_log2) - 1;
     // per-wave LDS budget: 20 KiB filtered (8 waves per CU), 12 KiB otherwise
     int wave_kb = filtered ? 20 : 12;
     if (const char* e = std::getenv("WV_HNSW_WAVE_KB")) wave_kb = std::max(4, std::atoi(e));
     const int budget = wave_kb * 1024 / 4;
     int vc_tbits = 0;
     const int vc_log2 = choose_vc_log2(budget, fixed, ix->gn, &vc_tbits);
-    int per_wave = wv_hnsw_per_wave_words(ix->dpad, efc, sc, vc_log2, xs_log2);
+    int per_wave = reg ? wv_hnsw_reg_per_wave_words(ix->dpad, vc_log2)
+                       : wv_hnsw_per_wave_words(ix->dpad, efc, sc, vc_log2, xs_log2);
     per_wave = (per_wave + 3) & ~3;
     int wpb = 4;
     while (wpb > 1 && (size_t)wpb * per_wave * 4 > 160 * 1024) --wpb;
@@ -1456,7 +1462,7 @@ int run_hnsw(wv_index* ix, const float* d_q, int nq, int k, int ef, const uint64
     // WV_HNSW_WG_MAX: the largest such batch; 0 turns it off.
     int wg_max = 512;
     if (const char* e = std::getenv("WV_HNSW_WG_MAX")) wg_max = std::atoi(e);
-    const bool wg = !filtered && !ix->pq_on && (efc == 64 || efc == 128) && nq <= wg_max;
+    const bool wg = !filtered && !ix->pq_on && reg && nq <= wg_max;
     if (wg) {
         hp.wg_helpers = 3;
         HIP_TRY(wv_launch_hnsw_wg(&hp, s));

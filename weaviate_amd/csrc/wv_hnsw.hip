@@ -443,15 +443,22 @@ __device__ __forceinline__ float wave_shr1(float v) { return __uint_as_float(wav
 // kept neighbours one by one ends in the same R as the LDS path's sorted batch
 // merge (the ef smallest keys of R and the kept neighbours, duplicates once),
 // so the expansion order and the results are the same, bit for bit.
+// (e is wave-uniform: the register is picked by scalar compares)
 template <int NR>
 __device__ __forceinline__ float reg_entry_d(const float (&rd)[NR], int e) {
-    if (NR == 1 || e < 64) return __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(rd[0]), e));
-    return __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(rd[NR - 1]), e - 64));
+    float v = rd[0];
+#pragma unroll
+    for (int r = 1; r < NR; ++r)
+        if ((e >> 6) == r) v = rd[r];
+    return __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(v), e & 63));
 }
 template <int NR>
 __device__ __forceinline__ uint32_t reg_entry_i(const uint32_t (&ri)[NR], int e) {
-    if (NR == 1 || e < 64) return (uint32_t)__builtin_amdgcn_readlane(ri[0], e);
-    return (uint32_t)__builtin_amdgcn_readlane(ri[NR - 1], e - 64);
+    uint32_t v = ri[0];
+#pragma unroll
+    for (int r = 1; r < NR; ++r)
+        if ((e >> 6) == r) v = ri[r];
+    return (uint32_t)__builtin_amdgcn_readlane(v, e & 63);
 }
 
 // Distances of a batch in a workgroup-per-query launch: wave v computes rows
@@ -491,7 +498,7 @@ template <int METRIC, bool PQ, int NR>
 __device__ __forceinline__ void search_layer_reg(const HnswParams& p, WaveState& w, int level, int ef, uint32_t ep,
                                                  float epd, float (&rd)[NR], uint32_t (&ri)[NR], int& Rl,
                                                  uint32_t& n_dist, uint32_t& n_exp, Stamps& ts) {
-    static_assert(NR == 1 || NR == 2, "64 or 128 results per wave");
+    static_assert(NR == 1 || NR == 2 || NR == 4, "64, 128 or 256 results per wave");
     const int lane = threadIdx.x & 63;
     const int VC = 1 << p.vc_log2;
     for (int i = lane; i < VC; i += 64) w.vc[i] = VC_EMPTY;
@@ -752,7 +759,16 @@ __device__ __forceinline__ void knn_one(const HnswParams& p, WaveState& w, int q
     }
 }
 
-// One instantiation per (metric, raw / PQ, LDS results / 64 / 128 register
+// LDS of a register-results wave (hnsw_reg_per_wave_words): query, batch,
+// visited cache, local tombstones
+__device__ __forceinline__ void reg_wave_state(const HnswParams& p, float* cur, WaveState& w) {
+    w.qv = cur; cur += p.dpad;
+    w.Bd = cur; cur += BATCH; w.Bi = reinterpret_cast<uint32_t*>(cur); cur += BATCH;
+    w.ltomb = reinterpret_cast<uint32_t*>(cur); cur += MAX_LOCAL_TOMB;
+    w.vc = reinterpret_cast<uint16_t*>(cur);
+}
+
+// One instantiation per (metric, raw / PQ, LDS results / 64 / 128 / 256 register
 // results): each gets its own register allocation (one kernel holding all six
 // inlined searches spilled 431 SGPRs into VGPR lanes); the host launches the
 // matching one.
@@ -765,20 +781,25 @@ __global__ __launch_bounds__(256) void wv_hnsw_kernel(HnswParams p) {
     if (p.redo && p.redo[q] == 0) return;   // (second pass: this query completed)
     float* base = lds + (uint64_t)wave * p.per_wave_words;
     WaveState w;
-    float* cur = base;
-    w.qv = cur; cur += p.dpad;
-    w.Rd = cur; cur += p.efc; w.Ri = reinterpret_cast<uint32_t*>(cur); cur += p.efc;
-    w.Rd2 = cur; cur += p.efc; w.Ri2 = reinterpret_cast<uint32_t*>(cur); cur += p.efc;
-    w.Sd = cur; cur += p.sc; w.Si = reinterpret_cast<uint32_t*>(cur); cur += p.sc;
-    w.Sd2 = cur; cur += p.sc; w.Si2 = reinterpret_cast<uint32_t*>(cur); cur += p.sc;
-    w.Bd = cur; cur += BATCH; w.Bi = reinterpret_cast<uint32_t*>(cur); cur += BATCH;
-    w.Cd = cur; cur += BATCH; w.Ci = reinterpret_cast<uint32_t*>(cur); cur += BATCH;
-    w.vc = reinterpret_cast<uint16_t*>(cur); cur += ((1 << p.vc_log2) + 1) / 2;
-    w.xs = reinterpret_cast<uint32_t*>(cur); cur += (1 << p.xs_log2);
-    w.ltomb = reinterpret_cast<uint32_t*>(cur); cur += MAX_LOCAL_TOMB;
-    w.ub = p.uniq ? p.uniq + (uint64_t)q * p.uniq_words : nullptr;
-    if constexpr (NR > 0) knn_one_reg<METRIC, PQ, NR>(p, w, q);
-    else knn_one<METRIC, PQ>(p, w, q);
+    if constexpr (NR > 0) {   // register results: no R, S, sorted batch or X in LDS
+        reg_wave_state(p, base, w);
+        w.ub = p.uniq ? p.uniq + (uint64_t)q * p.uniq_words : nullptr;
+        knn_one_reg<METRIC, PQ, NR>(p, w, q);
+    } else {
+        float* cur = base;
+        w.qv = cur; cur += p.dpad;
+        w.Rd = cur; cur += p.efc; w.Ri = reinterpret_cast<uint32_t*>(cur); cur += p.efc;
+        w.Rd2 = cur; cur += p.efc; w.Ri2 = reinterpret_cast<uint32_t*>(cur); cur += p.efc;
+        w.Sd = cur; cur += p.sc; w.Si = reinterpret_cast<uint32_t*>(cur); cur += p.sc;
+        w.Sd2 = cur; cur += p.sc; w.Si2 = reinterpret_cast<uint32_t*>(cur); cur += p.sc;
+        w.Bd = cur; cur += BATCH; w.Bi = reinterpret_cast<uint32_t*>(cur); cur += BATCH;
+        w.Cd = cur; cur += BATCH; w.Ci = reinterpret_cast<uint32_t*>(cur); cur += BATCH;
+        w.vc = reinterpret_cast<uint16_t*>(cur); cur += ((1 << p.vc_log2) + 1) / 2;
+        w.xs = reinterpret_cast<uint32_t*>(cur); cur += (1 << p.xs_log2);
+        w.ltomb = reinterpret_cast<uint32_t*>(cur); cur += MAX_LOCAL_TOMB;
+        w.ub = p.uniq ? p.uniq + (uint64_t)q * p.uniq_words : nullptr;
+        knn_one<METRIC, PQ>(p, w, q);
+    }
 }
 
 // Small unfiltered batches (wv_search_batch under ~64 queries: the batcher's
@@ -791,19 +812,9 @@ __global__ __launch_bounds__(256) void wv_hnsw_wg_kernel(HnswParams p) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int q = blockIdx.x;
     if (q >= p.nq) return;
-    float* cur = lds;
     WaveState w;
+    reg_wave_state(p, lds, w);
     w.wg_nb = reinterpret_cast<volatile int*>(lds + p.per_wave_words);
-    w.qv = cur; cur += p.dpad;
-    w.Rd = cur; cur += p.efc; w.Ri = reinterpret_cast<uint32_t*>(cur); cur += p.efc;
-    w.Rd2 = cur; cur += p.efc; w.Ri2 = reinterpret_cast<uint32_t*>(cur); cur += p.efc;
-    w.Sd = cur; cur += p.sc; w.Si = reinterpret_cast<uint32_t*>(cur); cur += p.sc;
-    w.Sd2 = cur; cur += p.sc; w.Si2 = reinterpret_cast<uint32_t*>(cur); cur += p.sc;
-    w.Bd = cur; cur += BATCH; w.Bi = reinterpret_cast<uint32_t*>(cur); cur += BATCH;
-    w.Cd = cur; cur += BATCH; w.Ci = reinterpret_cast<uint32_t*>(cur); cur += BATCH;
-    w.vc = reinterpret_cast<uint16_t*>(cur); cur += ((1 << p.vc_log2) + 1) / 2;
-    w.xs = reinterpret_cast<uint32_t*>(cur); cur += (1 << p.xs_log2);
-    w.ltomb = reinterpret_cast<uint32_t*>(cur); cur += MAX_LOCAL_TOMB;
     w.ub = p.uniq ? p.uniq + (uint64_t)q * p.uniq_words : nullptr;
     if (wave == 0) {
         knn_one_reg<METRIC, false, NR>(p, w, q);
@@ -1774,6 +1785,10 @@ int hnsw_side_per_wave_words(int dpad, int side_rows, int vc_log2, int xs_log2) 
     return dpad + 2 * BATCH + 128 * side_rows + (1 << xs_log2) + MAX_LOCAL_TOMB + 256 + ((1 << vc_log2) + 1) / 2;
 }
 
+int hnsw_reg_per_wave_words(int dpad, int vc_log2) {
+    return dpad + 2 * BATCH + MAX_LOCAL_TOMB + ((1 << vc_log2) + 1) / 2;
+}
+
 int hnsw_per_wave_words(int dpad, int efc, int sc, int vc_log2, int xs_log2) {
     return dpad + 4 * efc + 4 * sc + 4 * BATCH + ((1 << vc_log2) + 1) / 2 + (1 << xs_log2) + MAX_LOCAL_TOMB;
 }
@@ -1785,6 +1800,8 @@ extern "C" {
 int wv_hnsw_per_wave_words(int dpad, int efc, int sc, int vc_log2, int xs_log2) {
     return wv::hnsw_per_wave_words(dpad, efc, sc, vc_log2, xs_log2);
 }
+
+int wv_hnsw_reg_per_wave_words(int dpad, int vc_log2) { return wv::hnsw_reg_per_wave_words(dpad, vc_log2); }
 
 int wv_hnsw_side_per_wave_words(int dpad, int side_rows, int vc_log2, int xs_log2) {
     return wv::hnsw_side_per_wave_words(dpad, side_rows, vc_log2, xs_log2);
@@ -1865,13 +1882,14 @@ hipError_t wv_launch_build_link(const wv::BuildParams* b, hipStream_t s) {
 // workgroup-per-query launch of an unfiltered register-path search (no PQ)
 hipError_t wv_launch_hnsw_wg(const wv::HnswParams* p, hipStream_t s) {
     if (p->nq == 0) return hipSuccess;
-    const int nr = p->sc == 0 && !p->allow ? (p->efc == 64 ? 1 : p->efc == 128 ? 2 : 0) : 0;
+    const int nr = p->sc == 0 && !p->allow ? (p->efc == 64 ? 1 : p->efc == 128 ? 2 : p->efc <= 256 ? 4 : 0) : 0;
     if (nr == 0 || p->pq.codes || !p->wg_helpers) return hipErrorInvalidValue;
     const size_t lds = (size_t)p->per_wave_words * sizeof(float) + 16;
 #define WV_HNSW_WG(M)                                                                                              \
     do {                                                                                                           \
         if (nr == 1) hipLaunchKernelGGL((wv::wv_hnsw_wg_kernel<M, 1>), dim3(p->nq), dim3(256), lds, s, *p);       \
-        else hipLaunchKernelGGL((wv::wv_hnsw_wg_kernel<M, 2>), dim3(p->nq), dim3(256), lds, s, *p);               \
+        else if (nr == 2) hipLaunchKernelGGL((wv::wv_hnsw_wg_kernel<M, 2>), dim3(p->nq), dim3(256), lds, s, *p);  \
+        else hipLaunchKernelGGL((wv::wv_hnsw_wg_kernel<M, 4>), dim3(p->nq), dim3(256), lds, s, *p);               \
     } while (0)
     if (p->metric == WV_METRIC_L2) WV_HNSW_WG(WV_METRIC_L2);
     else if (p->metric == WV_METRIC_DOT) WV_HNSW_WG(WV_METRIC_DOT);
@@ -1886,12 +1904,14 @@ hipError_t wv_launch_hnsw(const wv::HnswParams* p, int waves_per_block, hipStrea
     if (blocks == 0) return hipSuccess;
     // results in registers: unfiltered (no side set) with ef <= 64 (one
     // register) or ef <= 128 (two)
-    const int nr = p->sc == 0 && !p->allow ? (p->efc == 64 ? 1 : p->efc == 128 ? 2 : 0) : 0;
+    const int nr = p->sc == 0 && !p->allow ? (p->efc == 64 ? 1 : p->efc == 128 ? 2 : p->efc <= 256 ? 4 : 0) : 0;
 #define WV_HNSW_LAUNCH(M, PQ)                                                                                        \
     do {                                                                                                             \
         if (nr == 1) hipLaunchKernelGGL((wv::wv_hnsw_kernel<M, PQ, 1>), dim3(blocks), dim3(64 * waves_per_block),   \
                                         lds, s, *p);                                                                 \
         else if (nr == 2) hipLaunchKernelGGL((wv::wv_hnsw_kernel<M, PQ, 2>), dim3(blocks),                          \
+                                             dim3(64 * waves_per_block), lds, s, *p);                                \
+        else if (nr == 4) hipLaunchKernelGGL((wv::wv_hnsw_kernel<M, PQ, 4>), dim3(blocks),                          \
                                              dim3(64 * waves_per_block), lds, s, *p);                                \
         else hipLaunchKernelGGL((wv::wv_hnsw_kernel<M, PQ, 0>), dim3(blocks), dim3(64 * waves_per_block), lds, s,   \
                                 *p);                                                                                 \
