@@ -636,25 +636,69 @@ def wide_k_line(args, ctx, st, W):
         if k == 100:
             d100 = od.cpu().numpy()
     # SearchByVectorDistance: target = each query's 150th-nearest distance, so
-    # the deepening runs two rounds (limit 100, then 200)
+    # the deepening runs two rounds (limit 100, then 1100).  The per-query
+    # host loop (wv_search_by_vector_distance), the device batch
+    # (wv_search_by_vector_distance_batch: every exact round one threshold
+    # pass + sort) for one query and for 64, and T concurrent callers through
+    # the micro-batcher (unfiltered on this graph-less index: flatSearch)
     n_local = st["n_local"]
     allow = W.AllowList.from_ids(np.arange(n_local, dtype=np.uint64), n_local)
     ix.update_user_config(flat_search_cutoff=n_local + 1)
-    o256 = _out_tensors(ctx, 4, 256)
-    qs4 = _query_tensor(ctx, st["queries"][:4], ix.query_ld())
-    ix.search_batch_device(qs4.data_ptr(), 4, 256, o256[0].data_ptr(), o256[1].data_ptr(), o256[2].data_ptr(),
+    nt = 64
+    o256 = _out_tensors(ctx, nt, 256)
+    qsn = _query_tensor(ctx, st["queries"][:nt], ix.query_ld())
+    ix.search_batch_device(qsn.data_ptr(), nt, 256, o256[0].data_ptr(), o256[1].data_ptr(), o256[2].data_ptr(),
                            mode="exact", stream=ctx.stream)
-    targets = o256[1].cpu().numpy()[:, 149]
+    targets = np.ascontiguousarray(o256[1].cpu().numpy()[:, 149])
     times, counts = [], []
     for i in range(4):
         t0 = time.perf_counter()
         ids, ds = ix.search_by_vector_distance(st["queries"][i], float(targets[i]), -1, allow=allow)
         times.append(time.perf_counter() - t0)
         counts.append(int(len(ids)))
+    one = []
+    for i in range(8):
+        t0 = time.perf_counter()
+        got1, _ = ix.search_by_vector_distance_batch(st["queries"][i:i + 1], targets[i:i + 1], -1, allow=allow,
+                                                     cap=1024)
+        one.append(time.perf_counter() - t0)
+    same1 = all(ix.search_by_vector_distance(st["queries"][i], float(targets[i]), -1, allow=allow)[0].tolist() ==
+                ix.search_by_vector_distance_batch(st["queries"][i:i + 1], targets[i:i + 1], -1, allow=allow,
+                                                   cap=1024)[0][0][0].tolist() for i in range(4))
+    ix.search_by_vector_distance_batch(st["queries"][:nt], targets, -1, allow=allow, cap=1024)
+    t0 = time.perf_counter()
+    reps = 3
+    for _ in range(reps):
+        got, cnt = ix.search_by_vector_distance_batch(st["queries"][:nt], targets, -1, allow=allow, cap=1024)
+    batch_s = (time.perf_counter() - t0) / reps
     ix.update_user_config(flat_search_cutoff=40000)
-    out["search_by_vector_distance"] = {"ms_per_query": round(1e3 * float(np.median(times[1:])), 3),
-                                        "results_per_query": counts, "note": "one query per call, host "
-                                        "entry point, flat allow list of every id, 150 results (two rounds)"}
+    out["search_by_vector_distance"] = {
+        "ms_per_query": round(1e3 * float(np.median(one[1:])), 3),
+        "ms_per_query_host_loop": round(1e3 * float(np.median(times[1:])), 3),
+        "results_per_query": counts, "batch_equals_host_loop": bool(same1),
+        "batch_64": {"ms_per_batch": round(1e3 * batch_s, 3), "queries_per_s": round(nt / batch_s, 1),
+                     "mean_results": round(float(np.mean(cnt)), 1)},
+        "note": "target = each query's 150th-nearest distance (rounds at limit 100 and 1100); flat allow list of "
+                "every id; ms_per_query: one query per wv_search_by_vector_distance_batch call (device threshold "
+                "pass + sort), ms_per_query_host_loop: the round-5 per-round host loop"}
+    path = os.path.join(ROOT, "tests", "native", "libwvload.so")
+    if args.concurrency and os.path.exists(path):
+        import ctypes as C
+        lib = C.CDLL(path)
+        if hasattr(lib, "wvl_concurrent_distance"):
+            lib.wvl_concurrent_distance.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
+                                                    C.c_double, C.c_int, C.c_void_p]
+            q = np.ascontiguousarray(st["queries"][:nt], dtype=np.float32)
+            cc = {}
+            for t in (1, 16, 64):
+                r = np.zeros(7, np.float64)
+                rc = lib.wvl_concurrent_distance(C.c_void_p(ix._h.value if hasattr(ix._h, "value") else ix._h),
+                                                 q.ctypes.data, targets.ctypes.data, nt, q.shape[1], t, 1.5,
+                                                 args.max_batch, r.ctypes.data)
+                cc[str(t)] = {"error": f"status {rc}"} if rc else {
+                    "value": round(r[0], 1), "unit": "queries/s", "p50_us": round(r[1], 1), "p99_us": round(r[2], 1),
+                    "mean_batch": round(r[3], 1), "mean_results": round(r[6], 1)}
+            out["search_by_vector_distance"]["concurrent_callers"] = cc
     return out
 
 

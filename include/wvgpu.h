@@ -185,6 +185,19 @@ int wv_search_by_vector_distance(wv_index *ix, const float *vector, float target
                                  int64_t max_limit, const uint64_t *allow_bits, uint64_t allow_nbits,
                                  uint64_t *out_ids, float *out_dists, int64_t out_cap, int64_t *out_n);
 
+/* SearchByVectorDistance for a batch of queries (each with its own target
+ * distance; one max_limit; allow lists shared or per query as in
+ * wv_search_batch).  Outputs [nq][out_cap]; out_n[q] = the number of results
+ * (entries past out_cap are not written).  Round 1 runs as the batch's
+ * SearchByVector where that is an HNSW search; every exact round (a flat
+ * round 1, all deeper rounds) is one threshold pass + segmented sort on the
+ * device, launched beside round 1 -- one device sync per batch instead of a
+ * host loop of single-query searches. */
+int wv_search_by_vector_distance_batch(wv_index *ix, const float *queries, int nq, const float *target_distances,
+                                       int64_t max_limit, const uint64_t *allow_bits, uint64_t allow_nbits,
+                                       uint64_t allow_stride_words, uint64_t *out_ids, float *out_dists,
+                                       int64_t out_cap, int64_t *out_n);
+
 /* Batched search of nq queries (row-major [nq][dim]).  ef <= 0 selects
  * searchTimeEF(k).  allow_bits may be NULL, one bitmap shared by the batch
  * (allow_stride_words == 0) or one bitmap per query.  out_* are [nq][k]. */
@@ -323,6 +336,12 @@ int wv_batcher_search(wv_batcher *b, const float *vector, int k, const uint64_t 
  * same list sends it once. */
 int wv_batcher_search_ids(wv_batcher *b, const float *vector, int k, int filtered, const uint64_t *allow_ids,
                           uint64_t n_allow, uint64_t *out_ids, float *out_dists, int32_t *out_n);
+/* SearchByVectorDistance through the micro-batcher: concurrent callers with
+ * the same maxLimit coalesce into one wv_search_by_vector_distance_batch.
+ * out_cap entries at most are written; *out_n receives the full count. */
+int wv_batcher_search_distance_ids(wv_batcher *b, const float *vector, float target_distance, int64_t max_limit,
+                                   int filtered, const uint64_t *allow_ids, uint64_t n_allow, uint64_t *out_ids,
+                                   float *out_dists, int64_t out_cap, int64_t *out_n);
 int wv_batcher_stats(wv_batcher *b, uint64_t *requests, uint64_t *batches);
 int wv_batcher_destroy(wv_batcher *b);
 
@@ -357,6 +376,12 @@ int wv_group_update_config(wv_group *g, const wv_config *cfg);
 int wv_group_search_batch(wv_group *g, const float *queries, int nq, int k, int ef, const uint64_t *allow_bits,
                           uint64_t allow_nbits, uint64_t allow_stride_words, int mode, uint64_t *out_ids,
                           float *out_dists, int32_t *out_n);
+/* SearchByVectorDistance over the group (wv_search_by_vector_distance_batch's
+ * arguments): a shard group merges its members' answers by distance. */
+int wv_group_search_by_vector_distance_batch(wv_group *g, const float *queries, int nq, const float *target_distances,
+                                             int64_t max_limit, const uint64_t *allow_bits, uint64_t allow_nbits,
+                                             uint64_t allow_stride_words, uint64_t *out_ids, float *out_dists,
+                                             int64_t out_cap, int64_t *out_n);
 /* the micro-batcher over a group (wv_batcher_search / _stats / _destroy as above) */
 int wv_batcher_create_group(wv_group *g, int dim, int max_batch, int max_wait_us, wv_batcher **out);
 

@@ -431,7 +431,7 @@ int main(int argc, char** argv) {
     deleted.resize(deleted.size() + N_ADD);   // (no reallocation while readers scan it)
     std::atomic<uint64_t> n_added{0};
     std::atomic<bool> writer_done{false}, stop_maint{false};
-    std::atomic<uint64_t> max_delta{0}, n_compact{0}, n_search{0}, n_added_checks{0}, n_filtered{0};
+    std::atomic<uint64_t> max_delta{0}, n_compact{0}, n_search{0}, n_added_checks{0}, n_filtered{0}, n_dist_search{0};
     std::mutex in_graph_mu;
     std::vector<uint8_t> compacted(CAP, 0);   // added rows that a compaction moved into the graph
     g_n_added = &n_added;
@@ -613,6 +613,30 @@ int main(int argc, char** argv) {
                 if (!(n > 0 && ids[0] == target && ds[0] == 0.f) && !deleted_since)
                     violation("added id " + std::to_string(target) + " not found first");
             }
+            // SearchByVectorDistance through the batcher, concurrently with
+            // the k-NN callers: within the target, no deleted or disallowed id
+            if (it % 7 == 3 && n > 0) {
+                const float td = ds[n - 1];
+                uint64_t dids[4 * K];
+                float dds[4 * K];
+                int64_t dn = 0;
+                const int drc = wv_mirror_search_by_distance(m, q.data(), DIM, td, -1, filtered, al.data(), al.size(),
+                                                             dids, dds, 4 * K, &dn);
+                if (drc == WV_ESTALE && (async_start || heal)) {
+                    stale_answers++;
+                    continue;
+                }
+                if (drc) { violation(std::string("search by distance: ") + wv_last_error()); return; }
+                n_dist_search++;
+                for (int64_t i = 0; i < std::min<int64_t>(dn, 4 * K); ++i) {
+                    if (dids[i] >= CAP) violation("distance search: id out of range");
+                    else if (del_now[dids[i]]) violation("distance search returned deleted id " + std::to_string(dids[i]));
+                    if (filtered && !std::binary_search(al.begin(), al.end(), dids[i]))
+                        violation("filtered distance search returned a disallowed id");
+                    if (!(dds[i] <= td || std::fabs((double)dds[i] - (double)td) <= 1e-6))
+                        violation("distance search returned an entry beyond the target");
+                }
+            }
         }
     };
     std::vector<std::thread> ts;
@@ -700,7 +724,7 @@ int main(int argc, char** argv) {
                 "\"stale_answers\": %llu, \"startup_call_s\": %.3f, \"startup_rows\": %llu, \"startup_missing\": %llu, "
                 "\"diffs_startup\": %d, \"diffs_final\": %d, \"exact_fallbacks\": %d, \"checked\": %d, \"adds\": %llu, \"deletes\": %d, "
                 "\"compactions\": %llu, \"max_delta\": %llu, \"capacity\": %llu, \"growths\": %llu, "
-                "\"searches\": %llu, \"added_checks\": %llu, \"filtered\": %llu, \"batcher_requests\": %llu, "
+                "\"searches\": %llu, \"distance_searches\": %llu, \"added_checks\": %llu, \"filtered\": %llu, \"batcher_requests\": %llu, "
                 "\"batcher_batches\": %llu, \"serve_s\": %.2f}\n",
                 mode.c_str(), (unsigned long long)st.resyncs, (unsigned long long)st.replayed_writes, st.pq,
                 (unsigned long long)stale_answers.load(), startup_call_s,
@@ -708,6 +732,7 @@ int main(int argc, char** argv) {
                 diffs_startup, diffs_final, exact_fallbacks, NQ_CHECK, (unsigned long long)n_added.load(), n_deleted.load(),
                 (unsigned long long)st.compactions, (unsigned long long)max_delta.load(),
                 (unsigned long long)st.capacity, (unsigned long long)st.growths, (unsigned long long)n_search.load(),
+                (unsigned long long)n_dist_search.load(),
                 (unsigned long long)n_added_checks.load(), (unsigned long long)n_filtered.load(),
                 (unsigned long long)st.batcher_requests, (unsigned long long)st.batcher_batches, serve_s);
     return 0;

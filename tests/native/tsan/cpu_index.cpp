@@ -187,8 +187,24 @@ int wv_search_by_vector_distance(wv_index* x, const float* v, float target, int6
     *out_n = (int64_t)c.size();
     return WV_OK;
 }
+int wv_search_by_vector_distance_batch(wv_index* x, const float* qs, int nq, const float* targets, int64_t max_limit,
+                                       const uint64_t* allow, uint64_t nbits, uint64_t stride, uint64_t* out_ids,
+                                       float* out_d, int64_t out_cap, int64_t* out_n) {
+    for (int q = 0; q < nq; ++q) {
+        const uint64_t* a = allow ? allow + (stride ? (size_t)q * stride : 0) : nullptr;
+        const int rc = wv_search_by_vector_distance(x, qs + (size_t)q * x->dim, targets[q], max_limit, a, nbits,
+                                                    out_ids + (size_t)q * out_cap, out_d + (size_t)q * out_cap,
+                                                    out_cap, out_n + q);
+        if (rc) return rc;
+    }
+    return WV_OK;
+}
 int wv_group_search_batch(wv_group*, const float*, int, int, int, const uint64_t*, uint64_t, uint64_t, int, uint64_t*,
                           float*, int32_t*) {
+    return fail(WV_EINVAL, "no groups in the TSAN stand-in");
+}
+int wv_group_search_by_vector_distance_batch(wv_group*, const float*, int, const float*, int64_t, const uint64_t*,
+                                             uint64_t, uint64_t, uint64_t*, float*, int64_t, int64_t*) {
     return fail(WV_EINVAL, "no groups in the TSAN stand-in");
 }
 

@@ -75,6 +75,72 @@ int wvl_concurrent(wv_index* ix, const float* queries, int nq, int dim, int k, i
     return WV_OK;
 }
 
+// T concurrent SearchByVectorDistance callers (search.go:90-158) through the
+// micro-batcher (wv_batcher_search_distance_ids), each query with its own
+// target (targets[i]), maxLimit -1, unfiltered.  out[0] QPS, out[1] p50 (us),
+// out[2] p99, out[3] mean batch size, out[4] requests, out[5] seconds, out[6]
+// mean results per call.
+int wvl_concurrent_distance(wv_index* ix, const float* queries, const float* targets, int nq, int dim, int threads,
+                            double seconds, int max_batch, double* out) {
+    if (!ix || !queries || !targets || nq <= 0 || dim <= 0 || threads <= 0 || seconds <= 0 || !out) return WV_EINVAL;
+    wv_batcher* b = nullptr;
+    int rc = wv_batcher_create(ix, dim, max_batch, 0, &b);
+    if (rc) return rc;
+    std::atomic<bool> go{false}, stop{false};
+    std::atomic<int> failed{0};
+    std::atomic<uint64_t> results{0}, calls{0};
+    std::vector<std::vector<float>> lat(threads);
+    std::vector<std::thread> ts;
+    for (int t = 0; t < threads; ++t) {
+        ts.emplace_back([&, t] {
+            const int64_t cap = 4096;
+            std::vector<uint64_t> ids(cap);
+            std::vector<float> ds(cap);
+            int64_t n = 0;
+            lat[t].reserve(1 << 14);
+            while (!go.load(std::memory_order_acquire)) std::this_thread::yield();
+            for (uint64_t i = 0; !stop.load(std::memory_order_relaxed); ++i) {
+                const size_t qi = (size_t)((t + i * threads) % nq);
+                const auto a = std::chrono::steady_clock::now();
+                if (wv_batcher_search_distance_ids(b, queries + qi * dim, targets[qi], -1, 0, nullptr, 0, ids.data(),
+                                                   ds.data(), cap, &n)) {
+                    failed = 1;
+                    return;
+                }
+                lat[t].push_back(std::chrono::duration<float, std::micro>(std::chrono::steady_clock::now() - a).count());
+                results += (uint64_t)n;
+                calls++;
+            }
+        });
+    }
+    uint64_t r0 = 0, b0 = 0, r1 = 0, b1 = 0;
+    go = true;
+    std::this_thread::sleep_for(std::chrono::milliseconds(250));
+    wv_batcher_stats(b, &r0, &b0);
+    const uint64_t res0 = results.load(), c0 = calls.load();
+    const auto t0 = std::chrono::steady_clock::now();
+    std::this_thread::sleep_for(std::chrono::duration<double>(seconds));
+    wv_batcher_stats(b, &r1, &b1);
+    const uint64_t res1 = results.load(), c1 = calls.load();
+    const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    stop = true;
+    for (auto& t : ts) t.join();
+    wv_batcher_destroy(b);
+    if (failed) return WV_EDEVICE;
+    std::vector<float> all;
+    for (auto& v : lat) all.insert(all.end(), v.begin() + v.size() / 8, v.end());
+    if (all.empty()) return WV_ESTATE;
+    std::sort(all.begin(), all.end());
+    out[0] = (double)(r1 - r0) / el;
+    out[1] = all[all.size() / 2];
+    out[2] = all[std::min(all.size() - 1, all.size() * 99 / 100)];
+    out[3] = b1 > b0 ? (double)(r1 - r0) / (double)(b1 - b0) : 0.0;
+    out[4] = (double)(r1 - r0);
+    out[5] = el;
+    out[6] = c1 > c0 ? (double)(res1 - res0) / (double)(c1 - c0) : 0.0;
+    return WV_OK;
+}
+
 // Open loop: requests arrive at Poisson times of rate `rate` (seed 7) for
 // `seconds`, each issued at its time by one of `pool` threads (a pool larger
 // than rate x latency keeps arrivals independent of completions); latency is

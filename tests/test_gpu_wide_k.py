@@ -129,3 +129,76 @@ def test_search_by_vector_distance_deepening_on_the_wide_path():
         assert gi.tolist() == oi.tolist()
         assert np.array_equal(gd.view(np.uint32), od.view(np.uint32))
     ix.close()
+
+
+def _single_calls(ix, qs, targets, max_limit, allows, cap):
+    out = []
+    for i, q in enumerate(qs):
+        a = allows[i] if isinstance(allows, list) else allows
+        out.append(ix.search_by_vector_distance(q, float(targets[i]), max_limit, allow=a, cap=cap))
+    return out
+
+
+def _assert_same(batch, single, n, cap):
+    for i, ((bi, bd), (si, sd)) in enumerate(zip(batch, single)):
+        assert bi.tolist() == si.tolist(), i
+        assert np.array_equal(bd.view(np.uint32), sd.view(np.uint32)), i
+
+
+@pytest.mark.parametrize("metric", [O.L2, O.DOT, O.COSINE])
+def test_search_by_vector_distance_batch_equals_single_calls(metric):
+    """wv_search_by_vector_distance_batch (round 1 the batch's SearchByVector
+    where it is an HNSW search, every exact round one threshold pass +
+    segmented sort on the device) answers each query as the single-query
+    deepening (search.go:90-158: limits 100, 1100, 11100 ...) does, bit for
+    bit: HNSW and flat round 1, targets that stop in round 1, 2 or 3, a
+    shared and per-query allow lists, maxLimit, results past the caller's
+    cap counted but not written."""
+    n, d, nq = 30_000, 32, 24
+    base, qs = _data(n, nq, d, 31, metric)
+    idx = O.Index(d, metric, 16, 64, capacity=n, seed=3)
+    idx.add_batch(base, threads=8)
+    ix = W.GPUVectorIndex(d, NAMES[metric], capacity=n, max_connections=16)
+    ix.upload_vectors(base)
+    ix.upload_graph(idx.export_graph())
+    b = O.normalize_rows(base) if metric == O.COSINE else base
+    q = O.normalize_rows(qs) if metric == O.COSINE else qs
+    full = np.sort(O.flat_scan(metric, b, q, 3000)[1], axis=1)
+    ranks = [20, 99, 100, 150, 1099, 1500, 2500]
+    targets = np.array([full[i, ranks[i % len(ranks)]] for i in range(nq)], np.float32)
+    rng = np.random.default_rng(4)
+    shared = W.AllowList.from_ids(np.nonzero(rng.random(n) < 0.5)[0], n)   # 15k >= cutoff: HNSW round 1
+    small = W.AllowList.from_ids(np.nonzero(rng.random(n) < 0.2)[0], n)    # 6k < cutoff 40k: flat
+    per_q = [shared if i % 2 else small for i in range(nq)]
+    for allow in (None, shared, small, per_q):
+        for max_limit in (-1, 150, 1100, 5000):
+            for cap in (4096, 120):
+                got, cnt = ix.search_by_vector_distance_batch(qs, targets, max_limit, allow=allow, cap=cap)
+                want = _single_calls(ix, qs, targets, max_limit, allow, cap)
+                _assert_same(got, want, cnt, cap)
+    ix.close()
+
+
+def test_search_by_vector_distance_batch_flat_index_equals_restatement():
+    """The flat (graph-less) index: every round exact; the batch equals the
+    restatement's SearchByVectorDistance (oracle/) on each query, up to the
+    order among equal distances."""
+    n, d = 100_000, 64
+    base, qs = _data(n, 6, d, 9, O.L2)
+    ix = W.GPUVectorIndex(d, "l2-squared", capacity=n, flat_search_cutoff=10**9)
+    ix.upload_vectors(base)
+    ref = O.Index(d, "l2-squared", 16, 64, capacity=n)
+    nil = np.uint32(0xFFFFFFFF)
+    ref.import_graph(base, dict(n=n, entrypoint=0, max_level=0, levels=np.zeros(n, np.int8),
+                                layer0=np.full((n, 1), nil, np.uint32), upper_row=np.full(n, nil, np.uint32),
+                                upper=np.zeros((1, 1, 1), np.uint32)))
+    ref.set_search_config(flat_search_cutoff=10**9)
+    allow = W.AllowList.from_ids(np.arange(n), n)
+    targets = [float(np.sort(((base - q) ** 2).sum(1))[r]) for q, r in zip(qs, (5, 99, 150, 1200, 3000, 40))]
+    got, cnt = ix.search_by_vector_distance_batch(qs, targets, -1, allow=allow, cap=8192)
+    for i, q in enumerate(qs):
+        oi, od = ref.search_by_vector_distance(q, targets[i], -1, allow=O.bits_from_ids(np.arange(n), n))
+        # (equal distances: the restatement's heap order vs (dist, id), SURVEY 8c)
+        same_tie_aware(got[i][0], got[i][1], oi, od)
+        assert cnt[i] == len(oi)
+    ix.close()

@@ -96,6 +96,8 @@ SIGNATURES = {
     "wv_search_by_vector": (C.c_int, [_vp, _vp, C.c_int, _vp, C.c_uint64, _vp, _vp, _vp]),
     "wv_search_by_vector_distance": (C.c_int, [_vp, _vp, C.c_float, C.c_int64, _vp, C.c_uint64, _vp, _vp, C.c_int64,
                                                C.POINTER(C.c_int64)]),
+    "wv_search_by_vector_distance_batch": (C.c_int, [_vp, _vp, C.c_int, _vp, C.c_int64, _vp, C.c_uint64, C.c_uint64,
+                                                     _vp, _vp, C.c_int64, _vp]),
     "wv_search_batch": (C.c_int, [_vp, _vp, C.c_int, C.c_int, C.c_int, _vp, C.c_uint64, C.c_uint64, C.c_int, _vp, _vp,
                                   _vp]),
     "wv_search_batch_device": (C.c_int, [_vp, _vp, C.c_int, C.c_int, C.c_int, _vp, C.c_uint64, C.c_uint64, C.c_int,

@@ -50,6 +50,9 @@ int wv_hnsw_per_wave_words(int dpad, int efc, int sc, int vc_log2, int xs_log2);
 int wv_hnsw_side_per_wave_words(int dpad, int side_rows, int vc_log2, int xs_log2);
 int wv_hnsw_reg_per_wave_words(int dpad, int vc_log2);
 hipError_t wv_launch_hnsw_side(const wv::HnswParams* p, int waves_per_block, int ev, hipStream_t s);
+hipError_t wv_launch_sbd_scan(const wv::SbdParams* p, hipStream_t s);
+hipError_t wv_sbd_sort(unsigned long long* keys, unsigned long long* tmp, const unsigned int* cnt, int nq, int cap,
+                       int* offsets, void** scratch, size_t* scratch_cap, hipStream_t s);
 hipError_t wv_launch_pq_encode(const float* X, int ldx, const uint64_t* ids, uint64_t n_rows, const wv::PqParams* pq,
                                uint8_t* codes, hipStream_t s);
 hipError_t wv_launch_pq_scan(const wv::PqScanParams* p, hipStream_t s);
@@ -294,6 +297,10 @@ struct wv_index {
     // scratch
     DevBuf stage;           // contiguous host->device staging
     DevBuf q_in, q_norm, q_nrm2, q_scaled, cand_d, cand_id, fail, status, counters;
+    // SearchByVectorDistance batches (wv_sbd.hip): targets, lists, counts, sort scratch
+    DevBuf sbd_t, sbd_keys, sbd_tmp, sbd_cnt, sbd_off, sbd_q;
+    void* sbd_scr = nullptr;
+    size_t sbd_scr_cap = 0;
     DevBuf scan_d, scan_i, sort_d, sort_i, sort_tmp;
     DevBuf g_idx, g_q, g_allow, g_ids, g_d, g_n, g_cnt;
     DevBuf out_ids, out_d, out_n;
@@ -1794,6 +1801,9 @@ int wv_index_destroy(wv_index* ix) {
         b->release();
     if (ix->stream) (void)hipStreamSynchronize(ix->stream);
     ix->allow_keep.release();
+    for (DevBuf* b : {&ix->sbd_t, &ix->sbd_keys, &ix->sbd_tmp, &ix->sbd_cnt, &ix->sbd_off, &ix->sbd_q}) b->release();
+    if (ix->sbd_scr) (void)hipFree(ix->sbd_scr);
+    ix->sbd_scr = nullptr;
     ix->cimg16.release();
     ix->cxnorm.release();
     ix->cexcl.release();
@@ -2695,6 +2705,241 @@ int wv_index_synchronize(wv_index* ix) {
 int wv_search_by_vector(wv_index* ix, const float* vector, int k, const uint64_t* allow_bits, uint64_t allow_nbits,
                         uint64_t* out_ids, float* out_dists, int32_t* out_n) {
     return wv_search_batch(ix, vector, 1, k, 0, allow_bits, allow_nbits, 0, WV_MODE_AUTO, out_ids, out_dists, out_n);
+}
+
+// SearchByVectorDistance (search.go:90-158) for a batch of queries, on the
+// device: round 1 (limit 100) is the batch's SearchByVector where it would
+// run HNSW; every exact round -- round 1 of a flat search, and all rounds
+// past the first (limit 1100, 11100, ...: their ef exceeds the beam) -- is
+// answered by one threshold pass + segmented sort (wv_sbd.hip), launched
+// beside round 1 so the batch syncs once.  The rounds' arithmetic
+// (searchByDistParams, :552-619) then runs on the host over the counts.  A
+// query whose within-target set outgrows its list (WV_SBD_CAP, 16384) or a
+// compressed index takes the per-query path.
+namespace {
+// the search.go:90-158 loop over an exact sorted list (from round r0: 1 when
+// round 1 is exact too, 2 after an HNSW round 1): the end of the kept prefix
+int64_t sbd_exact_rounds(int r0, int64_t Qn, int64_t A, int64_t n, int64_t max_limit) {
+    int64_t prev = 0, total = 100, limit = 100, kept = r0 == 1 ? 0 : 100;
+    for (int r = 1;; ++r) {
+        if (r > 1) {
+            prev = total;
+            limit *= 10;
+            total = prev + limit;
+            if (max_limit >= 0 && total > max_limit) break;   // maxLimitReached
+        }
+        if (total > (int64_t)1 << 40) break;
+        if (r < r0) continue;
+        const int64_t lo = std::min(prev, n), hi = std::min(total, n);
+        if (hi - lo <= 0) break;
+        kept = std::max(lo, std::min(hi, Qn));   // (appending stops at the first entry past the target)
+        if (!(hi <= A)) break;                   // lastFound <= target
+    }
+    return kept;
+}
+}  // namespace
+
+int wv_search_by_vector_distance_batch(wv_index* ix, const float* queries, int nq, const float* targets,
+                                       int64_t max_limit, const uint64_t* allow_bits, uint64_t allow_nbits,
+                                       uint64_t allow_stride_words, uint64_t* out_ids, float* out_dists,
+                                       int64_t out_cap, int64_t* out_n) {
+    if (check(ix) || nq < 0 || out_cap < 0 || (nq && (!queries || !targets || !out_n)) ||
+        (out_cap && nq && (!out_ids || !out_dists)))
+        return fail(WV_EINVAL, "wv_search_by_vector_distance_batch: bad argument");
+    if (nq == 0) return WV_OK;
+    HIP_TRY(hipSetDevice(ix->cfg.device));
+    const uint64_t words = (allow_nbits + 63) / 64;
+    const uint64_t astride = allow_stride_words ? allow_stride_words : words;
+    auto allow_of = [&](int q) -> const uint64_t* {
+        return allow_bits ? allow_bits + (allow_stride_words ? (uint64_t)q * allow_stride_words : 0) : nullptr;
+    };
+    std::vector<int> legacy;   // queries for the per-query path
+    std::vector<int> hnsw_q;   // queries whose round 1 is an HNSW search
+    {
+        std::lock_guard<std::mutex> g(ix->mu);
+        if (ix->pq_on) {
+            for (int q = 0; q < nq; ++q) legacy.push_back(q);
+        } else {
+            const int ef = search_time_ef(ix->cfg, 100);
+            const bool can_hnsw = ix->has_graph && ef <= wv::HNSW_EF_MAX;
+            for (int q = 0; q < nq; ++q) {
+                bool flat = !can_hnsw;
+                if (!flat && allow_bits && !ix->cfg.forbid_flat) {
+                    // allowList.Len() < flatSearchCutoff (search.go:74-78)
+                    const uint64_t* a = allow_of(q);
+                    uint64_t c = 0;
+                    for (uint64_t w = 0; w < words; ++w) c += (uint64_t)__builtin_popcountll(a[w]);
+                    flat = (int64_t)c < ix->cfg.flat_search_cutoff;
+                }
+                if (!flat) hnsw_q.push_back(q);
+            }
+        }
+    }
+    if ((int)legacy.size() < nq) {
+        int cap = 16384;
+        if (const char* e = std::getenv("WV_SBD_CAP")) cap = std::max(128, std::atoi(e));
+        const int nh = (int)hnsw_q.size();
+        std::vector<float> hq((size_t)std::max(nh, 1) * ix->dim);
+        std::vector<uint64_t> hallow;
+        for (int i = 0; i < nh; ++i)
+            std::memcpy(hq.data() + (size_t)i * ix->dim, queries + (size_t)hnsw_q[i] * ix->dim, 4 * (size_t)ix->dim);
+        if (allow_bits && allow_stride_words && nh) {
+            hallow.resize((size_t)nh * astride);
+            for (int i = 0; i < nh; ++i)
+                std::memcpy(hallow.data() + (size_t)i * astride, allow_of(hnsw_q[i]), 8 * astride);
+        }
+        std::vector<uint64_t> r1_ids((size_t)std::max(nh, 1) * 100);
+        std::vector<float> r1_d((size_t)std::max(nh, 1) * 100);
+        std::vector<int32_t> r1_n(std::max(nh, 1));
+        std::vector<unsigned int> cnt(3 * (size_t)nq);
+        std::vector<std::vector<unsigned long long>> lists(nq);
+        {
+            std::lock_guard<std::mutex> g(ix->mu);
+            hipStream_t s = ix->stream;
+            int rc = refresh_bitmaps(ix);
+            if (rc) return rc;
+            const uint64_t* dallow = nullptr;
+            if (allow_bits) {
+                const size_t ab = (allow_stride_words ? (size_t)nq : 1) * astride * 8;
+                HIP_TRY(ix->allow_keep.ensure(ab));
+                HIP_TRY(hipMemcpyAsync(ix->allow_keep.p, allow_bits, ab, hipMemcpyHostToDevice, s));
+                dallow = ix->allow_keep.as<uint64_t>();
+            }
+            // every query's threshold pass (its queries staged first: round
+            // 1's search restages q_in)
+            const float* dq = nullptr;
+            rc = stage_queries(ix, queries, nq, &dq, s);
+            if (rc) return rc;
+            HIP_TRY(ix->sbd_q.ensure((size_t)nq * ix->dpad * 4));
+            HIP_TRY(hipMemcpyAsync(ix->sbd_q.p, dq, (size_t)nq * ix->dpad * 4, hipMemcpyDeviceToDevice, s));
+            HIP_TRY(ix->sbd_t.ensure((size_t)nq * 4));
+            HIP_TRY(hipMemcpyAsync(ix->sbd_t.p, targets, (size_t)nq * 4, hipMemcpyHostToDevice, s));
+            HIP_TRY(ix->sbd_keys.ensure((size_t)nq * cap * 8));
+            HIP_TRY(ix->sbd_tmp.ensure((size_t)nq * cap * 8));
+            HIP_TRY(ix->sbd_cnt.ensure((size_t)nq * 12));
+            HIP_TRY(ix->sbd_off.ensure((size_t)nq * 8));
+            HIP_TRY(hipMemsetAsync(ix->sbd_cnt.p, 0, (size_t)nq * 12, s));
+            wv::SbdParams sp{};
+            sp.X = ix->vecs.as<float>();
+            sp.Q = ix->sbd_q.as<float>();
+            sp.target = ix->sbd_t.as<float>();
+            sp.excl = ix->excl.as<uint64_t>();
+            sp.excl_nbits = ix->capacity;
+            sp.allow = dallow;
+            sp.allow_nbits = allow_nbits;
+            sp.allow_stride = allow_stride_words;
+            sp.N = ix->n_rows;
+            sp.D = ix->dim;
+            sp.ldx = ix->ldx;
+            sp.dpad = ix->dpad;
+            sp.metric = ix->metric;
+            sp.nq = nq;
+            // ~4 blocks per CU over the batch, whole 4-wave steps of 256 rows
+            const uint64_t target_blocks = std::max<uint64_t>(1, (uint64_t)ix->n_cus * 4 / (uint64_t)nq);
+            sp.rows_per_block = std::max<uint64_t>(4096, (sp.N + target_blocks - 1) / target_blocks);
+            sp.rows_per_block = (sp.rows_per_block + 255) / 256 * 256;
+            while ((sp.N + sp.rows_per_block - 1) / sp.rows_per_block > 65535) sp.rows_per_block *= 2;
+            sp.cap = cap;
+            sp.keys = ix->sbd_keys.as<unsigned long long>();
+            sp.cnt = ix->sbd_cnt.as<unsigned int>();
+            HIP_TRY(wv_launch_sbd_scan(&sp, s));
+            HIP_TRY(wv_sbd_sort(ix->sbd_keys.as<unsigned long long>(), ix->sbd_tmp.as<unsigned long long>(),
+                                ix->sbd_cnt.as<unsigned int>(), nq, cap, ix->sbd_off.as<int>(), &ix->sbd_scr,
+                                &ix->sbd_scr_cap, s));
+            // round 1 of the HNSW queries: their SearchByVector(limit 100)
+            if (nh) {
+                rc = stage_queries(ix, hq.data(), nh, &dq, s);
+                if (rc) return rc;
+                const uint64_t* dal = dallow;
+                if (allow_bits && allow_stride_words) {
+                    HIP_TRY(ix->g_allow.ensure(hallow.size() * 8));
+                    HIP_TRY(hipMemcpyAsync(ix->g_allow.p, hallow.data(), hallow.size() * 8, hipMemcpyHostToDevice, s));
+                    dal = ix->g_allow.as<uint64_t>();
+                }
+                HIP_TRY(ix->out_ids.ensure((size_t)nh * 100 * 8));
+                HIP_TRY(ix->out_d.ensure((size_t)nh * 100 * 4));
+                HIP_TRY(ix->out_n.ensure((size_t)nh * 4));
+                rc = search_core(ix, dq, nh, 100, 0, dal, allow_nbits, allow_stride_words, WV_MODE_AUTO,
+                                 ix->out_ids.as<uint64_t>(), ix->out_d.as<float>(), ix->out_n.as<int32_t>(), s);
+                if (rc) return rc;
+                HIP_TRY(hipMemcpyAsync(r1_ids.data(), ix->out_ids.p, (size_t)nh * 100 * 8, hipMemcpyDeviceToHost, s));
+                HIP_TRY(hipMemcpyAsync(r1_d.data(), ix->out_d.p, (size_t)nh * 100 * 4, hipMemcpyDeviceToHost, s));
+                HIP_TRY(hipMemcpyAsync(r1_n.data(), ix->out_n.p, (size_t)nh * 4, hipMemcpyDeviceToHost, s));
+            }
+            HIP_TRY(hipMemcpyAsync(cnt.data(), ix->sbd_cnt.p, (size_t)nq * 12, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipStreamSynchronize(s));
+            // the sorted lists, as far as the rounds keep them (and the caller
+            // takes them)
+            std::vector<int64_t> need(nq, 0);
+            std::vector<char> is_h(nq, 0);
+            for (int q : hnsw_q) is_h[q] = 1;
+            std::vector<int> hs(nq, -1);
+            for (int i = 0; i < nh; ++i) hs[hnsw_q[i]] = i;
+            for (int q = 0; q < nq; ++q) {
+                const int64_t Qn = cnt[3 * q], A = cnt[3 * q + 1], n = cnt[3 * q + 2];
+                if (is_h[q]) {   // (an HNSW round 1 that ends the deepening needs no list)
+                    const int i = hs[q];
+                    const int64_t hi = std::min<int64_t>(100, r1_n[i]);
+                    if (!(hi > 0 && r1_d[(size_t)i * 100 + hi - 1] <= targets[q] && (max_limit < 0 || 1100 <= max_limit)))
+                        continue;
+                }
+                const int64_t kept = sbd_exact_rounds(is_h[q] ? 2 : 1, Qn, A, n, max_limit);
+                need[q] = std::min<int64_t>(kept, Qn);
+                if (Qn > cap && need[q] > 0) { legacy.push_back(q); need[q] = 0; continue; }
+                if (need[q] > 0) {
+                    lists[q].resize(need[q]);
+                    HIP_TRY(hipMemcpyAsync(lists[q].data(), ix->sbd_tmp.as<unsigned long long>() + (size_t)q * cap,
+                                           8 * need[q], hipMemcpyDeviceToHost, s));
+                }
+            }
+            HIP_TRY(hipStreamSynchronize(s));
+        }
+        std::vector<int> hslot(nq, -1);
+        for (int i = 0; i < nh; ++i) hslot[hnsw_q[i]] = i;
+        const uint64_t id_base = ix->cfg.id_base;
+        for (int q = 0; q < nq; ++q) {
+            if (std::find(legacy.begin(), legacy.end(), q) != legacy.end()) continue;
+            const float t = targets[q];
+            int64_t m = 0;
+            auto put = [&](uint64_t id, float d) {
+                if (m < out_cap) { out_ids[(size_t)q * out_cap + m] = id; out_dists[(size_t)q * out_cap + m] = d; }
+                m++;
+            };
+            auto qual = [&](float d) { return d <= t || std::fabs((double)d - (double)t) <= 1e-6; };
+            bool exact_more = true;
+            if (hslot[q] >= 0) {
+                // round 1 from the HNSW search: its qualifying prefix, and
+                // whether the deepening continues
+                const int i = hslot[q];
+                const int64_t hi = std::min<int64_t>(100, r1_n[i]);
+                for (int64_t j = 0; j < hi; ++j) {
+                    const float d = r1_d[(size_t)i * 100 + j];
+                    if (!qual(d)) break;
+                    put(r1_ids[(size_t)i * 100 + j], d);
+                }
+                exact_more = hi > 0 && r1_d[(size_t)i * 100 + hi - 1] <= t && (max_limit < 0 || 1100 <= max_limit);
+            }
+            if (exact_more) {
+                const int64_t from = hslot[q] >= 0 ? 100 : 0;
+                for (int64_t j = from; j < (int64_t)lists[q].size(); ++j) {
+                    const unsigned long long key = lists[q][j];
+                    uint32_t u = (uint32_t)(key >> 32);
+                    u = (u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u;
+                    float d;
+                    std::memcpy(&d, &u, 4);
+                    put(id_base + (uint32_t)key, d);
+                }
+            }
+            out_n[q] = m;
+        }
+    }
+    for (int q : legacy) {
+        int rc = wv_search_by_vector_distance(ix, queries + (size_t)q * ix->dim, targets[q], max_limit, allow_of(q),
+                                              allow_nbits, out_cap ? out_ids + (size_t)q * out_cap : nullptr,
+                                              out_cap ? out_dists + (size_t)q * out_cap : nullptr, out_cap, out_n + q);
+        if (rc) return rc;
+    }
+    return WV_OK;
 }
 
 int wv_search_by_vector_distance(wv_index* ix, const float* vector, float target, int64_t max_limit,

@@ -73,6 +73,12 @@ struct Request {
     uint64_t* out_ids;
     float* out_d;
     int32_t* out_n;
+    // SearchByVectorDistance (search.go:90-158): a target, maxLimit and an
+    // output of out_cap entries with a 64-bit count (dist: set)
+    bool dist = false;
+    float target = 0.f;
+    int64_t max_limit = -1, out_cap = 0;
+    int64_t* out_n64 = nullptr;
     int rc = WV_OK;
     std::string err;
     wait_clock::time_point arrived;
@@ -112,9 +118,11 @@ struct Staging {
     uint64_t seq = 0;   // the batch being run
     std::vector<Request*> take, g;
     std::vector<char> used;
-    std::vector<float> q, ds;
+    std::vector<float> q, ds, tg;
     std::vector<uint64_t> bits, ids;
     std::vector<int32_t> cnt;
+    std::vector<int64_t> cnt64;
+    int64_t cap = 0;    // (distance groups) entries per query in ids / ds
 };
 
 }  // namespace
@@ -183,10 +191,28 @@ struct wv_batcher {
             s.bits.assign((size_t)(shared ? 1 : n) * words, 0);
             for (int i = 0; i < (shared ? 1 : n); ++i) write_row(s.g[i], s.bits.data() + (size_t)i * words);
         }
+        const uint64_t* bits = filtered ? s.bits.data() : nullptr;
+        if (s.g[0]->dist) {
+            // one batched SearchByVectorDistance (same maxLimit in a group)
+            s.cap = 0;
+            s.tg.resize(n);
+            for (int i = 0; i < n; ++i) {
+                s.cap = std::max(s.cap, s.g[i]->out_cap);
+                s.tg[i] = s.g[i]->target;
+            }
+            s.ids.resize((size_t)n * std::max<int64_t>(s.cap, 1));
+            s.ds.resize((size_t)n * std::max<int64_t>(s.cap, 1));
+            s.cnt64.resize(n);
+            if (grp)
+                return wv_group_search_by_vector_distance_batch(grp, s.q.data(), n, s.tg.data(), s.g[0]->max_limit,
+                                                                bits, nbits, stride, s.ids.data(), s.ds.data(), s.cap,
+                                                                s.cnt64.data());
+            return wv_search_by_vector_distance_batch(ix, s.q.data(), n, s.tg.data(), s.g[0]->max_limit, bits, nbits,
+                                                      stride, s.ids.data(), s.ds.data(), s.cap, s.cnt64.data());
+        }
         s.ids.resize((size_t)n * k);
         s.ds.resize((size_t)n * k);
         s.cnt.resize(n);
-        const uint64_t* bits = filtered ? s.bits.data() : nullptr;
         return grp ? wv_group_search_batch(grp, s.q.data(), n, k, 0, bits, nbits, stride, WV_MODE_AUTO, s.ids.data(),
                                            s.ds.data(), s.cnt.data())
                    : wv_search_batch(ix, s.q.data(), n, k, 0, bits, nbits, stride, WV_MODE_AUTO, s.ids.data(),
@@ -203,6 +229,13 @@ struct wv_batcher {
             r->batch = s.seq;
             if (rc) {
                 r->err = msg;
+            } else if (r->dist) {
+                const int64_t m = std::min(s.cnt64[i], r->out_cap);
+                if (m > 0) {
+                    std::memcpy(r->out_ids, s.ids.data() + i * s.cap, sizeof(uint64_t) * m);
+                    std::memcpy(r->out_d, s.ds.data() + i * s.cap, sizeof(float) * m);
+                }
+                *r->out_n64 = s.cnt64[i];
             } else {
                 const int m = s.cnt[i];
                 std::memcpy(r->out_ids, s.ids.data() + i * k, sizeof(uint64_t) * m);
@@ -253,14 +286,18 @@ struct wv_batcher {
                 queue.pop_front();
             }
             l.unlock();
-            // group by (k, filtered), keeping arrival order inside a group
+            // group by (k, filtered) -- distance searches by (maxLimit,
+            // filtered) -- keeping arrival order inside a group
             s.used.assign(s.take.size(), 0);
             size_t left = s.take.size();
             for (size_t i = 0; i < s.take.size(); ++i) {
                 if (s.used[i]) continue;
                 s.g.clear();
                 for (size_t j = i; j < s.take.size(); ++j) {
-                    if (s.used[j] || s.take[j]->k != s.take[i]->k || s.take[j]->filtered != s.take[i]->filtered)
+                    const Request* a = s.take[i];
+                    const Request* c = s.take[j];
+                    if (s.used[j] || c->k != a->k || c->filtered != a->filtered || c->dist != a->dist ||
+                        (a->dist && c->max_limit != a->max_limit))
                         continue;
                     s.used[j] = 1;
                     s.g.push_back(s.take[j]);
@@ -388,6 +425,37 @@ int wv_batcher_search_ids(wv_batcher* b, const float* vector, int k, int filtere
     r.out_ids = out_ids;
     r.out_d = out_dists;
     r.out_n = out_n;
+    return submit(b, r);
+}
+
+int wv_batcher_search_distance_ids(wv_batcher* b, const float* vector, float target_distance, int64_t max_limit,
+                                   int filtered, const uint64_t* allow_ids, uint64_t n_allow, uint64_t* out_ids,
+                                   float* out_dists, int64_t out_cap, int64_t* out_n) {
+    if (!b || !vector || !out_n || out_cap < 0 || (out_cap && (!out_ids || !out_dists)) || (n_allow && !allow_ids)) {
+        wv_internal_set_error("wv_batcher_search_distance_ids: bad argument");
+        return WV_EINVAL;
+    }
+    for (uint64_t i = 1; i < n_allow; ++i)
+        if (allow_ids[i] <= allow_ids[i - 1]) {
+            wv_internal_set_error("wv_batcher_search_distance_ids: allow ids must be strictly ascending");
+            return WV_EINVAL;
+        }
+    Request r;
+    r.q = vector;
+    r.k = 0;
+    r.allow = nullptr;
+    r.allow_nbits = 0;
+    r.allow_ids = allow_ids;
+    r.n_ids = filtered ? n_allow : 0;
+    r.filtered = filtered != 0;
+    r.out_ids = out_ids;
+    r.out_d = out_dists;
+    r.out_n = nullptr;
+    r.dist = true;
+    r.target = target_distance;
+    r.max_limit = max_limit;
+    r.out_cap = out_cap;
+    r.out_n64 = out_n;
     return submit(b, r);
 }
 

@@ -541,6 +541,75 @@ int wv_group_update_config(wv_group* g, const wv_config* cfg) {
     return WV_OK;
 }
 
+// SearchByVectorDistance over the group (index.go:967-1044 with a distance:
+// every shard answers within the target, the union sorted by distance): a
+// replica group asks one member; a shard group asks each member its batch
+// over its id range (the allow lists sliced as in search_shards) and merges
+// each query's lists by (distance, id).
+int wv_group_search_by_vector_distance_batch(wv_group* g, const float* queries, int nq, const float* targets,
+                                             int64_t max_limit, const uint64_t* allow_bits, uint64_t allow_nbits,
+                                             uint64_t allow_stride, uint64_t* out_ids, float* out_dists,
+                                             int64_t out_cap, int64_t* out_n) {
+    if (!g || nq < 0 || out_cap < 0 || (nq && (!queries || !targets || !out_n)) ||
+        (out_cap && nq && (!out_ids || !out_dists)))
+        return gfail(WV_EINVAL, "wv_group_search_by_vector_distance_batch: bad argument");
+    if (nq == 0) return WV_OK;
+    std::lock_guard<std::mutex> l(g->mu);
+    if (g->layout == WV_GROUP_REPLICA || g->m.size() == 1)
+        return wv_search_by_vector_distance_batch(g->m[0].ix, queries, nq, targets, max_limit, allow_bits, allow_nbits,
+                                                  allow_stride, out_ids, out_dists, out_cap, out_n);
+    // each member's lists in full (a shard's entries past the merged cut are
+    // dropped only after the merge)
+    const int n = (int)g->m.size();
+    std::vector<std::vector<uint64_t>> mids(n);
+    std::vector<std::vector<float>> mds(n);
+    std::vector<std::vector<int64_t>> mcnt(n, std::vector<int64_t>(nq));
+    std::vector<int64_t> mcap(n);
+    for (int i = 0; i < n; ++i) {
+        Member& mb = g->m[i];
+        std::vector<uint64_t> slice;
+        uint64_t nbits = 0, stride = 0;
+        if (allow_bits) {
+            nbits = allow_nbits > mb.base ? std::min(allow_nbits - mb.base, mb.cap) : 0;
+            const uint64_t w = (nbits + 63) / 64, w0 = mb.base / 64;
+            const uint64_t gw = allow_stride ? allow_stride : (allow_nbits + 63) / 64;
+            const int rows_a = allow_stride ? nq : 1;
+            const uint64_t ws = std::max<uint64_t>(w, 1);
+            stride = allow_stride ? ws : 0;
+            slice.assign((size_t)rows_a * ws, 0);
+            for (int r = 0; r < rows_a; ++r)
+                for (uint64_t j = 0; j < ws; ++j)
+                    slice[(size_t)r * ws + j] = j < w && w0 + j < gw ? allow_bits[(size_t)r * gw + w0 + j] : 0;
+        }
+        int64_t cap = std::max<int64_t>(out_cap, 1);
+        for (int pass = 0; pass < 2; ++pass) {   // (once more with room for every result)
+            mids[i].assign((size_t)nq * cap, 0);
+            mds[i].assign((size_t)nq * cap, 0.f);
+            const int rc = wv_search_by_vector_distance_batch(mb.ix, queries, nq, targets, max_limit,
+                                                              allow_bits ? slice.data() : nullptr, nbits, stride,
+                                                              mids[i].data(), mds[i].data(), cap, mcnt[i].data());
+            if (rc) return rc;
+            const int64_t mx = *std::max_element(mcnt[i].begin(), mcnt[i].end());
+            if (mx <= cap) break;
+            cap = mx;
+        }
+        mcap[i] = cap;
+    }
+    for (int q = 0; q < nq; ++q) {
+        std::vector<std::pair<float, uint64_t>> u;
+        for (int i = 0; i < n; ++i)
+            for (int64_t j = 0; j < mcnt[i][q]; ++j)
+                u.emplace_back(mds[i][(size_t)q * mcap[i] + j], mids[i][(size_t)q * mcap[i] + j]);
+        std::sort(u.begin(), u.end());
+        out_n[q] = (int64_t)u.size();
+        for (int64_t j = 0; j < std::min<int64_t>(out_cap, (int64_t)u.size()); ++j) {
+            out_ids[(size_t)q * out_cap + j] = u[j].second;
+            out_dists[(size_t)q * out_cap + j] = u[j].first;
+        }
+    }
+    return WV_OK;
+}
+
 int wv_group_search_batch(wv_group* g, const float* queries, int nq, int k, int ef, const uint64_t* allow_bits,
                           uint64_t allow_nbits, uint64_t allow_stride_words, int mode, uint64_t* out_ids,
                           float* out_dists, int32_t* out_n) {

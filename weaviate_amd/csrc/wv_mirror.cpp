@@ -769,11 +769,12 @@ int wv_mirror_search_by_distance(wv_mirror* m, const float* vector, int len, flo
     if (!m->ix) { *out_n = 0; return WV_OK; }
     if (len != m->dim) return err(WV_ESTALE, "wv_mirror_search_by_distance: vector length differs from the index's");
     if (int rc = m->check_entrypoint(filtered, n_allow)) return rc;   // (each deepening round is a SearchByVector)
-    std::vector<uint64_t> bits;
-    uint64_t nbits = 0;
-    if (filtered) allow_bitmap(allow_ids, n_allow, m->capacity, bits, nbits);
-    return wv_search_by_vector_distance(m->ix, vector, target_distance, max_limit, filtered ? bits.data() : nullptr,
-                                        nbits, out_ids, out_dists, out_cap, out_n);
+    // through the micro-batcher: concurrent distance searches coalesce into
+    // one batched SearchByVectorDistance (ids past the capacity hold no row)
+    const uint64_t cap = m->capacity;
+    while (n_allow && allow_ids[n_allow - 1] >= cap) --n_allow;
+    return wv_batcher_search_distance_ids(m->b, vector, target_distance, max_limit, filtered, allow_ids, n_allow,
+                                          out_ids, out_dists, out_cap, out_n);
 }
 
 int wv_mirror_update_config(wv_mirror* m, const wv_config* cfg) {

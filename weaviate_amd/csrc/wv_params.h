@@ -393,6 +393,22 @@ struct HnswParams {
     unsigned long long* side_acc;
 };
 
+// SearchByVectorDistance's threshold pass (wv_sbd.hip): per query, the
+// allowed rows within the target distance, with their sort keys and counts
+struct SbdParams {
+    const float* X;
+    const float* Q;           // [nq][dpad] (normalized if cosine)
+    const float* target;      // [nq]
+    const uint64_t* excl;     // tombstones, nil nodes, missing rows
+    const uint64_t* allow;    // nullable; [nq][allow_stride] or shared
+    uint64_t excl_nbits, allow_nbits, allow_stride, N;
+    int D, ldx, dpad, metric, nq;
+    uint64_t rows_per_block;
+    int cap;                  // list entries per query
+    unsigned long long* keys; // [nq][cap]: (orderable d) << 32 | row
+    unsigned int* cnt;        // [nq][3]: |Q|, A (d <= target), n (rows searchable)
+};
+
 // Flat search over PQ codes (flat_search.go:19-74 on a compressed index):
 // distances of a chunk of queries against a row list, keyed for a stable
 // segmented sort by (dist, row).

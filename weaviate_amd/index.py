@@ -310,6 +310,22 @@ class GPUVectorIndex:
         m = min(n.value, cap)
         return ids[:m], ds[:m]
 
+    def search_by_vector_distance_batch(self, queries, targets, max_limit: int = -1, allow=None,
+                                        cap: int = 4096):
+        """SearchByVectorDistance for a batch (each query its own target): a
+        list of (ids, dists) per query; at most `cap` results are returned
+        per query (`n` counts them all)."""
+        qs = np.ascontiguousarray(queries, dtype=np.float32).reshape(-1, self.dim)
+        nq = qs.shape[0]
+        ts = np.ascontiguousarray(np.broadcast_to(np.asarray(targets, np.float32), (nq,)))
+        bits, nb, stride = self._allow_args(allow)
+        ids = np.zeros((nq, cap), np.uint64)
+        ds = np.zeros((nq, cap), np.float32)
+        n = np.zeros(nq, np.int64)
+        check(lib().wv_search_by_vector_distance_batch(self._h, _ptr(qs), nq, _ptr(ts), max_limit, _ptr(bits), nb,
+                                                       stride, _ptr(ids), _ptr(ds), cap, _ptr(n)))
+        return [(ids[i, :min(n[i], cap)], ds[i, :min(n[i], cap)]) for i in range(nq)], n
+
     def search_batch(self, queries, k: int, ef: int = 0, allow=None, mode: str = "auto"):
         """Batched search: (ids [nq,k] uint64, dists [nq,k] f32, n [nq] i32)."""
         qs = np.ascontiguousarray(queries, dtype=np.float32).reshape(-1, self.dim)
