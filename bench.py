@@ -1156,6 +1156,12 @@ def tombstoned_leg(args, ctx, ix, ref, queries, qt, NQ, K, D, n_local, res):
     achieved = by / (km * 1e-3) / 1e9
     free = res.get("value")
     val = NQ * args.steps / el
+    roof = {"bound": "hbm", "kernel": "wv_hnsw_side_kernel", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel_ms": round(km, 3),
+            "counts_from": "CPU restatement (oracle/) with the same tombstones",
+            "dist_evals_per_query": round(e / NQ, 1), "expansions_per_query": round(x / NQ, 1),
+            "gpu_dist_evals_per_query": round(st["dist_evals"] / NQ, 1)}
+    attach_traffic(roof, n_local, NQ, D, args.hnsw_data, allow_frac="tomb:%g" % args.tomb_frac)
     return {"value": round(val, 1), "unit": "queries/s", "ms_per_step": round(1000 * el / args.steps, 3),
             "tombstoned_ids": int(len(dead)), "tomb_frac": args.tomb_frac,
             "vs_tombstone_free_value": round(val / free, 4) if free else None,
@@ -1165,11 +1171,7 @@ def tombstoned_leg(args, ctx, ix, ref, queries, qt, NQ, K, D, n_local, res):
             "parity_sample": {"queries": NQ, "id_match_frac": id_eq, "dists_bitwise_equal_frac": d_eq,
                               "tie_aware_identical_frac": tie_ok},
             "lone_caller_through_batcher": lone,
-            "roofline": {"bound": "hbm", "kernel": "wv_hnsw_side_kernel", "achieved": round(achieved, 1),
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "kernel_ms": round(km, 3), "counts_from": "CPU restatement (oracle/) with the same tombstones",
-                         "dist_evals_per_query": round(e / NQ, 1), "expansions_per_query": round(x / NQ, 1),
-                         "gpu_dist_evals_per_query": round(st["dist_evals"] / NQ, 1)}}
+            "roofline": roof}
 
 
 def concurrent_callers(args, ix, queries):
