@@ -244,11 +244,13 @@ int wv_last_batch_stats(wv_index *ix, uint64_t *dist_evals, uint64_t *expansions
 /* The last batch's filtered-HNSW state (nullable outputs): the queries whose
  * side candidates outgrew the per-query spill (answered by the exact
  * fallback), the queries a light-filter first pass (lossy visited cache)
- * handed to the exact-visited pass, and the side-register launch's LDS side
+ * handed to the exact-visited pass, the visited-bitmap claims (atomics: the
+ * LDS visited cache's misses at layer 0), and the side-register launch's LDS side
  * array (rows of 64 entries) and spill capacity (entries per query; 0 when no
  * filtered HNSW search ran).  Waits for the batch to finish.  A measurement
  * hook (no reference counterpart). */
-int wv_last_side_stats(wv_index *ix, uint64_t *overflowed, uint64_t *redone, int *side_rows, int *spill_cap);
+int wv_last_side_stats(wv_index *ix, uint64_t *overflowed, uint64_t *redone, uint64_t *claims, int *side_rows,
+                       int *spill_cap);
 
 /* Kernel timing with HIP events on the launch stream (off by default).  When
  * enabled, every batch records the device time of its dominant kernels: the

@@ -86,5 +86,6 @@ for frac in fracs:
                     os.environ[k] = v
         print(f"allow {frac:.0%} [{s}] nq {nq}: hnsw {np.median(kms):.2f} ms ({nq / np.median(kms) * 1e3:,.0f} QPS), "
               f"gpu evals/q {st['dist_evals'] / nq:.0f}, exp/q {st['expansions'] / nq:.0f}, side {ss['side_rows']}x64 "
-              f"spill {ss['spill_cap']}, overflowed {ss['overflowed']}, redone {ss['redone']}, fallbacks {st['fallbacks']}", flush=True)
+              f"spill {ss['spill_cap']}, overflowed {ss['overflowed']}, redone {ss['redone']}, claims/q {ss['claims'] / nq:.0f}, "
+              f"fallbacks {st['fallbacks']}", flush=True)
 ix.close()

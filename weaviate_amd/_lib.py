@@ -106,7 +106,7 @@ SIGNATURES = {
     "wv_index_synchronize": (C.c_int, [_vp]),
     "wv_merge_shards_device": (C.c_int, [_vp, _vp, _vp, C.c_int, C.c_int, C.c_int, _vp, _vp, _vp, _vp]),
     "wv_last_batch_stats": (C.c_int, [_vp, _u64p, _u64p, _u64p]),
-    "wv_last_side_stats": (C.c_int, [_vp, _u64p, _u64p, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "wv_last_side_stats": (C.c_int, [_vp, _u64p, _u64p, _u64p, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "wv_index_set_timing": (C.c_int, [_vp, C.c_int]),
     "wv_last_kernel_times": (C.c_int, [_vp, _f32p, _f32p, _f32p]),
     "wv_last_seed_time": (C.c_int, [_vp, _f32p]),

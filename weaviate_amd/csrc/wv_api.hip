@@ -1441,6 +1441,7 @@ int run_hnsw(wv_index* ix, const float* d_q, int nq, int k, int ef, const uint64
         hs.wg_helpers = nq <= wg_max ? 3 : 0;
         HIP_TRY(ix->stat_acc.ensure(48));
         hs.side_acc = ix->stat_acc.as<unsigned long long>();
+        hs.ev_spec = std::getenv("WV_HNSW_EV_SPEC") ? 1 : 0;
         const int passes = ev_first ? 1 : 2;
         for (int pass = 0; pass < passes; ++pass) {
             for (int c0 = 0; c0 < nq; c0 += chunk) {
@@ -3062,17 +3063,19 @@ int wv_last_batch_stats(wv_index* ix, uint64_t* dist_evals, uint64_t* expansions
     return WV_OK;
 }
 
-int wv_last_side_stats(wv_index* ix, uint64_t* overflowed, uint64_t* redone, int* side_rows, int* spill_cap) {
+int wv_last_side_stats(wv_index* ix, uint64_t* overflowed, uint64_t* redone, uint64_t* claims, int* side_rows,
+                       int* spill_cap) {
     if (check(ix)) return WV_EINVAL;
     std::lock_guard<std::mutex> g(ix->mu);
     HIP_TRY(hipSetDevice(ix->cfg.device));
-    unsigned long long acc[5] = {0, 0, 0, 0, 0};
+    unsigned long long acc[6] = {0, 0, 0, 0, 0, 0};
     if (ix->stat_acc.p) {
-        HIP_TRY(hipMemcpyAsync(acc, ix->stat_acc.p, 40, hipMemcpyDeviceToHost, ix->stat_stream));
+        HIP_TRY(hipMemcpyAsync(acc, ix->stat_acc.p, 48, hipMemcpyDeviceToHost, ix->stat_stream));
         HIP_TRY(hipStreamSynchronize(ix->stat_stream));
     }
     if (overflowed) *overflowed = acc[3];
     if (redone) *redone = acc[4];
+    if (claims) *claims = acc[5];
     if (side_rows) *side_rows = ix->last_side_rows;
     if (spill_cap) *spill_cap = ix->last_side_xs;
     return WV_OK;

@@ -897,7 +897,7 @@ template <int METRIC, int NR, int RPG, bool EV>
 __device__ __forceinline__ void search_layer_side(const HnswParams& p, WaveState& w, int level, int ef, uint32_t ep,
                                                   float epd, const uint64_t* allow, int nlt, uint32_t* vb,
                                                   uint32_t* sp, float (&rd)[NR], uint32_t (&ri)[NR], int& Rl,
-                                                  int& status, uint32_t& n_dist, uint32_t& n_exp) {
+                                                  int& status, uint32_t& n_dist, uint32_t& n_exp, uint32_t& n_miss) {
     static_assert(NR == 1 || NR == 2, "64 or 128 results per wave");
     const int lane = threadIdx.x & 63;
     const int VC = 1 << p.vc_log2;
@@ -1222,17 +1222,27 @@ __device__ __forceinline__ void search_layer_side(const HnswParams& p, WaveState
                 if (v0 && id0 < p.allow_nbits) glds4(reinterpret_cast<const uint32_t*>(allow) + (id0 >> 5), eb + 512);
                 if (v1 && id1 < p.allow_nbits) glds4(reinterpret_cast<const uint32_t*>(allow) + (id1 >> 5), eb + 768);
             }
+            // (EV spec, an A/B switch: the rows of every cache miss are
+            // loaded beside the claims, the ones already visited dropped
+            // after -- one round trip less, more rows)
+            const bool spec = EV && p.ev_spec;
+            bool f0 = true, f1 = true;
             if (EV) {
                 // the cache's misses claim their bit: a node another expansion
                 // evaluated (the cache forgot it) is skipped, as the exact
                 // visited list skips it
+                n_miss += (uint32_t)(__popcll(__ballot(v0)) + __popcll(__ballot(v1)));
                 if (v0) {
                     const uint32_t b = 1u << (id0 & 31);
-                    v0 = !(atomicOr(vb + (id0 >> 5), b) & b);
+                    f0 = !(atomicOr(vb + (id0 >> 5), b) & b);
                 }
                 if (v1) {
                     const uint32_t b = 1u << (id1 & 31);
-                    v1 = !(atomicOr(vb + (id1 >> 5), b) & b);
+                    f1 = !(atomicOr(vb + (id1 >> 5), b) & b);
+                }
+                if (!spec) {
+                    v0 = v0 && f0;
+                    v1 = v1 && f1;
                 }
             }
             const uint64_t m0 = __ballot(v0), m1 = __ballot(v1);
@@ -1251,6 +1261,13 @@ __device__ __forceinline__ void search_layer_side(const HnswParams& p, WaveState
             }
             n_dist += (uint32_t)nb;
             wave_sync();
+            float bd_spec[2] = {FLT_MAX, FLT_MAX};
+            if (spec) {   // (distances by batch slot, then only the claimed ones go on)
+                bd_spec[0] = v0 ? w.Bd[mbcnt64(m0)] : FLT_MAX;
+                bd_spec[1] = v1 ? w.Bd[n0 + mbcnt64(m1)] : FLT_MAX;
+                v0 = v0 && f0;
+                v1 = v1 && f1;
+            }
             // ---- keep test against the batch's starting state (search.go:282),
             // on the neighbours' own lanes (batch order = lane order, id0s
             // first): eligible keys into R one by one, ineligible ones to S ----
@@ -1266,8 +1283,8 @@ __device__ __forceinline__ void search_layer_side(const HnswParams& p, WaveState
             float bd[2];
             uint32_t bi[2];
             uint64_t kmask[2], smask[2];
-            bd[0] = v0 ? w.Bd[mbcnt64(m0)] : FLT_MAX;
-            bd[1] = v1 ? w.Bd[n0 + mbcnt64(m1)] : FLT_MAX;
+            bd[0] = spec ? bd_spec[0] : v0 ? w.Bd[mbcnt64(m0)] : FLT_MAX;
+            bd[1] = spec ? bd_spec[1] : v1 ? w.Bd[n0 + mbcnt64(m1)] : FLT_MAX;
             bi[0] = id0;
             bi[1] = id1;
 #pragma unroll
@@ -1448,7 +1465,7 @@ __device__ __forceinline__ int knn_one_side(const HnswParams& p, WaveState& w, i
     }
     uint32_t* sp = p.spill + 2 * (uint64_t)q * p.spill_cap;
     int status = 0, nlt = 0;
-    uint32_t n_dist = 0, n_exp = 0;
+    uint32_t n_dist = 0, n_exp = 0, n_miss = 0;
     uint32_t ep = p.entrypoint;
     float epd = __shfl(exact_dist_group8<METRIC>(w.qv, p.X + (uint64_t)ep * p.ldx, p.D, g), 0, 64);
     n_dist++;
@@ -1459,7 +1476,7 @@ __device__ __forceinline__ int knn_one_side(const HnswParams& p, WaveState& w, i
     // result is tombstoned for the rest of the search (:496-507)
     for (int level = p.max_level; level >= 1 && !status; --level) {
         search_layer_side<METRIC, NR, RPG, false>(p, w, level, 1, ep, epd, nullptr, nlt, vb, sp, rd, ri, Rl, status,
-                                                  n_dist, n_exp);
+                                                  n_dist, n_exp, n_miss);
         if (Rl > 0) {
             const uint32_t cid = (uint32_t)__builtin_amdgcn_readlane(ri[0], 0) & WV_IDMASK;
             if (p.levels[cid] < 0) {
@@ -1476,7 +1493,7 @@ __device__ __forceinline__ int knn_one_side(const HnswParams& p, WaveState& w, i
     }
     if (!status)
         search_layer_side<METRIC, NR, RPG, EV0>(p, w, 0, p.ef, ep, epd, allow, nlt, vb, sp, rd, ri, Rl, status, n_dist,
-                                                n_exp);
+                                                n_exp, n_miss);
     const int n = status ? 0 : min(Rl, p.k);
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
@@ -1491,6 +1508,7 @@ __device__ __forceinline__ int knn_one_side(const HnswParams& p, WaveState& w, i
         p.status[q] = status;
         if (p.counters) { p.counters[2 * q] = n_dist; p.counters[2 * q + 1] = n_exp; }
         if (status && p.side_acc) atomicAdd(p.side_acc + (EV0 ? 3 : 4), 1ull);
+        if (EV0 && p.side_acc) atomicAdd(p.side_acc + 5, (unsigned long long)n_miss);   // (cache misses claimed)
     }
     return status;
 }

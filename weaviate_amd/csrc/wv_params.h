@@ -391,6 +391,7 @@ struct HnswParams {
     // exact-visited search (the exact fallback answers them), [4] += queries
     // a lossy first pass handed to the exact-visited search
     unsigned long long* side_acc;
+    int ev_spec;   // (A/B, WV_HNSW_EV_SPEC) exact-visited rows loaded beside the claims
 };
 
 // SearchByVectorDistance's threshold pass (wv_sbd.hip): per query, the

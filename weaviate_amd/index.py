@@ -371,9 +371,10 @@ class GPUVectorIndex:
         """filtered HNSW: queries whose side set outgrew its HBM spill (exact
         fallback), queries the light-filter pass re-ran with the exact visited
         bitmap, the LDS side array's rows of 64 and the spill capacity"""
-        a, r, b, c = C.c_uint64(), C.c_uint64(), C.c_int(), C.c_int()
-        check(lib().wv_last_side_stats(self._h, C.byref(a), C.byref(r), C.byref(b), C.byref(c)))
-        return {"overflowed": a.value, "redone": r.value, "side_rows": b.value, "spill_cap": c.value}
+        a, r, m, b, c = C.c_uint64(), C.c_uint64(), C.c_uint64(), C.c_int(), C.c_int()
+        check(lib().wv_last_side_stats(self._h, C.byref(a), C.byref(r), C.byref(m), C.byref(b), C.byref(c)))
+        return {"overflowed": a.value, "redone": r.value, "claims": m.value, "side_rows": b.value,
+                "spill_cap": c.value}
 
 
 class CommitLogGraph:
