@@ -857,6 +857,53 @@ def test_h16_key_pass_seeded_equals_unseeded_and_fp32(dim, metric):
         _same_tie_aware(gi[i], gd[i], oi[i], od[i])
 
 
+@pytest.mark.parametrize("metric", [O.L2, O.DOT, O.COSINE])
+def test_h16_seed_list_mode(metric):
+    """The seed pre-pass in list mode (WV_H16_SEED_LISTS; a 10k-ish batch: 19 query blocks, the
+    list pass's 13 slots x 16 entries fit the seed kernel's sort): minima over
+    every 64th tile, full lists over the corpus's last 69 of 1094 tiles
+    (keys above the minima thresholds dropped), the lists' 16 smallest handed
+    to the finalize as one more slot and the main pass over the other 1025
+    tiles.  Same ids and distances as minima mode (the default), as a
+    denser minima pass (WV_H16_LIST_MULT=1) and as the fp32 pass, with
+    tombstones, a shared allow list and a partial last query block; equal to
+    the restatement up to tie order on a sample of queries."""
+    import os
+    n, nq, dim = 70001, 9500, 128
+    base, qs = _data(n, dim, nq, seed=81, metric=metric)
+    rng = np.random.default_rng(82)
+    tomb_ids = np.nonzero(rng.random(n) < 0.02)[0]
+    allow_ids = np.nonzero(rng.random(n) < 0.6)[0]
+    al = W.AllowList.from_ids(allow_ids, n)
+    runs = []
+    for env in ({"WV_H16_SEED_LISTS": "1"}, {}, {"WV_H16_SEED_LISTS": "1", "WV_H16_LIST_MULT": "1"},
+                {"WV_BF_FP32": "1"}):
+        os.environ.update(env)
+        try:
+            ix = W.GPUVectorIndex(dim, METRIC_NAMES[metric], capacity=n)
+            ix.upload_vectors(base)
+            ix.set_tombstones(tomb_ids)
+            runs.append((ix.search_batch(qs, 10, mode="exact"), ix.search_batch(qs, 10, allow=al, mode="exact"),
+                         ix.last_batch_stats()["fallbacks"]))
+            ix.close()
+        finally:
+            for key in env:
+                os.environ.pop(key, None)
+    for other in runs[1:]:
+        for (ai, ad, an), (bi, bd, bn) in zip(runs[0][:2], other[:2]):
+            assert an.tolist() == bn.tolist()
+            _same(ai, ad, bi, bd)
+    assert runs[0][2] <= nq // 50, runs[0][2]
+    b = O.normalize_rows(base) if metric == O.COSINE else base
+    q = O.normalize_rows(qs) if metric == O.COSINE else qs
+    tb = O.bits_from_ids(tomb_ids, n)
+    sample = np.arange(0, nq, 19)
+    for allow_bits, (gi, gd, gn) in ((None, runs[0][0]), (al.words, runs[0][1])):
+        oi, od, on = O.flat_scan(metric, b, q[sample], 10, allow_bits=allow_bits, tomb_bits=tb, threads=16)
+        for j, i in enumerate(sample):
+            _same_tie_aware(gi[i], gd[i], oi[j], od[j])
+
+
 def test_h16_integer_data_keys_exact():
     """SIFT-shaped integer data: f16(s_x x) is exact (integers below 2048 x
     2^k), so the residual terms of the certificate vanish and the f16 keys are

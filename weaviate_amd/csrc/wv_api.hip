@@ -265,7 +265,7 @@ struct wv_index {
     bool h16_wide = false;  // D > 128: wv_bf_h16w_kernel (both operands through LDS, 128-row tiles)
     int h16_ns = 0;
     float h16_sx = 0.f, h16_ex = 0.f;
-    DevBuf ximg16, xns, qimg16, qres, qmax, qscale, tau, gtau, marg, allow_pad, ex_bits, gslot;
+    DevBuf ximg16, xns, qimg16, qres, qmax, qscale, tau, gtau, marg, allow_pad, ex_bits, gslot, seed_d, seed_id;
     // the f16 pass's block order (block_order), cached for its schedule
     DevBuf blk_order;
     std::vector<int> blk_order_host;
@@ -762,42 +762,20 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     int sample = wv::H_SAMPLE;   // (WV_H16_SAMPLE: the seed's tile stride, for measurements)
     if (const char* e = std::getenv("WV_H16_SAMPLE")) sample = std::max(1, std::atoi(e));
     const bool seed = !wd && ntl >= 64 * (uint64_t)sample && !std::getenv("WV_H16_NO_SEED");
-    if (seed) {
-        const uint64_t nts = (ntl + sample - 1) / sample;
-        const wv::BfSchedule ss = wv::bf_schedule(nq, nts * wv::H_BN, target(nts), bq, wv::H_BN);
-        HIP_TRY(ix->cand_d.ensure((size_t)nq * ss.n_slots * seed_prod * 4));
-        hp.ntiles = ss.ntiles;
-        hp.ntiles_real = ss.ntiles;
-        hp.units_per_block = ss.units_per_block;
-        hp.n_slots = ss.n_slots;
-        hp.tile_stride = sample;
-        hp.tau = nullptr;
-        hp.out_d = ix->cand_d.as<float>();
-        hp.out_id = nullptr;
-        TREC(6);
-        HIP_TRY(wv_launch_bf_h16(&hp, ns, 1, s));
-        wv::H16SeedParams sp{};
-        sp.minima = ix->cand_d.as<float>();
-        sp.n_slots = ss.n_slots;
-        sp.ntiles = ss.ntiles;
-        sp.units_per_block = ss.units_per_block;
-        sp.nq = nq;
-        sp.k = k;
-        sp.metric = ix->metric;
-        sp.D = ix->dim;
-        sp.qscale = ix->qscale.as<float>();
-        sp.sx = ix->h16_sx;
-        sp.qnorm = ix->q_nrm2.as<float>();
-        sp.xnorm_max = ix->maxnorm_host;
-        sp.ex_max = ix->h16_ex;
-        sp.qres = ix->qres.as<float>();
-        sp.tau = ix->tau.as<float>();
-        sp.gtau = ix->gtau.as<unsigned int>();
-        sp.bq = bq;
-        sp.prod = seed_prod;
-        HIP_TRY(wv_launch_h16_seed(&sp, s));
-        TREC(7);
-    }
+    // The seed pre-pass over 1 / sample of the tiles.  List mode
+    // (WV_H16_SEED_LISTS, where its lists fit the seed kernel's one-wave
+    // sort; measured slower, profiles/r06/h16_seed_list_mode.log): the
+    // pre-pass scans the corpus's last nts tiles with full lists, the seed
+    // kernel takes the thresholds from them and hands their 2 BF_KP smallest
+    // to the finalize as one more slot, and the main pass scans only the
+    // other tiles -- no tile is scanned twice.  Otherwise (minima mode) it
+    // scans every sample-th tile keeping minima, and the main pass all tiles.
+    const uint64_t nts = seed ? (ntl + sample - 1) / sample : 0;
+    wv::BfSchedule ss{};
+    if (seed) ss = wv::bf_schedule(nq, nts * wv::H_BN, target(nts), bq, wv::H_BN);
+    const bool seed_lists = seed && !wide && !n_dev && k <= 64 &&
+                            (uint64_t)ss.n_slots * wv::H_PROD * wv::BF_KP <= 256 && std::getenv("WV_H16_SEED_LISTS");
+    const uint64_t ntl_main = seed_lists ? ntl - nts : ntl;
     // the wide pass: query blocks cut at the same tile offsets where that
     // costs no work (bf_schedule_aligned)
     wv::BfSchedule sch{};
@@ -814,13 +792,95 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
         sch.n_slots = S + 1;
     }
     if (wd && !wide && sch.n_blocks == 0) sch = wv::bf_schedule_aligned(nq, N, target(ntl), bq, tile_rows, false);
-    if (sch.n_blocks == 0) sch = wv::bf_schedule(nq, N, target(ntl), bq, tile_rows);
+    if (sch.n_blocks == 0)
+        sch = wv::bf_schedule(nq, seed_lists ? ntl_main * tile_rows : N, target(ntl_main), bq, tile_rows);
     if (wide && (uint64_t)sch.n_slots * prod * kp > (uint64_t)wv::FINW_NE)
         return fail(WV_ESTATE, "run_h16: too many lists for the wide finalize");
-    HIP_TRY(ix->cand_d.ensure((size_t)nq * sch.n_slots * prod * kp * 4));
-    HIP_TRY(ix->cand_id.ensure((size_t)nq * sch.n_slots * prod * kp * 4));
+    // list slots per query: the main pass's, + the seed's slot (list mode)
+    const int out_slots = sch.n_slots + (seed_lists ? 1 : 0);
+    HIP_TRY(ix->cand_d.ensure((size_t)nq * out_slots * prod * kp * 4));
+    HIP_TRY(ix->cand_id.ensure((size_t)nq * out_slots * prod * kp * 4));
+    // a seed pre-pass: minima over every stride-th tile -> thresholds (tau)
+    auto seed_minima = [&](int stride) -> int {
+        const uint64_t nt = (ntl + stride - 1) / stride;
+        const wv::BfSchedule ms = wv::bf_schedule(nq, nt * wv::H_BN, target(nt), bq, wv::H_BN);
+        HIP_TRY(ix->cand_d.ensure((size_t)nq * std::max(ms.n_slots * seed_prod, out_slots * prod * kp) * 4));
+        hp.ntiles = ms.ntiles;
+        hp.ntiles_real = ms.ntiles;
+        hp.units_per_block = ms.units_per_block;
+        hp.n_slots = ms.n_slots;
+        hp.tile_stride = stride;
+        hp.tile_base = 0;
+        hp.tau = nullptr;
+        hp.out_d = ix->cand_d.as<float>();
+        hp.out_id = nullptr;
+        HIP_TRY(wv_launch_bf_h16(&hp, ns, 1, s));
+        wv::H16SeedParams sp{};
+        sp.minima = ix->cand_d.as<float>();
+        sp.n_slots = ms.n_slots;
+        sp.ntiles = ms.ntiles;
+        sp.units_per_block = ms.units_per_block;
+        sp.nq = nq;
+        sp.k = k;
+        sp.metric = ix->metric;
+        sp.D = ix->dim;
+        sp.qscale = ix->qscale.as<float>();
+        sp.sx = ix->h16_sx;
+        sp.qnorm = ix->q_nrm2.as<float>();
+        sp.xnorm_max = ix->maxnorm_host;
+        sp.ex_max = ix->h16_ex;
+        sp.qres = ix->qres.as<float>();
+        sp.tau = ix->tau.as<float>();
+        sp.gtau = ix->gtau.as<unsigned int>();
+        sp.bq = bq;
+        sp.prod = seed_prod;
+        if (seed_lists) {
+            // list mode: the list pass over the corpus's last nts tiles,
+            // keys above the minima's thresholds dropped; its lists give
+            // tighter thresholds (min with the minima's) and the finalize's
+            // extra slot
+            HIP_TRY(wv_launch_h16_seed(&sp, s));
+            HIP_TRY(ix->seed_d.ensure((size_t)nq * ss.n_slots * prod * kp * 4));
+            HIP_TRY(ix->seed_id.ensure((size_t)nq * ss.n_slots * prod * kp * 4));
+            hp.ntiles = ss.ntiles;
+            hp.ntiles_real = ss.ntiles;
+            hp.units_per_block = ss.units_per_block;
+            hp.n_slots = ss.n_slots;
+            hp.tile_stride = 1;
+            hp.tile_base = ntl_main;
+            hp.tau = ix->tau.as<float>();
+            hp.out_d = ix->seed_d.as<float>();
+            hp.out_id = ix->seed_id.as<uint32_t>();
+            HIP_TRY(wv_launch_bf_h16(&hp, ns, 0, s));
+            hp.tile_base = 0;
+            hp.tau = nullptr;
+            sp.minima = ix->seed_d.as<float>();
+            sp.ids = ix->seed_id.as<uint32_t>();
+            sp.n_slots = ss.n_slots;
+            sp.ntiles = ss.ntiles;
+            sp.units_per_block = ss.units_per_block;
+            sp.prod = prod * kp;
+            sp.out_d = ix->cand_d.as<float>();
+            sp.out_id = ix->cand_id.as<uint32_t>();
+            sp.out_slots = out_slots;
+            sp.out_ntiles = sch.ntiles;
+            sp.out_upb = sch.units_per_block;
+        }
+        HIP_TRY(wv_launch_h16_seed(&sp, s));
+        return WV_OK;
+    };
+    if (seed) {
+        TREC(6);
+        // (list mode: minima over every 4 sample-th tile for the list pass;
+        // WV_H16_LIST_MULT: that factor, for measurements)
+        int mult = 4;
+        if (const char* e = std::getenv("WV_H16_LIST_MULT")) mult = std::max(1, std::atoi(e));
+        if (int rc = seed_minima(seed_lists ? mult * sample : sample)) return rc;
+        TREC(7);
+    }
     hp.ntiles = sch.ntiles;
-    hp.ntiles_real = ntl;
+    hp.ntiles_real = ntl_main;
+    hp.out_slots = seed_lists ? out_slots : 0;
     hp.units_per_block = sch.units_per_block;
     hp.n_slots = sch.n_slots;
     hp.n_dev = n_dev;
@@ -860,7 +920,7 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     // the 8-wave D <= 128 pass on the flat schedule: tiles rotated per query
     // block (locality bit 2): 2.73-2.75 -> 2.66-2.68 ms per 1M x 10k pass,
     // L2-miss bytes 5.23 -> 0.66 GB
-    const bool rotate = !wd && nqb >= 2 && sch.ntiles == ntl;
+    const bool rotate = !wd && nqb >= 2 && sch.ntiles == ntl_main;
     if (rotate) hp.locality |= 2;
     if (int rc = block_order(ix, (uint64_t)nqb, sch, s, &hp.block_order, rotate)) return rc;
     TREC(0);
@@ -879,7 +939,8 @@ int run_h16(wv_index* ix, const float* d_q, int nq, int k, const uint64_t* d_all
     }
     fp.cand_d = ix->cand_d.as<float>();
     fp.cand_id = ix->cand_id.as<uint32_t>();
-    fp.n_slots = sch.n_slots;
+    fp.n_slots = out_slots;
+    fp.extra_slot = seed_lists ? 1 : 0;
     fp.ntiles = sch.ntiles;
     fp.units_per_block = sch.units_per_block;
     HIP_TRY(wv_launch_h16_gtau(ix->gtau.as<unsigned int>(), nq, ix->h16_sx, ix->qscale.as<float>(), ix->tau.as<float>(),

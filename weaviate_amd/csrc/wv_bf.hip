@@ -629,71 +629,7 @@ __global__ __launch_bounds__(128 * WN, 4 / WN) void wv_bf_split_kernel(BfParams 
 // ---------------------------------------------------------------------------
 // Finalize: one wave per query.
 
-// Finalize sort keys: (dist, id) as one u64 whose unsigned order is
-// key_less's (dist's bits made monotonic -- -0 folded into +0 first, as the
-// float compare ties them -- then the id's 31 bits; nil ids come back as nil:
-// no row id reaches 2^31 - 1).  One v_cmp_lt_u64 per compare: key_less's
-// short-circuit form compiled to exec-mask branches in these sorts, ~10x
-// their shuffle cost at one wave per SIMD (in-kernel stamps).
-__device__ __forceinline__ uint64_t fin_key(float d, uint32_t id) {
-    uint32_t u = __float_as_uint(d + 0.0f);
-    u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-    return ((uint64_t)u << 32) | (uint64_t)(id & WV_IDMASK);
-}
-__device__ __forceinline__ void fin_unkey(uint64_t k, float& d, uint32_t& id) {
-    uint32_t u = (uint32_t)(k >> 32);
-    u = (u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u;
-    d = __uint_as_float(u);
-    const uint32_t lo = (uint32_t)k;
-    id = lo == WV_IDMASK ? WV_NIL : lo;
-}
-
-// A wave-wide bitonic sort of 256 fin_key keys, element i = 64 j + lane in
-// register j: strides >= 64 inside the lane, smaller ones by shuffles; the
-// smallest FIN_KF end in lanes 0 .. FIN_KF - 1 of j = 0.
-__device__ __forceinline__ void bitonic256_wave(uint64_t (&kk)[4], int lane) {
-#pragma unroll
-    for (int k = 2; k <= 256; k <<= 1) {
-#pragma unroll
-        for (int jj = k >> 1; jj > 0; jj >>= 1) {
-            if (jj >= 64) {
-                // (register pairs named by literal indices: a runtime
-                // j ^ (jj / 64) made the arrays dynamically indexed)
-                auto cas = [&](auto jc, auto pc) {
-                    constexpr int j = decltype(jc)::value, pj = decltype(pc)::value;
-                    const bool up = ((64 * j + lane) & k) == 0;   // element j is the lower index
-                    // (operands selected, then one compare: a ternary of two
-                    // compares compiled to exec-mask branches)
-                    const uint64_t a = up ? kk[pj] : kk[j], b = up ? kk[j] : kk[pj];
-                    const bool sw = a < b;
-                    const uint64_t t = kk[j];
-                    kk[j] = sw ? kk[pj] : kk[j];
-                    kk[pj] = sw ? t : kk[pj];
-                };
-                using I0 = std::integral_constant<int, 0>;
-                using I1 = std::integral_constant<int, 1>;
-                using I2 = std::integral_constant<int, 2>;
-                using I3 = std::integral_constant<int, 3>;
-                if (jj == 64) { cas(I0{}, I1{}); cas(I2{}, I3{}); }
-                else { cas(I0{}, I2{}); cas(I1{}, I3{}); }
-            } else {
-                const bool lower = (lane & jj) == 0;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const uint32_t plo = (uint32_t)__shfl_xor((int)(uint32_t)kk[j], jj, 64);
-                    const uint32_t phi = (uint32_t)__shfl_xor((int)(uint32_t)(kk[j] >> 32), jj, 64);
-                    const uint64_t pk = ((uint64_t)phi << 32) | plo;
-                    const bool up = ((64 * j + lane) & k) == 0;
-                    // the lower index of an ascending pair keeps the min
-                    const bool c = lower == up;
-                    const uint64_t a = c ? pk : kk[j], b = c ? kk[j] : pk;
-                    const bool take = a < b;
-                    kk[j] = take ? pk : kk[j];
-                }
-            }
-        }
-    }
-}
+// (fin_key, fin_unkey, bitonic256_wave: wv_topk.h)
 
 // FAST: every query has <= 256 list entries (n_slots * prod * kp): one
 // bitonic selection; otherwise the list heads bound a short list that is
@@ -704,7 +640,7 @@ template <int METRIC, bool FAST>
 __device__ __forceinline__ void finalize_one(const BfFinParams& p, int q, float* sd, uint32_t* si, float* qv,
                                              float* kept_d, uint32_t* kept_i) {
     const int lane = threadIdx.x & 63;
-    const int n_lists = bf_slots_of((uint64_t)(q / p.bq), p.ntiles, p.units_per_block) * p.prod;
+    const int n_lists = (bf_slots_of((uint64_t)(q / p.bq), p.ntiles, p.units_per_block) + p.extra_slot) * p.prod;
     const int kp = p.kp ? p.kp : BF_KP;   // entries per list
     const int n_ent = n_lists * kp;
     const float* cd = p.cand_d + (size_t)q * p.n_slots * p.prod * kp;

@@ -101,7 +101,7 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16_kernel(H16Params p) {
     // word on wave 0): a lane offset per share, computed once
     const uint32_t voff = (uint32_t)(wave * 1024 + lane * 16);
     auto fill = [&](uint64_t t, int st) {
-        const uint64_t tile = t * (uint64_t)p.tile_stride;
+        const uint64_t tile = p.tile_base + t * (uint64_t)p.tile_stride;
         const uint32_t dst = lds0 + (uint32_t)(st * St::U4 * 16) + (uint32_t)(wave * 1024);
         const uint4* src = uniform_ptr(X + tile * St::IMG_U4);
 #pragma unroll
@@ -290,7 +290,7 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16_kernel(H16Params p) {
         // rows 4 khalf + ..., low word: rows 0-31, high word: rows 32-63)
         // (the lane-dependent shifts happen only when a tile needs the mask)
         auto tile_ok = [&](uint64_t t, uint64_t& okw) -> bool {
-            const uint64_t ct = t * (uint64_t)p.tile_stride;
+            const uint64_t ct = p.tile_base + t * (uint64_t)p.tile_stride;
             if (ct < p.clean_tiles) {   // (the host's clean prefix: no word to read)
                 okw = ~0ull;
                 return false;
@@ -471,9 +471,10 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16_kernel(H16Params p) {
         // row base of tile t (scalar; wraps with the rotation)
         uint32_t rbase = (uint32_t)(phys(t_begin) * (uint64_t)p.tile_stride * H_BN);
         const uint32_t rb_step = (uint32_t)(p.tile_stride * H_BN), rb_wrap = (uint32_t)(p.ntiles * p.tile_stride * H_BN);
+        const uint32_t rb_base = (uint32_t)(p.tile_base * H_BN);   // (rows of the scanned range's first tile)
         int xs_next = XS && xs ? xs1 : -1;   // the next cross-slot exchange tile
         for (int t = 0; t < ntile; ++t) {
-            const uint32_t rb0 = rbase + 4 * khalf;
+            const uint32_t rb0 = rb_base + rbase + 4 * khalf;
             rbase += rb_step;
             if (rbase >= rb_wrap) rbase -= rb_wrap;
             WV_DBG_COUNT(0)
@@ -556,7 +557,7 @@ __global__ __launch_bounds__(512, 1) void wv_bf_h16_kernel(H16Params p) {
             if (jq1 < p.nq) p.out_d[((size_t)jq1 * p.n_slots + slot) * H_PROD + khalf] = l1d[0];
             continue;
         }
-        const size_t per_q = (size_t)p.n_slots * H_PROD * BF_KP;
+        const size_t per_q = (size_t)(p.out_slots ? p.out_slots : p.n_slots) * H_PROD * BF_KP;
         if (jq0 < p.nq) {
             const size_t base = (size_t)jq0 * per_q + ((size_t)slot * H_PROD + khalf) * BF_KP;
 #pragma unroll
@@ -1007,7 +1008,34 @@ __global__ __launch_bounds__(64) void wv_h16_seed_kernel(H16SeedParams p) {
     const float* m = p.minima + (size_t)q * p.n_slots * prod;
     const float inv_s = 1.0f / (p.sx * p.qscale[0]);
     float mk = __builtin_inff();
-    if (n <= 256) {
+    if (p.ids) {
+        // list mode (n <= 256, k <= 64: the host's condition): every entry
+        // sorted by (key, id); the k-th a real row's, or none
+        const size_t off = (size_t)q * p.n_slots * prod;
+        uint64_t kk[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int e = 64 * j + lane;
+            const uint32_t id = e < n ? p.ids[off + e] : WV_NIL;
+            kk[j] = fin_key(id != WV_NIL ? p.minima[off + e] : FLT_MAX, id);
+        }
+        bitonic256_wave(kk, lane);
+        float d;
+        uint32_t id;
+        fin_unkey(kk[0], d, id);
+        const float dk = __shfl(d, p.k - 1, 64);
+        const uint32_t ik = (uint32_t)__shfl((int)id, p.k - 1, 64);
+        if (ik != WV_NIL) mk = dk;
+        // the 2 BF_KP smallest: one more slot of the main pass's lists (even
+        // ranks, odd ranks), after the query block's own slots
+        const int os = bf_slots_of((uint64_t)(q / p.bq), p.out_ntiles, p.out_upb);
+        const size_t ob = ((size_t)q * p.out_slots + os) * H_PROD * BF_KP;
+        if (lane < H_PROD * BF_KP) {
+            const size_t o = ob + (size_t)(lane & 1) * BF_KP + (lane >> 1);
+            p.out_d[o] = d;
+            p.out_id[o] = id;
+        }
+    } else if (n <= 256) {
         // the k-th smallest by a wave-wide bitonic sort of the (<= 256)
         // minima, element i = 64 j + lane in register j
         float v[4];
@@ -1077,6 +1105,9 @@ __global__ __launch_bounds__(64) void wv_h16_seed_kernel(H16SeedParams p) {
             tau = key + 2.f * eps;
             tau += 4.f * 5.9604645e-08f * (fabsf(key) + 2.f * eps) + 1e-3f * eps;   // this sum's rounding
         }
+        // (list mode: the list pass dropped keys above the minima pass's
+        // threshold, already in p.tau -- the thresholds only decrease)
+        if (p.ids) tau = fminf(tau, p.tau[q]);
         p.tau[q] = tau;
         if (p.gtau) p.gtau[q] = h16_key_enc(tau * (p.sx * p.qscale[0]));
     }
@@ -1335,7 +1366,8 @@ hipError_t wv_launch_bf_h16(const wv::H16Params* p, int ns, int seed, hipStream_
     const uint64_t total = (uint64_t)p->n_qblocks * p->ntiles;
     const unsigned nb = (unsigned)((total + p->units_per_block - 1) / p->units_per_block);
     if (nb == 0) return hipSuccess;
-    if (ns < 1 || ns > wv::H_NS_MAX || !p->X || !p->Q || !p->excl || !p->qscale || p->tile_stride < 1)
+    if (ns < 1 || ns > wv::H_NS_MAX || !p->X || !p->Q || !p->excl || !p->qscale || p->tile_stride < 1 ||
+        (p->out_slots && p->out_slots < p->n_slots) || (seed && (p->out_slots || p->tile_base)))
         return hipErrorInvalidValue;
     const bool l2 = p->metric == WV_METRIC_L2;
     if (l2 && !p->xns) return hipErrorInvalidValue;
@@ -1387,7 +1419,7 @@ hipError_t wv_launch_bf_h16w(const wv::H16Params* p, hipStream_t s) {
     const unsigned nb = (unsigned)((total + p->units_per_block - 1) / p->units_per_block);
     if (nb == 0) return hipSuccess;
     if (p->ns < 2 * wv::HW_KC || p->ns > wv::HW_NS_MAX || p->ns % wv::HW_KC || !p->X || !p->Q || !p->excl ||
-        p->tile_stride != 1)
+        p->tile_stride != 1 || p->tile_base != 0 || p->out_slots != 0)
         return hipErrorInvalidValue;
     const bool l2 = p->metric == WV_METRIC_L2;
     if (l2 && !p->xns) return hipErrorInvalidValue;
@@ -1403,6 +1435,9 @@ hipError_t wv_launch_bf_h16w(const wv::H16Params* p, hipStream_t s) {
 hipError_t wv_launch_h16_seed(const wv::H16SeedParams* p, hipStream_t s) {
     if (p->nq == 0) return hipSuccess;
     if (p->k < 1 || p->k > wv::BF_WIDE_KMAX) return hipErrorInvalidValue;
+    if (p->ids && (p->k > 64 || p->prod != wv::H_PROD * wv::BF_KP || (size_t)p->n_slots * p->prod > 256 ||
+                   !p->out_d || !p->out_id || p->out_slots < 1))
+        return hipErrorInvalidValue;
     hipLaunchKernelGGL(wv::wv_h16_seed_kernel, dim3(p->nq), dim3(64), 0, s, *p);
     return hipGetLastError();
 }

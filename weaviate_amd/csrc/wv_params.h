@@ -158,7 +158,9 @@ struct H16Params {
     int n_qblocks, n_slots;
     uint64_t ntiles, units_per_block;   // ntiles: tiles scanned (the sample's when tile_stride > 1)
     uint64_t ntiles_real;     // the wide-D pass: the corpus's tiles (ntiles, the unit grid per query block, may pad it)
-    int tile_stride;          // corpus tile = scanned tile * tile_stride (seed pre-pass)
+    int tile_stride;          // corpus tile = tile_base + scanned tile * tile_stride (seed pre-pass)
+    uint64_t tile_base;       // (the D <= 128 pass; 0 elsewhere)
+    int out_slots;            // list slots per query in out_d / out_id (0: n_slots)
     uint64_t clean_tiles;     // corpus tiles [0, clean_tiles) have no excluded row (no allow list either): no mask
     int locality;             // bit 1: XCD-contiguous workgroup ids
     const int* block_order;   // optional: XCD-contiguous position -> block (run_h16's block_order)
@@ -235,6 +237,17 @@ struct H16SeedParams {
     unsigned int* gtau;       // [nq] out (nullable): h16_key_enc(tau * s), the running threshold's start
     int bq;                   // queries per block of the pre-pass
     int prod;                 // minima per query per slot (0: H_PROD)
+    // list mode (ids != nullptr; tau holds the minima pre-pass's thresholds,
+    // which the result never exceeds): `minima` are the list pre-pass's lists
+    // ([nq][n_slots][prod] entries, prod = H_PROD BF_KP), the key of each a
+    // distinct row; their 2 BF_KP smallest also go to the main pass's lists as
+    // one more slot (slot bf_slots_of(qb) of out_ntiles / out_upb, out_slots
+    // per query): even ranks to its first list, odd ranks to its second
+    const uint32_t* ids;
+    float* out_d;
+    uint32_t* out_id;
+    int out_slots;
+    uint64_t out_ntiles, out_upb;
 };
 
 struct BfFinParams {
@@ -245,6 +258,7 @@ struct BfFinParams {
     const float* qnorm;     // |q|^2 (L2) or |q| (dot, cosine)
     float xnorm_max;        // max |x| over the corpus (rounded up)
     int n_slots;            // list slots per query (BfParams.n_slots)
+    int extra_slot;         // 1: one more slot of lists after a query block's slots (the seed pre-pass's)
     uint64_t ntiles, units_per_block;
     int nq, D, ldx, ldq, metric, k;
     uint64_t id_base;       // global id of local id 0
