@@ -6,6 +6,7 @@
 # within the per-block limits: FETCH_SIZE alone, 8 SQ + 1 GRBM).
 #   LINE=head  wv_bf_h16_kernel main pass, configs[1] (1M x 128, 10k queries)
 #   LINE=c4    wv_bf_h16w_kernel, configs[3] 100 % leg (10M x 768, 1000 queries)
+#   LINE=c4_50 / c4_10 / c4_1  the same kernel on the 50 / 10 / 1 % allow-list legs
 #   LINE=c5    wv_hnsw_kernel, configs[4] over the 100M corpus (ef 128)
 # Output: gpurun_out/pmc_bench/<LINE>/ (logs, kernel stats) and
 # gpurun_out/pmc_bench/pmc_<kernel>[_<shape>].json; the raw traces and counter
@@ -24,6 +25,11 @@ case $LINE in
   c4)   ARGS="$OFF --no-hnsw-line --no-c3-line --no-c5-line --c4-fracs 1.0"
         KNAME=wv_bf_h16w_kernel; KSUB="wv_bf_h16w_kernel<false, 128>"; SHAPE="10000000 1000 768 gauss"
         OUTJ=pmc_wv_bf_h16w_kernel_c4.json; T=300;;
+  c4_50|c4_10|c4_1)
+        F=${LINE#c4_}; FR=$(python3 -c "print({'50': '0.5', '10': '0.1', '1': '0.01'}['$F'])")
+        ARGS="$OFF --no-hnsw-line --no-c3-line --no-c5-line --c4-fracs $FR"
+        KNAME=wv_bf_h16w_kernel; KSUB="wv_bf_h16w_kernel<false, 128>"; SHAPE="10000000 1000 768 gauss_allow$FR"
+        OUTJ=pmc_wv_bf_h16w_kernel_c4_$F.json; T=300;;
   c5)   ARGS="$OFF --no-hnsw-line --no-c3-line --no-c4-line"
         KNAME=wv_hnsw_kernel; KSUB="wv_hnsw_kernel<0, false, 2>"; SHAPE="100000000 10000 96 sift"
         OUTJ=pmc_wv_hnsw_kernel_c5.json; T=900;;
