@@ -8,6 +8,7 @@
 #   LINE=c4    wv_bf_h16w_kernel, configs[3] 100 % leg (10M x 768, 1000 queries)
 #   LINE=c4_50 / c4_10 / c4_1  the same kernel on the 50 / 10 / 1 % allow-list legs
 #   LINE=c5    wv_hnsw_kernel, configs[4] over the 100M corpus (ef 128)
+#   LINE=c3t1  wv_hnsw_side_kernel, configs[2]'s line with 1 % of ids tombstoned
 # Output: gpurun_out/pmc_bench/<LINE>/ (logs, kernel stats) and
 # gpurun_out/pmc_bench/pmc_<kernel>[_<shape>].json; the raw traces and counter
 # tables stay in /tmp (a full run's trace exceeds what gpurun merges back);
@@ -30,11 +31,16 @@ case $LINE in
         ARGS="$OFF --no-hnsw-line --no-c3-line --no-c5-line --c4-fracs $FR"
         KNAME=wv_bf_h16w_kernel; KSUB="wv_bf_h16w_kernel<false, 128>"; SHAPE="10000000 1000 768 gauss_allow$FR"
         OUTJ=pmc_wv_bf_h16w_kernel_c4_$F.json; T=300;;
+  c3t1) # (the tombstoned leg needs the restatement's counts: CPU baseline on, short)
+        ARGS="--no-corpus-leg --no-group-leg --no-wide-line --steps 5 --warmup 2 --cpu-seconds 2 --cpu-seconds-t1 1"
+        ARGS="$ARGS --no-hnsw-line --no-c4-line --no-c5-line --no-seq-build"
+        KNAME=wv_hnsw_side_kernel; KSUB="wv_hnsw_side_kernel<2, 1, 3, 3, false>"; SHAPE="1200000 10000 100 glove"
+        AF="tomb:0.01"; OUTJ=pmc_wv_hnsw_side_kernel_c3t1.json; T=300;;
   c5)   ARGS="$OFF --no-hnsw-line --no-c3-line --no-c4-line"
         KNAME=wv_hnsw_kernel; KSUB="wv_hnsw_kernel<0, false, 2>"; SHAPE="100000000 10000 96 sift"
         OUTJ=pmc_wv_hnsw_kernel_c5.json; T=900;;
 esac
-export KNAME KSUB SHAPE OUTJ O
+export KNAME KSUB SHAPE OUTJ O AF
 export WV_BUILD_HASH=$(python3 -c "import sys; sys.path.insert(0, 'tools'); from build_hash import build_hash; print(build_hash('$KNAME'))")
 timeout -k 10 $T rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 bench.py $ARGS > $G/$LINE/trace.log 2>&1
 i=0
@@ -65,6 +71,8 @@ js = {"kernel": kname, "N": int(N), "nq": int(nq), "dim": int(dim), "data": data
       "note": "median over the dispatches of bench.py's own run of this line (tools/pmc_bench.sh); "
               "read = 2*FETCH_SIZE*1024 (gfx950 half-count correction)",
       "source": "profiles/%s (tools/pmc_bench.sh LINE=%s)" % (os.environ["OUTJ"], os.path.basename(O))}
+if os.environ.get("AF"):
+    js["allow_frac"] = os.environ["AF"]
 if "FETCH_SIZE" in out:
     js["hbm_read_bytes_per_launch"] = js["hbm_bytes_per_launch"] = 2.0 * out["FETCH_SIZE"] * 1024
 sq = js["sq"]
