@@ -1493,6 +1493,7 @@ def main():
             a1 = argparse.Namespace(**vars(args))
             a1.seq_build = (args.seq_build or (not args.no_seq_build and args.rows == 1_000_000)) and ws == 1
             a1.filtered_fracs = [] if args.no_filtered_hnsw else [0.1, 0.5, 0.01]
+            a1.dump_ids = ""   # (--dump-ids holds the exact line's answers)
             phase("configs[0] hnsw line")
             h = run_hnsw(a1, ctx, W, with_cpu)
             h.pop("metric", None)
@@ -1502,7 +1503,7 @@ def main():
             a3 = argparse.Namespace(**vars(args))
             a3.rows, a3.dim, a3.metric, a3.hnsw_data = 1_200_000, 100, "cosine-dot", "glove"
             a3.ef, a3.ef_sweep, a3.concurrency, a3.split = 64, [32, 64, 128, 256], [], "corpus"
-            a3.cpu_seconds, a3.cpu_seconds_t1, a3.graph_build = 4.0, 2.0, "gpu"
+            a3.cpu_seconds, a3.cpu_seconds_t1, a3.graph_build, a3.dump_ids = 4.0, 2.0, "gpu", ""
             # north_star's 0.5-pt recall check against the insert-by-insert
             # graph at this line's ef and 128 (~50 s of CPU at 1.2M rows)
             a3.seq_build = not args.no_seq_build and ws == 1
